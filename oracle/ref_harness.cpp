@@ -1,0 +1,839 @@
+/*
+ * oracle/ref_harness.cpp — drives the REAL reference (Stan Math 3.0.0 headers
+ * under /root/reference, compiled by oracle/Makefile into oracle/_ref/) to
+ *   (1) generate the golden fixtures committed under tests/golden/  ("gen")
+ *   (2) time the reference CPU path for bench.py's cpu_baseline     ("bench")
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in math_amd/ links or calls this; it is
+ * the checker / baseline, never the product.
+ *
+ * Build note: the reference always includes rev/core/init_chainablestack.hpp,
+ * whose TBB task-scheduler observer needs libtbb at link time.  It is only
+ * there to give STAN_THREADS worker threads their tapes; this harness is
+ * single-threaded, so it defines that header's include guard and owns the
+ * main-thread tape through the documented AutodiffStackSingleton instance
+ * (rev/core/autodiffstackstorage.hpp:55-60).  No reference source is copied
+ * or replaced: everything below calls the reference's own functions.
+ *
+ * Functions exercised (reference file:line):
+ *   gradient                 stan/math/rev/mat/functor/gradient.hpp:41-57
+ *   gp_exp_quad_cov (var)    stan/math/rev/mat/fun/gp_exp_quad_cov.hpp:213-242
+ *   add_diag                 stan/math/prim/mat/fun/add_diag.hpp:20-55
+ *   cholesky_decompose       stan/math/rev/mat/fun/cholesky_decompose.hpp:378-427
+ *   multi_normal_cholesky    stan/math/prim/mat/prob/multi_normal_cholesky_lpdf.hpp:40-160
+ *   multiply                 stan/math/rev/mat/fun/multiply.hpp:562-661
+ *   mdivide_left_tri         stan/math/rev/mat/fun/mdivide_left_tri.hpp:311-373
+ *   log_sum_exp              stan/math/rev/mat/fun/log_sum_exp.hpp:20-53,
+ *                            stan/math/rev/scal/fun/log_sum_exp.hpp:15-68
+ *   lgamma / digamma (var)   stan/math/rev/scal/fun/lgamma.hpp:13-32, digamma.hpp:13-22
+ *   trigamma (double)        stan/math/prim/scal/fun/trigamma.hpp:33-125
+ *   normal_lpdf              stan/math/prim/scal/prob/normal_lpdf.hpp:36-119
+ *   bernoulli_logit_glm_lpmf stan/math/prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138
+ *   map_rect                 stan/math/prim/mat/functor/map_rect.hpp:120-177
+ *   hessian_times_vector     stan/math/mix/mat/functor/hessian_times_vector.hpp:13-40
+ */
+#define STAN_MATH_REV_CORE_INIT_CHAINABLESTACK_HPP
+#include <stan/math/mix/mat.hpp>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "gen.h"
+
+stan::math::ChainableStack main_thread_tape;  // owns the main-thread tape
+
+using Eigen::Dynamic;
+using Eigen::Matrix;
+using Eigen::MatrixXd;
+using Eigen::VectorXd;
+using stan::math::var;
+
+// ----------------------------------------------------------------- JSON out
+struct Json {
+  std::ostringstream os;
+  bool first = true;
+  Json() { os << "{"; }
+  void key(const std::string& k) {
+    os << (first ? "\n" : ",\n") << "  \"" << k << "\": ";
+    first = false;
+  }
+  static std::string num(double v) {
+    if (std::isnan(v)) return "\"nan\"";
+    if (std::isinf(v)) return v > 0 ? "\"inf\"" : "\"-inf\"";
+    char b[40];
+    std::snprintf(b, sizeof b, "%.17g", v);
+    return b;
+  }
+  void put(const std::string& k, double v) {
+    key(k);
+    os << num(v);
+  }
+  void put_int(const std::string& k, long long v) {
+    key(k);
+    os << v;
+  }
+  void put_str(const std::string& k, const std::string& v) {
+    key(k);
+    os << "\"" << v << "\"";
+  }
+  template <typename V>
+  void put_vec(const std::string& k, const V& v, size_t n) {
+    key(k);
+    os << "[";
+    for (size_t i = 0; i < n; ++i) os << (i ? ", " : "") << num(v[i]);
+    os << "]";
+  }
+  void put_vec(const std::string& k, const std::vector<double>& v) {
+    put_vec(k, v, v.size());
+  }
+  void put_vec(const std::string& k, const VectorXd& v) {
+    put_vec(k, v.data(), (size_t)v.size());
+  }
+  void put_mat(const std::string& k, const MatrixXd& m) {  // column-major
+    put_vec(k, m.data(), (size_t)m.size());
+  }
+  void put_ivec(const std::string& k, const std::vector<int>& v) {
+    key(k);
+    os << "[";
+    for (size_t i = 0; i < v.size(); ++i) os << (i ? ", " : "") << v[i];
+    os << "]";
+  }
+  std::string str() { return os.str() + "\n}\n"; }
+};
+
+static std::string g_outdir = "tests/golden";
+static void write_fixture(const std::string& name, Json& j) {
+  std::string path = g_outdir + "/" + name + ".json";
+  std::ofstream f(path);
+  f << j.str();
+  std::fprintf(stderr, "wrote %s\n", path.c_str());
+}
+
+// -------------------------------------------------------------- generators
+static std::vector<double> unif(uint64_t seed, size_t n, double a, double b) {
+  std::vector<double> v(n);
+  smg_fill_unif(seed, n, a, b, v.data());
+  return v;
+}
+// Box-Muller normals (stored in fixtures, never regenerated elsewhere)
+static std::vector<double> normals(uint64_t seed, size_t n) {
+  smg_rng r = smg_rng_make(seed);
+  std::vector<double> v(n);
+  for (size_t i = 0; i < n; i += 2) {
+    double u1 = 1.0 - smg_rng_u01(&r), u2 = smg_rng_u01(&r);
+    double rad = std::sqrt(-2.0 * std::log(u1));
+    v[i] = rad * std::cos(2 * M_PI * u2);
+    if (i + 1 < n) v[i + 1] = rad * std::sin(2 * M_PI * u2);
+  }
+  return v;
+}
+
+static const uint64_t SEED = 20260101ULL;
+
+// GP inputs (config 3): x ~ U(-10,10), y = sin(x) + 0.3 eps
+static void gp_inputs(int N, std::vector<double>& x, VectorXd& y) {
+  x = unif(SEED + 3, N, -10.0, 10.0);
+  std::vector<double> e = normals(SEED + 33, N);
+  y.resize(N);
+  for (int i = 0; i < N; ++i) y(i) = std::sin(x[i]) + 0.3 * e[i];
+}
+
+struct gp_functor {
+  const std::vector<double>& x;
+  const VectorXd& y;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    using namespace stan::math;
+    const int N = (int)x.size();
+    Matrix<T, Dynamic, Dynamic> K = gp_exp_quad_cov(x, th(0), th(1));
+    Matrix<T, Dynamic, Dynamic> Kd = add_diag(K, square(th(2)));
+    Matrix<T, Dynamic, Dynamic> L = cholesky_decompose(Kd);
+    VectorXd mu = VectorXd::Zero(N);
+    return multi_normal_cholesky_lpdf(y, mu, L);
+  }
+};
+
+// config 2: f(A) = sum(cholesky_decompose(add_diag(multiply(A, A'), N)))
+struct mulchol_functor {
+  int N;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& a) const {
+    using namespace stan::math;
+    Matrix<T, Dynamic, Dynamic> A(N, N);
+    for (int i = 0; i < N * N; ++i) A(i) = a(i);
+    Matrix<T, Dynamic, Dynamic> C = multiply(A, transpose(A));
+    Matrix<T, Dynamic, Dynamic> Cd = add_diag(C, (double)N);
+    return sum(cholesky_decompose(Cd));
+  }
+};
+static VectorXd mulchol_input(int N) {
+  std::vector<double> a = unif(SEED + 2, (size_t)N * N, -1.0, 1.0);
+  const double s = std::sqrt(3.0 / N);
+  VectorXd v(N * N);
+  for (int i = 0; i < N * N; ++i) v(i) = a[i] * s;
+  return v;
+}
+
+// config 4 inputs (column-major x, R x M)
+struct glm_data {
+  int R, M;
+  MatrixXd x;
+  std::vector<int> y;
+  VectorXd theta;  // (alpha, beta_1..M)
+};
+static glm_data glm_inputs(int R, int M) {
+  glm_data d;
+  d.R = R;
+  d.M = M;
+  std::vector<double> xv = unif(SEED + 41, (size_t)R * M, -1.0, 1.0);
+  const double s3 = std::sqrt(3.0);
+  d.x.resize(R, M);
+  for (size_t i = 0; i < (size_t)R * M; ++i) d.x.data()[i] = xv[i] * s3;
+  d.y.resize(R);
+  smg_fill_bernoulli(SEED + 42, R, 0.5, d.y.data());
+  std::vector<double> b = unif(SEED + 43, M, -1.0, 1.0);
+  const double sb = std::sqrt(3.0 / M);
+  d.theta.resize(M + 1);
+  d.theta(0) = 0.1;
+  for (int j = 0; j < M; ++j) d.theta(j + 1) = b[j] * sb;
+  return d;
+}
+struct glm_functor {
+  const glm_data& d;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, 1> beta = th.tail(d.M);
+    return stan::math::bernoulli_logit_glm_lpmf(d.y, d.x, th(0), beta);
+  }
+};
+
+// map_rect job functor: one shard of rows; x_r = shard of x (col-major), x_i = y
+struct glm_shard_functor {
+  template <typename T1, typename T2>
+  Matrix<stan::return_type_t<T1, T2>, Dynamic, 1> operator()(
+      const Matrix<T1, Dynamic, 1>& eta, const Matrix<T2, Dynamic, 1>& /*phi*/,
+      const std::vector<double>& x_r, const std::vector<int>& x_i,
+      std::ostream* /*msgs*/) const {
+    const int M = eta.size() - 1;
+    const int r = (int)x_i.size();
+    MatrixXd xs = Eigen::Map<const MatrixXd>(x_r.data(), r, M);
+    Matrix<T1, Dynamic, 1> beta = eta.tail(M);
+    Matrix<stan::return_type_t<T1, T2>, Dynamic, 1> out(1);
+    out(0) = stan::math::bernoulli_logit_glm_lpmf(x_i, xs, eta(0), beta);
+    return out;
+  }
+};
+struct glm_maprect_functor {
+  const std::vector<std::vector<double>>& xr;
+  const std::vector<std::vector<int>>& xi;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    std::vector<Matrix<double, Dynamic, 1>> job(xr.size());
+    return stan::math::sum(
+        stan::math::map_rect<1, glm_shard_functor>(th, job, xr, xi));
+  }
+};
+
+static void shard_glm(const glm_data& d, int shards,
+                      std::vector<std::vector<double>>& xr,
+                      std::vector<std::vector<int>>& xi) {
+  xr.assign(shards, {});
+  xi.assign(shards, {});
+  for (int s = 0; s < shards; ++s) {
+    int r0 = (int)((long long)d.R * s / shards);
+    int r1 = (int)((long long)d.R * (s + 1) / shards);
+    int r = r1 - r0;
+    xr[s].resize((size_t)r * d.M);
+    for (int j = 0; j < d.M; ++j)
+      for (int i = 0; i < r; ++i) xr[s][(size_t)j * r + i] = d.x(r0 + i, j);
+    xi[s].assign(d.y.begin() + r0, d.y.begin() + r1);
+  }
+}
+
+// normal_lpdf (config 1)
+struct normal_functor {
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    return stan::math::normal_lpdf(th, 0.0, 1.0);
+  }
+};
+
+// --------------------------------------------------------------- fixtures
+static void fix_gp() {
+  for (int N : {16, 64, 256, 1024, 4096}) {
+    std::vector<double> x;
+    VectorXd y;
+    gp_inputs(N, x, y);
+    VectorXd th(3);
+    th << 1.0, 1.5, 0.3;
+    double fx;
+    VectorXd g;
+    auto t0 = std::chrono::steady_clock::now();
+    stan::math::gradient(gp_functor{x, y}, th, fx, g);
+    double sec = std::chrono::duration<double>(
+                     std::chrono::steady_clock::now() - t0).count();
+    Json j;
+    j.put_str("what", "gradient of multi_normal_cholesky_lpdf(y|0,cholesky_decompose(add_diag(gp_exp_quad_cov(x,alpha,rho),sigma^2))) wrt (alpha,rho,sigma)");
+    j.put_int("N", N);
+    j.put_vec("theta", th);
+    j.put_vec("x", x);
+    j.put_vec("y", y);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    j.put("ref_seconds", sec);
+    write_fixture("gp_N" + std::to_string(N), j);
+  }
+}
+
+static void fix_mulchol() {
+  for (int N : {8, 40, 128, 2048}) {
+    VectorXd a = mulchol_input(N);
+    double fx;
+    VectorXd g;
+    auto t0 = std::chrono::steady_clock::now();
+    stan::math::gradient(mulchol_functor{N}, a, fx, g);
+    double sec = std::chrono::duration<double>(
+                     std::chrono::steady_clock::now() - t0).count();
+    Json j;
+    j.put_str("what", "gradient of sum(cholesky_decompose(add_diag(multiply(A,A^T),N))) wrt A (col-major); A = unif(seed 20260102)*sqrt(3/N)");
+    j.put_int("N", N);
+    j.put("fx", fx);
+    j.put("grad_sum", g.sum());
+    j.put("grad_l2", g.norm());
+    if (N <= 128) {
+      j.put_vec("grad", g);
+    } else {
+      smg_rng r = smg_rng_make(SEED + 222);
+      std::vector<double> idx, val;
+      for (int s = 0; s < 1024; ++s) {
+        size_t k = smg_rng_next(&r) % ((size_t)N * N);
+        idx.push_back((double)k);
+        val.push_back(g((Eigen::Index)k));
+      }
+      j.put_vec("sample_index", idx);
+      j.put_vec("sample_grad", val);
+    }
+    j.put("ref_seconds", sec);
+    write_fixture("mulchol_N" + std::to_string(N), j);
+  }
+}
+
+// weighted-sum seeds: f = sum_ij W_ij out_ij, W = unif(-1,1)
+static std::vector<double> weights(uint64_t seed, size_t n) {
+  return unif(seed, n, -1.0, 1.0);
+}
+
+static MatrixXd spd(int N, uint64_t seed) {
+  std::vector<double> b = unif(seed, (size_t)N * N, -1.0, 1.0);
+  MatrixXd B = Eigen::Map<MatrixXd>(b.data(), N, N);
+  MatrixXd A = B * B.transpose() / N;
+  A.diagonal().array() += 1.0;
+  A = 0.5 * (A + A.transpose()).eval();
+  return A;
+}
+
+static void fix_cholesky() {
+  for (int N : {1, 5, 35, 36, 100, 200}) {
+    MatrixXd A = spd(N, SEED + 100 + N);
+    std::vector<double> W = weights(SEED + 500 + N, (size_t)N * N);
+    Matrix<var, Dynamic, Dynamic> Av(N, N);
+    for (int i = 0; i < N * N; ++i) Av(i) = A(i);
+    Matrix<var, Dynamic, Dynamic> L = stan::math::cholesky_decompose(Av);
+    var f = 0;
+    for (int jj = 0; jj < N; ++jj)
+      for (int ii = jj; ii < N; ++ii) f += W[(size_t)jj * N + ii] * L(ii, jj);
+    f.grad();
+    MatrixXd Lv(N, N), Ag(N, N);
+    for (int i = 0; i < N * N; ++i) {
+      Lv(i) = L(i).val();
+      Ag(i) = Av(i).adj();
+    }
+    Json j;
+    j.put_str("what", "cholesky_decompose(A) value and gradient of f=sum_{i>=j} W_ij L_ij wrt every A_ij (independent varis; upper triangle gets 0)");
+    j.put_int("N", N);
+    j.put_mat("A", A);
+    j.put_vec("W", W);
+    j.put("fx", f.val());
+    j.put_mat("L", Lv);
+    j.put_mat("grad_A", Ag);
+    write_fixture("cholesky_N" + std::to_string(N), j);
+    stan::math::recover_memory();
+  }
+}
+
+static void fix_multiply() {
+  struct Case {
+    int m, k, n;
+    int kind;  // 0 vv, 1 vd, 2 dv
+  };
+  for (Case c : {Case{5, 7, 4, 0}, Case{5, 7, 4, 1}, Case{5, 7, 4, 2},
+                 Case{64, 48, 33, 0}, Case{1, 9, 1, 0}}) {
+    std::vector<double> a = unif(SEED + 600 + c.m, (size_t)c.m * c.k, -1, 1);
+    std::vector<double> b = unif(SEED + 700 + c.n, (size_t)c.k * c.n, -1, 1);
+    std::vector<double> W = weights(SEED + 800, (size_t)c.m * c.n);
+    MatrixXd Ad = Eigen::Map<MatrixXd>(a.data(), c.m, c.k);
+    MatrixXd Bd = Eigen::Map<MatrixXd>(b.data(), c.k, c.n);
+    Matrix<var, Dynamic, Dynamic> Av = Ad.cast<var>(), Bv = Bd.cast<var>();
+    Matrix<var, Dynamic, Dynamic> C;
+    if (c.kind == 0) C = stan::math::multiply(Av, Bv);
+    if (c.kind == 1) C = stan::math::multiply(Av, Bd);
+    if (c.kind == 2) C = stan::math::multiply(Ad, Bv);
+    var f = 0;
+    for (int i = 0; i < c.m * c.n; ++i) f += W[i] * C(i);
+    f.grad();
+    MatrixXd Cv(c.m, c.n), Ag(c.m, c.k), Bg(c.k, c.n);
+    for (int i = 0; i < c.m * c.n; ++i) Cv(i) = C(i).val();
+    for (int i = 0; i < c.m * c.k; ++i) Ag(i) = Av(i).adj();
+    for (int i = 0; i < c.k * c.n; ++i) Bg(i) = Bv(i).adj();
+    Json j;
+    j.put_str("what", "multiply(A,B) (kind 0 var*var, 1 var*double, 2 double*var) and gradient of sum W.*C");
+    j.put_int("m", c.m);
+    j.put_int("k", c.k);
+    j.put_int("n", c.n);
+    j.put_int("kind", c.kind);
+    j.put_mat("A", Ad);
+    j.put_mat("B", Bd);
+    j.put_vec("W", W);
+    j.put_mat("C", Cv);
+    j.put("fx", f.val());
+    j.put_mat("grad_A", Ag);
+    j.put_mat("grad_B", Bg);
+    write_fixture("multiply_" + std::to_string(c.m) + "x" + std::to_string(c.k) +
+                      "x" + std::to_string(c.n) + "_k" + std::to_string(c.kind),
+                  j);
+    stan::math::recover_memory();
+  }
+}
+
+static void fix_mdivide() {
+  struct Case {
+    int m, n;
+    int lower;  // 1 Lower, 0 Upper
+    int kind;   // 0 vv, 1 dv, 2 vd
+  };
+  for (Case c : {Case{6, 3, 1, 0}, Case{6, 3, 0, 0}, Case{6, 3, 1, 1},
+                 Case{6, 3, 1, 2}, Case{50, 20, 1, 0}, Case{50, 1, 0, 0}}) {
+    MatrixXd S = spd(c.m, SEED + 900 + c.m);
+    MatrixXd T = S.llt().matrixL();
+    if (!c.lower) T = T.transpose().eval();
+    // put junk in the unused triangle: the reference must ignore it
+    std::vector<double> junk = unif(SEED + 901, (size_t)c.m * c.m, -3, 3);
+    for (int jj = 0; jj < c.m; ++jj)
+      for (int ii = 0; ii < c.m; ++ii)
+        if ((c.lower && ii < jj) || (!c.lower && ii > jj))
+          T(ii, jj) = junk[(size_t)jj * c.m + ii];
+    std::vector<double> b = unif(SEED + 902, (size_t)c.m * c.n, -1, 1);
+    MatrixXd Bd = Eigen::Map<MatrixXd>(b.data(), c.m, c.n);
+    std::vector<double> W = weights(SEED + 903, (size_t)c.m * c.n);
+    Matrix<var, Dynamic, Dynamic> Av = T.cast<var>(), Bv = Bd.cast<var>();
+    Matrix<var, Dynamic, Dynamic> C;
+    using stan::math::mdivide_left_tri;
+    if (c.lower) {
+      if (c.kind == 0) C = mdivide_left_tri<Eigen::Lower>(Av, Bv);
+      if (c.kind == 1) C = mdivide_left_tri<Eigen::Lower>(T, Bv);
+      if (c.kind == 2) C = mdivide_left_tri<Eigen::Lower>(Av, Bd);
+    } else {
+      if (c.kind == 0) C = mdivide_left_tri<Eigen::Upper>(Av, Bv);
+      if (c.kind == 1) C = mdivide_left_tri<Eigen::Upper>(T, Bv);
+      if (c.kind == 2) C = mdivide_left_tri<Eigen::Upper>(Av, Bd);
+    }
+    var f = 0;
+    for (int i = 0; i < c.m * c.n; ++i) f += W[i] * C(i);
+    f.grad();
+    MatrixXd Cv(c.m, c.n), Ag(c.m, c.m), Bg(c.m, c.n);
+    for (int i = 0; i < c.m * c.n; ++i) Cv(i) = C(i).val();
+    for (int i = 0; i < c.m * c.m; ++i) Ag(i) = Av(i).adj();
+    for (int i = 0; i < c.m * c.n; ++i) Bg(i) = Bv(i).adj();
+    Json j;
+    j.put_str("what", "mdivide_left_tri<TriView>(A,B) (kind 0 vv, 1 dv, 2 vd) and gradient of sum W.*C; unused triangle of A holds junk");
+    j.put_int("m", c.m);
+    j.put_int("n", c.n);
+    j.put_int("lower", c.lower);
+    j.put_int("kind", c.kind);
+    j.put_mat("A", T);
+    j.put_mat("B", Bd);
+    j.put_vec("W", W);
+    j.put_mat("C", Cv);
+    j.put("fx", f.val());
+    j.put_mat("grad_A", Ag);
+    j.put_mat("grad_B", Bg);
+    write_fixture("mdivide_left_tri_" + std::string(c.lower ? "L" : "U") +
+                      std::to_string(c.m) + "x" + std::to_string(c.n) + "_k" +
+                      std::to_string(c.kind),
+                  j);
+    stan::math::recover_memory();
+  }
+}
+
+static void fix_mvn() {
+  for (int N : {3, 20, 100}) {
+    MatrixXd S = spd(N, SEED + 1000 + N);
+    MatrixXd L = S.llt().matrixL();
+    std::vector<double> yv = unif(SEED + 1001, N, -2, 2);
+    std::vector<double> mv = unif(SEED + 1002, N, -1, 1);
+    VectorXd y = Eigen::Map<VectorXd>(yv.data(), N);
+    VectorXd mu = Eigen::Map<VectorXd>(mv.data(), N);
+    // all of y, mu, L var: full reference partials, upper triangle included
+    Matrix<var, Dynamic, 1> yvv = y.cast<var>(), muv = mu.cast<var>();
+    Matrix<var, Dynamic, Dynamic> Lv = L.cast<var>();
+    var lp = stan::math::multi_normal_cholesky_lpdf(yvv, muv, Lv);
+    lp.grad();
+    MatrixXd gL(N, N);
+    VectorXd gy(N), gm(N);
+    for (int i = 0; i < N * N; ++i) gL(i) = Lv(i).adj();
+    for (int i = 0; i < N; ++i) {
+      gy(i) = yvv(i).adj();
+      gm(i) = muv(i).adj();
+    }
+    Json j;
+    j.put_str("what", "multi_normal_cholesky_lpdf(y|mu,L) with y,mu,L all var; gradient wrt every entry (upper triangle of L included)");
+    j.put_int("N", N);
+    j.put_vec("y", y);
+    j.put_vec("mu", mu);
+    j.put_mat("L", L);
+    j.put("fx", lp.val());
+    j.put_vec("grad_y", gy);
+    j.put_vec("grad_mu", gm);
+    j.put_mat("grad_L", gL);
+    write_fixture("mvn_cholesky_N" + std::to_string(N), j);
+    stan::math::recover_memory();
+  }
+  {  // reference known answer: test/unit/math/rev/mat/prob/multi_normal_cholesky_test.cpp:9-20
+    Json j;
+    j.put_str("what", "known answer from the reference's own test (multi_normal_cholesky_test.cpp:9-20), EXPECT_FLOAT_EQ");
+    j.put_vec("y", std::vector<double>{2.0, -2.0, 11.0});
+    j.put_vec("mu", std::vector<double>{1.0, -1.0, 3.0});
+    j.put_vec("Sigma", std::vector<double>{9.0, -3.0, 0.0, -3.0, 4.0, 0.0, 0.0, 0.0, 5.0});
+    j.put("expected", -11.73908);
+    write_fixture("mvn_cholesky_known", j);
+  }
+}
+
+static void fix_lse() {
+  for (int kind = 0; kind < 3; ++kind) {
+    int N = kind == 2 ? 1000 : 50;
+    std::vector<double> v = unif(SEED + 1100 + kind, N, -5, 5);
+    if (kind == 1)
+      for (auto& e : v) e += 700.0;  // would overflow exp without the shift
+    Matrix<var, Dynamic, 1> xv(N);
+    for (int i = 0; i < N; ++i) xv(i) = v[i];
+    var f = stan::math::log_sum_exp(xv);
+    f.grad();
+    VectorXd g(N);
+    for (int i = 0; i < N; ++i) g(i) = xv(i).adj();
+    Json j;
+    j.put_str("what", "log_sum_exp(Matrix<var,-1,1>) value and gradient");
+    j.put_int("N", N);
+    j.put_vec("x", v);
+    j.put("fx", f.val());
+    j.put_vec("grad", g);
+    write_fixture("log_sum_exp_" + std::to_string(kind), j);
+    stan::math::recover_memory();
+  }
+  {  // scalar pairs
+    std::vector<double> a = {1.0, -3.0, 1000.0, 0.0, -INFINITY};
+    std::vector<double> b = {2.0, -3.0, 999.0, -50.0, 1.0};
+    std::vector<double> f, ga, gb;
+    for (size_t i = 0; i < a.size(); ++i) {
+      var av = a[i], bv = b[i];
+      var r = stan::math::log_sum_exp(av, bv);
+      r.grad();
+      f.push_back(r.val());
+      ga.push_back(av.adj());
+      gb.push_back(bv.adj());
+      stan::math::recover_memory();
+    }
+    Json j;
+    j.put_str("what", "log_sum_exp(var a, var b) values and gradients");
+    j.put_vec("a", a);
+    j.put_vec("b", b);
+    j.put_vec("f", f);
+    j.put_vec("grad_a", ga);
+    j.put_vec("grad_b", gb);
+    write_fixture("log_sum_exp_pair", j);
+  }
+}
+
+static void fix_special() {
+  std::vector<double> xs = {-4.5, -3.7, -2.5, -1.5, -1.25, -0.5, -1e-5, 1e-8,
+                            1e-4, 1e-3, 0.1, 0.25, 0.5, 0.9, 1.0, 1.4616321449683623,
+                            1.5, 2.0, 2.5, 3.0, 4.99, 5.0, 7.5, 9.99, 10.0, 10.01,
+                            20.0, 55.5, 100.0, 1e3, 1e5, 1e10, 1e15};
+  std::vector<double> more = unif(SEED + 1200, 64, 0.01, 30.0);
+  std::vector<double> neg = unif(SEED + 1201, 16, -20.0, -0.01);
+  xs.insert(xs.end(), more.begin(), more.end());
+  xs.insert(xs.end(), neg.begin(), neg.end());
+  std::vector<double> lg, dg, tg, dlg, ddg;
+  for (double x : xs) {
+    lg.push_back(stan::math::lgamma(x));
+    dg.push_back(stan::math::digamma(x));
+    tg.push_back(stan::math::trigamma(x));
+    var xv = x;
+    var y = stan::math::lgamma(xv);
+    y.grad();
+    dlg.push_back(xv.adj());
+    stan::math::recover_memory();
+    var xv2 = x;
+    var y2 = stan::math::digamma(xv2);
+    y2.grad();
+    ddg.push_back(xv2.adj());
+    stan::math::recover_memory();
+  }
+  Json j;
+  j.put_str("what", "lgamma (glibc lgamma_r), digamma (boost, boost_policy_t), trigamma (stan AS121-style) values; d/dx lgamma(var) and d/dx digamma(var)");
+  j.put_vec("x", xs);
+  j.put_vec("lgamma", lg);
+  j.put_vec("digamma", dg);
+  j.put_vec("trigamma", tg);
+  j.put_vec("grad_lgamma", dlg);
+  j.put_vec("grad_digamma", ddg);
+  write_fixture("special", j);
+  // vectorised form on a matrix of vars
+  {
+    int N = 200;
+    std::vector<double> v = unif(SEED + 1202, N, 0.05, 50.0);
+    std::vector<double> W = weights(SEED + 1203, N);
+    Matrix<var, Dynamic, Dynamic> X(10, 20);
+    for (int i = 0; i < N; ++i) X(i) = v[i];
+    Matrix<var, Dynamic, Dynamic> Y = stan::math::lgamma(X);
+    Matrix<var, Dynamic, Dynamic> Z = stan::math::digamma(X);
+    var f = 0;
+    for (int i = 0; i < N; ++i) f += W[i] * (Y(i) + 0.5 * Z(i));
+    f.grad();
+    std::vector<double> g(N);
+    for (int i = 0; i < N; ++i) g[i] = X(i).adj();
+    Json k;
+    k.put_str("what", "vectorised lgamma/digamma on Matrix<var> 10x20; f = sum W.*(lgamma(X) + 0.5 digamma(X))");
+    k.put_vec("x", v);
+    k.put_vec("W", W);
+    k.put("fx", f.val());
+    k.put_vec("grad", g);
+    write_fixture("special_vectorised", k);
+    stan::math::recover_memory();
+  }
+}
+
+static void fix_normal() {
+  {
+    int N = 1024;
+    std::vector<double> th = normals(SEED + 1, N);
+    VectorXd x = Eigen::Map<VectorXd>(th.data(), N);
+    double fx;
+    VectorXd g;
+    stan::math::gradient(normal_functor{}, x, fx, g);
+    Json j;
+    j.put_str("what", "gradient of normal_lpdf(theta|0,1), N=1024 (config 1)");
+    j.put_int("N", N);
+    j.put_vec("theta", x);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    write_fixture("normal_N1024", j);
+  }
+  {  // vector y, mu, sigma all var
+    int N = 9;
+    std::vector<double> y = unif(SEED + 1301, N, -3, 3),
+                        mu = unif(SEED + 1302, N, -1, 1),
+                        sg = unif(SEED + 1303, N, 0.2, 3);
+    Matrix<var, Dynamic, 1> yv(N), mv(N), sv(N);
+    for (int i = 0; i < N; ++i) {
+      yv(i) = y[i];
+      mv(i) = mu[i];
+      sv(i) = sg[i];
+    }
+    var f = stan::math::normal_lpdf(yv, mv, sv);
+    var fp = stan::math::normal_lpdf<true>(yv, mv, sv);
+    f.grad();
+    std::vector<double> gy(N), gm(N), gs(N);
+    for (int i = 0; i < N; ++i) {
+      gy[i] = yv(i).adj();
+      gm[i] = mv(i).adj();
+      gs[i] = sv(i).adj();
+    }
+    Json j;
+    j.put_str("what", "normal_lpdf(y|mu,sigma) all vector var; propto=false value+grad, propto=true value");
+    j.put_vec("y", y);
+    j.put_vec("mu", mu);
+    j.put_vec("sigma", sg);
+    j.put("fx", f.val());
+    j.put("fx_propto", fp.val());
+    j.put_vec("grad_y", gy);
+    j.put_vec("grad_mu", gm);
+    j.put_vec("grad_sigma", gs);
+    write_fixture("normal_vec9", j);
+    stan::math::recover_memory();
+  }
+  {  // the reference's own golden values (test/prob/normal/normal_test.hpp:9-32)
+    Json j;
+    j.put_str("what", "known answers from test/prob/normal/normal_test.hpp:9-32 (checked to 1e-8 by test_fixture_distr.hpp:120)");
+    j.put_vec("y", std::vector<double>{0, 1, -2, -3.5});
+    j.put_vec("mu", std::vector<double>{0, 0, 0, 1.9});
+    j.put_vec("sigma", std::vector<double>{1, 1, 1, 7.2});
+    j.put_vec("expected", std::vector<double>{-0.918938533204672669541, -1.418938533204672669541,
+                                              -2.918938533204672669541, -3.174269559226682080322});
+    write_fixture("normal_known", j);
+  }
+}
+
+static void fix_glm() {
+  struct Case {
+    int R, M;
+  };
+  for (Case c : {Case{1000, 8}, Case{10000, 256}, Case{100000, 256}}) {
+    glm_data d = glm_inputs(c.R, c.M);
+    double fx;
+    VectorXd g;
+    stan::math::gradient(glm_functor{d}, d.theta, fx, g);
+    Json j;
+    j.put_str("what", "gradient of bernoulli_logit_glm_lpmf(y|x,alpha,beta) wrt (alpha,beta); inputs regenerated from oracle/gen.h seeds 20260142/43/44");
+    j.put_int("R", c.R);
+    j.put_int("M", c.M);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    if (c.R == 100000) {
+      std::vector<std::vector<double>> xr;
+      std::vector<std::vector<int>> xi;
+      shard_glm(d, 32, xr, xi);
+      double fx2;
+      VectorXd g2;
+      stan::math::gradient(glm_maprect_functor{xr, xi}, d.theta, fx2, g2);
+      j.put("fx_map_rect32", fx2);
+      j.put_vec("grad_map_rect32", g2);
+    }
+    write_fixture("glm_R" + std::to_string(c.R) + "_M" + std::to_string(c.M), j);
+  }
+  {  // extreme linear predictors exercise the +-20 cutoff branches
+    int R = 64, M = 2;
+    MatrixXd x(R, M);
+    std::vector<int> y(R);
+    std::vector<double> xv = unif(SEED + 1401, (size_t)R * M, -30, 30);
+    for (int i = 0; i < R * M; ++i) x.data()[i] = xv[i];
+    smg_fill_bernoulli(SEED + 1402, R, 0.5, y.data());
+    glm_data d;
+    d.R = R;
+    d.M = M;
+    d.x = x;
+    d.y = y;
+    d.theta.resize(M + 1);
+    d.theta << 0.5, 1.3, -0.9;
+    double fx;
+    VectorXd g;
+    stan::math::gradient(glm_functor{d}, d.theta, fx, g);
+    Json j;
+    j.put_str("what", "bernoulli_logit_glm_lpmf with |eta| > 20 rows (cutoff branches)");
+    j.put_int("R", R);
+    j.put_int("M", M);
+    j.put_mat("x", x);
+    j.put_ivec("y", y);
+    j.put_vec("theta", d.theta);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    write_fixture("glm_extreme", j);
+  }
+}
+
+static void fix_hvp() {
+  for (int N : {8, 32}) {
+    std::vector<double> x;
+    VectorXd y;
+    gp_inputs(N, x, y);
+    VectorXd th(3), v(3);
+    th << 1.0, 1.5, 0.3;
+    v << 1.0, -0.5, 0.25;
+    double fx;
+    VectorXd Hv;
+    stan::math::hessian_times_vector(gp_functor{x, y}, th, v, fx, Hv);
+    Json j;
+    j.put_str("what", "hessian_times_vector (fwd-over-rev) of the GP marginal log density");
+    j.put_int("N", N);
+    j.put_vec("theta", th);
+    j.put_vec("v", v);
+    j.put_vec("x", x);
+    j.put_vec("y", y);
+    j.put("fx", fx);
+    j.put_vec("Hv", Hv);
+    write_fixture("hvp_gp_N" + std::to_string(N), j);
+  }
+}
+
+// ------------------------------------------------------------------ bench
+static double now() {
+  return std::chrono::duration<double>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static int bench(const std::string& cfg, int N, int reps) {
+  double t0 = 0, t1 = 0, fx = 0;
+  VectorXd g;
+  if (cfg == "gp") {
+    std::vector<double> x;
+    VectorXd y;
+    gp_inputs(N, x, y);
+    VectorXd th(3);
+    th << 1.0, 1.5, 0.3;
+    t0 = now();
+    for (int r = 0; r < reps; ++r)
+      stan::math::gradient(gp_functor{x, y}, th, fx, g);
+    t1 = now();
+  } else if (cfg == "mulchol") {
+    VectorXd a = mulchol_input(N);
+    t0 = now();
+    for (int r = 0; r < reps; ++r)
+      stan::math::gradient(mulchol_functor{N}, a, fx, g);
+    t1 = now();
+  } else if (cfg == "glm") {
+    glm_data d = glm_inputs(N, 256);
+    t0 = now();
+    for (int r = 0; r < reps; ++r)
+      stan::math::gradient(glm_functor{d}, d.theta, fx, g);
+    t1 = now();
+  } else if (cfg == "normal") {
+    std::vector<double> th = normals(SEED + 1, N);
+    VectorXd x = Eigen::Map<VectorXd>(th.data(), N);
+    t0 = now();
+    for (int r = 0; r < reps; ++r)
+      stan::math::gradient(normal_functor{}, x, fx, g);
+    t1 = now();
+  } else {
+    std::fprintf(stderr, "unknown bench config %s\n", cfg.c_str());
+    return 2;
+  }
+  double per = (t1 - t0) / reps;
+  std::printf("{\"config\": \"%s\", \"N\": %d, \"reps\": %d, \"seconds_per_eval\": %.9g, "
+              "\"evals_per_sec\": %.9g, \"fx\": %.17g, \"threads\": 1}\n",
+              cfg.c_str(), N, reps, per, 1.0 / per, fx);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc >= 2 && std::string(argv[1]) == "gen") {
+    if (argc >= 3) g_outdir = argv[2];
+    std::string only = argc >= 4 ? argv[3] : "";
+    auto want = [&](const char* s) { return only.empty() || only == s; };
+    if (want("normal")) fix_normal();
+    if (want("special")) fix_special();
+    if (want("lse")) fix_lse();
+    if (want("multiply")) fix_multiply();
+    if (want("mdivide")) fix_mdivide();
+    if (want("cholesky")) fix_cholesky();
+    if (want("mvn")) fix_mvn();
+    if (want("glm")) fix_glm();
+    if (want("hvp")) fix_hvp();
+    if (want("mulchol")) fix_mulchol();
+    if (want("gp")) fix_gp();
+    return 0;
+  }
+  if (argc >= 5 && std::string(argv[1]) == "bench")
+    return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
+  std::fprintf(stderr,
+               "usage: %s gen [outdir] [only]\n       %s bench gp|mulchol|glm|normal N reps\n",
+               argv[0], argv[0]);
+  return 2;
+}

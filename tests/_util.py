@@ -1,0 +1,112 @@
+"""Shared test helpers: golden fixtures, tolerance checks, oracle bindings.
+
+The oracle (oracle/_build/libsmg_oracle.so) is the CPU restatement of the
+reference: it is imported ONLY here, in tests, as the checker.
+"""
+import ctypes
+import json
+import math
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def golden(name: str) -> dict:
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        d = json.load(f)
+
+    def conv(v):
+        if isinstance(v, list):
+            return np.array([conv(e) for e in v], dtype=np.float64) if v and not isinstance(v[0], list) else v
+        if v == "nan":
+            return math.nan
+        if v == "inf":
+            return math.inf
+        if v == "-inf":
+            return -math.inf
+        return v
+
+    return {k: conv(v) for k, v in d.items()}
+
+
+def near_rel(actual, expected, rtol, atol=None, what=""):
+    """expect_near_rel semantics (test/unit/math/expect_near_rel.hpp:33-52):
+    relative error 2|a-b|/(|a|+|b|) <= rtol, absolute |a-b| <= atol where
+    either side is below atol (atol defaults to rtol).  NaN/inf must match."""
+    a = np.asarray(actual, dtype=np.float64).ravel()
+    b = np.asarray(expected, dtype=np.float64).ravel()
+    assert a.shape == b.shape, f"{what}: shape {a.shape} vs {b.shape}"
+    atol = rtol if atol is None else atol
+    fin = np.isfinite(a) & np.isfinite(b)
+    same_nonfinite = (np.isnan(a) & np.isnan(b)) | (a == b)
+    assert np.all(fin | same_nonfinite), f"{what}: non-finite mismatch at {np.where(~(fin | same_nonfinite))[0][:5]}"
+    a, b = a[fin], b[fin]
+    small = (np.abs(a) < atol) | (np.abs(b) < atol)
+    absdiff = np.abs(a - b)
+    rel = absdiff / np.maximum(0.5 * (np.abs(a) + np.abs(b)), 1e-300)
+    bad = np.where(small, absdiff > atol, rel > rtol)
+    if np.any(bad):
+        i = np.where(bad)[0][0]
+        raise AssertionError(
+            f"{what}: {bad.sum()} / {bad.size} entries off; first at {i}: "
+            f"{a[i]!r} vs {b[i]!r} (rel {rel[i]:.3e}, abs {absdiff[i]:.3e}, rtol {rtol}, atol {atol})")
+    return float(rel[~small].max()) if np.any(~small) else 0.0
+
+
+# --------------------------------------------------------------- oracle
+_ORACLE = None
+_D = ctypes.POINTER(ctypes.c_double)
+_I = ctypes.POINTER(ctypes.c_int)
+
+
+def ptr(a):
+    if a is None:
+        return None
+    if a.dtype == np.int32:
+        return a.ctypes.data_as(_I)
+    return a.ctypes.data_as(_D)
+
+
+def oracle():
+    global _ORACLE
+    if _ORACLE is None:
+        path = os.path.join(ROOT, "oracle", "_build", "libsmg_oracle.so")
+        if not os.path.exists(path):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "cpu"])
+        lib = ctypes.CDLL(path)
+        dd = ctypes.c_double
+        ii = ctypes.c_int
+        sig = {
+            "oracle_gp_cov": (None, [_D, ii, dd, dd, _D]),
+            "oracle_gp_cov_rev": (None, [_D, ii, dd, dd, _D, _D, _D]),
+            "oracle_cholesky": (ii, [_D, ii, _D]),
+            "oracle_cholesky_rev": (None, [_D, _D, ii, _D]),
+            "oracle_mvn_cholesky": (None, [_D, _D, _D, ii, _D, _D, _D, _D]),
+            "oracle_multiply": (None, [_D, _D, ii, ii, ii, _D]),
+            "oracle_multiply_rev": (None, [_D, _D, _D, ii, ii, ii, _D, _D]),
+            "oracle_mdivide_left_tri": (None, [ii, _D, _D, ii, ii, _D]),
+            "oracle_mdivide_left_tri_rev": (None, [ii, _D, _D, _D, ii, ii, _D, _D]),
+            "oracle_log_sum_exp": (dd, [_D, ii]),
+            "oracle_log_sum_exp_rev": (None, [_D, ii, dd, dd, _D]),
+            "oracle_lgamma": (dd, [dd]),
+            "oracle_digamma": (dd, [dd]),
+            "oracle_trigamma": (dd, [dd]),
+            "oracle_normal_lpdf": (dd, [_D, ii, _D, ii, _D, ii, ii, _D, _D, _D]),
+            "oracle_glm": (dd, [_I, _D, ctypes.c_longlong, ii, dd, _D, _D, _D]),
+            "oracle_gp_marginal": (None, [_D, _D, ii, _D, _D, _D]),
+            "oracle_mulchol": (None, [_D, ii, _D, _D]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _ORACLE = lib
+    return _ORACLE
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)

@@ -1,0 +1,46 @@
+"""Python mirror of oracle/gen.h (SplitMix64 + 53-bit uniforms), bit-exact.
+
+Test infrastructure: regenerates the synthetic inputs the reference harness
+(oracle/ref_harness.cpp) used for the fixtures whose inputs are not stored.
+"""
+import numpy as np
+
+SEED = 20260101
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def _splitmix(seed: int, n: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        idx = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) + idx * _GOLDEN
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def u01(seed: int, n: int) -> np.ndarray:
+    return (_splitmix(seed, n) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def unif(seed: int, n: int, a: float, b: float) -> np.ndarray:
+    return a + (b - a) * u01(seed, n)
+
+
+def bernoulli(seed: int, n: int, p: float) -> np.ndarray:
+    return (u01(seed, n) < p).astype(np.int32)
+
+
+def mulchol_input(n: int) -> np.ndarray:
+    """config 2 input A (n x n, column-major flat), ref_harness.cpp mulchol_input."""
+    return unif(SEED + 2, n * n, -1.0, 1.0) * np.sqrt(3.0 / n)
+
+
+def glm_inputs(R: int, M: int):
+    """config 4 inputs, ref_harness.cpp glm_inputs: x (R x M col-major), y, theta."""
+    x = unif(SEED + 41, R * M, -1.0, 1.0) * np.sqrt(3.0)
+    y = bernoulli(SEED + 42, R, 0.5)
+    b = unif(SEED + 43, M, -1.0, 1.0) * np.sqrt(3.0 / M)
+    theta = np.concatenate([[0.1], b])
+    return x.reshape(M, R).T.copy(order="F"), y, theta
