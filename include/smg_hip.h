@@ -1,0 +1,236 @@
+/*
+ * smg_hip.h — the C-ABI of libsmg_hip.so, the MI355X (gfx950) device side of
+ * the Stan-Math-compatible reverse-mode hot path.
+ *
+ * The reference (Stan Math 3.0.0) is header-only C++ with no FFI; its device
+ * offload boundary is the set of `#ifdef STAN_OPENCL` hooks inside the rev
+ * functors' constructors (forward) and chain() (reverse).  Each entry point
+ * below replaces one such forward or chain() body and is called only by the
+ * header-only host layer in math_amd/include/stan/math/ (vari subclasses) or,
+ * in tests, through ctypes.  The replaced reference code is cited per entry.
+ *
+ * Conventions
+ *  - every matrix is column-major fp64 with an explicit leading dimension;
+ *  - every pointer argument is a DEVICE pointer unless named *_host;
+ *  - work is enqueued on the context's HIP stream and is asynchronous; the
+ *    only synchronising calls are smg_sync / smg_status / smg_memcpy_d2h_sync;
+ *  - adjoint outputs ACCUMULATE (+=), like vari::adj_ in the reference
+ *    (rev/core/vari.hpp:30-143): callers zero them once per sweep;
+ *  - nothing throws across this boundary: every function returns SMG_OK or an
+ *    error code; device-detected domain errors (not positive definite,
+ *    not symmetric, non-finite) are latched in the context status word and
+ *    read with smg_status(), which the C++ layer turns into the reference's
+ *    std::domain_error (prim/scal/err/domain_error.hpp:28-33).
+ */
+#ifndef SMG_HIP_H
+#define SMG_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum smg_status_code {
+  SMG_OK = 0,
+  SMG_ERR_HIP = 1,            /* a HIP runtime call failed */
+  SMG_ERR_NOT_PD = 2,         /* check_pos_definite (prim/mat/err/check_pos_definite.hpp:77-81) */
+  SMG_ERR_NOT_SYMMETRIC = 4,  /* check_symmetric, abs tol 1e-8 (prim/mat/err/check_symmetric.hpp:43-44) */
+  SMG_ERR_NONFINITE = 8,      /* check_finite / not_nan family */
+  SMG_ERR_ARG = 16,           /* bad sizes / null pointers (host-side check) */
+  SMG_ERR_OOM = 32,           /* device arena exhausted */
+  SMG_ERR_NOT_POSITIVE = 64   /* check_positive */
+};
+
+typedef struct smg_ctx smg_ctx;
+
+/* ------------------------------------------------------------ context ---
+ * One context per host thread = one HIP stream + one device bump arena.
+ * Mirrors the per-thread AutodiffStackSingleton tape
+ * (rev/core/autodiffstackstorage.hpp:88-143) and its stack_alloc arena
+ * (memory/stack_alloc.hpp:72-287): blocks double in size, nested marks,
+ * bulk release only. */
+int smg_device_count(int* n_host);
+int smg_ctx_create(int device, size_t initial_arena_bytes, smg_ctx** out_host);
+int smg_ctx_destroy(smg_ctx* ctx);
+int smg_ctx_device(const smg_ctx* ctx);
+void* smg_ctx_stream(smg_ctx* ctx); /* hipStream_t */
+
+/* stack_alloc::alloc (:169-178); 256-byte aligned; NULL + SMG_ERR_OOM latched on failure */
+void* smg_arena_alloc(smg_ctx* ctx, size_t bytes);
+/* stack_alloc::start_nested / recover_nested (:209-231) as explicit marks */
+size_t smg_arena_mark(smg_ctx* ctx);
+int smg_arena_rewind(smg_ctx* ctx, size_t mark);
+/* stack_alloc::recover_all (:199) and bytes_allocated (:251) */
+int smg_arena_recover_all(smg_ctx* ctx);
+size_t smg_arena_used(const smg_ctx* ctx);
+size_t smg_arena_reserved(const smg_ctx* ctx);
+/* pinned host staging buffer (lifetime of the context) */
+void* smg_host_scratch(smg_ctx* ctx, size_t bytes);
+
+int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src_host, size_t bytes);
+int smg_memcpy_d2h(smg_ctx* ctx, void* dst_host, const void* src, size_t bytes);
+int smg_memcpy_d2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes);
+int smg_memset(smg_ctx* ctx, void* dst, int value, size_t bytes);
+int smg_sync(smg_ctx* ctx);
+/* synchronise, return the latched status bits (0 = ok) and clear them */
+int smg_status(smg_ctx* ctx, int* status_host);
+
+/* ------------------------------------------------------- instrumentation ---
+ * HIP-event timing of the kernel families on the context stream (used by
+ * bench.py to report the dominant kernel's average launch duration). */
+enum smg_family {
+  SMG_FAM_GEMM = 0, SMG_FAM_CHOL_FWD = 1, SMG_FAM_CHOL_REV = 2,
+  SMG_FAM_GP = 3, SMG_FAM_MVN = 4, SMG_FAM_TRSV = 5, SMG_FAM_GLM = 6,
+  SMG_FAM_ELEMWISE = 7, SMG_FAM_COUNT = 8
+};
+int smg_profile_enable(smg_ctx* ctx, int on);
+/* total milliseconds and number of timed regions per family since enable */
+int smg_profile_read(smg_ctx* ctx, int family, double* total_ms_host, long long* count_host);
+
+/* --------------------------------------------------------------- BLAS-3 ---
+ * C = alpha op(A) op(B) + beta C  (op = transpose when trans != 0), fp64 MFMA
+ * (v_mfma_f64_16x16x4_f64).  uplo: 0 = full C, 1 = only the lower triangle of
+ * C (i >= j) is computed and written (SYRK-style).  Replaces the Eigen GEMMs
+ * in multiply_mat_vari (rev/mat/fun/multiply.hpp:65-135) and
+ * cholesky_block::chain (rev/mat/fun/cholesky_decompose.hpp:135-158). */
+int smg_gemm(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n, int k,
+             double alpha, const double* A, int lda, const double* B, int ldb,
+             double beta, double* C, int ldc);
+
+/* ---------------------------------------------------------- functors ---- */
+
+/* gp_exp_quad_cov(std::vector<double> x, var sigma, var l)
+ *   fwd: rev/mat/fun/gp_exp_quad_cov.hpp:64-94   K (n x n full, symmetric)
+ *   rev: :96-112  out[0] += d/dsigma, out[1] += d/dl given the full adjoint
+ *        Kadj (entries (i,j),(j,i) alias one vari in the reference, :233-238). */
+int smg_gp_exp_quad_cov_fwd(smg_ctx* ctx, const double* x, int n, double sigma,
+                            double l, double* K, int ldk);
+int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma,
+                            double l, const double* Kadj, int ldka, double* out2);
+
+/* add_diag(A, d) (prim/mat/fun/add_diag.hpp:20-55): B = A + diag(d) where d is
+ * the host scalar d_scalar (d_vec == NULL) or the device vector d_vec.
+ * rev: Aadj += Badj (NULL skips); dadj (device) += diag(Badj), summed into
+ * dadj[0] when d_is_vec == 0 (NULL skips). */
+int smg_add_diag_fwd(smg_ctx* ctx, const double* A, int lda, int n,
+                     double d_scalar, const double* d_vec, double* B, int ldb);
+int smg_add_diag_rev(smg_ctx* ctx, const double* Badj, int ldb, int n,
+                     double* Aadj, int ldaa, double* dadj, int d_is_vec);
+
+/* cholesky_decompose(Matrix<var>) (rev/mat/fun/cholesky_decompose.hpp:378-427)
+ *   check: latches SMG_ERR_NOT_SYMMETRIC when |A_ij - A_ji| > 1e-8 (:383)
+ *   fwd:   L = lower Cholesky factor (upper zeroed); latches SMG_ERR_NOT_PD.
+ *          Dinv (n x nb per diagonal block, may be NULL) receives the inverse
+ *          diagonal blocks for reuse by the reverse pass and by TRSV.
+ *   rev:   Murray's blocked adjoint (:118-165): Aadj(lower) += f(L, Ladj);
+ *          Ladj (lower) is used as workspace and overwritten. */
+int smg_cholesky_block_size(int n);
+int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n);
+int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L,
+                     int ldl, double* Dinv);
+int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
+                     double* Ladj, int ldla, int n, double* Aadj, int ldaa);
+
+/* mdivide_left_tri<TriView>(A, B) (rev/mat/fun/mdivide_left_tri.hpp:16-373)
+ *   fwd: C = tri(A)^{-1} B              (lower != 0: Eigen::Lower, else Upper)
+ *   rev: Badj += tri(A)^{-T} Cadj ; Aadj(tri) -= (tri(A)^{-T} Cadj) C^T
+ * Aadj / Badj may be NULL (double operands).  ws: >= m*n doubles workspace. */
+int smg_mdivide_left_tri_fwd(smg_ctx* ctx, int lower, const double* A, int lda,
+                             const double* B, int ldb, int m, int n, double* C,
+                             int ldc);
+int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda,
+                             const double* C, int ldc, const double* Cadj,
+                             int ldca, int m, int n, double* Aadj, int ldaa,
+                             double* Badj, int ldba, double* ws);
+
+/* multiply(A, B) (rev/mat/fun/multiply.hpp:65-135): fwd C = A B;
+ * rev Aadj += Cadj B^T, Badj += A^T Cadj (NULL skips an operand). */
+int smg_multiply_fwd(smg_ctx* ctx, const double* A, int lda, const double* B,
+                     int ldb, int m, int k, int n, double* C, int ldc);
+int smg_multiply_rev(smg_ctx* ctx, const double* A, int lda, const double* B,
+                     int ldb, const double* Cadj, int ldca, int m, int k, int n,
+                     double* Aadj, int ldaa, double* Badj, int ldba);
+
+/* multi_normal_cholesky_lpdf<false>(y | mu, L)
+ * (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:40-160).
+ *   fwd: out3 = [lp, -, -]; w = L^{-1}(y - mu), sd = L^{-T} w kept in ws
+ *        (ws >= 2n doubles); Dinv optional (from smg_cholesky_fwd).
+ *   rev: with adj = d(root)/d(lp) (host scalar):
+ *        yadj -= adj sd, muadj += adj sd  (NULL skips)
+ *        lower_only != 0: Ladj(lower) += adj (tril(sd w^T) - diag(1/L_ii))
+ *          (exact when L's upper triangle is structurally zero, as the output
+ *           of cholesky_decompose is: those entries alias a dummy vari, :34-48)
+ *        lower_only == 0: Ladj += adj (sd w^T - L^{-T}) over all n^2 entries,
+ *          the reference's full partials (:147,155). */
+int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu,
+                         const double* L, int ldl, const double* Dinv, int n,
+                         double* ws, double* out_lp);
+int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
+                         const double* Dinv, int n, const double* ws, double adj,
+                         int lower_only, double* yadj, double* muadj,
+                         double* Ladj, int ldla);
+
+/* log_sum_exp(vector<var>) (rev/mat/fun/log_sum_exp.hpp:20-53):
+ *   fwd: out = max + log(sum exp(x - max)); empty -> -inf; non-finite max -> max
+ *   rev: xadj_i += adj * exp(x_i - lse)   (lse, adj: host values of the vari) */
+int smg_log_sum_exp_fwd(smg_ctx* ctx, const double* x, long long n, double* out);
+int smg_log_sum_exp_rev(smg_ctx* ctx, const double* x, long long n,
+                        double lse, double adj, double* xadj);
+
+/* vectorised lgamma / digamma / trigamma (apply_scalar_unary,
+ * rev/mat/vectorize/apply_scalar_unary.hpp:18-32):
+ *   lgamma rev: xadj += yadj * digamma(x)   (rev/scal/fun/lgamma.hpp:13-32)
+ *   digamma rev: xadj += yadj * trigamma(x) (rev/scal/fun/digamma.hpp:13-22) */
+int smg_lgamma_fwd(smg_ctx* ctx, const double* x, long long n, double* y);
+int smg_lgamma_rev(smg_ctx* ctx, const double* x, long long n, const double* yadj, double* xadj);
+int smg_digamma_fwd(smg_ctx* ctx, const double* x, long long n, double* y);
+int smg_digamma_rev(smg_ctx* ctx, const double* x, long long n, const double* yadj, double* xadj);
+int smg_trigamma_fwd(smg_ctx* ctx, const double* x, long long n, double* y);
+
+/* normal_lpdf<propto>(y | mu, sigma) (prim/scal/prob/normal_lpdf.hpp:36-119):
+ * each operand is a device vector (stride 1) or scalar (stride 0) of n
+ * broadcast elements.  include bits: 1 = NEG_LOG_SQRT_TWO_PI term,
+ * 2 = -log(sigma) term, 4 = -z^2/2 term (include_summand<propto, ...>).
+ * Writes out[0] = logp and per-element partials (NULL skips; scalar operands
+ * get their partial summed into element 0). */
+int smg_normal_lpdf(smg_ctx* ctx, const double* y, int sy, const double* mu,
+                    int smu, const double* sigma, int ssig, long long n,
+                    int include, double* out, double* gy, double* gmu,
+                    double* gsigma);
+
+/* bernoulli_logit_glm_lpmf<false>(y | x, alpha, beta), scalar alpha
+ * (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138) in ONE fused pass over
+ * x (R x M column-major, leading dimension ldx):
+ *   out[0] = logp, out[1] = sum theta', out[2..M+1] = x^T theta'.
+ * Deterministic (fixed-order two-stage reduction).  ws: >= smg_glm_ws_doubles. */
+long long smg_glm_ws_doubles(long long R, int M);
+int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x,
+                            long long R, int M, long long ldx,
+                            const double* alpha_beta, double* ws, double* out);
+
+/* generic helpers used by the host layer's reverse sweep */
+/* y[i*incy] += alpha * x[i*incx] with alpha read from host */
+int smg_axpy(smg_ctx* ctx, long long n, double alpha, const double* x, int incx,
+             double* y, int incy);
+/* y[i] += (*alpha_d) * x[i], alpha read from device */
+int smg_axpy_dev(smg_ctx* ctx, long long n, const double* alpha_d, const double* x, double* y);
+/* out += sum(x) (deterministic) */
+int smg_sum(smg_ctx* ctx, const double* x, long long n, double* out);
+/* B(i,j) = A(j,i) style copy helpers */
+int smg_copy_matrix(smg_ctx* ctx, int m, int n, const double* A, int lda,
+                    double* B, int ldb, int trans, int uplo_zero_upper);
+
+/* ------------------------------------------------------ multi-GPU ------
+ * One RCCL communicator per process/device; a single fp64 sum all-reduce of
+ * [logp, alpha_adj, beta_adj...] per gradient (replaces the Boost.MPI
+ * gather/reduce of map_rect, prim/mat/functor/mpi_parallel_call.hpp:332-392). */
+int smg_comm_unique_id(char* id_host /* 128 bytes */);
+int smg_comm_init(smg_ctx* ctx, int nranks, int rank, const char* id_host);
+int smg_comm_allreduce_sum(smg_ctx* ctx, double* buf, long long count);
+int smg_comm_destroy(smg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

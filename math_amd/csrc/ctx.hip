@@ -1,0 +1,307 @@
+// Context, device arena, transfers, status latch, profiling, reductions.
+// The arena mirrors stack_alloc (memory/stack_alloc.hpp:72-287): a list of
+// device blocks, each twice the previous, bump allocation, marks = positions.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "smg_internal.h"
+
+namespace {
+
+constexpr size_t kAlign = 256;
+
+__global__ void k_reduce_partials(const double* __restrict__ p, int nparts,
+                                  int width, double* out, int accumulate) {
+  // one block per output column; fixed-order tree => deterministic
+  __shared__ double lds[16];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += p[(size_t)i * width + c];
+  s = block_sum(s, lds);
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + s : s;
+}
+
+}  // namespace
+
+smg_prof_scope::smg_prof_scope(smg_ctx* c, int f) : ctx(c), fam(f), on(c && c->prof_on) {
+  if (!on) return;
+  if (ctx->prof_pool.size() < 2) {
+    for (int i = 0; i < 64; ++i) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) == hipSuccess) ctx->prof_pool.push_back(e);
+    }
+  }
+  a = ctx->prof_pool.back();
+  ctx->prof_pool.pop_back();
+  b = ctx->prof_pool.back();
+  ctx->prof_pool.pop_back();
+  hipEventRecord(a, ctx->stream);
+}
+
+smg_prof_scope::~smg_prof_scope() {
+  if (!on) return;
+  hipEventRecord(b, ctx->stream);
+  ctx->prof_pending.push_back({a, b, fam});
+}
+
+static void prof_drain(smg_ctx* ctx) {
+  for (auto& s : ctx->prof_pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(s.stop) == hipSuccess &&
+        hipEventElapsedTime(&ms, s.start, s.stop) == hipSuccess) {
+      ctx->prof_ms[s.family] += ms;
+      ctx->prof_count[s.family] += 1;
+    }
+    ctx->prof_pool.push_back(s.start);
+    ctx->prof_pool.push_back(s.stop);
+  }
+  ctx->prof_pending.clear();
+}
+
+double* smg_ws(smg_ctx* ctx, int id, size_t doubles) {
+  if (doubles > ctx->ws_doubles[id]) {
+    if (ctx->ws[id]) {
+      hipStreamSynchronize(ctx->stream);
+      hipFree(ctx->ws[id]);
+    }
+    size_t n = doubles < (1u << 18) ? (1u << 18) : doubles + doubles / 4;
+    if (hipMalloc(&ctx->ws[id], n * sizeof(double)) != hipSuccess) {
+      hipGetLastError();
+      ctx->ws[id] = nullptr;
+      ctx->ws_doubles[id] = 0;
+      ctx->host_status |= SMG_ERR_OOM;
+      return nullptr;
+    }
+    ctx->ws_doubles[id] = n;
+  }
+  return ctx->ws[id];
+}
+
+void smg_reduce_partials(smg_ctx* ctx, const double* partials, int nparts,
+                         int width, double* out, int accumulate) {
+  hipLaunchKernelGGL(k_reduce_partials, dim3(width), dim3(256), 0, ctx->stream,
+                     partials, nparts, width, out, accumulate);
+}
+
+extern "C" {
+
+int smg_device_count(int* n) {
+  smg_ctx* ctx = nullptr;
+  SMG_HIP_TRY(hipGetDeviceCount(n));
+  return SMG_OK;
+}
+
+int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
+  if (!out) return SMG_ERR_ARG;
+  *out = nullptr;
+  smg_ctx* ctx = nullptr;
+  SMG_HIP_TRY(hipSetDevice(device));
+  ctx = new smg_ctx();
+  ctx->device = device;
+  ctx->cur_block = 0;
+  ctx->offset = 0;
+  ctx->host_status = 0;
+  for (int i = 0; i < 4; ++i) {
+    ctx->ws[i] = nullptr;
+    ctx->ws_doubles[i] = 0;
+  }
+  ctx->prof_on = 0;
+  ctx->comm = nullptr;
+  for (int i = 0; i < SMG_FAM_COUNT; ++i) {
+    ctx->prof_ms[i] = 0;
+    ctx->prof_count[i] = 0;
+  }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return SMG_ERR_HIP;
+  }
+  if (initial < (size_t)(64u << 20)) initial = (size_t)(64u << 20);
+  char* base = nullptr;
+  if (hipMalloc(&base, initial) != hipSuccess) {
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SMG_ERR_OOM;
+  }
+  ctx->blocks.push_back({base, initial});
+  if (hipMalloc(&ctx->status_d, 256) != hipSuccess ||
+      hipHostMalloc(&ctx->status_h, 256, hipHostMallocDefault) != hipSuccess) {
+    delete ctx;
+    return SMG_ERR_HIP;
+  }
+  hipMemset(ctx->status_d, 0, 256);
+  ctx->host_scratch_size = 1u << 20;
+  if (hipHostMalloc(&ctx->host_scratch, ctx->host_scratch_size, hipHostMallocDefault) != hipSuccess) {
+    delete ctx;
+    return SMG_ERR_HIP;
+  }
+  hipDeviceSynchronize();
+  *out = ctx;
+  return SMG_OK;
+}
+
+int smg_ctx_destroy(smg_ctx* ctx) {
+  if (!ctx) return SMG_OK;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  prof_drain(ctx);
+  smg_comm_destroy(ctx);
+  for (auto& b : ctx->blocks) hipFree(b.base);
+  for (auto e : ctx->prof_pool) hipEventDestroy(e);
+  for (int i = 0; i < 4; ++i)
+    if (ctx->ws[i]) hipFree(ctx->ws[i]);
+  hipFree(ctx->status_d);
+  hipHostFree(ctx->status_h);
+  hipHostFree(ctx->host_scratch);
+  hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return SMG_OK;
+}
+
+int smg_ctx_device(const smg_ctx* ctx) { return ctx ? ctx->device : -1; }
+void* smg_ctx_stream(smg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+void* smg_arena_alloc(smg_ctx* ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  bytes = (bytes + kAlign - 1) & ~(kAlign - 1);
+  if (bytes == 0) bytes = kAlign;
+  smg_arena_block* b = &ctx->blocks[ctx->cur_block];
+  if (ctx->offset + bytes <= b->size) {
+    void* p = b->base + ctx->offset;
+    ctx->offset += bytes;
+    return p;
+  }
+  // move_to_next_block (stack_alloc.hpp:94-119)
+  size_t nb = ctx->cur_block + 1;
+  while (nb < ctx->blocks.size() && ctx->blocks[nb].size < bytes) ++nb;
+  if (nb >= ctx->blocks.size()) {
+    size_t newsize = ctx->blocks.back().size * 2;
+    if (newsize < bytes) newsize = bytes;
+    char* base = nullptr;
+    if (hipMalloc(&base, newsize) != hipSuccess) {
+      // retry with exactly what is needed before giving up
+      if (newsize == bytes || hipMalloc(&base, bytes) != hipSuccess) {
+        hipGetLastError();
+        ctx->host_status |= SMG_ERR_OOM;
+        return nullptr;
+      }
+      newsize = bytes;
+    }
+    ctx->blocks.push_back({base, newsize});
+    nb = ctx->blocks.size() - 1;
+  }
+  ctx->cur_block = nb;
+  ctx->offset = bytes;
+  return ctx->blocks[nb].base;
+}
+
+// mark encodes (block, offset): block in the top 16 bits
+size_t smg_arena_mark(smg_ctx* ctx) {
+  return ((size_t)ctx->cur_block << 48) | ctx->offset;
+}
+
+int smg_arena_rewind(smg_ctx* ctx, size_t mark) {
+  size_t blk = mark >> 48, off = mark & ((1ull << 48) - 1);
+  if (blk >= ctx->blocks.size()) return SMG_ERR_ARG;
+  ctx->cur_block = blk;
+  ctx->offset = off;
+  return SMG_OK;
+}
+
+int smg_arena_recover_all(smg_ctx* ctx) {
+  ctx->cur_block = 0;
+  ctx->offset = 0;
+  return SMG_OK;
+}
+
+size_t smg_arena_used(const smg_ctx* ctx) {
+  size_t s = 0;
+  for (size_t i = 0; i < ctx->cur_block; ++i) s += ctx->blocks[i].size;
+  return s + ctx->offset;
+}
+
+size_t smg_arena_reserved(const smg_ctx* ctx) {
+  size_t s = 0;
+  for (auto& b : ctx->blocks) s += b.size;
+  return s;
+}
+
+void* smg_host_scratch(smg_ctx* ctx, size_t bytes) {
+  if (bytes > ctx->host_scratch_size) {
+    hipStreamSynchronize(ctx->stream);
+    hipHostFree(ctx->host_scratch);
+    size_t n = ctx->host_scratch_size;
+    while (n < bytes) n *= 2;
+    if (hipHostMalloc(&ctx->host_scratch, n, hipHostMallocDefault) != hipSuccess) {
+      ctx->host_scratch = nullptr;
+      ctx->host_scratch_size = 0;
+      return nullptr;
+    }
+    ctx->host_scratch_size = n;
+  }
+  return ctx->host_scratch;
+}
+
+int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return SMG_OK;
+  SMG_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return SMG_OK;
+}
+
+int smg_memcpy_d2h(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return SMG_OK;
+  SMG_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return SMG_OK;
+}
+
+int smg_memcpy_d2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return SMG_OK;
+  SMG_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return SMG_OK;
+}
+
+int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
+  if (!bytes) return SMG_OK;
+  SMG_HIP_TRY(hipMemsetAsync(dst, v, bytes, ctx->stream));
+  return SMG_OK;
+}
+
+int smg_sync(smg_ctx* ctx) {
+  SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (ctx->prof_on) prof_drain(ctx);
+  return SMG_OK;
+}
+
+int smg_status(smg_ctx* ctx, int* status) {
+  SMG_HIP_TRY(hipMemcpyAsync(ctx->status_h, ctx->status_d, sizeof(int),
+                             hipMemcpyDeviceToHost, ctx->stream));
+  SMG_HIP_TRY(hipMemsetAsync(ctx->status_d, 0, sizeof(int), ctx->stream));
+  SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (ctx->prof_on) prof_drain(ctx);
+  int s = ctx->status_h[0] | ctx->host_status;
+  ctx->host_status = 0;
+  if (status) *status = s;
+  return SMG_OK;
+}
+
+int smg_profile_enable(smg_ctx* ctx, int on) {
+  hipStreamSynchronize(ctx->stream);
+  prof_drain(ctx);
+  ctx->prof_on = on;
+  for (int i = 0; i < SMG_FAM_COUNT; ++i) {
+    ctx->prof_ms[i] = 0;
+    ctx->prof_count[i] = 0;
+  }
+  return SMG_OK;
+}
+
+int smg_profile_read(smg_ctx* ctx, int family, double* ms, long long* count) {
+  if (family < 0 || family >= SMG_FAM_COUNT) return SMG_ERR_ARG;
+  hipStreamSynchronize(ctx->stream);
+  prof_drain(ctx);
+  if (ms) *ms = ctx->prof_ms[family];
+  if (count) *count = ctx->prof_count[family];
+  return SMG_OK;
+}
+
+}  // extern "C"

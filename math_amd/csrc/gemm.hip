@@ -1,0 +1,287 @@
+// fp64 GEMM on the CDNA4 matrix cores (v_mfma_f64_16x16x4_f64).
+//
+// C = alpha op(A) op(B) + beta C, optionally only the lower triangle of C.
+// Used for the dense contractions of multiply (rev/mat/fun/multiply.hpp:65-135)
+// and of the blocked Cholesky forward / Murray adjoint
+// (rev/mat/fun/cholesky_decompose.hpp:135-158).
+//
+// Tiling: a 256-thread workgroup (4 waves, 2x2) owns a BM x BN tile of C;
+// each wave owns (BM/2) x (BN/2) = TM x TN MFMA tiles of 16x16 held in
+// accumulators.  K advances in steps of BK = 16 staged through LDS:
+//   operand contiguous along the output dim (A no-trans, B trans): LDS [k][dim+16]
+//   operand contiguous along k (A trans, B no-trans):               LDS [dim][k+1]
+// Both make the MFMA fragment reads (16 consecutive rows/cols x 4 k) bank-
+// conflict free for ds_read_b64 (row stride = 16 mod 32 doubles, resp. 17).
+// Global->LDS staging goes through registers with one tile of prefetch.
+// Split-K writes fixed-order partial slabs reduced by a second kernel, so the
+// result is bitwise deterministic run to run.
+#include "smg_internal.h"
+
+namespace {
+
+constexpr int BK = 16;
+
+template <int BM, bool KCONTIG>
+struct lds_layout;
+template <int BM>
+struct lds_layout<BM, false> {  // [k][BM + 16]
+  static constexpr int S = BM + 16;
+  static constexpr int size = BK * S;
+  __device__ static int at(int i, int kk) { return kk * S + i; }
+};
+template <int BM>
+struct lds_layout<BM, true> {  // [BM][BK + 1]
+  static constexpr int S = BK + 1;
+  static constexpr int size = BM * S;
+  __device__ static int at(int i, int kk) { return i * S + kk; }
+};
+
+// Operand X viewed as a (rows x k) matrix in the kernel's orientation:
+//   KCONTIG == false : element (i, kk) at X[i + kk*ld]
+//   KCONTIG == true  : element (i, kk) at X[kk + i*ld]
+template <int BM, bool KCONTIG>
+__device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
+                                          int rows, int k, int i0, int k0,
+                                          double (&r)[BM * BK / 256]) {
+  constexpr int PER = BM * BK / 256;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    int i, kk;
+    if (KCONTIG) {
+      i = e / BK;
+      kk = e % BK;
+    } else {
+      kk = e / BM;
+      i = e % BM;
+    }
+    const int gi = i0 + i, gk = k0 + kk;
+    double v = 0.0;
+    if (gi < rows && gk < k)
+      v = KCONTIG ? X[(size_t)gi * ld + gk] : X[gi + (size_t)gk * ld];
+    r[q] = v;
+  }
+}
+
+template <int BM, bool KCONTIG>
+__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256]) {
+  constexpr int PER = BM * BK / 256;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    int i, kk;
+    if (KCONTIG) {
+      i = e / BK;
+      kk = e % BK;
+    } else {
+      kk = e / BM;
+      i = e % BM;
+    }
+    lds[lds_layout<BM, KCONTIG>::at(i, kk)] = r[q];
+  }
+}
+
+__device__ __forceinline__ void tri_decode(int t, int& bi, int& bj) {
+  // t -> (bi, bj) with bj <= bi, row-major over the lower triangle of tiles
+  int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  bi = r;
+  bj = t - r * (r + 1) / 2;
+}
+
+// MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n)
+template <int BM, int BN, bool TA, bool TB, int MODE>
+__global__ __launch_bounds__(256) void k_gemm(
+    int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
+    const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
+    int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab) {
+  // A-side contiguity: no-trans A is m-contiguous; trans A is k-contiguous.
+  // B-side as an (n x k) operand: no-trans B is k-contiguous; trans B is n-contiguous.
+  constexpr bool AK = TA;
+  constexpr bool BKC = !TB;
+  using LA = lds_layout<BM, AK>;
+  using LB = lds_layout<BN, BKC>;
+  __shared__ double As[LA::size];
+  __shared__ double Bs[LB::size];
+
+  const int tile = blockIdx.x % ntiles;
+  const int split = blockIdx.x / ntiles;
+  int bi, bj;
+  if (MODE == 1) {
+    tri_decode(tile, bi, bj);
+  } else if (MODE == 2) {
+    tri_decode(tile, bj, bi);
+  } else {
+    bi = tile % tiles_m;
+    bj = tile / tiles_m;
+  }
+  const int i0 = bi * BM, j0 = bj * BN;
+  const int kbeg = split * kchunk;
+  const int kend = min(k, kbeg + kchunk);
+
+  constexpr int TM = BM / 32, TN = BN / 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  d4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+
+  double ra[BM * BK / 256], rb[BN * BK / 256];
+  const int kq = kend - kbeg;
+  // A as (m x k) operand; B as (n x k) operand
+  if (kq > 0) {
+    load_tile<BM, AK>(A, lda, m, kend, i0, kbeg, ra);
+    load_tile<BN, BKC>(B, ldb, n, kend, j0, kbeg, rb);
+  }
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    store_tile<BM, AK>(As, ra);
+    store_tile<BN, BKC>(Bs, rb);
+    __syncthreads();
+    if (k0 + BK < kend) {
+      load_tile<BM, AK>(A, lda, m, kend, i0, k0 + BK, ra);
+      load_tile<BN, BKC>(B, ldb, n, kend, j0, k0 + BK, rb);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      double af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[a] = As[LA::at(wr * (BM / 2) + a * 16 + fr, ks * 4 + fk)];
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[b] = Bs[LB::at(wc * (BN / 2) + b * 16 + fr, ks * 4 + fk)];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+  }
+
+  // epilogue: D layout of v_mfma_f64_16x16x4_f64: reg r of lane l holds
+  // row (l>>4) + 4r, col l&15 of the 16x16 tile.
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r;
+        const int j = j0 + wc * (BN / 2) + b * 16 + (lane & 15);
+        if (i >= m || j >= n) continue;
+        if (MODE == 1 && i < j) continue;
+        if (MODE == 2 && i > j) continue;
+        const double v = acc[a][b][r];
+        if (slab) {
+          slab[(size_t)split * m * n + (size_t)j * m + i] = v;
+        } else {
+          double* c = C + i + (size_t)j * ldc;
+          *c = (beta == 0.0) ? alpha * v : alpha * v + beta * *c;
+        }
+      }
+}
+
+__global__ void k_splitk_reduce(int m, int n, int splits, const double* __restrict__ slab,
+                                double alpha, double beta, double* __restrict__ C,
+                                int ldc, int lower) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)m * n) return;
+  const int i = (int)(idx % m), j = (int)(idx / m);
+  if (lower == 1 && i < j) return;
+  if (lower == 2 && i > j) return;
+  double s = 0.0;
+  for (int t = 0; t < splits; ++t) s += slab[(size_t)t * m * n + idx];
+  double* c = C + i + (size_t)j * ldc;
+  *c = (beta == 0.0) ? alpha * s : alpha * s + beta * *c;
+}
+
+template <int BM, int BN, bool TA, bool TB, int MODE>
+int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
+           int lda, const double* B, int ldb, double beta, double* C, int ldc) {
+  const int tm = smg_ceil_div(m, BM), tn = smg_ceil_div(n, BN);
+  const int ntiles = MODE != 0 ? tm * (tm + 1) / 2 : tm * tn;
+  // split K when the tile grid cannot fill the 256 CUs and K is long
+  int splits = 1;
+  const int target = 512;
+  if (ntiles < target && k >= 4 * BK * 2) {
+    splits = smg_ceil_div(target, ntiles);
+    const int maxs = k / (4 * BK);
+    if (splits > maxs) splits = maxs;
+    if (splits > 64) splits = 64;
+    if (splits < 1) splits = 1;
+  }
+  int kchunk = smg_ceil_div(smg_ceil_div(k, splits), BK) * BK;
+  splits = smg_ceil_div(k, kchunk);
+  double* slab = nullptr;
+  if (splits > 1) {
+    slab = smg_ws(ctx, SMG_WS_GEMM, (size_t)splits * m * n);
+    if (!slab) return SMG_ERR_OOM;
+  }
+  hipLaunchKernelGGL((k_gemm<BM, BN, TA, TB, MODE>), dim3(ntiles * splits), dim3(256), 0,
+                     ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
+                     ntiles, kchunk, slab);
+  if (splits > 1) {
+    const long long tot = (long long)m * n;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
+                       ctx->stream, m, n, splits, slab, alpha, beta, C, ldc, MODE);
+  }
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+template <bool TA, bool TB, int MODE>
+int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
+                  int lda, const double* B, int ldb, double beta, double* C, int ldc) {
+  const long long big_tiles = (long long)smg_ceil_div(m, 128) * smg_ceil_div(n, 128);
+  if (big_tiles >= 256)
+    return launch<128, 128, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  return launch<64, 64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}
+
+}  // namespace
+
+int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
+                  double alpha, const double* A, int lda, const double* B, int ldb,
+                  double beta, double* C, int ldc) {
+  if (m <= 0 || n <= 0) return SMG_OK;
+  if (k <= 0 || alpha == 0.0) {
+    if (beta == 1.0) return SMG_OK;
+    return smg_scale_impl(ctx, m, n, beta, C, ldc, uplo);
+  }
+  smg_prof_scope prof(ctx, SMG_FAM_GEMM);
+  if (uplo == 1) {
+    if (m != n) return SMG_ERR_ARG;
+    if (!ta && tb) return dispatch_tile<false, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (ta && !tb) return dispatch_tile<true, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (!ta && !tb) return dispatch_tile<false, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return dispatch_tile<true, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  }
+  if (uplo == 2) {
+    if (m != n) return SMG_ERR_ARG;
+    if (!ta && tb) return dispatch_tile<false, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (ta && !tb) return dispatch_tile<true, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (!ta && !tb) return dispatch_tile<false, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return dispatch_tile<true, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  }
+  if (!ta && !tb) return dispatch_tile<false, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  if (!ta && tb) return dispatch_tile<false, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  if (ta && !tb) return dispatch_tile<true, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  return dispatch_tile<true, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}
+
+extern "C" int smg_gemm(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
+                        double alpha, const double* A, int lda, const double* B,
+                        int ldb, double beta, double* C, int ldc) {
+  if (!ctx || m < 0 || n < 0 || k < 0) return SMG_ERR_ARG;
+  if ((m > 0 && n > 0) && (!C || ldc < m)) return SMG_ERR_ARG;
+  if (k > 0 && m > 0 && n > 0 && alpha != 0.0) {
+    if (!A || !B) return SMG_ERR_ARG;
+    if (lda < (ta ? k : m) || ldb < (tb ? n : k)) return SMG_ERR_ARG;
+  }
+  return smg_gemm_impl(ctx, ta, tb, uplo, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}

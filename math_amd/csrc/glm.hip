@@ -1,0 +1,186 @@
+// bernoulli_logit_glm_lpmf<false>(y | x, alpha, beta), scalar alpha, in ONE
+// pass over x.
+//
+// Reference: prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138
+//   ytheta = sign .* (x beta + alpha), sign = 2y - 1            (:92-94)
+//   logp   = sum( ytheta > 20 ? -exp(-ytheta)
+//               : ytheta < -20 ? ytheta : -log1p(exp(-ytheta)) )  (:99-104)
+//   theta' = ytheta > 20 ? -exp(-ytheta) : ytheta < -20 ? sign
+//               : sign exp(-ytheta) / (exp(-ytheta) + 1)         (:115-121)
+//   d/dbeta = x^T theta',  d/dalpha = sum theta'                  (:123, :133)
+// The reference makes two GEMV passes over x (HBM-bound).  Here persistent
+// workgroups stream 32-row tiles of x (column-major) through LDS once: the
+// tile yields eta for its rows, then theta', then its contribution to x^T
+// theta' while it is still on chip.  Each workgroup keeps per-column
+// accumulators in registers and writes one [logp, alpha', beta'(M)] partial;
+// a fixed-order second pass sums the partials (deterministic).
+#include <cmath>
+
+#include "smg_internal.h"
+
+namespace {
+
+constexpr int RB = 32;            // rows per tile
+constexpr int MMAX = 256;         // fused path: M <= 256
+constexpr int XS = RB + 1;        // LDS column stride (bank-conflict free)
+constexpr int PER = RB * MMAX / 256;
+
+__global__ __launch_bounds__(256) void k_glm_fused(const int* __restrict__ y,
+                                                   const double* __restrict__ x, long long R,
+                                                   int M, long long ldx,
+                                                   const double* __restrict__ ab,
+                                                   double* __restrict__ part) {
+  __shared__ double X[MMAX * XS];
+  __shared__ double beta[MMAX];
+  __shared__ double etap[8 * RB];
+  __shared__ double thd[RB];
+  __shared__ double lds[16];
+  const int t = threadIdx.x;
+  if (t < M) beta[t] = ab[1 + t];
+  const double alpha = ab[0];
+  const long long ntiles = (R + RB - 1) / RB;
+  double gacc = 0.0;                 // column t's beta' accumulator (t < M)
+  double lp_acc = 0.0, ga_acc = 0.0; // rows' logp / alpha' (threads < RB)
+  double reg[PER];
+
+  auto load = [&](long long tile) {
+    const long long r0 = tile * RB;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      const int r = e % RB, c = e / RB;
+      const long long gr = r0 + r;
+      reg[q] = (c < M && gr < R) ? x[gr + (size_t)c * ldx] : 0.0;
+    }
+  };
+
+  long long tile = blockIdx.x;
+  if (tile < ntiles) load(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // previous tile fully consumed
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      X[(e / RB) * XS + (e % RB)] = reg[q];
+    }
+    __syncthreads();
+    const long long next = tile + gridDim.x;
+    if (next < ntiles) load(next);  // in flight during the compute below
+    // eta: thread (r, g) sums columns c = g, g+8, ...
+    {
+      const int r = t % RB, g = t / RB;
+      double s = 0.0;
+      for (int c = g; c < M; c += 8) s += X[c * XS + r] * beta[c];
+      etap[g * RB + r] = s;
+    }
+    __syncthreads();
+    if (t < RB) {
+      const long long gr = tile * RB + t;
+      double th = 0.0;
+      if (gr < R) {
+        double eta = 0.0;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) eta += etap[g * RB + t];
+        const double sgn = 2.0 * y[gr] - 1.0;
+        const double yt = sgn * (eta + alpha);
+        const double e = exp(-yt);
+        lp_acc += yt > 20.0 ? -e : (yt < -20.0 ? yt : -log1p(e));
+        th = yt > 20.0 ? -e : (yt < -20.0 ? sgn : sgn * e / (e + 1));
+        ga_acc += th;
+      }
+      thd[t] = th;
+    }
+    __syncthreads();
+    if (t < M) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) s += X[t * XS + r] * thd[r];
+      gacc += s;
+    }
+  }
+  // per-block partial [logp, alpha', beta'(M)]
+  const int W = M + 2;
+  double* p = part + (size_t)blockIdx.x * W;
+  __syncthreads();
+  const double lp = block_sum(lp_acc, lds);
+  __syncthreads();
+  const double ga = block_sum(ga_acc, lds);
+  if (t == 0) {
+    p[0] = lp;
+    p[1] = ga;
+  }
+  if (t < M) p[2 + t] = gacc;
+}
+
+int glm_blocks(long long R) {
+  const long long ntiles = (R + RB - 1) / RB;
+  long long nb = 512;  // 2 workgroups per CU (67.6 KB LDS each)
+  if (nb > ntiles) nb = ntiles;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
+// ------------------------------------------------ generic path (M > 256)
+__global__ void k_glm_rows(const int* __restrict__ y, const double* __restrict__ eta, long long R,
+                           double alpha, double* __restrict__ th, double* part) {
+  __shared__ double lds[16];
+  double lp = 0.0, ga = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < R;
+       i += (long long)gridDim.x * blockDim.x) {
+    const double sgn = 2.0 * y[i] - 1.0;
+    const double yt = sgn * (eta[i] + alpha);
+    const double e = exp(-yt);
+    lp += yt > 20.0 ? -e : (yt < -20.0 ? yt : -log1p(e));
+    const double d = yt > 20.0 ? -e : (yt < -20.0 ? sgn : sgn * e / (e + 1));
+    th[i] = d;
+    ga += d;
+  }
+  lp = block_sum(lp, lds);
+  __syncthreads();
+  ga = block_sum(ga, lds);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = lp;
+    part[2 * blockIdx.x + 1] = ga;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+long long smg_glm_ws_doubles(long long R, int M) {
+  if (M <= MMAX) return (long long)glm_blocks(R) * (M + 2);
+  return 2 * R + 2 * 1024;
+}
+
+int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x, long long R, int M,
+                            long long ldx, const double* ab, double* ws, double* out) {
+  if (!ctx || R < 0 || M < 0 || !ab || !ws || !out) return SMG_ERR_ARG;
+  if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GLM);
+  if (M <= MMAX) {
+    const int nb = glm_blocks(R);
+    hipLaunchKernelGGL(k_glm_fused, dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx, ab, ws);
+    smg_reduce_partials(ctx, ws, nb, M + 2, out, 0);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
+  // eta = x beta (GEMM n = 1), theta' per row, beta' = x^T theta'
+  double* eta = ws;
+  double* th = ws + R;
+  double* part = ws + 2 * R;
+  int rc = smg_gemm_impl(ctx, 0, 0, 0, (int)R, 1, M, 1.0, x, (int)ldx, ab + 1, M, 0.0, eta, (int)R);
+  if (rc) return rc;
+  double alpha_h;
+  rc = smg_memcpy_d2h(ctx, &alpha_h, ab, sizeof(double));
+  if (rc) return rc;
+  rc = smg_sync(ctx);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_glm_rows, dim3(1024), dim3(256), 0, ctx->stream, y, eta, R, alpha_h, th, part);
+  smg_reduce_partials(ctx, part, 1024, 2, out, 0);
+  rc = smg_gemm_impl(ctx, 1, 0, 0, M, 1, (int)R, 1.0, x, (int)ldx, th, (int)R, 0.0, out + 2, M);
+  SMG_LAUNCH_CHECK();
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,185 @@
+// gp_exp_quad_cov and add_diag, forward and reverse.
+//
+// gp_exp_quad_cov(std::vector<double> x, var sigma, var l)
+//   rev/mat/fun/gp_exp_quad_cov.hpp:64-94 (forward), :96-112 (chain)
+// The reference stores the N(N-1)/2 lower entries once and aliases the upper
+// triangle to them (:233-238), so the adjoint of each lower vari is the sum of
+// the adjoints of positions (i,j) and (j,i).  Here the node keeps the full
+// N x N adjoint and the reverse kernel sweeps every position once (coalesced),
+// which sums exactly those pairs:
+//   d/dl     = sum_{i != j} Kadj_ij K_ij d_ij^2 / l^3
+//   d/dsigma = 2/sigma (sum_{i != j} Kadj_ij K_ij + sum_i Kadj_ii sigma^2)
+// K_ij is recomputed from x instead of re-read (HBM: one read of Kadj).
+// Reductions are fixed-order (per-block partials + one ordered pass).
+//
+// add_diag: prim/mat/fun/add_diag.hpp:20-55.
+#include "smg_internal.h"
+
+namespace {
+
+constexpr int GP_BLOCKS = 2048;
+
+__global__ __launch_bounds__(256) void k_gp_fwd(const double* __restrict__ x, int n, double s2,
+                                                double inv_half_sq_l, double* __restrict__ K,
+                                                int ldk) {
+  // 2D: blockIdx.y over columns j, x-dim over rows i (coalesced stores)
+  const int j = blockIdx.y;
+  const double xj = x[j];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    double v;
+    if (i == j) {
+      v = s2;
+    } else {
+      const double d = (i > j) ? x[i] - xj : xj - x[i];
+      v = s2 * exp(-(d * d) * inv_half_sq_l);
+    }
+    K[i + (size_t)j * ldk] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gp_rev_partials(const double* __restrict__ x, int n,
+                                                         double s2, double inv_half_sq_l,
+                                                         const double* __restrict__ Ka, int lda,
+                                                         double* __restrict__ part) {
+  __shared__ double lds[16];
+  double al = 0.0, as = 0.0;
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    const double a = Ka[i + (size_t)j * lda];
+    if (i == j) {
+      as += a * s2;
+    } else {
+      const double d = (i > j) ? x[i] - x[j] : x[j] - x[i];
+      const double dist = d * d;
+      const double prod = a * (s2 * exp(-dist * inv_half_sq_l));
+      al += prod * dist;
+      as += prod;
+    }
+  }
+  const double sl = block_sum(al, lds);
+  __syncthreads();
+  const double ss = block_sum(as, lds);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x + 0] = ss;
+    part[2 * blockIdx.x + 1] = sl;
+  }
+}
+
+__global__ void k_gp_rev_final(const double* __restrict__ part, int nparts, double sigma, double l,
+                               double* out2) {
+  __shared__ double lds[16];
+  double ss = 0.0, sl = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    ss += part[2 * i];
+    sl += part[2 * i + 1];
+  }
+  ss = block_sum(ss, lds);
+  __syncthreads();
+  sl = block_sum(sl, lds);
+  if (threadIdx.x == 0) {
+    out2[0] += ss * 2 / sigma;     // :110
+    out2[1] += sl / (l * l * l);   // :109
+  }
+}
+
+__global__ void k_add_diag_fwd(const double* __restrict__ A, int lda, int n, double d,
+                               const double* __restrict__ dv, double* __restrict__ B, int ldb) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    double v = A[i + (size_t)j * lda];
+    if (i == j) v += dv ? dv[i] : d;
+    B[i + (size_t)j * ldb] = v;
+  }
+}
+
+__global__ void k_add_full(const double* __restrict__ X, int ldx, int n, double* __restrict__ Y,
+                           int ldy) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    Y[i + (size_t)j * ldy] += X[i + (size_t)j * ldx];
+  }
+}
+
+__global__ void k_diag_adj(const double* __restrict__ Ba, int ldb, int n, double* dadj, int vec) {
+  __shared__ double lds[16];
+  if (vec) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dadj[i] += Ba[i + (size_t)i * ldb];
+    return;
+  }
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += Ba[i + (size_t)i * ldb];
+  s = block_sum(s, lds);
+  if (threadIdx.x == 0) dadj[0] += s;
+}
+
+inline int grid_for(long long tot) {
+  long long g = (tot + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int smg_gp_exp_quad_cov_fwd(smg_ctx* ctx, const double* x, int n, double sigma, double l,
+                            double* K, int ldk) {
+  if (!ctx || n < 0 || (n > 0 && (!x || !K || ldk < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  const double s2 = sigma * sigma;
+  const double ihl = 0.5 / (l * l);
+  dim3 grid(smg_ceil_div(n, 256) > 16 ? 16 : smg_ceil_div(n, 256), n);
+  hipLaunchKernelGGL(k_gp_fwd, grid, dim3(256), 0, ctx->stream, x, n, s2, ihl, K, ldk);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma, double l,
+                            const double* Kadj, int ldka, double* out2) {
+  if (!ctx || n < 0 || (n > 0 && (!x || !Kadj || !out2 || ldka < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  const long long tot = (long long)n * n;
+  int nb = grid_for(tot);
+  if (nb > GP_BLOCKS) nb = GP_BLOCKS;
+  double* part = smg_ws(ctx, SMG_WS_RED, 2 * (size_t)nb);
+  if (!part) return SMG_ERR_OOM;
+  hipLaunchKernelGGL(k_gp_rev_partials, dim3(nb), dim3(256), 0, ctx->stream, x, n, sigma * sigma,
+                     0.5 / (l * l), Kadj, ldka, part);
+  hipLaunchKernelGGL(k_gp_rev_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, sigma, l, out2);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_add_diag_fwd(smg_ctx* ctx, const double* A, int lda, int n, double d, const double* dv,
+                     double* B, int ldb) {
+  if (!ctx || n < 0 || (n > 0 && (!A || !B || lda < n || ldb < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  hipLaunchKernelGGL(k_add_diag_fwd, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, A,
+                     lda, n, d, dv, B, ldb);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_add_diag_rev(smg_ctx* ctx, const double* Ba, int ldb, int n, double* Aa, int ldaa,
+                     double* dadj, int vec) {
+  if (!ctx || n < 0 || (n > 0 && !Ba)) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (Aa)
+    hipLaunchKernelGGL(k_add_full, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, Ba,
+                       ldb, n, Aa, ldaa);
+  if (dadj)
+    hipLaunchKernelGGL(k_diag_adj, dim3(1), dim3(1024), 0, ctx->stream, Ba, ldb, n, dadj, vec);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// Internal declarations shared by the libsmg_hip.so translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/smg_hip.h"
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+struct smg_arena_block {
+  char* base;
+  size_t size;
+};
+
+struct smg_prof_slot {
+  hipEvent_t start, stop;
+  int family;
+};
+
+struct smg_ctx {
+  int device;
+  hipStream_t stream;
+  // device bump arena: blocks double in size (memory/stack_alloc.hpp:94-119)
+  std::vector<smg_arena_block> blocks;
+  size_t cur_block;
+  size_t offset;  // within cur_block
+  // status word (device) + pinned host mirror
+  int* status_d;
+  int* status_h;
+  int host_status;  // host-detected errors (OOM, HIP)
+  // pinned host scratch
+  void* host_scratch;
+  size_t host_scratch_size;
+  // persistent device workspaces (grow on demand; NOT arena-managed)
+  double* ws[4];
+  size_t ws_doubles[4];
+  // profiling
+  int prof_on;
+  std::vector<smg_prof_slot> prof_pending;
+  std::vector<hipEvent_t> prof_pool;
+  double prof_ms[SMG_FAM_COUNT];
+  long long prof_count[SMG_FAM_COUNT];
+  // RCCL communicator (opaque)
+  void* comm;
+};
+
+// latch helpers
+#define SMG_HIP_TRY(expr)                          \
+  do {                                             \
+    hipError_t _e = (expr);                        \
+    if (_e != hipSuccess) {                        \
+      if (ctx) ctx->host_status |= SMG_ERR_HIP;    \
+      return SMG_ERR_HIP;                          \
+    }                                              \
+  } while (0)
+
+#define SMG_LAUNCH_CHECK()                         \
+  do {                                             \
+    hipError_t _e = hipGetLastError();             \
+    if (_e != hipSuccess) {                        \
+      ctx->host_status |= SMG_ERR_HIP;             \
+      return SMG_ERR_HIP;                          \
+    }                                              \
+  } while (0)
+
+// profiling scope: records events around a region of launches on ctx->stream
+struct smg_prof_scope {
+  smg_ctx* ctx;
+  int fam;
+  hipEvent_t a, b;
+  bool on;
+  smg_prof_scope(smg_ctx* c, int f);
+  ~smg_prof_scope();
+};
+
+// named persistent workspaces (grow on demand; a growth synchronises the
+// stream, so steady-state evaluations never reallocate)
+enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3 };
+double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
+// C = beta C (lower != 0: lower triangle only)
+int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int lower);
+
+// internal GEMM entry used by other units (no argument re-validation)
+int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
+                  int k, double alpha, const double* A, int lda, const double* B,
+                  int ldb, double beta, double* C, int ldc);
+
+// deterministic device reductions: out[0] (+)= sum of per-block partials
+// partial layout: nparts doubles (or nparts x width for vector partials)
+void smg_reduce_partials(smg_ctx* ctx, const double* partials, int nparts,
+                         int width, double* out, int accumulate);
+
+static inline int smg_ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// wave (64-lane) reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// block-wide sum of one value per thread (blockDim.x multiple of 64, <= 1024)
+// fixed order => deterministic
+__device__ __forceinline__ double block_sum(double v, double* lds /* >= 16 */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) lds[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < nw; ++i) s += lds[i];
+  return s;  // valid in thread 0 only
+}

@@ -1,0 +1,189 @@
+// Blocked triangular solves and the multiply / mdivide_left_tri functors.
+//
+//   trsm: B <- op(tri(A))^{-1} B in place, op = identity or transpose,
+//         SMG_NB diagonal blocks inverted in LDS (k_trtri_blocks) and applied
+//         with the MFMA GEMM; off-diagonal updates are GEMMs as well.
+//   mdivide_left_tri<TriView>  rev/mat/fun/mdivide_left_tri.hpp:16-373
+//   multiply                   rev/mat/fun/multiply.hpp:65-135
+#include "smg_internal.h"
+#include "tri_small.h"
+
+namespace {
+
+// W_p = inverse of the lower-triangular form of diagonal block p:
+//   lower: W_p = D_p^{-1};  upper: W_p = (U_p^T)^{-1} = (U_p^{-1})^T.
+// W is m x SMG_NB (block p in rows p*NB.., ld m).
+__global__ __launch_bounds__(256) void k_trtri_blocks(const double* __restrict__ A, int lda,
+                                                      int m, int upper, double* __restrict__ W) {
+  __shared__ double D[SMG_NB * SMG_NBP];
+  __shared__ double X[SMG_NB * SMG_NBP];
+  const int j = blockIdx.x * SMG_NB;
+  const int b = min(SMG_NB, m - j);
+  const double* Ab = A + j + (size_t)j * lda;
+  for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
+    const int c = e / SMG_NB, r = e % SMG_NB;
+    double v = 0.0;
+    if (r < b && c < b && r >= c) v = upper ? Ab[c + (size_t)r * lda] : Ab[r + (size_t)c * lda];
+    D[r * SMG_NBP + c] = v;
+  }
+  __syncthreads();
+  lds_tri_inverse_lower(D, X, b);
+  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
+    const int c = e / b, r = e % b;
+    W[j + r + (size_t)c * m] = X[r * SMG_NBP + c];
+  }
+}
+
+__global__ void k_copy(int m, int n, const double* __restrict__ A, int lda,
+                       double* __restrict__ B, int ldb, double alpha, int accumulate) {
+  const long long tot = (long long)m * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / m), i = (int)(e % m);
+    const double v = alpha * A[i + (size_t)j * lda];
+    double* d = B + i + (size_t)j * ldb;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+__global__ void k_scale(int m, int n, double beta, double* C, int ldc, int tri) {
+  const long long tot = (long long)m * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / m), i = (int)(e % m);
+    if (tri == 1 && i < j) continue;
+    if (tri == 2 && i > j) continue;
+    if (tri == 3 && i >= j) continue;
+    double* c = C + i + (size_t)j * ldc;
+    *c = beta == 0.0 ? 0.0 : beta * *c;
+  }
+}
+
+inline int grid_for(long long tot) {
+  long long g = (tot + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int tri) {
+  hipLaunchKernelGGL(k_scale, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n,
+                     beta, C, ldc, tri);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
+                  double alpha, int accumulate) {
+  if (m <= 0 || n <= 0) return SMG_OK;
+  hipLaunchKernelGGL(k_copy, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n,
+                     A, lda, B, ldb, alpha, accumulate);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+// W: inverse diagonal blocks (m x SMG_NB, ld m) or NULL (computed here)
+int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
+                  int ldw, double* B, int ldb, int m, int n) {
+  if (m <= 0 || n <= 0) return SMG_OK;
+  const int nblk = (m + SMG_NB - 1) / SMG_NB;
+  if (!W) {
+    double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)m * SMG_NB);
+    if (!w) return SMG_ERR_OOM;
+    hipLaunchKernelGGL(k_trtri_blocks, dim3(nblk), dim3(256), 0, ctx->stream, A, lda, m,
+                       lower ? 0 : 1, w);
+    W = w;
+    ldw = m;
+  }
+  const bool forward = (lower && !trans) || (!lower && trans);
+  const bool wt = (trans != 0) != (lower == 0);  // X_p = W_p^T B_p
+  int rc;
+  for (int q = 0; q < nblk; ++q) {
+    const int p = forward ? q : nblk - 1 - q;
+    const int j = p * SMG_NB, b = min(SMG_NB, m - j), k = j + b;
+    double* Bp = B + j;
+    // X_p = W_p (or W_p^T) B_p, in place (the row extent b fits one tile)
+    rc = smg_gemm_impl(ctx, wt ? 1 : 0, 0, 0, b, n, b, 1.0, W + j, ldw, Bp, ldb, 0.0, Bp, ldb);
+    if (rc) return rc;
+    if (forward && k < m) {
+      if (lower)  // B[k:] -= L[k:, j:k] X_p
+        rc = smg_gemm_impl(ctx, 0, 0, 0, m - k, n, b, -1.0, A + k + (size_t)j * lda, lda, Bp, ldb,
+                           1.0, B + k, ldb);
+      else  // B[k:] -= (U[j:k, k:])^T X_p
+        rc = smg_gemm_impl(ctx, 1, 0, 0, m - k, n, b, -1.0, A + j + (size_t)k * lda, lda, Bp, ldb,
+                           1.0, B + k, ldb);
+      if (rc) return rc;
+    }
+    if (!forward && j > 0) {
+      if (!lower)  // B[0:j] -= U[0:j, j:k] X_p
+        rc = smg_gemm_impl(ctx, 0, 0, 0, j, n, b, -1.0, A + (size_t)j * lda, lda, Bp, ldb, 1.0, B,
+                           ldb);
+      else  // B[0:j] -= (L[j:k, 0:j])^T X_p
+        rc = smg_gemm_impl(ctx, 1, 0, 0, j, n, b, -1.0, A + j, lda, Bp, ldb, 1.0, B, ldb);
+      if (rc) return rc;
+    }
+  }
+  return SMG_OK;
+}
+
+extern "C" {
+
+int smg_copy_matrix(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
+                    int trans, int zero_upper) {
+  if (!ctx || trans) return SMG_ERR_ARG;  // transposed copies are not needed by the host layer
+  int rc = smg_copy_impl(ctx, m, n, A, lda, B, ldb, 1.0, 0);
+  if (rc || !zero_upper) return rc;
+  return smg_scale_impl(ctx, m, n, 0.0, B, ldb, 3);
+}
+
+int smg_mdivide_left_tri_fwd(smg_ctx* ctx, int lower, const double* A, int lda, const double* B,
+                             int ldb, int m, int n, double* C, int ldc) {
+  if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
+  if (m == 0 || n == 0) return SMG_OK;
+  if (!A || !B || !C || lda < m || ldb < m || ldc < m) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_TRSV);
+  int rc = smg_copy_impl(ctx, m, n, B, ldb, C, ldc, 1.0, 0);
+  if (rc) return rc;
+  return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, C, ldc, m, n);
+}
+
+int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda, const double* C,
+                             int ldc, const double* Cadj, int ldca, int m, int n, double* Aadj,
+                             int ldaa, double* Badj, int ldba, double* ws) {
+  if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
+  if (m == 0 || n == 0) return SMG_OK;
+  if (!A || !C || !Cadj || !ws) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_TRSV);
+  // adjB = tri(A)^{-T} Cadj   (mdivide_left_tri.hpp:104-107)
+  int rc = smg_copy_impl(ctx, m, n, Cadj, ldca, ws, m, 1.0, 0);
+  if (rc) return rc;
+  rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, ws, m, m, n);
+  if (rc) return rc;
+  if (Aadj) {  // adjA = -adjB C^T on the triangle only (:108, :111-123)
+    rc = smg_gemm_impl(ctx, 0, 1, lower ? 1 : 2, m, m, n, -1.0, ws, m, C, ldc, 1.0, Aadj, ldaa);
+    if (rc) return rc;
+  }
+  if (Badj) return smg_copy_impl(ctx, m, n, ws, m, Badj, ldba, 1.0, 1);
+  return SMG_OK;
+}
+
+int smg_multiply_fwd(smg_ctx* ctx, const double* A, int lda, const double* B, int ldb, int m, int k,
+                     int n, double* C, int ldc) {
+  if (!ctx) return SMG_ERR_ARG;
+  return smg_gemm(ctx, 0, 0, 0, m, n, k, 1.0, A, lda, B, ldb, 0.0, C, ldc);
+}
+
+int smg_multiply_rev(smg_ctx* ctx, const double* A, int lda, const double* B, int ldb,
+                     const double* Cadj, int ldca, int m, int k, int n, double* Aadj, int ldaa,
+                     double* Badj, int ldba) {
+  if (!ctx) return SMG_ERR_ARG;
+  int rc = SMG_OK;
+  if (Aadj) rc = smg_gemm(ctx, 0, 1, 0, m, k, n, 1.0, Cadj, ldca, B, ldb, 1.0, Aadj, ldaa);
+  if (rc) return rc;
+  if (Badj) rc = smg_gemm(ctx, 1, 0, 0, k, n, m, 1.0, A, lda, Cadj, ldca, 1.0, Badj, ldba);
+  return rc;
+}
+
+}  // extern "C"

@@ -35,8 +35,10 @@ def golden(name: str) -> dict:
 
 def near_rel(actual, expected, rtol, atol=None, what=""):
     """expect_near_rel semantics (test/unit/math/expect_near_rel.hpp:33-52):
-    relative error 2|a-b|/(|a|+|b|) <= rtol, absolute |a-b| <= atol where
-    either side is below atol (atol defaults to rtol).  NaN/inf must match."""
+    each entry passes when its relative error 2|a-b|/(|a|+|b|) <= rtol or its
+    absolute error |a-b| <= atol (atol defaults to rtol, the reference's
+    absolute fallback near zero; callers pass a norm-scaled atol for matrices
+    whose small entries carry cancellation).  NaN/inf must match exactly."""
     a = np.asarray(actual, dtype=np.float64).ravel()
     b = np.asarray(expected, dtype=np.float64).ravel()
     assert a.shape == b.shape, f"{what}: shape {a.shape} vs {b.shape}"
@@ -48,7 +50,7 @@ def near_rel(actual, expected, rtol, atol=None, what=""):
     small = (np.abs(a) < atol) | (np.abs(b) < atol)
     absdiff = np.abs(a - b)
     rel = absdiff / np.maximum(0.5 * (np.abs(a) + np.abs(b)), 1e-300)
-    bad = np.where(small, absdiff > atol, rel > rtol)
+    bad = (absdiff > atol) & (rel > rtol)
     if np.any(bad):
         i = np.where(bad)[0][0]
         raise AssertionError(

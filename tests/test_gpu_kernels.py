@@ -1,0 +1,379 @@
+"""GPU parity tests of every C-ABI entry point (libsmg_hip.so through ctypes)
+against the golden vectors produced by the real reference and against the
+CPU restatement (oracle) on seeded inputs.
+
+Tolerances are written per test: 1e-10 relative (expect_near_rel semantics)
+for values and gradients unless stated; plain BLAS products are checked at
+1e-13 relative to the operand norms.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import gen
+from _util import GOLDEN, f64, golden, near_rel, oracle, ptr
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from math_amd import hip
+    c = hip.Context(0, 1 << 30)
+    yield c
+    c.close()
+
+
+@pytest.fixture(autouse=True)
+def _rewind(ctx):
+    m = ctx.mark()
+    yield
+    assert ctx.status() == 0
+    ctx.rewind(m)
+
+
+def F(a):  # column-major flat
+    return np.asfortranarray(a).ravel(order="F")
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(16, 16, 4), (70, 33, 45), (130, 257, 64), (64, 64, 4096), (512, 384, 300)])
+def test_gemm(ctx, ta, tb, m, n, k):
+    rng = np.random.default_rng(m * 7 + n * 3 + k)
+    A = rng.standard_normal((k, m) if ta else (m, k))
+    B = rng.standard_normal((n, k) if tb else (k, n))
+    C = rng.standard_normal((m, n))
+    ref = 1.5 * (A.T if ta else A) @ (B.T if tb else B) - 0.5 * C
+    dA, dB, dC = ctx.put(F(A)), ctx.put(F(B)), ctx.put(F(C))
+    ctx.call("smg_gemm", ta, tb, 0, m, n, k, 1.5, dA, A.shape[0], dB, B.shape[0], -0.5, dC, m)
+    out = ctx.get(dC, m * n).reshape(n, m).T
+    scale = np.abs(A).max() * np.abs(B).max() * k + np.abs(C).max()
+    assert np.abs(out - ref).max() <= 1e-13 * scale
+
+
+@pytest.mark.parametrize("uplo", [1, 2])
+def test_gemm_triangle(ctx, uplo):
+    rng = np.random.default_rng(5)
+    n, k = 200, 77
+    A = rng.standard_normal((n, k))
+    C = rng.standard_normal((n, n))
+    ref = C - A @ A.T
+    dA, dC = ctx.put(F(A)), ctx.put(F(C))
+    ctx.call("smg_gemm", 0, 1, uplo, n, n, k, -1.0, dA, n, dA, n, 1.0, dC, n)
+    out = ctx.get(dC, n * n).reshape(n, n).T
+    mask = np.tril(np.ones((n, n), bool)) if uplo == 1 else np.triu(np.ones((n, n), bool))
+    assert np.abs(out[mask] - ref[mask]).max() < 1e-12
+    assert np.array_equal(out[~mask], C[~mask])  # other triangle untouched
+
+
+def test_mfma_layout_asymmetric(ctx):
+    """A = I with an asymmetric B catches a transposed D layout."""
+    n = 16
+    B = np.arange(n * n, dtype=np.float64).reshape(n, n)
+    I = np.eye(n)
+    dA, dB, dC = ctx.put(F(I)), ctx.put(F(B)), ctx.zeros(n * n)
+    ctx.call("smg_gemm", 0, 0, 0, n, n, n, 1.0, dA, n, dB, n, 0.0, dC, n)
+    out = ctx.get(dC, n * n).reshape(n, n).T
+    assert np.array_equal(out, B)
+
+
+# ------------------------------------------------------- gp_exp_quad_cov
+@pytest.mark.parametrize("n", [1, 2, 33, 300])
+def test_gp_cov(ctx, n):
+    x = gen.unif(11 + n, n, -10, 10)
+    K_ref = np.zeros(n * n)
+    oracle().oracle_gp_cov(ptr(x), n, 1.3, 0.7, ptr(K_ref))
+    dx, dK = ctx.put(x), ctx.zeros(n * n)
+    ctx.call("smg_gp_exp_quad_cov_fwd", dx, n, 1.3, 0.7, dK, n)
+    near_rel(ctx.get(dK, n * n), K_ref, 1e-14, atol=1e-300, what="K")
+    W = gen.unif(12 + n, n * n, -1, 1)
+    ga, gl = np.zeros(1), np.zeros(1)
+    oracle().oracle_gp_cov_rev(ptr(x), n, 1.3, 0.7, ptr(W), ptr(ga), ptr(gl))
+    dW, dout = ctx.put(W), ctx.zeros(2)
+    ctx.call("smg_gp_exp_quad_cov_rev", dx, n, 1.3, 0.7, dW, n, dout)
+    out = ctx.get(dout, 2)
+    near_rel(out, [ga[0], gl[0]], 1e-11, what="gp rev")
+
+
+# ------------------------------------------------------------- cholesky
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "cholesky_N*.json"))))
+def test_cholesky_golden(ctx, path):
+    d = golden(os.path.basename(path)[:-5])
+    N = int(d["N"])
+    nb = 64
+    dA, dL, dD = ctx.put(f64(d["A"])), ctx.zeros(N * N), ctx.zeros(N * nb)
+    ctx.call("smg_check_symmetric", dA, N, N)
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
+    assert ctx.status() == 0
+    near_rel(ctx.get(dL, N * N), d["L"], 1e-12, atol=1e-300, what="L")
+    W = d["W"].reshape(N, N).T
+    dLa, dAa = ctx.put(F(np.tril(W))), ctx.zeros(N * N)
+    ctx.call("smg_cholesky_rev", dL, N, dD, dLa, N, N, dAa, N)
+    g = ctx.get(dAa, N * N)
+    near_rel(g, d["grad_A"], RTOL, atol=RTOL * np.abs(d["grad_A"]).max(), what="grad_A")
+
+
+@pytest.mark.parametrize("N", [65, 300, 1000])
+def test_cholesky_vs_oracle(ctx, N):
+    rng = np.random.default_rng(N)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + np.eye(N)
+    A = 0.5 * (A + A.T)
+    Lref = np.zeros(N * N)
+    assert oracle().oracle_cholesky(ptr(F(A)), N, ptr(Lref)) == 0
+    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(N * 64)
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
+    L = ctx.get(dL, N * N)
+    near_rel(L, Lref, 1e-11, atol=1e-11 * np.abs(Lref).max(), what="L")
+    W = np.tril(rng.uniform(-1, 1, (N, N)))
+    Aref = np.zeros(N * N)
+    oracle().oracle_cholesky_rev(ptr(Lref), ptr(F(W)), N, ptr(Aref))
+    dLa, dAa = ctx.put(F(W)), ctx.zeros(N * N)
+    ctx.call("smg_cholesky_rev", dL, N, dD, dLa, N, N, dAa, N)
+    g = ctx.get(dAa, N * N)
+    near_rel(g, Aref, 1e-10, atol=1e-10 * np.abs(Aref).max(), what="grad_A")
+
+
+def test_cholesky_not_pd_and_not_symmetric(ctx):
+    N = 70
+    A = np.eye(N)
+    A[40, 40] = -1.0
+    dA, dL = ctx.put(F(A)), ctx.zeros(N * N)
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, ctx.zeros(N * 64))
+    assert ctx.status() & 2
+    A = np.eye(N)
+    A[5, 3] = 1e-7
+    dA = ctx.put(F(A))
+    ctx.call("smg_check_symmetric", dA, N, N)
+    assert ctx.status() & 4
+    A[5, 3] = 5e-9  # within CONSTRAINT_TOLERANCE
+    dA = ctx.put(F(A))
+    ctx.call("smg_check_symmetric", dA, N, N)
+    assert ctx.status() == 0
+
+
+# ------------------------------------------------------ mdivide_left_tri
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "mdivide_left_tri_*.json"))))
+def test_mdivide_golden(ctx, path):
+    d = golden(os.path.basename(path)[:-5])
+    m, n, lower, kind = (int(d[s]) for s in ("m", "n", "lower", "kind"))
+    dA, dB, dC = ctx.put(f64(d["A"])), ctx.put(f64(d["B"])), ctx.zeros(m * n)
+    ctx.call("smg_mdivide_left_tri_fwd", lower, dA, m, dB, m, m, n, dC, m)
+    near_rel(ctx.get(dC, m * n), d["C"], 1e-12, atol=1e-13, what="C")
+    dW, dAa, dBa, ws = ctx.put(f64(d["W"])), ctx.zeros(m * m), ctx.zeros(m * n), ctx.zeros(m * n)
+    ctx.call("smg_mdivide_left_tri_rev", lower, dA, m, dC, m, dW, m, m, n,
+             dAa if kind != 1 else None, m, dBa if kind != 2 else None, m, ws)
+    if kind != 1:
+        near_rel(ctx.get(dAa, m * m), d["grad_A"], RTOL, atol=1e-12, what="gA")
+    if kind != 2:
+        near_rel(ctx.get(dBa, m * n), d["grad_B"], RTOL, atol=1e-12, what="gB")
+
+
+def test_mdivide_large_vs_oracle(ctx):
+    m, n = 300, 7
+    rng = np.random.default_rng(3)
+    S = rng.uniform(-1, 1, (m, m))
+    S = S @ S.T / m + np.eye(m)
+    L = np.linalg.cholesky(S)
+    for lower, T in ((1, L), (0, L.T.copy())):
+        B = rng.uniform(-1, 1, (m, n))
+        Cref = np.zeros(m * n)
+        oracle().oracle_mdivide_left_tri(lower, ptr(F(T)), ptr(F(B)), m, n, ptr(Cref))
+        dA, dB, dC = ctx.put(F(T)), ctx.put(F(B)), ctx.zeros(m * n)
+        ctx.call("smg_mdivide_left_tri_fwd", lower, dA, m, dB, m, m, n, dC, m)
+        near_rel(ctx.get(dC, m * n), Cref, 1e-11, atol=1e-13, what="C")
+
+
+# ------------------------------------------------------------- multiply
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "multiply_*.json"))))
+def test_multiply_golden(ctx, path):
+    d = golden(os.path.basename(path)[:-5])
+    m, k, n, kind = (int(d[s]) for s in ("m", "k", "n", "kind"))
+    dA, dB, dC = ctx.put(f64(d["A"])), ctx.put(f64(d["B"])), ctx.zeros(m * n)
+    ctx.call("smg_multiply_fwd", dA, m, dB, k, m, k, n, dC, m)
+    near_rel(ctx.get(dC, m * n), d["C"], 1e-12, atol=1e-14, what="C")
+    dW, dAa, dBa = ctx.put(f64(d["W"])), ctx.zeros(m * k), ctx.zeros(k * n)
+    ctx.call("smg_multiply_rev", dA, m, dB, k, dW, m, m, k, n, dAa if kind != 2 else None, m,
+             dBa if kind != 1 else None, k)
+    if kind != 2:
+        near_rel(ctx.get(dAa, m * k), d["grad_A"], RTOL, atol=1e-13, what="gA")
+    if kind != 1:
+        near_rel(ctx.get(dBa, k * n), d["grad_B"], RTOL, atol=1e-13, what="gB")
+
+
+# ------------------------------------------------------------------ mvn
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "mvn_cholesky_N*.json"))))
+def test_mvn_golden(ctx, path):
+    d = golden(os.path.basename(path)[:-5])
+    N = int(d["N"])
+    dy, dmu, dL = ctx.put(f64(d["y"])), ctx.put(f64(d["mu"])), ctx.put(f64(d["L"]))
+    ws, dlp = ctx.zeros(2 * N), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd", dy, dmu, dL, N, None, N, ws, dlp)
+    near_rel(ctx.get(dlp, 1), [d["fx"]], 1e-12, what="lp")
+    gy, gm, gL = ctx.zeros(N), ctx.zeros(N), ctx.zeros(N * N)
+    ctx.call("smg_mvn_cholesky_rev", dL, N, None, N, ws, 1.0, 0, gy, gm, gL, N)
+    near_rel(ctx.get(gy, N), d["grad_y"], RTOL, what="gy")
+    near_rel(ctx.get(gm, N), d["grad_mu"], RTOL, what="gmu")
+    gref = d["grad_L"]
+    near_rel(ctx.get(gL, N * N), gref, RTOL, atol=RTOL * np.abs(gref).max(), what="gL")
+    # lower_only mode == the lower triangle of the full partials
+    gL2 = ctx.zeros(N * N)
+    ctx.call("smg_mvn_cholesky_rev", dL, N, None, N, ws, 1.0, 1, None, None, gL2, N)
+    low = np.tril(np.ones((N, N), bool)).ravel(order="F")
+    g2 = ctx.get(gL2, N * N)
+    near_rel(g2[low], gref[low], RTOL, atol=RTOL * np.abs(gref).max(), what="gL lower")
+    assert np.all(g2[~low] == 0.0)
+
+
+def test_mvn_known_answer(ctx):
+    d = golden("mvn_cholesky_known")
+    L = np.linalg.cholesky(d["Sigma"].reshape(3, 3))
+    dy, dmu, dL = ctx.put(f64(d["y"])), ctx.put(f64(d["mu"])), ctx.put(F(L))
+    ws, dlp = ctx.zeros(6), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd", dy, dmu, dL, 3, None, 3, ws, dlp)
+    assert abs(ctx.get(dlp, 1)[0] - d["expected"]) < 1e-5  # EXPECT_FLOAT_EQ
+
+
+# ------------------------------------------------- lse / special / normal
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_log_sum_exp(ctx, kind):
+    d = golden(f"log_sum_exp_{kind}")
+    x = f64(d["x"])
+    n = len(x)
+    dx, dout, dg = ctx.put(x), ctx.zeros(1), ctx.zeros(n)
+    ctx.call("smg_log_sum_exp_fwd", dx, n, dout)
+    lse = ctx.get(dout, 1)[0]
+    near_rel(lse, d["fx"], 1e-14, what="lse")
+    ctx.call("smg_log_sum_exp_rev", dx, n, lse, 1.0, dg)
+    near_rel(ctx.get(dg, n), d["grad"], 1e-12, atol=1e-15, what="grad")
+
+
+def test_log_sum_exp_edge(ctx):
+    dout = ctx.zeros(1)
+    ctx.call("smg_log_sum_exp_fwd", ctx.zeros(1), 0, dout)
+    assert ctx.get(dout, 1)[0] == -np.inf
+    x = np.array([1.0, np.inf, 3.0])
+    ctx.call("smg_log_sum_exp_fwd", ctx.put(x), 3, dout)
+    assert ctx.get(dout, 1)[0] == np.inf
+
+
+def test_special(ctx):
+    d = golden("special")
+    x = f64(d["x"])
+    n = len(x)
+    dx = ctx.put(x)
+    outs = {}
+    for f in ("lgamma", "digamma", "trigamma"):
+        dy = ctx.zeros(n)
+        ctx.call(f"smg_{f}_fwd", dx, n, dy)
+        outs[f] = ctx.get(dy, n)
+    # lgamma: ROCm libm vs glibc lgamma_r, both faithful: 1e-13 relative
+    # (absolute 1e-13 near the roots at 1 and 2)
+    near_rel(outs["lgamma"], d["lgamma"], 1e-13, atol=1e-13, what="lgamma")
+    near_rel(outs["digamma"], d["digamma"], 1e-13, atol=1e-13, what="digamma")
+    near_rel(outs["trigamma"], d["trigamma"], 1e-13, what="trigamma")
+    ones = ctx.put(np.ones(n))
+    g1, g2 = ctx.zeros(n), ctx.zeros(n)
+    ctx.call("smg_lgamma_rev", dx, n, ones, g1)
+    ctx.call("smg_digamma_rev", dx, n, ones, g2)
+    near_rel(ctx.get(g1, n), d["grad_lgamma"], 1e-13, atol=1e-13, what="dlgamma")
+    near_rel(ctx.get(g2, n), d["grad_digamma"], 1e-13, what="ddigamma")
+
+
+def test_normal(ctx):
+    d = golden("normal_N1024")
+    th = f64(d["theta"])
+    dth, d0, d1 = ctx.put(th), ctx.put(np.zeros(1)), ctx.put(np.ones(1))
+    out, gy = ctx.zeros(1), ctx.zeros(1024)
+    ctx.call("smg_normal_lpdf", dth, 1, d0, 0, d1, 0, 1024, 7, out, gy, None, None)
+    near_rel(ctx.get(out, 1), [d["fx"]], 1e-13, what="fx")
+    near_rel(ctx.get(gy, 1024), d["grad"], 1e-14, what="grad")
+    d = golden("normal_vec9")
+    dy, dm, ds = ctx.put(f64(d["y"])), ctx.put(f64(d["mu"])), ctx.put(f64(d["sigma"]))
+    out, gy, gm, gs = ctx.zeros(1), ctx.zeros(9), ctx.zeros(9), ctx.zeros(9)
+    ctx.call("smg_normal_lpdf", dy, 1, dm, 1, ds, 1, 9, 7, out, gy, gm, gs)
+    near_rel(ctx.get(out, 1), [d["fx"]], 1e-13, what="fx")
+    near_rel(ctx.get(gy, 9), d["grad_y"], 1e-13, what="gy")
+    near_rel(ctx.get(gm, 9), d["grad_mu"], 1e-13, what="gmu")
+    near_rel(ctx.get(gs, 9), d["grad_sigma"], 1e-13, what="gs")
+    out = ctx.zeros(1)  # propto: only sigma and quadratic terms (all operands var)
+    ctx.call("smg_normal_lpdf", dy, 1, dm, 1, ds, 1, 9, 6, out, None, None, None)
+    near_rel(ctx.get(out, 1), [d["fx_propto"]], 1e-13, what="fx propto")
+
+
+# --------------------------------------------------------------- GLM
+def _glm(ctx, x, y, th, R, M):
+    dx, dy, dab = ctx.put(F(x) if x.ndim == 2 else x), ctx.put(y.astype(np.int32)), ctx.put(f64(th))
+    ws = ctx.zeros(int(ctx.lib.smg_glm_ws_doubles(R, M)))
+    out = ctx.zeros(M + 2)
+    ctx.call("smg_bernoulli_logit_glm", dy, dx, R, M, R, dab, ws, out)
+    return ctx.get(out, M + 2)
+
+
+@pytest.mark.parametrize("name", ["glm_R1000_M8", "glm_R10000_M256", "glm_R100000_M256"])
+def test_glm_golden(ctx, name):
+    d = golden(name)
+    R, M = int(d["R"]), int(d["M"])
+    x, y, th = gen.glm_inputs(R, M)
+    out = _glm(ctx, x, y, th, R, M)
+    near_rel(out[0], d["fx"], 1e-12, what="fx")
+    near_rel(out[1:], d["grad"], RTOL, what="grad")
+
+
+def test_glm_extreme(ctx):
+    d = golden("glm_extreme")
+    R, M = int(d["R"]), int(d["M"])
+    x = f64(d["x"]).reshape(M, R).T
+    out = _glm(ctx, x, np.array(d["y"], dtype=np.int32), d["theta"], R, M)
+    near_rel(out[0], d["fx"], 1e-12, what="fx")
+    near_rel(out[1:], d["grad"], RTOL, what="grad")
+
+
+def test_glm_wide_fallback(ctx):
+    R, M = 3000, 300  # M > 256 takes the two-GEMV path
+    x = gen.unif(77, R * M, -1, 1).reshape(M, R).T
+    y = gen.bernoulli(78, R, 0.5)
+    th = np.concatenate([[0.2], gen.unif(79, M, -0.1, 0.1)])
+    ga, gb = np.zeros(1), np.zeros(M)
+    lp = oracle().oracle_glm(ptr(y), ptr(F(x)), R, M, th[0], ptr(f64(th[1:])), ptr(ga), ptr(gb))
+    out = _glm(ctx, x, y, th, R, M)
+    near_rel(out[0], lp, 1e-12, what="fx")
+    near_rel(out[1:], np.concatenate([ga, gb]), RTOL, what="grad")
+
+
+# ------------------------------------------- GP composed through the C-ABI
+def gp_gradient_abi(ctx, x, y, theta):
+    """The GP functor of BASELINE config 3 composed from the C-ABI calls in the
+    order the reverse sweep makes them (the C++ host layer does the same)."""
+    n = len(x)
+    a, r, s = theta
+    dx, dy = ctx.put(f64(x)), ctx.put(f64(y))
+    K, Kd, L, Dinv = ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * 64)
+    ws, lp = ctx.zeros(2 * n), ctx.zeros(1)
+    ctx.call("smg_gp_exp_quad_cov_fwd", dx, n, a, r, K, n)
+    ctx.call("smg_add_diag_fwd", K, n, n, s * s, None, Kd, n)
+    ctx.call("smg_check_symmetric", Kd, n, n)
+    ctx.call("smg_cholesky_fwd", Kd, n, n, L, n, Dinv)
+    ctx.call("smg_mvn_cholesky_fwd", dy, None, L, n, Dinv, n, ws, lp)
+    fx = ctx.get(lp, 1)[0]
+    La, Kda, Ka, sadj, hyp = ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(1), ctx.zeros(2)
+    ctx.call("smg_mvn_cholesky_rev", L, n, Dinv, n, ws, 1.0, 1, None, None, La, n)
+    ctx.call("smg_cholesky_rev", L, n, Dinv, La, n, n, Kda, n)
+    ctx.call("smg_add_diag_rev", Kda, n, n, Ka, n, sadj, 0)
+    ctx.call("smg_gp_exp_quad_cov_rev", dx, n, a, r, Ka, n, hyp)
+    h = ctx.get(hyp, 2)
+    sa = ctx.get(sadj, 1)[0]
+    return fx, np.array([h[0], h[1], sa * 2 * s])
+
+
+@pytest.mark.parametrize("N", [16, 64, 256, 1024, 4096])
+def test_gp_marginal_golden(ctx, N):
+    d = golden(f"gp_N{N}")
+    fx, g = gp_gradient_abi(ctx, d["x"], d["y"], d["theta"])
+    assert ctx.status() == 0
+    near_rel(fx, d["fx"], 1e-12, what="fx")
+    near_rel(g, d["grad"], RTOL, what="grad")
