@@ -87,6 +87,14 @@ enum smg_family {
 int smg_profile_enable(smg_ctx* ctx, int on);
 /* total milliseconds and number of timed regions per family since enable */
 int smg_profile_read(smg_ctx* ctx, int family, double* total_ms_host, long long* count_host);
+/* algorithmic flops issued per family since enable (GEMM: 2mnk per call) */
+int smg_profile_flops(smg_ctx* ctx, int family, double* flops_host);
+
+/* deterministic synthetic data on the device (SplitMix64, oracle/gen.h):
+ * out[i] = a + (b - a) * u_i  /  out[i] = (u_i < p) */
+int smg_fill_unif(smg_ctx* ctx, double* out, long long n, unsigned long long seed,
+                  double a, double b, double scale);
+int smg_fill_bernoulli(smg_ctx* ctx, int* out, long long n, unsigned long long seed, double p);
 
 /* --------------------------------------------------------------- BLAS-3 ---
  * C = alpha op(A) op(B) + beta C  (op = transpose when trans != 0), fp64 MFMA

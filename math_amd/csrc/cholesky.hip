@@ -31,7 +31,8 @@ __global__ void k_check_symmetric(const double* __restrict__ A, int lda, int n, 
        e += (long long)gridDim.x * blockDim.x) {
     const int j = (int)(e / n), i = (int)(e % n);
     if (i <= j) continue;
-    if (fabs(A[i + (size_t)j * lda] - A[j + (size_t)i * lda]) > 1e-8) bad = true;
+    // !(|d| <= tol) so that NaN entries fail too (check_symmetric.hpp:45-46)
+    if (!(fabs(A[i + (size_t)j * lda] - A[j + (size_t)i * lda]) <= 1e-8)) bad = true;
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
 }
@@ -62,11 +63,10 @@ __global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ L, int 
                                                     int* status) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
+  __shared__ double T[3 * 256];
   lds_load_block(D, L, ldl, b, true);
   __syncthreads();
-  lds_potrf_lower(D, b, status);
-  lds_tri_inverse_lower(D, X, b);
-  __syncthreads();
+  lds_potrf_inv64(D, X, T, status);
   lds_store_block(D, L, ldl, b, true);
   // Dinv block stored full (upper zeros) so GEMMs may read it as dense
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
@@ -80,9 +80,10 @@ __global__ __launch_bounds__(256) void k_trtri_diag(const double* __restrict__ L
                                                     int b, double* __restrict__ Dinv, int ldd) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
+  __shared__ double T[3 * 256];
   lds_load_block(D, L, ldl, b, true);
   __syncthreads();
-  lds_tri_inverse_lower(D, X, b);
+  lds_trtri64(D, X, T);
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
     const int c = e / b, r = e % b;
     Dinv[r + (size_t)c * ldd] = X[r * SMG_NBP + c];
@@ -96,45 +97,23 @@ __global__ __launch_bounds__(256) void k_symbolic_rev(const double* __restrict__
                                                       const double* __restrict__ Dinv, int ldd,
                                                       double* __restrict__ Dadj, int lda,
                                                       int b, double* __restrict__ Ssym) {
-  __shared__ double D[SMG_NB * SMG_NBP];   // D, later reused
+  __shared__ double D[SMG_NB * SMG_NBP];   // D, later Dinv
   __shared__ double G[SMG_NB * SMG_NBP];   // tril(Dadj), later temp
   __shared__ double S[SMG_NB * SMG_NBP];
-  lds_load_block(D, L, ldl, b, true);
-  lds_load_block(G, Dadj, lda, b, true);
+  // zero padding beyond b keeps every 64x64 product exact on the b x b block
+  lds_load_block0(D, L, ldl, b, true);
+  lds_load_block0(G, Dadj, lda, b, true);
   __syncthreads();
-  // S = D^T G : S(r,c) = sum_{t >= max(r,c)} D(t,r) G(t,c)
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int r = e / b, c = e % b;
-    double s = 0.0;
-    for (int t = max(r, c); t < b; ++t) s += D[t * SMG_NBP + r] * G[t * SMG_NBP + c];
-    S[r * SMG_NBP + c] = s;
-  }
-  __syncthreads();
+  lds_mma64<true, false>(S, D, G, 1.0, 0.0);  // S = D^T tril(Dadj)
   // mirror the lower triangle into the upper (:106-107)
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int r = e / b, c = e % b;
+  for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
+    const int r = e / SMG_NB, c = e % SMG_NB;
     if (r < c) S[r * SMG_NBP + c] = S[c * SMG_NBP + r];
   }
-  // D <- Dinv (lower)
+  lds_load_block0(D, Dinv, ldd, b, true);  // D <- Dinv (lower)
   __syncthreads();
-  lds_load_block(D, Dinv, ldd, b, true);
-  __syncthreads();
-  // G = Dinv^T S : G(r,c) = sum_{t >= r} Dinv(t,r) S(t,c)
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int r = e / b, c = e % b;
-    double s = 0.0;
-    for (int t = r; t < b; ++t) s += D[t * SMG_NBP + r] * S[t * SMG_NBP + c];
-    G[r * SMG_NBP + c] = s;
-  }
-  __syncthreads();
-  // S = G Dinv : S(r,c) = sum_{t >= c} G(r,t) Dinv(t,c)
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int r = e / b, c = e % b;
-    double s = 0.0;
-    for (int t = c; t < b; ++t) s += G[r * SMG_NBP + t] * D[t * SMG_NBP + c];
-    S[r * SMG_NBP + c] = s;
-  }
-  __syncthreads();
+  lds_mma64<true, false>(G, D, S, 1.0, 0.0);   // G = Dinv^T S
+  lds_mma64<false, false>(S, G, D, 1.0, 0.0);  // S = G Dinv
   // outputs: selfadjointView<Lower> of S, and tril(S) with halved diagonal (:160-161)
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
     const int c = e / b, r = e % b;

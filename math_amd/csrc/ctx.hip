@@ -111,6 +111,7 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
     ctx->prof_ms[i] = 0;
     ctx->prof_count[i] = 0;
+    ctx->prof_flops[i] = 0;
   }
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
@@ -291,6 +292,7 @@ int smg_profile_enable(smg_ctx* ctx, int on) {
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
     ctx->prof_ms[i] = 0;
     ctx->prof_count[i] = 0;
+    ctx->prof_flops[i] = 0;
   }
   return SMG_OK;
 }
@@ -304,4 +306,52 @@ int smg_profile_read(smg_ctx* ctx, int family, double* ms, long long* count) {
   return SMG_OK;
 }
 
+int smg_profile_flops(smg_ctx* ctx, int family, double* flops) {
+  if (!ctx || family < 0 || family >= SMG_FAM_COUNT || !flops) return SMG_ERR_ARG;
+  *flops = ctx->prof_flops[family];
+  return SMG_OK;
+}
+
 }  // extern "C"
+
+namespace {
+__device__ __forceinline__ unsigned long long splitmix(unsigned long long seed, long long i) {
+  unsigned long long z = seed + (unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+__global__ void k_fill_unif(double* out, long long n, unsigned long long seed, double a, double b,
+                            double scale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const double u = (double)(splitmix(seed, i) >> 11) * (1.0 / 9007199254740992.0);
+    const double v = __dadd_rn(a, __dmul_rn(b - a, u));  // no contraction: matches oracle/gen.h
+    out[i] = scale == 1.0 ? v : __dmul_rn(v, scale);
+  }
+}
+__global__ void k_fill_bern(int* out, long long n, unsigned long long seed, double p) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const double u = (double)(splitmix(seed, i) >> 11) * (1.0 / 9007199254740992.0);
+    out[i] = u < p ? 1 : 0;
+  }
+}
+}  // namespace
+
+extern "C" int smg_fill_unif(smg_ctx* ctx, double* out, long long n, unsigned long long seed,
+                             double a, double b, double scale) {
+  if (!ctx || n < 0 || (n > 0 && !out)) return SMG_ERR_ARG;
+  if (!n) return SMG_OK;
+  hipLaunchKernelGGL(k_fill_unif, dim3(8192), dim3(256), 0, ctx->stream, out, n, seed, a, b, scale);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+extern "C" int smg_fill_bernoulli(smg_ctx* ctx, int* out, long long n, unsigned long long seed,
+                                  double p) {
+  if (!ctx || n < 0 || (n > 0 && !out)) return SMG_ERR_ARG;
+  if (!n) return SMG_OK;
+  hipLaunchKernelGGL(k_fill_bern, dim3(8192), dim3(256), 0, ctx->stream, out, n, seed, p);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}

@@ -254,6 +254,8 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
     return smg_scale_impl(ctx, m, n, beta, C, ldc, uplo);
   }
   smg_prof_scope prof(ctx, SMG_FAM_GEMM);
+  if (ctx->prof_on)
+    ctx->prof_flops[SMG_FAM_GEMM] += uplo ? (double)k * m * (m + 1) : 2.0 * m * n * k;
   if (uplo == 1) {
     if (m != n) return SMG_ERR_ARG;
     if (!ta && tb) return dispatch_tile<false, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);

@@ -43,6 +43,7 @@ struct smg_ctx {
   std::vector<smg_prof_slot> prof_pending;
   std::vector<hipEvent_t> prof_pool;
   double prof_ms[SMG_FAM_COUNT];
+  double prof_flops[SMG_FAM_COUNT];
   long long prof_count[SMG_FAM_COUNT];
   // RCCL communicator (opaque)
   void* comm;

@@ -17,17 +17,18 @@ __global__ __launch_bounds__(256) void k_trtri_blocks(const double* __restrict__
                                                       int m, int upper, double* __restrict__ W) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
+  __shared__ double T[3 * 256];
   const int j = blockIdx.x * SMG_NB;
   const int b = min(SMG_NB, m - j);
   const double* Ab = A + j + (size_t)j * lda;
   for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
     const int c = e / SMG_NB, r = e % SMG_NB;
-    double v = 0.0;
-    if (r < b && c < b && r >= c) v = upper ? Ab[c + (size_t)r * lda] : Ab[r + (size_t)c * lda];
+    double v = (r == c) ? 1.0 : 0.0;  // identity padding beyond b
+    if (r < b && c < b) v = r >= c ? (upper ? Ab[c + (size_t)r * lda] : Ab[r + (size_t)c * lda]) : 0.0;
     D[r * SMG_NBP + c] = v;
   }
   __syncthreads();
-  lds_tri_inverse_lower(D, X, b);
+  lds_trtri64(D, X, T);
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
     const int c = e / b, r = e % b;
     W[j + r + (size_t)c * m] = X[r * SMG_NBP + c];

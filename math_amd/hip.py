@@ -43,6 +43,9 @@ _SIGS = {
     "smg_status": (_I, [_P, ctypes.POINTER(_I)]),
     "smg_profile_enable": (_I, [_P, _I]),
     "smg_profile_read": (_I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
+    "smg_profile_flops": (_I, [_P, _I, ctypes.POINTER(_D)]),
+    "smg_fill_unif": (_I, [_P, _P, _L, ctypes.c_ulonglong, _D, _D, _D]),
+    "smg_fill_bernoulli": (_I, [_P, _P, _L, ctypes.c_ulonglong, _D]),
     "smg_gemm": (_I, [_P, _I, _I, _I, _I, _I, _I, _D, _P, _I, _P, _I, _D, _P, _I]),
     "smg_gp_exp_quad_cov_fwd": (_I, [_P, _P, _I, _D, _D, _P, _I]),
     "smg_gp_exp_quad_cov_rev": (_I, [_P, _P, _I, _D, _D, _P, _I, _P]),
@@ -189,7 +192,14 @@ class Context:
         check(self.lib.smg_profile_enable(self.ptr, 1 if on else 0), "profile")
 
     def profile_read(self, family):
-        ms = _D(0)
-        cnt = _L(0)
-        check(self.lib.smg_profile_read(self.ptr, FAMILIES[family], ctypes.byref(ms), ctypes.byref(cnt)), "profile_read")
-        return ms.value, cnt.value
+        return profile_read(self.lib, self.ptr, family)
+
+
+def profile_read(lib_, ctx_ptr, family):
+    """(total ms, regions, algorithmic flops) of a kernel family on a context."""
+    ms = _D(0)
+    cnt = _L(0)
+    fl = _D(0)
+    check(lib_.smg_profile_read(ctx_ptr, FAMILIES[family], ctypes.byref(ms), ctypes.byref(cnt)), "profile_read")
+    check(lib_.smg_profile_flops(ctx_ptr, FAMILIES[family], ctypes.byref(fl)), "profile_flops")
+    return ms.value, cnt.value, fl.value

@@ -1,0 +1,18 @@
+#ifndef STAN_MATH_HPP
+#define STAN_MATH_HPP
+
+// Public entry point, mirroring the reference's `#include <stan/math.hpp>`
+// (stan/math.hpp:148).  Header-only host layer over libsmg_hip.so; needs
+// Eigen on the include path and -lsmg_hip at link time.
+#include <Eigen/Dense>
+#define STAN_MATH_AMD_HAS_EIGEN 1
+
+#include <stan/math/rev/core.hpp>
+#include <stan/math/amd/matrix.hpp>
+#include <stan/math/rev/fun/gp_exp_quad_cov.hpp>
+#include <stan/math/rev/fun/cholesky_decompose.hpp>
+#include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
+#include <stan/math/rev/functor/gradient.hpp>
+#include <stan/math/eigen/interop.hpp>
+
+#endif

@@ -1,0 +1,162 @@
+#ifndef STAN_MATH_AMD_DEVICE_HPP
+#define STAN_MATH_AMD_DEVICE_HPP
+
+// Per-thread device context: the MI355X side of the autodiff tape.
+//
+// The reference keeps one tape per thread (rev/core/autodiffstackstorage.hpp:
+// 11-25, 88-143).  Every tape here owns, lazily, one smg_ctx from the C-ABI
+// (include/smg_hip.h): a HIP stream and a device bump arena that start_nested
+// / recover_memory(_nested) mark and rewind exactly like the host arena.
+// Device selection: set_device(d) before the first device op, else the
+// environment variable SMG_DEVICE, else 0.
+//
+// Error mapping: C-ABI status bits become the reference's exceptions
+// (std::domain_error for domain checks, prim/scal/err/domain_error.hpp:28-33;
+// std::invalid_argument for size mismatches; std::bad_alloc for OOM;
+// std::runtime_error for HIP failures).
+
+#include <smg_hip.h>
+
+#include <cstdlib>
+#include <new>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+
+namespace stan {
+namespace math {
+namespace amd {
+
+struct device_state {
+  smg_ctx* ctx = nullptr;
+  int device = -1;
+  ~device_state() {
+    if (ctx) smg_ctx_destroy(ctx);
+  }
+};
+
+inline device_state& state() {
+  static thread_local device_state s;
+  return s;
+}
+
+inline int default_device() {
+  const char* e = std::getenv("SMG_DEVICE");
+  return e ? std::atoi(e) : 0;
+}
+
+/** Select the device for this thread's tape (before its first device op). */
+inline void set_device(int d) {
+  device_state& s = state();
+  if (s.ctx && s.device != d)
+    throw std::logic_error("stan::math::amd::set_device: context already created");
+  s.device = d;
+}
+
+inline void throw_status(int st, const char* function, const char* what = "") {
+  if (st == SMG_OK) return;
+  std::ostringstream m;
+  m << function << ": ";
+  if (st & SMG_ERR_NOT_PD) {
+    m << "Matrix " << what << " is not positive definite";
+    throw std::domain_error(m.str());
+  }
+  if (st & SMG_ERR_NOT_SYMMETRIC) {
+    m << what << " is not symmetric";
+    throw std::domain_error(m.str());
+  }
+  if (st & SMG_ERR_NOT_POSITIVE) {
+    m << what << " is not positive";
+    throw std::domain_error(m.str());
+  }
+  if (st & SMG_ERR_NONFINITE) {
+    m << what << " is not finite";
+    throw std::domain_error(m.str());
+  }
+  if (st & SMG_ERR_OOM) throw std::bad_alloc();
+  if (st & SMG_ERR_ARG) {
+    m << "invalid argument " << what;
+    throw std::invalid_argument(m.str());
+  }
+  m << "HIP runtime failure (status " << st << ")";
+  throw std::runtime_error(m.str());
+}
+
+/** This thread's device context (created on first use). */
+inline smg_ctx* ctx() {
+  device_state& s = state();
+  if (__builtin_expect(s.ctx == nullptr, 0)) {
+    if (s.device < 0) s.device = default_device();
+    smg_ctx* c = nullptr;
+    const int rc = smg_ctx_create(s.device, size_t(256) << 20, &c);
+    if (rc != SMG_OK) throw_status(rc, "stan::math::amd::ctx", "(device context)");
+    s.ctx = c;
+  }
+  return s.ctx;
+}
+
+inline bool has_ctx() { return state().ctx != nullptr; }
+
+/** Check a C-ABI return code. */
+inline void check(int rc, const char* function, const char* what = "") {
+  if (__builtin_expect(rc != SMG_OK, 0)) throw_status(rc, function, what);
+}
+
+/** Synchronise and translate latched device-side domain errors. */
+inline void check_status(const char* function, const char* what = "") {
+  int st = 0;
+  check(smg_status(ctx(), &st), function);
+  throw_status(st, function, what);
+}
+
+/** Device arena allocation (recovered with the tape). */
+inline double* alloc_doubles(size_t n) {
+  void* p = smg_arena_alloc(ctx(), (n ? n : 1) * sizeof(double));
+  if (!p) throw std::bad_alloc();
+  return static_cast<double*>(p);
+}
+inline int* alloc_ints(size_t n) {
+  void* p = smg_arena_alloc(ctx(), (n ? n : 1) * sizeof(int));
+  if (!p) throw std::bad_alloc();
+  return static_cast<int*>(p);
+}
+
+/** Blocking host -> device copy of a host buffer (safe for pageable memory). */
+inline void to_device(double* dst, const double* src, size_t n) {
+  if (!n) return;
+  smg_ctx* c = ctx();
+  void* stage = smg_host_scratch(c, n * sizeof(double));
+  if (!stage) throw std::bad_alloc();
+  __builtin_memcpy(stage, src, n * sizeof(double));
+  check(smg_memcpy_h2d(c, dst, stage, n * sizeof(double)), "to_device");
+  check(smg_sync(c), "to_device");
+}
+inline void to_device_int(int* dst, const int* src, size_t n) {
+  if (!n) return;
+  smg_ctx* c = ctx();
+  void* stage = smg_host_scratch(c, n * sizeof(int));
+  if (!stage) throw std::bad_alloc();
+  __builtin_memcpy(stage, src, n * sizeof(int));
+  check(smg_memcpy_h2d(c, dst, stage, n * sizeof(int)), "to_device");
+  check(smg_sync(c), "to_device");
+}
+
+/** Blocking device -> host copy. */
+inline void to_host(double* dst, const double* src, size_t n) {
+  if (!n) return;
+  smg_ctx* c = ctx();
+  void* stage = smg_host_scratch(c, n * sizeof(double));
+  if (!stage) throw std::bad_alloc();
+  check(smg_memcpy_d2h(c, stage, src, n * sizeof(double)), "to_host");
+  check(smg_sync(c), "to_host");
+  __builtin_memcpy(dst, stage, n * sizeof(double));
+}
+
+inline void zero(double* p, size_t n) {
+  if (n) check(smg_memset(ctx(), p, 0, n * sizeof(double)), "zero");
+}
+
+}  // namespace amd
+}  // namespace math
+}  // namespace stan
+#endif

@@ -1,0 +1,97 @@
+#ifndef STAN_MATH_REV_CORE_AUTODIFFSTACKSTORAGE_HPP
+#define STAN_MATH_REV_CORE_AUTODIFFSTACKSTORAGE_HPP
+
+// The per-thread autodiff tape.
+//
+// Same members and nesting semantics as the reference's AutodiffStackSingleton
+// (stan/math/rev/core/autodiffstackstorage.hpp:88-143): var_stack_ (varis
+// whose chain() runs in the reverse sweep), var_nochain_stack_ (varis that
+// only hold values/adjoints), var_alloc_stack_ (arena objects with
+// destructors), the host arena memalloc_, and the nested size stacks.
+// The tape is always thread-local here (the reference makes it thread-local
+// under STAN_THREADS).
+//
+// MI355X extension: matrix-valued nodes keep their values and adjoints in the
+// thread's device arena (stan/math/amd/device.hpp).  The tape therefore also
+// records
+//   dev_adj_stack_      device adjoint buffers (zeroed by set_zero_all_adjoints)
+//   nested_dev_marks_   device-arena marks per nesting level
+//   pending_            device -> host adjoint contributions that must land in
+//                       host vari::adj_ before the next host chain() runs.
+
+#include <stan/math/memory/stack_alloc.hpp>
+
+#include <cstddef>
+#include <vector>
+
+namespace stan {
+namespace math {
+
+class vari;
+class chainable_alloc;
+
+struct dev_buffer {
+  double* ptr;
+  size_t n;
+};
+struct pending_adjoint {
+  vari* target;       // host vari whose adj_ receives the value
+  const double* src;  // device scalar
+};
+
+template <typename ChainableT, typename ChainableAllocT>
+struct AutodiffStackSingleton {
+  using AutodiffStackSingleton_t = AutodiffStackSingleton<ChainableT, ChainableAllocT>;
+
+  struct AutodiffStackStorage {
+    AutodiffStackStorage& operator=(const AutodiffStackStorage&) = delete;
+
+    std::vector<ChainableT*> var_stack_;
+    std::vector<ChainableT*> var_nochain_stack_;
+    std::vector<ChainableAllocT*> var_alloc_stack_;
+    stack_alloc memalloc_;
+
+    std::vector<size_t> nested_var_stack_sizes_;
+    std::vector<size_t> nested_var_nochain_stack_sizes_;
+    std::vector<size_t> nested_var_alloc_stack_starts_;
+
+    // device side
+    std::vector<dev_buffer> dev_adj_stack_;
+    std::vector<size_t> nested_dev_adj_sizes_;
+    std::vector<size_t> nested_dev_marks_;
+    std::vector<pending_adjoint> pending_;
+  };
+
+  AutodiffStackSingleton() : own_instance_(init()) {}
+  ~AutodiffStackSingleton() {
+    if (own_instance_) {
+      delete instance_;
+      instance_ = nullptr;
+    }
+  }
+  AutodiffStackSingleton(const AutodiffStackSingleton_t&) = delete;
+  AutodiffStackSingleton& operator=(const AutodiffStackSingleton_t&) = delete;
+
+  static inline thread_local AutodiffStackStorage* instance_ = nullptr;
+
+ private:
+  static bool init() {
+    if (!instance_) {
+      instance_ = new AutodiffStackStorage();
+      return true;
+    }
+    return false;
+  }
+  bool own_instance_;
+};
+
+using ChainableStack = AutodiffStackSingleton<vari, chainable_alloc>;
+
+// The main thread's tape (the reference instantiates it in
+// rev/core/init_chainablestack.hpp); other threads construct a
+// ChainableStack object before touching the AD system.
+inline ChainableStack main_thread_tape_owner_;
+
+}  // namespace math
+}  // namespace stan
+#endif

@@ -1,0 +1,157 @@
+#ifndef STAN_MATH_REV_CORE_GRAD_HPP
+#define STAN_MATH_REV_CORE_GRAD_HPP
+
+// Reverse sweep and tape management.
+//   grad                     rev/core/grad.hpp:30-46
+//   start_nested             rev/core/start_nested.hpp:13
+//   recover_memory(_nested)  rev/core/recover_memory.hpp:18-31,
+//                            rev/core/recover_memory_nested.hpp:20-45
+//   set_zero_all_adjoints(_nested)  rev/core/set_zero_all_adjoints*.hpp
+//   empty_nested / nested_size
+// Device extension: the same calls mark / rewind the device arena, zero the
+// device adjoint buffers, and land pending device->host adjoint
+// contributions (flush_pending) before any host chain() that could read them.
+
+#include <stan/math/amd/device.hpp>
+#include <stan/math/rev/core/vari.hpp>
+
+#include <cstdint>
+#include <stdexcept>
+#include <vector>
+
+namespace stan {
+namespace math {
+
+/** Register a device adjoint buffer with the tape (zeroed now and by
+ * set_zero_all_adjoints). */
+inline void register_device_adjoint(double* p, size_t n) {
+  amd::zero(p, n);
+  ChainableStack::instance_->dev_adj_stack_.push_back({p, n});
+}
+
+/** Queue target->adj_ += *src (src: device scalar) for the next flush. */
+inline void add_pending_adjoint(vari* target, const double* src) {
+  ChainableStack::instance_->pending_.push_back({target, src});
+}
+
+/** Land every queued device->host adjoint contribution (one sync). */
+inline void flush_pending() {
+  auto& pend = ChainableStack::instance_->pending_;
+  if (pend.empty()) return;
+  smg_ctx* c = amd::ctx();
+  double* stage = static_cast<double*>(smg_host_scratch(c, pend.size() * sizeof(double)));
+  if (!stage) throw std::bad_alloc();
+  for (size_t i = 0; i < pend.size(); ++i)
+    amd::check(smg_memcpy_d2h(c, stage + i, pend[i].src, sizeof(double)), "flush_pending");
+  amd::check(smg_sync(c), "flush_pending");
+  for (size_t i = 0; i < pend.size(); ++i) pend[i].target->adj_ += stage[i];
+  pend.clear();
+}
+
+static inline bool empty_nested() {
+  return ChainableStack::instance_->nested_var_stack_sizes_.empty();
+}
+
+static inline size_t nested_size() {
+  return ChainableStack::instance_->var_stack_.size()
+         - ChainableStack::instance_->nested_var_stack_sizes_.back();
+}
+
+/**
+ * Reverse sweep from vi: adj(vi) = 1, then chain() over var_stack_ in reverse
+ * (only the innermost nested window when nested).  Device nodes enqueue their
+ * adjoint kernels on the thread's stream; host nodes run inline.
+ */
+static void grad(vari* vi) {
+  using it_t = std::vector<vari*>::reverse_iterator;
+  auto* st = ChainableStack::instance_;
+  vi->init_dependent();
+  it_t begin = st->var_stack_.rbegin();
+  it_t end = empty_nested() ? st->var_stack_.rend() : begin + nested_size();
+  for (it_t it = begin; it < end; ++it) {
+    if (__builtin_expect(!st->pending_.empty(), 0)) flush_pending();
+    (*it)->chain();
+  }
+  flush_pending();
+}
+
+static inline void start_nested() {
+  auto* st = ChainableStack::instance_;
+  st->nested_var_stack_sizes_.push_back(st->var_stack_.size());
+  st->nested_var_nochain_stack_sizes_.push_back(st->var_nochain_stack_.size());
+  st->nested_var_alloc_stack_starts_.push_back(st->var_alloc_stack_.size());
+  st->nested_dev_adj_sizes_.push_back(st->dev_adj_stack_.size());
+  st->nested_dev_marks_.push_back(amd::has_ctx() ? smg_arena_mark(amd::ctx()) : SIZE_MAX);
+  st->memalloc_.start_nested();
+}
+
+static inline void recover_memory_nested() {
+  if (empty_nested())
+    throw std::logic_error("empty_nested() must be false before calling recover_memory_nested()");
+  auto* st = ChainableStack::instance_;
+  st->var_stack_.resize(st->nested_var_stack_sizes_.back());
+  st->nested_var_stack_sizes_.pop_back();
+  st->var_nochain_stack_.resize(st->nested_var_nochain_stack_sizes_.back());
+  st->nested_var_nochain_stack_sizes_.pop_back();
+  for (size_t i = st->nested_var_alloc_stack_starts_.back(); i < st->var_alloc_stack_.size(); ++i)
+    delete st->var_alloc_stack_[i];
+  st->var_alloc_stack_.resize(st->nested_var_alloc_stack_starts_.back());
+  st->nested_var_alloc_stack_starts_.pop_back();
+  st->dev_adj_stack_.resize(st->nested_dev_adj_sizes_.back());
+  st->nested_dev_adj_sizes_.pop_back();
+  const size_t mark = st->nested_dev_marks_.back();
+  st->nested_dev_marks_.pop_back();
+  st->pending_.clear();
+  if (amd::has_ctx()) {
+    if (mark == SIZE_MAX)
+      smg_arena_recover_all(amd::ctx());
+    else
+      smg_arena_rewind(amd::ctx(), mark);
+  }
+  st->memalloc_.recover_nested();
+}
+
+static inline void recover_memory() {
+  if (!empty_nested())
+    throw std::logic_error("empty_nested() must be true before calling recover_memory()");
+  auto* st = ChainableStack::instance_;
+  st->var_stack_.clear();
+  st->var_nochain_stack_.clear();
+  for (auto* a : st->var_alloc_stack_) delete a;
+  st->var_alloc_stack_.clear();
+  st->dev_adj_stack_.clear();
+  st->pending_.clear();
+  if (amd::has_ctx()) smg_arena_recover_all(amd::ctx());
+  st->memalloc_.recover_all();
+}
+
+static inline void set_zero_all_adjoints() {
+  auto* st = ChainableStack::instance_;
+  for (auto* v : st->var_stack_) v->set_zero_adjoint();
+  for (auto* v : st->var_nochain_stack_) v->set_zero_adjoint();
+  for (auto& b : st->dev_adj_stack_) amd::zero(b.ptr, b.n);
+  st->pending_.clear();
+}
+
+static inline void set_zero_all_adjoints_nested() {
+  if (empty_nested())
+    throw std::logic_error(
+        "empty_nested() must be false before calling set_zero_all_adjoints_nested()");
+  auto* st = ChainableStack::instance_;
+  const size_t s1 = st->nested_var_stack_sizes_.back();
+  for (size_t i = (s1 == 0U) ? 0U : (s1 - 1); i < st->var_stack_.size(); ++i)
+    st->var_stack_[i]->set_zero_adjoint();
+  const size_t s2 = st->nested_var_nochain_stack_sizes_.back();
+  for (size_t i = (s2 == 0U) ? 0U : (s2 - 1); i < st->var_nochain_stack_.size(); ++i)
+    st->var_nochain_stack_[i]->set_zero_adjoint();
+  for (size_t i = st->nested_dev_adj_sizes_.back(); i < st->dev_adj_stack_.size(); ++i)
+    amd::zero(st->dev_adj_stack_[i].ptr, st->dev_adj_stack_[i].n);
+  st->pending_.clear();
+}
+
+/** Free every arena block but the first (reference: recover_memory + free_all). */
+static inline void free_memory() { ChainableStack::instance_->memalloc_.free_all(); }
+
+}  // namespace math
+}  // namespace stan
+#endif

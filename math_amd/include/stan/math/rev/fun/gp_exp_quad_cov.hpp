@@ -1,0 +1,109 @@
+#ifndef STAN_MATH_REV_FUN_GP_EXP_QUAD_COV_HPP
+#define STAN_MATH_REV_FUN_GP_EXP_QUAD_COV_HPP
+
+// gp_exp_quad_cov(x, sigma, length_scale) for scalar inputs x.
+// Reference: rev/mat/fun/gp_exp_quad_cov.hpp:32-286.  Same checks
+// (check_positive sigma / length_scale, check_not_nan x, :216-221), same
+// value K_ij = sigma^2 exp(-(x_i - x_j)^2 / (2 l^2)) and adjoint
+//   l' += sum_lower Kadj K d^2 / l^3,  sigma' += 2 (sum_lower Kadj K + sum_diag Kadj K) / sigma
+// (:96-112), with the whole matrix on the device (kernels: smg_gp_exp_quad_cov_*).
+
+#include <stan/math/amd/matrix.hpp>
+#include <stan/math/rev/core.hpp>
+
+#include <cmath>
+#include <sstream>
+#include <stdexcept>
+#include <vector>
+
+namespace stan {
+namespace math {
+
+namespace internal {
+inline void gp_check_positive(const char* fn, const char* name, double v) {
+  if (!(v > 0)) {
+    std::ostringstream m;
+    m << fn << ": " << name << " is " << v << ", but must be > 0!";
+    throw std::domain_error(m.str());
+  }
+}
+
+class gp_exp_quad_cov_dev_vari : public vari {
+ public:
+  const double* x_;
+  const int n_;
+  const double sigma_d_, l_d_;
+  vari* sigma_vi_;  // null when sigma is data
+  vari* l_vi_;      // null when l is data
+  dev_matrix_vari* K_;
+  double* out2_;
+
+  gp_exp_quad_cov_dev_vari(const double* x, int n, double sigma, vari* sigma_vi, double l,
+                           vari* l_vi)
+      : vari(0.0),
+        x_(x),
+        n_(n),
+        sigma_d_(sigma),
+        l_d_(l),
+        sigma_vi_(sigma_vi),
+        l_vi_(l_vi),
+        K_(new dev_matrix_vari(n, n)),
+        out2_(amd::alloc_doubles(2)) {
+    amd::check(smg_gp_exp_quad_cov_fwd(amd::ctx(), x_, n_, sigma_d_, l_d_, K_->val_, n_),
+               "gp_exp_quad_cov");
+  }
+
+  void chain() override {
+    smg_ctx* c = amd::ctx();
+    amd::check(smg_memset(c, out2_, 0, 2 * sizeof(double)), "gp_exp_quad_cov");
+    amd::check(smg_gp_exp_quad_cov_rev(c, x_, n_, sigma_d_, l_d_, K_->adj_, n_, out2_),
+               "gp_exp_quad_cov");
+    if (sigma_vi_) add_pending_adjoint(sigma_vi_, out2_);
+    if (l_vi_) add_pending_adjoint(l_vi_, out2_ + 1);
+  }
+};
+
+inline dev_var_matrix gp_exp_quad_cov_dev(const dev_data<double>& x, double sigma,
+                                          vari* sigma_vi, double l, vari* l_vi) {
+  const char* fn = "gp_exp_quad_cov";
+  gp_check_positive(fn, sigma_vi ? "sigma" : "marginal variance", sigma);
+  gp_check_positive(fn, l_vi ? "length_scale" : "length-scale", l);
+  auto* node = new gp_exp_quad_cov_dev_vari(x.data(), int(x.size()), sigma, sigma_vi, l, l_vi);
+  return dev_var_matrix(node->K_);
+}
+
+inline dev_data<double> gp_x_to_device(const std::vector<double>& x) {
+  for (size_t i = 0; i < x.size(); ++i)
+    if (std::isnan(x[i])) {
+      std::ostringstream m;
+      m << "gp_exp_quad_cov: x[" << i + 1 << "] is nan, but must not be nan!";
+      throw std::domain_error(m.str());
+    }
+  return to_dev_data(x);
+}
+}  // namespace internal
+
+inline dev_var_matrix gp_exp_quad_cov(const std::vector<double>& x, const var& sigma,
+                                      const var& length_scale) {
+  return internal::gp_exp_quad_cov_dev(internal::gp_x_to_device(x), sigma.val(), sigma.vi_,
+                                       length_scale.val(), length_scale.vi_);
+}
+inline dev_var_matrix gp_exp_quad_cov(const std::vector<double>& x, double sigma,
+                                      const var& length_scale) {
+  return internal::gp_exp_quad_cov_dev(internal::gp_x_to_device(x), sigma, nullptr,
+                                       length_scale.val(), length_scale.vi_);
+}
+/** Device-resident x (kept across gradient evaluations by the caller). */
+inline dev_var_matrix gp_exp_quad_cov(const dev_data<double>& x, const var& sigma,
+                                      const var& length_scale) {
+  return internal::gp_exp_quad_cov_dev(x, sigma.val(), sigma.vi_, length_scale.val(),
+                                       length_scale.vi_);
+}
+inline dev_var_matrix gp_exp_quad_cov(const dev_data<double>& x, double sigma,
+                                      const var& length_scale) {
+  return internal::gp_exp_quad_cov_dev(x, sigma, nullptr, length_scale.val(), length_scale.vi_);
+}
+
+}  // namespace math
+}  // namespace stan
+#endif

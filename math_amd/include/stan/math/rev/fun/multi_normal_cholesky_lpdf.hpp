@@ -1,0 +1,115 @@
+#ifndef STAN_MATH_REV_FUN_MULTI_NORMAL_CHOLESKY_LPDF_HPP
+#define STAN_MATH_REV_FUN_MULTI_NORMAL_CHOLESKY_LPDF_HPP
+
+// multi_normal_cholesky_lpdf<propto>(y | mu, L) with a device Cholesky factor.
+// Reference: prim/mat/prob/multi_normal_cholesky_lpdf.hpp:40-160 (single
+// vector y).  Value: -n log(sqrt(2 pi)) - |L^{-1}(y-mu)|^2/2 - sum log L_ii;
+// partials for L: sd half^T - inv_L^T (:147,155) applied by chain() on the
+// device; when L is a cholesky_decompose output (structurally lower) the
+// upper-triangle partials land on the reference's dummy vari and are skipped,
+// which removes the explicit O(n^3) inverse (see math_amd/csrc/mvn.hip).
+// y and mu are data here (double); y or mu as vars go through the host path.
+// With L a var, propto = true drops only the constant NEG_LOG_SQRT_TWO_PI
+// term (include_summand<propto>, :107-109).
+
+#include <stan/math/amd/matrix.hpp>
+#include <stan/math/rev/core.hpp>
+
+#include <cmath>
+#include <sstream>
+#include <stdexcept>
+#include <vector>
+
+namespace stan {
+namespace math {
+
+namespace internal {
+
+class mvn_cholesky_dev_vari : public vari {
+ public:
+  dev_matrix_vari* L_;
+  const double* ws_;  // [w, sd] on device
+  int n_;
+
+  mvn_cholesky_dev_vari(double lp, dev_matrix_vari* L, const double* ws)
+      : vari(lp), L_(L), ws_(ws), n_(L->rows_) {}
+
+  void chain() override {
+    const int lower_only = L_->structure_ == dev_structure::lower ? 1 : 0;
+    amd::check(smg_mvn_cholesky_rev(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, adj_, lower_only,
+                                    nullptr, nullptr, L_->adj_, n_),
+               "multi_normal_cholesky_lpdf");
+  }
+};
+
+inline void mvn_check_sizes(int ny, int nmu, const dev_var_matrix& L) {
+  const char* fn = "multi_normal_cholesky_lpdf";
+  auto mismatch = [&](const char* a, int x, const char* b, int y) {
+    std::ostringstream m;
+    m << fn << ": " << a << " (" << x << ") and " << b << " (" << y << ") must match in size";
+    throw std::invalid_argument(m.str());
+  };
+  if (ny != nmu) mismatch("Size of random variable", ny, "size of location parameter", nmu);
+  if (ny != L.rows()) mismatch("Size of random variable", ny, "rows of covariance parameter", L.rows());
+  if (ny != L.cols()) mismatch("Size of random variable", ny, "columns of covariance parameter", L.cols());
+}
+
+template <bool propto>
+inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const dev_var_matrix& L) {
+  const char* fn = "multi_normal_cholesky_lpdf";
+  if (n == 0) return var(0.0);
+  smg_ctx* c = amd::ctx();
+  double* ws = amd::alloc_doubles(2 * size_t(n) + 1);
+  double* lp_d = ws + 2 * size_t(n);
+  amd::check(smg_mvn_cholesky_fwd(c, y_d, mu_d, L.val_ptr(), n, L.vi_->aux_, n, ws, lp_d), fn);
+  double lp = 0;
+  amd::to_host(&lp, lp_d, 1);
+  if (propto) lp -= -std::log(std::sqrt(2.0 * 3.14159265358979323846)) * n;
+  return var(new mvn_cholesky_dev_vari(lp, L.vi_, ws));
+}
+
+inline void mvn_check_data(const std::vector<double>& y, const std::vector<double>* mu) {
+  const char* fn = "multi_normal_cholesky_lpdf";
+  for (size_t i = 0; i < y.size(); ++i)
+    if (std::isnan(y[i])) {
+      std::ostringstream m;
+      m << fn << ": Random variable is nan, but must not be nan!";
+      throw std::domain_error(m.str());
+    }
+  if (mu)
+    for (double v : *mu)
+      if (!std::isfinite(v)) {
+        std::ostringstream m;
+        m << fn << ": Location parameter is " << v << ", but must be finite!";
+        throw std::domain_error(m.str());
+      }
+}
+
+}  // namespace internal
+
+template <bool propto = false>
+inline var multi_normal_cholesky_lpdf(const std::vector<double>& y, const std::vector<double>& mu,
+                                      const dev_var_matrix& L) {
+  internal::mvn_check_sizes(int(y.size()), int(mu.size()), L);
+  internal::mvn_check_data(y, &mu);
+  if (y.empty()) return var(0.0);
+  dev_data<double> yd = to_dev_data(y), md = to_dev_data(mu);
+  return internal::mvn_cholesky_dev<propto>(yd.data(), md.data(), int(y.size()), L);
+}
+
+/** Zero mean (mu == 0), y device-resident. */
+template <bool propto = false>
+inline var multi_normal_cholesky_lpdf(const dev_data<double>& y, const dev_var_matrix& L) {
+  internal::mvn_check_sizes(int(y.size()), int(y.size()), L);
+  return internal::mvn_cholesky_dev<propto>(y.data(), nullptr, int(y.size()), L);
+}
+template <bool propto = false>
+inline var multi_normal_cholesky_lpdf(const dev_data<double>& y, const dev_data<double>& mu,
+                                      const dev_var_matrix& L) {
+  internal::mvn_check_sizes(int(y.size()), int(mu.size()), L);
+  return internal::mvn_cholesky_dev<propto>(y.data(), mu.data(), int(y.size()), L);
+}
+
+}  // namespace math
+}  // namespace stan
+#endif

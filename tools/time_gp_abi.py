@@ -20,5 +20,5 @@ for r in range(reps):
     ctx.rewind(m)
     print(f"rep {r}: {dt*1e3:.2f} ms fx={fx:.12g} g={g} ref={d['grad']}", flush=True)
 for f in hip.FAMILIES:
-    ms, c = ctx.profile_read(f)
+    ms, c, fl = ctx.profile_read(f)
     print(f"{f:12s} {ms:9.3f} ms total  {c} regions")
