@@ -57,37 +57,26 @@ __global__ void k_add_lower(const double* __restrict__ X, int ldx, int n,
   }
 }
 
-// factor the diagonal block in place and write its inverse
-__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ L, int ldl, int b,
+// factor the diagonal block in place and write its inverse (dense, upper
+// zeros, so GEMMs may read it as a plain matrix); ONE wave
+__global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int ldl, int b,
                                                     double* __restrict__ Dinv, int ldd,
                                                     int* status) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
-  __shared__ double T[3 * 256];
   lds_load_block(D, L, ldl, b, true);
   __syncthreads();
-  lds_potrf_inv64(D, X, T, status);
-  lds_store_block(D, L, ldl, b, true);
-  // Dinv block stored full (upper zeros) so GEMMs may read it as dense
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int c = e / b, r = e % b;
-    Dinv[r + (size_t)c * ldd] = X[r * SMG_NBP + c];
-  }
+  lds_potrf_inv64_blk(D, X, b, L, ldl, Dinv, ldd, status, true);
 }
 
 // inverse of a lower-triangular diagonal block (no factorisation)
-__global__ __launch_bounds__(256) void k_trtri_diag(const double* __restrict__ L, int ldl,
+__global__ __launch_bounds__(512) void k_trtri_diag(const double* __restrict__ L, int ldl,
                                                     int b, double* __restrict__ Dinv, int ldd) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
-  __shared__ double T[3 * 256];
   lds_load_block(D, L, ldl, b, true);
   __syncthreads();
-  lds_trtri64(D, X, T);
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int c = e / b, r = e % b;
-    Dinv[r + (size_t)c * ldd] = X[r * SMG_NBP + c];
-  }
+  lds_potrf_inv64_blk(D, X, b, nullptr, 0, Dinv, ldd, nullptr, false);
 }
 
 // symbolic_rev (cholesky_decompose.hpp:101-111) on one diagonal block:
@@ -165,7 +154,7 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
     const int m = n - j - b;
     double* L11 = L + j + (size_t)j * ldl;
     double* Di = Dinv + j;  // rows j..j+b, columns 0..b, ld n
-    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, L11, ldl, b, Di, n,
+    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L11, ldl, b, Di, n,
                        ctx->status_d);
     if (m > 0) {
       double* L21 = L + (j + b) + (size_t)j * ldl;
@@ -193,7 +182,7 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
     if (!Dv) return SMG_ERR_OOM;
     for (int j = 0; j < n; j += SMG_NB) {
       const int b = min(SMG_NB, n - j);
-      hipLaunchKernelGGL(k_trtri_diag, dim3(1), dim3(256), 0, ctx->stream,
+      hipLaunchKernelGGL(k_trtri_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream,
                          L + j + (size_t)j * ldl, ldl, b, Dv + j, n);
     }
   }

@@ -7,31 +7,32 @@
 //
 // Tiling: a 256-thread workgroup (4 waves, 2x2) owns a BM x BN tile of C;
 // each wave owns (BM/2) x (BN/2) = TM x TN MFMA tiles of 16x16 held in
-// accumulators.  K advances in steps of BK = 16 staged through LDS:
+// accumulators.  K advances in stages of BK (16 for 128x128 tiles, 32 for
+// 64x64 tiles, whose GEMMs in the blocked Cholesky have K = 64: two stages,
+// one exposed global-load latency) staged through LDS:
 //   operand contiguous along the output dim (A no-trans, B trans): LDS [k][dim+16]
-//   operand contiguous along k (A trans, B no-trans):               LDS [dim][k+1]
+//   operand contiguous along k (A trans, B no-trans):               LDS [dim][k+BK/2+1 (BK=16: +1)]
 // Both make the MFMA fragment reads (16 consecutive rows/cols x 4 k) bank-
 // conflict free for ds_read_b64 (row stride = 16 mod 32 doubles, resp. 17).
-// Global->LDS staging goes through registers with one tile of prefetch.
+// Global->LDS staging goes through registers with one stage of prefetch; the
+// beta * C operand of the epilogue is fetched before the K loop.
 // Split-K writes fixed-order partial slabs reduced by a second kernel, so the
 // result is bitwise deterministic run to run.
 #include "smg_internal.h"
 
 namespace {
 
-constexpr int BK = 16;
-
-template <int BM, bool KCONTIG>
+template <int BM, int BK, bool KCONTIG>
 struct lds_layout;
-template <int BM>
-struct lds_layout<BM, false> {  // [k][BM + 16]
+template <int BM, int BK>
+struct lds_layout<BM, BK, false> {  // [k][BM + 16]
   static constexpr int S = BM + 16;
   static constexpr int size = BK * S;
   __device__ static int at(int i, int kk) { return kk * S + i; }
 };
-template <int BM>
-struct lds_layout<BM, true> {  // [BM][BK + 1]
-  static constexpr int S = BK + 1;
+template <int BM, int BK>
+struct lds_layout<BM, BK, true> {  // [BM][S], S = 17 mod 32
+  static constexpr int S = BK == 16 ? 17 : BK + 17;
   static constexpr int size = BM * S;
   __device__ static int at(int i, int kk) { return i * S + kk; }
 };
@@ -39,7 +40,7 @@ struct lds_layout<BM, true> {  // [BM][BK + 1]
 // Operand X viewed as a (rows x k) matrix in the kernel's orientation:
 //   KCONTIG == false : element (i, kk) at X[i + kk*ld]
 //   KCONTIG == true  : element (i, kk) at X[kk + i*ld]
-template <int BM, bool KCONTIG>
+template <int BM, int BK, bool KCONTIG>
 __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
                                           int rows, int k, int i0, int k0,
                                           double (&r)[BM * BK / 256]) {
@@ -63,7 +64,7 @@ __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
   }
 }
 
-template <int BM, bool KCONTIG>
+template <int BM, int BK, bool KCONTIG>
 __device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256]) {
   constexpr int PER = BM * BK / 256;
 #pragma unroll
@@ -77,7 +78,7 @@ __device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * B
       kk = e / BM;
       i = e % BM;
     }
-    lds[lds_layout<BM, KCONTIG>::at(i, kk)] = r[q];
+    lds[lds_layout<BM, BK, KCONTIG>::at(i, kk)] = r[q];
   }
 }
 
@@ -91,7 +92,7 @@ __device__ __forceinline__ void tri_decode(int t, int& bi, int& bj) {
 }
 
 // MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n)
-template <int BM, int BN, bool TA, bool TB, int MODE>
+template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
 __global__ __launch_bounds__(256) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
@@ -100,8 +101,8 @@ __global__ __launch_bounds__(256) void k_gemm(
   // B-side as an (n x k) operand: no-trans B is k-contiguous; trans B is n-contiguous.
   constexpr bool AK = TA;
   constexpr bool BKC = !TB;
-  using LA = lds_layout<BM, AK>;
-  using LB = lds_layout<BN, BKC>;
+  using LA = lds_layout<BM, BK, AK>;
+  using LB = lds_layout<BN, BK, BKC>;
   __shared__ double As[LA::size];
   __shared__ double Bs[LB::size];
 
@@ -133,18 +134,31 @@ __global__ __launch_bounds__(256) void k_gemm(
   const int kq = kend - kbeg;
   // A as (m x k) operand; B as (n x k) operand
   if (kq > 0) {
-    load_tile<BM, AK>(A, lda, m, kend, i0, kbeg, ra);
-    load_tile<BN, BKC>(B, ldb, n, kend, j0, kbeg, rb);
+    load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg, ra);
+    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg, rb);
   }
+  // epilogue operand in flight during the K loop
+  double cpre[TM][TN][4];
+  const bool use_c = !slab && beta != 0.0;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r;
+        const int j = j0 + wc * (BN / 2) + b * 16 + (lane & 15);
+        cpre[a][b][r] = (use_c && i < m && j < n) ? C[i + (size_t)j * ldc] : 0.0;
+      }
   const int fr = lane & 15, fk = lane >> 4;
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
-    store_tile<BM, AK>(As, ra);
-    store_tile<BN, BKC>(Bs, rb);
+    store_tile<BM, BK, AK>(As, ra);
+    store_tile<BN, BK, BKC>(Bs, rb);
     __syncthreads();
     if (k0 + BK < kend) {
-      load_tile<BM, AK>(A, lda, m, kend, i0, k0 + BK, ra);
-      load_tile<BN, BKC>(B, ldb, n, kend, j0, k0 + BK, rb);
+      load_tile<BM, BK, AK>(A, lda, m, kend, i0, k0 + BK, ra);
+      load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, k0 + BK, rb);
     }
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
@@ -180,8 +194,7 @@ __global__ __launch_bounds__(256) void k_gemm(
         if (slab) {
           slab[(size_t)split * m * n + (size_t)j * m + i] = v;
         } else {
-          double* c = C + i + (size_t)j * ldc;
-          *c = (beta == 0.0) ? alpha * v : alpha * v + beta * *c;
+          C[i + (size_t)j * ldc] = use_c ? alpha * v + beta * cpre[a][b][r] : alpha * v;
         }
       }
 }
@@ -200,7 +213,7 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
   *c = (beta == 0.0) ? alpha * s : alpha * s + beta * *c;
 }
 
-template <int BM, int BN, bool TA, bool TB, int MODE>
+template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
 int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
            int lda, const double* B, int ldb, double beta, double* C, int ldc) {
   const int tm = smg_ceil_div(m, BM), tn = smg_ceil_div(n, BN);
@@ -208,9 +221,10 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   // split K when the tile grid cannot fill the 256 CUs and K is long
   int splits = 1;
   const int target = 512;
-  if (ntiles < target && k >= 4 * BK * 2) {
+  constexpr int KMIN = 64;  // shortest K chunk of a split
+  if (ntiles < target && k >= 2 * KMIN) {
     splits = smg_ceil_div(target, ntiles);
-    const int maxs = k / (4 * BK);
+    const int maxs = k / KMIN;
     if (splits > maxs) splits = maxs;
     if (splits > 64) splits = 64;
     if (splits < 1) splits = 1;
@@ -222,7 +236,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
     slab = smg_ws(ctx, SMG_WS_GEMM, (size_t)splits * m * n);
     if (!slab) return SMG_ERR_OOM;
   }
-  hipLaunchKernelGGL((k_gemm<BM, BN, TA, TB, MODE>), dim3(ntiles * splits), dim3(256), 0,
+  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntiles * splits), dim3(256), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
                      ntiles, kchunk, slab);
   if (splits > 1) {
@@ -239,8 +253,8 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
                   int lda, const double* B, int ldb, double beta, double* C, int ldc) {
   const long long big_tiles = (long long)smg_ceil_div(m, 128) * smg_ceil_div(n, 128);
   if (big_tiles >= 256)
-    return launch<128, 128, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  return launch<64, 64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  return launch<64, 64, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
 }
 
 }  // namespace

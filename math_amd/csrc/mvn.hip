@@ -109,12 +109,21 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
   smg_prof_scope prof(ctx, SMG_FAM_MVN);
   double* w = ws;
   double* sd = ws + n;
-  hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(256), 0, ctx->stream, y, mu, n, w);
-  int rc = smg_trsm_impl(ctx, 1, 0, L, ldl, Dinv, n, w, n, n, 1);  // w = L^{-1}(y - mu)
+  double* r = smg_ws(ctx, SMG_WS_RED, 2 * (size_t)n);
+  if (!r) return SMG_ERR_OOM;
+  double* res = r + n;
+  int rc;
+  if (!Dinv) {  // diagonal-block inverses of L (the Cholesky forward normally provides them)
+    double* W = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_NB);
+    if (!W) return SMG_ERR_OOM;
+    rc = smg_trtri_blocks_impl(ctx, L, ldl, n, W);
+    if (rc) return rc;
+    Dinv = W;
+  }
+  hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(256), 0, ctx->stream, y, mu, n, res);
+  rc = smg_trsv_lower_impl(ctx, 0, L, ldl, Dinv, n, res, w, r, n);  // w = L^{-1}(y - mu)
   if (rc) return rc;
-  rc = smg_copy_impl(ctx, n, 1, w, n, sd, n, 1.0, 0);
-  if (rc) return rc;
-  rc = smg_trsm_impl(ctx, 1, 1, L, ldl, Dinv, n, sd, n, n, 1);  // sd = L^{-T} w
+  rc = smg_trsv_lower_impl(ctx, 1, L, ldl, Dinv, n, w, sd, r, n);  // sd = L^{-T} w
   if (rc) return rc;
   hipLaunchKernelGGL(k_mvn_lp, dim3(1), dim3(1024), 0, ctx->stream, w, L, ldl, n, out_lp);
   SMG_LAUNCH_CHECK();

@@ -85,6 +85,15 @@ double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 // C = beta C (lower != 0: lower triangle only)
 int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int lower);
 
+// blocked triangular helpers (tri.hip, trsv.hip)
+int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
+                  int ldw, double* B, int ldb, int m, int n);
+int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
+                  double alpha, int accumulate);
+int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);
+int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W,
+                        int ldw, const double* x, double* y, double* r, int n);
+
 // internal GEMM entry used by other units (no argument re-validation)
 int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
                   int k, double alpha, const double* A, int lda, const double* B,

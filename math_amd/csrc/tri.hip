@@ -13,11 +13,10 @@ namespace {
 // W_p = inverse of the lower-triangular form of diagonal block p:
 //   lower: W_p = D_p^{-1};  upper: W_p = (U_p^T)^{-1} = (U_p^{-1})^T.
 // W is m x SMG_NB (block p in rows p*NB.., ld m).
-__global__ __launch_bounds__(256) void k_trtri_blocks(const double* __restrict__ A, int lda,
+__global__ __launch_bounds__(512) void k_trtri_blocks(const double* __restrict__ A, int lda,
                                                       int m, int upper, double* __restrict__ W) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
-  __shared__ double T[3 * 256];
   const int j = blockIdx.x * SMG_NB;
   const int b = min(SMG_NB, m - j);
   const double* Ab = A + j + (size_t)j * lda;
@@ -28,11 +27,7 @@ __global__ __launch_bounds__(256) void k_trtri_blocks(const double* __restrict__
     D[r * SMG_NBP + c] = v;
   }
   __syncthreads();
-  lds_trtri64(D, X, T);
-  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
-    const int c = e / b, r = e % b;
-    W[j + r + (size_t)c * m] = X[r * SMG_NBP + c];
-  }
+  lds_potrf_inv64_blk(D, X, b, nullptr, 0, W + j, m, nullptr, false);
 }
 
 __global__ void k_copy(int m, int n, const double* __restrict__ A, int lda,
@@ -85,6 +80,14 @@ int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* 
   return SMG_OK;
 }
 
+int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W) {
+  if (n <= 0) return SMG_OK;
+  hipLaunchKernelGGL(k_trtri_blocks, dim3((n + SMG_NB - 1) / SMG_NB), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
+                     ldl, n, 0, W);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
 // W: inverse diagonal blocks (m x SMG_NB, ld m) or NULL (computed here)
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
                   int ldw, double* B, int ldb, int m, int n) {
@@ -93,7 +96,7 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
   if (!W) {
     double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)m * SMG_NB);
     if (!w) return SMG_ERR_OOM;
-    hipLaunchKernelGGL(k_trtri_blocks, dim3(nblk), dim3(256), 0, ctx->stream, A, lda, m,
+    hipLaunchKernelGGL(k_trtri_blocks, dim3(nblk), dim3(SMG_DIAG_THREADS), 0, ctx->stream, A, lda, m,
                        lower ? 0 : 1, w);
     W = w;
     ldw = m;

@@ -14,6 +14,7 @@
 
 constexpr int SMG_NB = 64;           // diagonal block size of every blocked kernel
 constexpr int SMG_NBP = SMG_NB + 1;  // padded LDS row stride
+constexpr int SMG_DIAG_THREADS = 512;  // threads of the fused diagonal-block kernels
 
 __device__ __forceinline__ double bcast(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
@@ -203,9 +204,343 @@ __device__ inline void lds_trtri64(const double* D, double* X, double* T) {
   lds_trtri_offdiag(D, X, T);
 }
 
+// ---------------------------------------------------------------------------
+// Single-wave 64x64 Cholesky, register resident (one wave = 64 lanes).
+// Lane i holds row i of the block.  Step j: pivot = a[j] of lane j
+// (v_readlane); l_jj = sqrt(pivot); lanes i > j divide a[j] by l_jj (Eigen
+// LLT's column scaling); the new column goes to LDS with ONE ds_write per lane
+// and is read back as broadcast LDS reads, 8 at a time (sched_barrier bounds
+// the live registers), for the rank-1 update of the trailing columns.
+// upper: load the block as the lower-triangular U^T of an upper-stored U.
+// Writes L row-major into Lrow (LDS [64][SMG_NBP], strict upper zeroed) and,
+// if Lout, col-major to global.  col: LDS >= 64 doubles.
+__device__ __forceinline__ void wave_potrf64_reg(const double* __restrict__ A, int lda, int b, bool upper,
+                                        double* Lout, int ldl, double* col, double* Lrow,
+                                        int* status, bool factor) {
+  const int l = threadIdx.x & 63;
+  // stage through LDS (runtime loop: no per-element address registers)
+#pragma unroll 4
+  for (int c = 0; c < 64; ++c) {
+    double v = (l == c) ? 1.0 : 0.0;  // identity padding beyond b
+    if (l < b && c < b && c <= l) v = upper ? A[c + (size_t)l * lda] : A[l + (size_t)c * lda];
+    Lrow[l * SMG_NBP + c] = v;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  double a[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) a[c] = Lrow[l * SMG_NBP + c];
+  if (factor) {
+    // lanes l < j only touch their (unused) strict-upper entries; a non-PD
+    // pivot propagates NaN and is latched below.  Constant trip counts keep
+    // a[] in VGPRs once fully unrolled.
+    double minpiv = 1.0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const double piv = bcast(a[j], j);
+      minpiv = fmin(minpiv, piv > 0.0 && piv < INFINITY ? 1.0 : -1.0);
+      const double ljj = sqrt(piv);
+      const double lij = (l == j) ? ljj : a[j] / ljj;
+      a[j] = lij;
+      col[l] = lij;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's write is visible
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = 0; c < 64; ++c)
+        if (c > j) a[c] -= lij * col[c];
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!(minpiv > 0.0) && l == 0) atomicOr(status, (int)SMG_ERR_NOT_PD);
+  }
+#pragma unroll
+  for (int c = 0; c < 64; ++c) Lrow[l * SMG_NBP + c] = (c <= l) ? a[c] : 0.0;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  if (Lout && l < b) {
+#pragma unroll 4
+    for (int c = 0; c < b; ++c) Lout[l + (size_t)c * ldl] = Lrow[l * SMG_NBP + c];
+  }
+}
+
+// X = L^{-1} from Lrow (LDS, lower, row-major stride SMG_NBP), one wave:
+// lane c owns column c; the column lives in LDS (Xcol, same layout) so no
+// register array is indexed at run time.  Four partial sums per entry.
+__device__ inline void wave_trtri64_lds(const double* Lrow, double* Xcol, double* Xout, int ldx,
+                                        int b) {
+  const int c = threadIdx.x & 63;
+  for (int r = 0; r < 64; ++r) {
+    double s0 = (r == c) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int t = c;  // X(t, c) = 0 for t < c
+    for (; t + 3 < r; t += 4) {
+      s0 -= Lrow[r * SMG_NBP + t] * Xcol[t * SMG_NBP + c];
+      s1 -= Lrow[r * SMG_NBP + t + 1] * Xcol[(t + 1) * SMG_NBP + c];
+      s2 -= Lrow[r * SMG_NBP + t + 2] * Xcol[(t + 2) * SMG_NBP + c];
+      s3 -= Lrow[r * SMG_NBP + t + 3] * Xcol[(t + 3) * SMG_NBP + c];
+    }
+    for (; t < r; ++t) s0 -= Lrow[r * SMG_NBP + t] * Xcol[t * SMG_NBP + c];
+    const double xv = (r < c) ? 0.0 : ((s0 + s1) + (s2 + s3)) / Lrow[r * SMG_NBP + r];
+    Xcol[r * SMG_NBP + c] = xv;
+    if (Xout && r < b && c < b) Xout[r + (size_t)c * ldx] = xv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused 64x64 Cholesky + inverse by right-looking elimination, all waves of
+// the workgroup (blockDim.x = 64 * G), ONE barrier per column.
+// Thread (i = lane, g = wave) owns row i and the column class c = g (mod G).
+// Step j (all threads compute l_jj = sqrt(D[j][j]) redundantly -- no
+// broadcast, no extra barrier):
+//   l_ij = D[i][j] / l_jj                        (Eigen LLT column scaling)
+//   D[i][c] -= l_ij * (D[c][j] / l_jj)  j < c <= i   (trailing update)
+//   X[i][c] -= l_ij * (X[j][c] / l_jj)  c <= j, i > j (same row ops on I)
+//   X_final[j][:] = X[j][:] / l_jj,  L[:, j] final
+// D's column j and X's row j are only READ during step j; every write goes
+// to a different row/column, so no intra-step hazard.  With factor == false
+// D already holds L and l_ij = D[i][j] (no scaling): X = L^{-1} only.
+// D, X: LDS [64][SMG_NBP]; X must hold the identity on entry.
+// Lout / Xout: col-major global destinations (b x b; Lout may be null).
+__device__ inline void lds_potrf_inv64_v2(double* D, double* X, int b, double* Lout, int ldl,
+                                          double* Xout, int ldx, int* status, bool factor) {
+  constexpr int GC = SMG_DIAG_THREADS / 64;  // column classes (waves)
+  const int i = threadIdx.x & 63;
+  const int g = threadIdx.x >> 6;
+  bool bad = false;
+  double li_prev = 0.0, inv_prev = 1.0;
+  for (int j = 0; j < 64; ++j) {
+    // deferred finalisation of step j-1 (column j-1 of D / row j-1 of X are
+    // not read in step j): l_{i,j-1} into D, row j-1 of X scaled in place
+    if (j > 0) {
+      if (factor && g == 0 && i >= j - 1) D[i * SMG_NBP + j - 1] = li_prev;
+      if (i == j - 1)
+#pragma unroll
+        for (int q = 0; q < 64 / GC; ++q) {
+          const int c = g + q * GC;
+          if (c <= i) X[i * SMG_NBP + c] *= inv_prev;
+        }
+    }
+    const double piv = D[j * SMG_NBP + j];
+    double ljj, inv, li;
+    // the pivot chain is the kernel's critical path: v_rsq_f64 + two Newton
+    // steps (~1 ulp, vs ~360 cycles for IEEE sqrt + divide on gfx950)
+    if (factor) {
+      bad |= !(piv > 0.0 && piv < INFINITY);
+      double r = __builtin_amdgcn_rsq(piv);
+      r = r * (1.5 - 0.5 * piv * r * r);
+      r = r * (1.5 - 0.5 * piv * r * r);
+      inv = r;
+      ljj = piv * r;
+      li = (i > j) ? D[i * SMG_NBP + j] * inv : (i == j ? ljj : 0.0);
+    } else {
+      ljj = piv;
+      double r = __builtin_amdgcn_rcp(piv);
+      r = r * (2.0 - piv * r);
+      inv = r * (2.0 - piv * r);
+      li = (i >= j) ? D[i * SMG_NBP + j] : 0.0;
+    }
+    if (i > j) {
+      // fixed trip counts (64 / GC per loop), predicated: all loads of a
+      // loop issue back to back instead of one LDS round trip per element
+      if (factor) {
+        double lc[64 / GC], dv[64 / GC];
+#pragma unroll
+        for (int q = 0; q < 64 / GC; ++q) {
+          const int c = g + q * GC;
+          lc[q] = D[c * SMG_NBP + j];
+          dv[q] = D[i * SMG_NBP + c];
+        }
+#pragma unroll
+        for (int q = 0; q < 64 / GC; ++q) {
+          const int c = g + q * GC;
+          if (c > j && c <= i) D[i * SMG_NBP + c] = dv[q] - li * (lc[q] * inv);
+        }
+      }
+      const double lx = li * inv;
+      double xj[64 / GC], xi[64 / GC];
+#pragma unroll
+      for (int q = 0; q < 64 / GC; ++q) {
+        const int c = g + q * GC;
+        xj[q] = X[j * SMG_NBP + c];
+        xi[q] = X[i * SMG_NBP + c];
+      }
+#pragma unroll
+      for (int q = 0; q < 64 / GC; ++q) {
+        const int c = g + q * GC;
+        if (c <= j) X[i * SMG_NBP + c] = xi[q] - lx * xj[q];
+      }
+    }
+    li_prev = li;
+    inv_prev = inv;
+    __syncthreads();
+  }
+  // finalisation of step 63
+  if (factor && g == 0 && i == 63) D[63 * SMG_NBP + 63] = li_prev;
+  if (i == 63)
+#pragma unroll
+    for (int q = 0; q < 64 / GC; ++q) X[63 * SMG_NBP + g + q * GC] *= inv_prev;
+  __syncthreads();
+  if (bad && threadIdx.x == 0) atomicOr(status, (int)SMG_ERR_NOT_PD);
+  // one coalesced write of L (lower, upper zeroed) and X (dense, upper zeros)
+  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
+    const int c = e / b, r = e % b;
+    if (Lout) Lout[r + (size_t)c * ldl] = (r >= c) ? D[r * SMG_NBP + c] : 0.0;
+    if (Xout) Xout[r + (size_t)c * ldx] = (r >= c) ? X[r * SMG_NBP + c] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Blocked 64x64 Cholesky in LDS (512 threads = 8 waves), 8-wide panels.
+//   panel p (columns j0 = 8p .. j0+7): wave 0, lane i = row i holds the 8
+//     panel values in registers; 8 pivot steps with v_readlane broadcasts;
+//     l_jj = sqrt(pivot) via v_rsq_f64 + 2 Newton steps (~1 ulp), the
+//     column scaled by the reciprocal (Eigen LLT divides; same to ~1 ulp).
+//   trailing rank-8 update of the lower triangle below the panel: thread
+//     (row i = lane, column class g = wave) keeps row i's panel in registers
+//     and walks columns c = g (mod 8): 8 FMAs per loaded D[i][c].
+// D: LDS [64][SMG_NBP], lower triangle holds A (identity padded); on exit the
+// lower triangle holds L (strict upper untouched).
+__device__ inline void lds_potrf64_blocked(double* D, int* status) {
+  const int i = threadIdx.x & 63;
+  const int g = threadIdx.x >> 6;
+  bool bad = false;
+  for (int p = 0; p < 8; ++p) {
+    const int j0 = 8 * p;
+    if (g == 0) {
+      double a[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) a[t] = (i >= j0) ? D[i * SMG_NBP + j0 + t] : 0.0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const double piv = bcast(a[t], j0 + t);
+        bad |= !(piv > 0.0 && piv < INFINITY);
+        double r = __builtin_amdgcn_rsq(piv);
+        r = r * (1.5 - 0.5 * piv * r * r);
+        r = r * (1.5 - 0.5 * piv * r * r);
+        const double li = (i == j0 + t) ? piv * r : a[t] * r;
+        a[t] = li;
+#pragma unroll
+        for (int c = t + 1; c < 8; ++c) a[c] -= li * bcast(li, j0 + c);
+      }
+      if (i >= j0)
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if (i >= j0 + t) D[i * SMG_NBP + j0 + t] = a[t];
+    }
+    __syncthreads();
+    const int c1 = j0 + 8;
+    if (c1 < 64 && i >= c1) {
+      double li[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) li[t] = D[i * SMG_NBP + j0 + t];
+      // columns c = c1 + g + 8q (q = 0..6), c <= i
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        const int c = c1 + g + 8 * q;
+        if (c <= i) {
+          double s = D[i * SMG_NBP + c];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) s -= li[t] * D[c * SMG_NBP + j0 + t];
+          D[i * SMG_NBP + c] = s;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (bad && threadIdx.x == 0) atomicOr(status, (int)SMG_ERR_NOT_PD);
+}
+
+// X = L^{-1} (64x64, LDS) for L lower in D (LDS), 512 threads, 8x8 blocks.
+//   leaves: wave w inverts the 8x8 diagonal block w (lane c < 8 owns column c)
+//   block rows p = 1..7 in order: T = -sum_{k<p} L_pk X_k (all columns c < 8p),
+//   then X_p = X_pp T (thread (row r = wave, column c = lane)).
+// X: LDS [64][SMG_NBP] (fully written, upper zeros); T: LDS >= 8*64 doubles.
+__device__ inline void lds_trtri64_blocked(const double* D, double* X, double* T) {
+  const int l = threadIdx.x & 63;
+  const int g = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < 64 * SMG_NBP; e += blockDim.x) X[e] = 0.0;
+  __syncthreads();
+  {  // diagonal leaf g
+    const int j0 = 8 * g;
+    double x[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      double s = (l == r) ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < r; ++t) s -= D[(j0 + r) * SMG_NBP + j0 + t] * x[t];
+      double rr = __builtin_amdgcn_rcp(D[(j0 + r) * SMG_NBP + j0 + r]);
+      const double dd = D[(j0 + r) * SMG_NBP + j0 + r];
+      rr = rr * (2.0 - dd * rr);
+      rr = rr * (2.0 - dd * rr);
+      x[r] = s * rr;
+    }
+    if (l < 8)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) X[(j0 + r) * SMG_NBP + j0 + l] = x[r];
+  }
+  __syncthreads();
+  for (int p = 1; p < 8; ++p) {
+    const int j0 = 8 * p;
+    // T[r][c] = -sum_{t < j0} L[j0+r][t] X[t][c], c < j0 ; thread (r = g, c = l)
+    if (l < j0) {
+      double s[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int t0 = 0; t0 < j0; t0 += 8) {  // 16 independent LDS reads per trip
+        double dl[8], xl[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          dl[t] = D[(j0 + g) * SMG_NBP + t0 + t];
+          xl[t] = X[(t0 + t) * SMG_NBP + l];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s[t & 3] -= dl[t] * xl[t];
+      }
+      T[g * 64 + l] = (s[0] + s[1]) + (s[2] + s[3]);
+    }
+    __syncthreads();
+    // X[j0+r][c] = sum_{t <= r} Xpp[r][t] T[t][c]
+    if (l < j0) {
+      double s = 0.0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (t <= g) s += X[(j0 + g) * SMG_NBP + j0 + t] * T[t * 64 + l];
+      X[(j0 + g) * SMG_NBP + l] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// Drop-in for lds_potrf_inv64_v2 built from the blocked pieces: factor (if
+// asked) then invert, then one coalesced write of L (lower) and X = L^{-1}.
+__device__ inline void lds_potrf_inv64_blk(double* D, double* X, int b, double* Lout, int ldl,
+                                           double* Xout, int ldx, int* status, bool factor) {
+  __shared__ double T[8 * 64];
+  if (factor) lds_potrf64_blocked(D, status);
+  lds_trtri64_blocked(D, X, T);
+  for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
+    const int c = e / b, r = e % b;
+    if (Lout) Lout[r + (size_t)c * ldl] = (r >= c) ? D[r * SMG_NBP + c] : 0.0;
+    if (Xout) Xout[r + (size_t)c * ldx] = (r >= c) ? X[r * SMG_NBP + c] : 0.0;
+  }
+}
+
 // load a b x b block (col-major, ld) into LDS [r][c]; lower_only zeroes the
 // strict upper triangle; rows/cols >= b are identity padding
 __device__ inline void lds_load_block(double* D, const double* A, int ld, int b, bool lower_only) {
+  constexpr int PER = SMG_NB * SMG_NB / SMG_DIAG_THREADS;
+  if (blockDim.x == SMG_DIAG_THREADS) {  // all global loads in flight at once
+    double v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = threadIdx.x + q * SMG_DIAG_THREADS;
+      const int c = e / SMG_NB, r = e % SMG_NB;
+      v[q] = (r < b && c < b && (!lower_only || r >= c)) ? A[r + (size_t)c * ld] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = threadIdx.x + q * SMG_DIAG_THREADS;
+      const int c = e / SMG_NB, r = e % SMG_NB;
+      D[r * SMG_NBP + c] = (r < b && c < b) ? v[q] : (r == c ? 1.0 : 0.0);
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
     const int c = e / SMG_NB, r = e % SMG_NB;
     double v;
