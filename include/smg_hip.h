@@ -228,6 +228,23 @@ int smg_sum(smg_ctx* ctx, const double* x, long long n, double* out);
 /* B(i,j) = A(j,i) style copy helpers */
 int smg_copy_matrix(smg_ctx* ctx, int m, int n, const double* A, int lda,
                     double* B, int ldb, int trans, int uplo_zero_upper);
+/* B (n x m) = A^T + beta B, A m x n (transpose(Matrix<var>): forward copy and
+ * the reverse Aadj += Badj^T) */
+int smg_transpose(smg_ctx* ctx, int m, int n, const double* A, int lda,
+                  double* B, int ldb, double beta);
+/* Y += c on every entry (uplo == 1: lower triangle only); the reverse of
+ * sum(Matrix<var>) (rev/mat/fun/sum.hpp:18-60) */
+int smg_shift(smg_ctx* ctx, int m, int n, double c, double* Y, int ldy, int uplo);
+/* out += sum_i x_i y_i (deterministic) */
+int smg_dot(smg_ctx* ctx, const double* x, const double* y, long long n, double* out);
+/* argument checks of the lpdf reducers (prim/scal/err/check_*.hpp): *flag (a
+ * device double the caller zeroes) becomes 1.0 if any x_i fails.  kind 0:
+ * check_not_nan, 1: check_finite, 2: check_positive, 3: check_positive_finite.
+ * The host layer reads the flags back with the value and throws the
+ * reference's std::domain_error for the first failing argument. */
+int smg_check_domain(smg_ctx* ctx, const double* x, long long n, int kind, double* flag);
+/* *flag = 1.0 if any y_i is outside [lo, hi] (check_bounded) */
+int smg_check_bounded_int(smg_ctx* ctx, const int* y, long long n, int lo, int hi, double* flag);
 
 /* ------------------------------------------------------ multi-GPU ------
  * One RCCL communicator per process/device; a single fp64 sum all-reduce of

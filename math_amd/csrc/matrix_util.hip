@@ -1,0 +1,152 @@
+// Small dense helpers behind the host layer's matrix functors:
+//   transpose  (rev/mat/fun/transpose / Eigen .transpose() in multiply(A, A^T))
+//   shift      (sum(Matrix<var>) reverse: every operand adjoint += adj,
+//               rev/mat/fun/sum.hpp:18-60)
+//   dot        (dot_product / the scalar side of multiply(var, Matrix<var>),
+//               rev/mat/fun/multiply.hpp:562-600)
+// All deterministic (fixed-order reductions).
+#include "smg_internal.h"
+
+namespace {
+
+constexpr int TT = 64;  // transpose tile
+
+// B (n x m) = A^T + beta B; A is m x n.  64 x 64 tiles through LDS so both the
+// read of A and the write of B are column-coalesced.
+__global__ __launch_bounds__(256) void k_transpose(int m, int n, const double* __restrict__ A,
+                                                   int lda, double* __restrict__ B, int ldb,
+                                                   double beta) {
+  __shared__ double t[TT][TT + 1];
+  const int i0 = blockIdx.x * TT, j0 = blockIdx.y * TT;
+  const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    const int i = i0 + r, j = j0 + c;
+    t[c][r] = (i < m && j < n) ? A[i + (size_t)j * lda] : 0.0;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    // B(j0 + r, i0 + c) = A(i0 + c, j0 + r)
+    const int bi = j0 + r, bj = i0 + c;
+    if (bi < n && bj < m) {
+      double* d = B + bi + (size_t)bj * ldb;
+      const double v = t[r][c];
+      *d = beta == 0.0 ? v : v + beta * *d;
+    }
+  }
+}
+
+__global__ void k_shift(int m, int n, double c, double* __restrict__ Y, int ldy, int uplo) {
+  const long long tot = (long long)m * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / m), i = (int)(e % m);
+    if (uplo == 1 && i < j) continue;
+    Y[i + (size_t)j * ldy] += c;
+  }
+}
+
+__global__ void k_dot_part(const double* __restrict__ x, const double* __restrict__ y, long long n,
+                           double* part) {
+  __shared__ double lds[16];
+  double s = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    s += x[i] * y[i];
+  s = block_sum(s, lds);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// flag <- 1.0 if any element violates the check (all writers store 1.0)
+//   kind 0: not nan (check_not_nan)   1: finite (check_finite)
+//   2: > 0 (check_positive)           3: finite and > 0 (check_positive_finite)
+__global__ void k_check_domain(const double* __restrict__ x, long long n, int kind,
+                               double* flag) {
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    if (kind == 0) bad |= v != v;
+    else if (kind == 1) bad |= !(fabs(v) <= 1.7976931348623157e308);
+    else if (kind == 2) bad |= !(v > 0.0);
+    else bad |= !(v > 0.0 && v <= 1.7976931348623157e308);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1.0;
+}
+
+__global__ void k_check_bounded_int(const int* __restrict__ y, long long n, int lo, int hi,
+                                    double* flag) {
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    bad |= y[i] < lo || y[i] > hi;
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1.0;
+}
+
+inline int grid_for(long long tot, int cap = 4096) {
+  long long g = (tot + 255) / 256;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int smg_transpose(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
+                  double beta) {
+  if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
+  if (m == 0 || n == 0) return SMG_OK;
+  if (!A || !B || lda < m || ldb < n) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_transpose, dim3(smg_ceil_div(m, TT), smg_ceil_div(n, TT)), dim3(256), 0,
+                     ctx->stream, m, n, A, lda, B, ldb, beta);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_shift(smg_ctx* ctx, int m, int n, double c, double* Y, int ldy, int uplo) {
+  if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
+  if (m == 0 || n == 0 || c == 0.0) return SMG_OK;
+  if (!Y || ldy < m) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_shift, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n,
+                     c, Y, ldy, uplo);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_dot(smg_ctx* ctx, const double* x, const double* y, long long n, double* out) {
+  if (!ctx || n < 0 || !out) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!x || !y) return SMG_ERR_ARG;
+  const int nb = grid_for(n, 1024);
+  double* part = smg_ws(ctx, SMG_WS_RED, (size_t)nb);
+  if (!part) return SMG_ERR_OOM;
+  hipLaunchKernelGGL(k_dot_part, dim3(nb), dim3(256), 0, ctx->stream, x, y, n, part);
+  smg_reduce_partials(ctx, part, nb, 1, out, 1);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_check_domain(smg_ctx* ctx, const double* x, long long n, int kind, double* flag) {
+  if (!ctx || n < 0 || !flag || kind < 0 || kind > 3) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!x) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_check_domain, dim3(grid_for(n, 1024)), dim3(256), 0, ctx->stream, x, n,
+                     kind, flag);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_check_bounded_int(smg_ctx* ctx, const int* y, long long n, int lo, int hi, double* flag) {
+  if (!ctx || n < 0 || !flag) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!y) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_check_bounded_int, dim3(grid_for(n, 1024)), dim3(256), 0, ctx->stream, y,
+                     n, lo, hi, flag);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+}  // extern "C"

@@ -75,6 +75,11 @@ _SIGS = {
     "smg_axpy_dev": (_I, [_P, _L, _P, _P, _P]),
     "smg_sum": (_I, [_P, _P, _L, _P]),
     "smg_copy_matrix": (_I, [_P, _I, _I, _P, _I, _P, _I, _I, _I]),
+    "smg_transpose": (_I, [_P, _I, _I, _P, _I, _P, _I, _D]),
+    "smg_shift": (_I, [_P, _I, _I, _D, _P, _I, _I]),
+    "smg_dot": (_I, [_P, _P, _P, _L, _P]),
+    "smg_check_domain": (_I, [_P, _P, _L, _I, _P]),
+    "smg_check_bounded_int": (_I, [_P, _P, _L, _I, _I, _P]),
     "smg_comm_unique_id": (_I, [ctypes.c_char_p]),
     "smg_comm_init": (_I, [_P, _I, _I, ctypes.c_char_p]),
     "smg_comm_allreduce_sum": (_I, [_P, _P, _L]),

@@ -7,11 +7,19 @@
 #include <Eigen/Dense>
 #define STAN_MATH_AMD_HAS_EIGEN 1
 
+#include <stan/math/rev/core/var.hpp>
+#include <stan/math/eigen/num_traits.hpp>
 #include <stan/math/rev/core.hpp>
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/fun/gp_exp_quad_cov.hpp>
 #include <stan/math/rev/fun/cholesky_decompose.hpp>
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
+#include <stan/math/rev/fun/multiply.hpp>
+#include <stan/math/rev/fun/mdivide_left_tri.hpp>
+#include <stan/math/rev/fun/log_sum_exp.hpp>
+#include <stan/math/rev/fun/lgamma.hpp>
+#include <stan/math/rev/fun/normal_lpdf.hpp>
+#include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
 #include <stan/math/rev/functor/gradient.hpp>
 #include <stan/math/eigen/interop.hpp>
 

@@ -17,8 +17,10 @@
 
 #include <stan/math/amd/device.hpp>
 #include <stan/math/rev/core/grad.hpp>
+#include <stan/math/rev/core/var.hpp>
 #include <stan/math/rev/core/vari.hpp>
 
+#include <stdexcept>
 #include <vector>
 
 namespace stan {
@@ -125,6 +127,71 @@ inline dev_var_matrix to_dev_var_matrix(const double* host_colmajor, int rows, i
   auto* vi = new dev_matrix_vari(rows, cols);
   amd::to_device(vi->val_, host_colmajor, size_t(rows) * cols);
   return dev_var_matrix(vi);
+}
+
+namespace internal {
+// device -> host varis (reverse: host adjoints -> device adjoint)
+class dev_to_host_vari : public vari {
+ public:
+  dev_matrix_vari* src_;
+  vari** elems_;
+  double* stage_;  // device scratch for the gathered adjoints
+  dev_to_host_vari(dev_matrix_vari* src, vari** elems)
+      : vari(0.0), src_(src), elems_(elems), stage_(amd::alloc_doubles(src->size())) {}
+  void chain() override {
+    const size_t n = src_->size();
+    std::vector<double> h(n);
+    for (size_t i = 0; i < n; ++i) h[i] = elems_[i]->adj_;
+    amd::to_device(stage_, h.data(), n);
+    amd::check(smg_axpy(amd::ctx(), (long long)n, 1.0, stage_, 1, src_->adj_, 1), "to_host");
+  }
+};
+
+// host varis -> device (reverse: device adjoint -> host adjoints)
+class host_to_dev_vari : public vari {
+ public:
+  dev_matrix_vari* dst_;
+  vari** elems_;
+  host_to_dev_vari(dev_matrix_vari* dst, vari** elems) : vari(0.0), dst_(dst), elems_(elems) {}
+  void chain() override {
+    const size_t n = dst_->size();
+    std::vector<double> h(n);
+    amd::to_host(h.data(), dst_->adj_, n);
+    for (size_t i = 0; i < n; ++i) elems_[i]->adj_ += h[i];
+  }
+};
+}  // namespace internal
+
+/** Host vars (column-major; a column vector by default) -> device node
+ * (bridged in the reverse sweep). */
+inline dev_var_matrix to_dev(const std::vector<var>& v, int rows = -1, int cols = 1) {
+  const size_t n = v.size();
+  if (rows < 0) rows = int(n);
+  if (size_t(rows) * size_t(cols) != n) throw std::invalid_argument("to_dev: rows * cols != size");
+  auto* d = new dev_matrix_vari(rows, cols);
+  std::vector<double> vals(n);
+  vari** elems = ChainableStack::instance_->memalloc_.alloc_array<vari*>(n ? n : 1);
+  for (size_t i = 0; i < n; ++i) {
+    vals[i] = v[i].val();
+    elems[i] = v[i].vi_;
+  }
+  amd::to_device(d->val_, vals.data(), n);
+  new internal::host_to_dev_vari(d, elems);
+  return dev_var_matrix(d);
+}
+
+/** Device node -> host vars, column-major (bridged in the reverse sweep). */
+inline std::vector<var> to_var_vector(const dev_var_matrix& m) {
+  const size_t n = m.size();
+  std::vector<double> vals = m.val();
+  vari** elems = ChainableStack::instance_->memalloc_.alloc_array<vari*>(n ? n : 1);
+  std::vector<var> out(n);
+  for (size_t i = 0; i < n; ++i) {
+    elems[i] = new vari(vals[i], false);
+    out[i] = var(elems[i]);
+  }
+  new internal::dev_to_host_vari(m.vi_, elems);
+  return out;
 }
 
 }  // namespace math

@@ -24,35 +24,18 @@
 #include <stan/math/rev/core.hpp>
 #include <stan/math/rev/fun/cholesky_decompose.hpp>
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
+#include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
+#include <stan/math/rev/fun/lgamma.hpp>
+#include <stan/math/rev/fun/log_sum_exp.hpp>
+#include <stan/math/rev/fun/mdivide_left_tri.hpp>
+#include <stan/math/rev/fun/multiply.hpp>
+#include <stan/math/rev/fun/normal_lpdf.hpp>
 #include <stan/math/rev/functor/gradient.hpp>
 
 #include <limits>
 #include <vector>
 
-namespace Eigen {
-// NumTraits for var (reference: rev/mat/fun/Eigen_NumTraits.hpp:20-60)
-template <>
-struct NumTraits<stan::math::var> : GenericNumTraits<stan::math::var> {
-  using Real = stan::math::var;
-  using NonInteger = stan::math::var;
-  using Nested = stan::math::var;
-  using Literal = stan::math::var;
-  static inline Real epsilon() { return std::numeric_limits<double>::epsilon(); }
-  static inline Real dummy_precision() { return 1e-12; }
-  static inline Real highest() { return std::numeric_limits<double>::max(); }
-  static inline Real lowest() { return -std::numeric_limits<double>::max(); }
-  enum {
-    IsComplex = 0,
-    IsInteger = 0,
-    IsSigned = 1,
-    RequireInitialization = 0,
-    ReadCost = 1,
-    AddCost = 1,
-    MulCost = 1
-  };
-  static inline int digits10() { return std::numeric_limits<double>::digits10; }
-};
-}  // namespace Eigen
+#include <stan/math/eigen/num_traits.hpp>
 
 namespace stan {
 namespace math {
@@ -69,36 +52,6 @@ struct var_vector_of<Eigen::Matrix<double, Eigen::Dynamic, 1>> {
   using type = Eigen::Matrix<var, Eigen::Dynamic, 1>;
 };
 
-// device -> host varis (reverse: host adjoints -> device adjoint)
-class dev_to_host_vari : public vari {
- public:
-  dev_matrix_vari* src_;
-  vari** elems_;
-  double* stage_;  // device scratch for the gathered adjoints
-  dev_to_host_vari(dev_matrix_vari* src, vari** elems)
-      : vari(0.0), src_(src), elems_(elems), stage_(amd::alloc_doubles(src->size())) {}
-  void chain() override {
-    const size_t n = src_->size();
-    std::vector<double> h(n);
-    for (size_t i = 0; i < n; ++i) h[i] = elems_[i]->adj_;
-    amd::to_device(stage_, h.data(), n);
-    amd::check(smg_axpy(amd::ctx(), (long long)n, 1.0, stage_, 1, src_->adj_, 1), "to_host");
-  }
-};
-
-// host varis -> device (reverse: device adjoint -> host adjoints)
-class host_to_dev_vari : public vari {
- public:
-  dev_matrix_vari* dst_;
-  vari** elems_;
-  host_to_dev_vari(dev_matrix_vari* dst, vari** elems) : vari(0.0), dst_(dst), elems_(elems) {}
-  void chain() override {
-    const size_t n = dst_->size();
-    std::vector<double> h(n);
-    amd::to_host(h.data(), dst_->adj_, n);
-    for (size_t i = 0; i < n; ++i) elems_[i]->adj_ += h[i];
-  }
-};
 }  // namespace internal
 
 /** Materialise a device matrix of vars as host varis. */
@@ -166,10 +119,104 @@ inline matrix_v cholesky_decompose(const matrix_v& A) {
   return to_host_matrix(cholesky_decompose(to_dev(A)));
 }
 
+inline dev_data<double> to_dev_data(const matrix_d& m) {
+  return to_dev_data(m.data(), size_t(m.size()), int(m.rows()), int(m.cols()));
+}
+
+/** multiply.hpp:619-661 signatures (Matrix<var> / Matrix<double> operands). */
+inline matrix_v multiply(const matrix_v& A, const matrix_v& B) {
+  internal::check_multiplicable("multiply", int(A.rows()), int(A.cols()), int(B.rows()), int(B.cols()));
+  return to_host_matrix(multiply(to_dev(A), to_dev(B)));
+}
+inline matrix_v multiply(const matrix_v& A, const matrix_d& B) {
+  internal::check_multiplicable("multiply", int(A.rows()), int(A.cols()), int(B.rows()), int(B.cols()));
+  return to_host_matrix(multiply(to_dev(A), to_dev_data(B)));
+}
+inline matrix_v multiply(const matrix_d& A, const matrix_v& B) {
+  internal::check_multiplicable("multiply", int(A.rows()), int(A.cols()), int(B.rows()), int(B.cols()));
+  return to_host_matrix(multiply(to_dev_data(A), to_dev(B)));
+}
+inline matrix_v multiply(const var& c, const matrix_v& A) { return to_host_matrix(multiply(c, to_dev(A))); }
+inline matrix_v multiply(const matrix_v& A, const var& c) { return multiply(c, A); }
+inline matrix_v multiply(double c, const matrix_v& A) { return to_host_matrix(multiply(c, to_dev(A))); }
+inline matrix_v multiply(const matrix_v& A, double c) { return multiply(c, A); }
+
+/** prim/mat/fun/transpose.hpp: a plain Eigen transpose (shares the varis). */
+template <typename T, int R, int C>
+inline Eigen::Matrix<T, C, R> transpose(const Eigen::Matrix<T, R, C>& m) {
+  return m.transpose();
+}
+
+template <int R, int C>
+inline var sum(const Eigen::Matrix<var, R, C>& m) {
+  return sum(to_dev(m));
+}
+inline matrix_v add_diag(const matrix_v& A, double d) { return to_host_matrix(add_diag(to_dev(A), d)); }
+inline matrix_v add_diag(const matrix_v& A, const var& d) {
+  return to_host_matrix(add_diag(to_dev(A), d));
+}
+
+template <int R, int C>
+inline var log_sum_exp(const Eigen::Matrix<var, R, C>& x) {
+  return log_sum_exp(to_dev(x));
+}
+template <int R, int C>
+inline Eigen::Matrix<var, R, C> lgamma(const Eigen::Matrix<var, R, C>& x) {
+  matrix_v m = to_host_matrix(lgamma(to_dev(x)));
+  return Eigen::Map<Eigen::Matrix<var, R, C>>(m.data(), x.rows(), x.cols());
+}
+template <int R, int C>
+inline Eigen::Matrix<var, R, C> digamma(const Eigen::Matrix<var, R, C>& x) {
+  matrix_v m = to_host_matrix(digamma(to_dev(x)));
+  return Eigen::Map<Eigen::Matrix<var, R, C>>(m.data(), x.rows(), x.cols());
+}
+
+/** mdivide_left_tri<TriView>(A, b), rev/mat/fun/mdivide_left_tri.hpp:322-373. */
+template <int TriView, int R2, int C2>
+inline Eigen::Matrix<var, Eigen::Dynamic, C2> mdivide_left_tri(const matrix_v& A,
+                                                               const Eigen::Matrix<var, R2, C2>& b) {
+  matrix_v m = to_host_matrix(mdivide_left_tri<TriView>(to_dev(A), to_dev(b)));
+  return Eigen::Map<Eigen::Matrix<var, Eigen::Dynamic, C2>>(m.data(), m.rows(), m.cols());
+}
+template <int TriView, int R2, int C2>
+inline Eigen::Matrix<var, Eigen::Dynamic, C2> mdivide_left_tri(
+    const matrix_d& A, const Eigen::Matrix<var, R2, C2>& b) {
+  matrix_v m = to_host_matrix(mdivide_left_tri<TriView>(to_dev_data(A), to_dev(b)));
+  return Eigen::Map<Eigen::Matrix<var, Eigen::Dynamic, C2>>(m.data(), m.rows(), m.cols());
+}
+template <int TriView, int R2, int C2>
+inline Eigen::Matrix<var, Eigen::Dynamic, C2> mdivide_left_tri(
+    const matrix_v& A, const Eigen::Matrix<double, R2, C2>& b) {
+  const matrix_d bd = b;
+  matrix_v m = to_host_matrix(mdivide_left_tri<TriView>(to_dev(A), to_dev_data(bd)));
+  return Eigen::Map<Eigen::Matrix<var, Eigen::Dynamic, C2>>(m.data(), m.rows(), m.cols());
+}
+template <int TriView>
+inline matrix_v mdivide_left_tri(const matrix_v& A) {
+  return to_host_matrix(mdivide_left_tri<TriView>(to_dev(A)));
+}
+
+/** bernoulli_logit_glm_lpmf(y, x, alpha, beta) with Eigen x / beta (:46-144). */
+template <bool propto = false, typename T_alpha, int RB>
+inline var bernoulli_logit_glm_lpmf(const std::vector<int>& y, const matrix_d& x,
+                                    const T_alpha& alpha, const Eigen::Matrix<var, RB, 1>& beta) {
+  std::vector<var> b(beta.data(), beta.data() + beta.size());
+  std::vector<double> xv(x.data(), x.data() + x.size());
+  if (y.size() != size_t(x.rows()))
+    throw std::invalid_argument(
+        "bernoulli_logit_glm_lpmf: Vector of dependent variables has dimension = " +
+        std::to_string(y.size()) + ", expecting dimension = " + std::to_string(x.rows()));
+  return bernoulli_logit_glm_lpmf<propto>(y, xv, int(x.cols()), alpha, b);
+}
+
 template <bool propto = false>
 inline var multi_normal_cholesky_lpdf(const vector_d& y, const vector_d& mu, const dev_var_matrix& L) {
   std::vector<double> yv(y.data(), y.data() + y.size()), mv(mu.data(), mu.data() + mu.size());
   return multi_normal_cholesky_lpdf<propto>(yv, mv, L);
+}
+template <bool propto = false>
+inline var multi_normal_cholesky_lpdf(const vector_v& y, const vector_v& mu, const matrix_v& L) {
+  return multi_normal_cholesky_lpdf<propto>(to_dev(y), to_dev(mu), to_dev(L));
 }
 template <bool propto = false>
 inline var multi_normal_cholesky_lpdf(const vector_d& y, const vector_d& mu, const matrix_v& L) {

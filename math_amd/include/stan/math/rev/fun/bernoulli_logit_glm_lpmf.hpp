@@ -1,0 +1,264 @@
+#ifndef STAN_MATH_REV_FUN_BERNOULLI_LOGIT_GLM_LPMF_HPP
+#define STAN_MATH_REV_FUN_BERNOULLI_LOGIT_GLM_LPMF_HPP
+
+// bernoulli_logit_glm_lpmf<propto>(y | x, alpha, beta), scalar intercept
+// (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-144), with x and y resident
+// on the device: ONE fused pass over x yields [logp, sum theta', x^T theta']
+// (smg_bernoulli_logit_glm), read back with the y-bounds flag in one copy.
+// Semantics kept: check_consistent_size of y / beta (:63-64), check_bounded(y,
+// 0, 1) (:69), size_zero -> 0 (:71-73), include_summand<propto, x, alpha,
+// beta> (:75-77), the non-finite logp checks of beta, alpha, then the linear
+// predictor (:106-110), partials beta' = x^T theta', alpha' = sum theta'
+// (:113-135) in one precomputed-gradients node.
+//
+// Row sharding (the reduce_sum / map_rect path): each rank
+// holds a contiguous row block of (y, x) on its own GPU (glm_shard); every
+// rank computes its local [logp, alpha', beta'] and ONE RCCL all-reduce sums
+// the M + 2 doubles across ranks (smg_comm_allreduce_sum); every rank then
+// builds the same node.  Replaces map_rect's MPI/TBB gather
+// (prim/mat/functor/map_rect.hpp:120-177, map_rect_combine.hpp:36-92).
+
+#include <stan/math/amd/matrix.hpp>
+#include <stan/math/rev/core.hpp>
+#include <stan/math/rev/fun/normal_lpdf.hpp>
+
+#include <cmath>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+namespace stan {
+namespace math {
+
+namespace amd {
+/** Join this process to an RCCL communicator (one per process / GPU).
+ * id: 128 bytes from smg_comm_unique_id on rank 0, shared by the launcher. */
+inline void comm_init(int nranks, int rank, const char* id) {
+  check(smg_comm_init(ctx(), nranks, rank, id), "comm_init");
+}
+inline void comm_destroy() {
+  if (has_ctx()) check(smg_comm_destroy(ctx()), "comm_destroy");
+}
+}  // namespace amd
+
+/** Device-resident GLM data: a row block [row0, row0 + rows) of y and x.
+ * x: rows x M column-major with leading dimension ldx (ldx >= rows). */
+struct glm_shard {
+  const int* y = nullptr;
+  const double* x = nullptr;
+  long long rows = 0;
+  int M = 0;
+  long long ldx = 0;
+  long long row0 = 0;      // first global row (bookkeeping)
+  long long total_rows = 0;
+  bool distributed = false;  // all-reduce across the communicator
+};
+
+/** Contiguous row partition used by every sharded reducer: rank r of W owns
+ * rows [r*R/W, (r+1)*R/W) (integer division), so the blocks tile [0, R). */
+inline void row_partition(long long R, int world, int rank, long long* begin, long long* end) {
+  *begin = R * rank / world;
+  *end = R * (rank + 1) / world;
+}
+
+namespace internal {
+
+class glm_dev_vari : public vari {
+ public:
+  vari* alpha_vi_;
+  vari** beta_vi_;           // host varis of beta (null when beta is data / on device)
+  dev_matrix_vari* beta_dev_;  // device beta vars
+  double* g_;                // [alpha', beta'(M)] on host (arena)
+  const double* g_dev_;      // beta' on device
+  int M_;
+  glm_dev_vari(double lp, vari* a, vari** b, dev_matrix_vari* bd, double* g, const double* gd, int M)
+      : vari(lp), alpha_vi_(a), beta_vi_(b), beta_dev_(bd), g_(g), g_dev_(gd), M_(M) {}
+  void chain() override {
+    if (alpha_vi_) alpha_vi_->adj_ += adj_ * g_[0];
+    if (beta_vi_)
+      for (int j = 0; j < M_; ++j) beta_vi_[j]->adj_ += adj_ * g_[1 + j];
+    if (beta_dev_)
+      amd::check(smg_axpy(amd::ctx(), M_, adj_, g_dev_, 1, beta_dev_->adj_, 1),
+                 "bernoulli_logit_glm_lpmf");
+  }
+};
+
+struct glm_params {
+  double alpha = 0;
+  vari* alpha_vi = nullptr;
+  std::vector<double> beta;       // host values (for upload and the finite check)
+  vari** beta_vi = nullptr;       // host beta varis
+  dev_matrix_vari* beta_dev = nullptr;
+  bool any_var() const { return alpha_vi || beta_vi || beta_dev; }
+};
+
+inline void glm_alpha(glm_params& p, double a) { p.alpha = a; }
+inline void glm_alpha(glm_params& p, const var& a) {
+  p.alpha = a.val();
+  p.alpha_vi = a.vi_;
+}
+inline void glm_beta(glm_params& p, const std::vector<double>& b) { p.beta = b; }
+inline void glm_beta(glm_params& p, const std::vector<var>& b) {
+  p.beta.resize(b.size());
+  p.beta_vi = ChainableStack::instance_->memalloc_.alloc_array<vari*>(b.size() ? b.size() : 1);
+  for (size_t j = 0; j < b.size(); ++j) {
+    p.beta[j] = b[j].val();
+    p.beta_vi[j] = b[j].vi_;
+  }
+}
+inline void glm_beta(glm_params& p, const dev_var_matrix& b) {
+  p.beta = b.val();
+  p.beta_dev = b.vi_;
+}
+
+struct glm_result {
+  double lp = 0.0;
+  vari* node = nullptr;  // null: constant result
+};
+
+template <bool propto>
+inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
+  static const char* fn = "bernoulli_logit_glm_lpmf";
+  const int M = s.M;
+  if (int(p.beta.size()) != M) {
+    std::ostringstream m;
+    m << fn << ": Weight vector has dimension = " << p.beta.size()
+      << ", expecting dimension = " << M
+      << "; a function was called with arguments of different scalar, array, vector, or matrix "
+         "types, and they were not consistently sized;  all arguments must be scalars or "
+         "multidimensional values of the same shape.";
+    throw std::invalid_argument(m.str());
+  }
+  smg_ctx* c = amd::ctx();
+  // [alpha, beta(M) | out: logp, alpha', beta'(M) | flag]
+  double* buf = amd::alloc_doubles(size_t(2 * M + 4));
+  double* ab = buf;
+  double* out = buf + M + 1;
+  double* flag = buf + 2 * M + 3;
+  std::vector<double> h(size_t(2 * M + 4), 0.0);
+  h[0] = p.alpha;
+  for (int j = 0; j < M; ++j) h[1 + j] = p.beta[j];
+  amd::to_device(buf, h.data(), h.size());
+  amd::check(smg_check_bounded_int(c, s.y, s.rows, 0, 1, flag), fn);
+  if (s.rows > 0) {
+    double* ws = amd::alloc_doubles(size_t(smg_glm_ws_doubles(s.rows, M)));
+    amd::check(smg_bernoulli_logit_glm(c, s.y, s.x, s.rows, M, s.ldx, ab, ws, out), fn);
+  }
+  if (s.distributed) amd::check(smg_comm_allreduce_sum(c, out, M + 2), fn);
+  amd::to_host(h.data(), buf, h.size());
+  if (h[2 * M + 3] != 0.0)
+    throw std::domain_error(std::string(fn) +
+                            ": Vector of dependent variables is out of bounds, but must be in the "
+                            "interval [0, 1]");
+  if (s.total_rows == 0 || !(p.any_var() || !propto)) return glm_result{};
+  const double lp = h[M + 1];
+  if (!std::isfinite(lp)) {
+    for (int j = 0; j < M; ++j)
+      if (!std::isfinite(p.beta[j])) {
+        std::ostringstream m;
+        m << fn << ": Weight vector[" << j + 1 << "] is " << p.beta[j] << ", but must be finite!";
+        throw std::domain_error(m.str());
+      }
+    if (!std::isfinite(p.alpha)) {
+      std::ostringstream m;
+      m << fn << ": Intercept is " << p.alpha << ", but must be finite!";
+      throw std::domain_error(m.str());
+    }
+    throw std::domain_error(std::string(fn) +
+                            ": Matrix of independent variables is not finite, but must be finite!");
+  }
+  if (!p.any_var()) return glm_result{lp, nullptr};
+  double* g = ChainableStack::instance_->memalloc_.alloc_array<double>(size_t(M + 1));
+  for (int j = 0; j <= M; ++j) g[j] = h[M + 2 + j];
+  return glm_result{lp, new glm_dev_vari(lp, p.alpha_vi, p.beta_vi, p.beta_dev, g, out + 2, M)};
+}
+
+template <typename T>
+struct glm_is_var
+    : std::integral_constant<bool, !std::is_same<T, double>::value &&
+                                       !std::is_same<T, std::vector<double>>::value> {};
+
+}  // namespace internal
+
+/** Device-resident (y, x) -- the config-4 layout; one GPU or one shard. */
+template <bool propto, typename T_alpha, typename T_beta>
+inline typename std::conditional<internal::glm_is_var<T_alpha>::value ||
+                                     internal::glm_is_var<T_beta>::value,
+                                 var, double>::type
+bernoulli_logit_glm_lpmf(const glm_shard& s, const T_alpha& alpha, const T_beta& beta) {
+  internal::glm_params p;
+  internal::glm_alpha(p, alpha);
+  internal::glm_beta(p, beta);
+  const internal::glm_result r = internal::glm_eval<propto>(s, p);
+  if (r.node) return typename std::conditional<internal::glm_is_var<T_alpha>::value ||
+                                                   internal::glm_is_var<T_beta>::value,
+                                               var, double>::type(var(r.node));
+  return typename std::conditional<internal::glm_is_var<T_alpha>::value ||
+                                       internal::glm_is_var<T_beta>::value,
+                                   var, double>::type(r.lp);
+}
+
+template <bool propto, typename T_alpha, typename T_beta>
+inline auto bernoulli_logit_glm_lpmf(const dev_data<int>& y, const dev_data<double>& x,
+                                     const T_alpha& alpha, const T_beta& beta) {
+  static const char* fn = "bernoulli_logit_glm_lpmf";
+  if ((long long)y.size() != (long long)x.rows()) {
+    std::ostringstream m;
+    m << fn << ": Vector of dependent variables has dimension = " << y.size()
+      << ", expecting dimension = " << x.rows()
+      << "; a function was called with arguments of different scalar, array, vector, or matrix "
+         "types, and they were not consistently sized;  all arguments must be scalars or "
+         "multidimensional values of the same shape.";
+    throw std::invalid_argument(m.str());
+  }
+  glm_shard s;
+  s.y = y.data();
+  s.x = x.data();
+  s.rows = x.rows();
+  s.M = x.cols();
+  s.ldx = x.rows();
+  s.total_rows = s.rows;
+  return bernoulli_logit_glm_lpmf<propto>(s, alpha, beta);
+}
+
+template <typename T_alpha, typename T_beta>
+inline auto bernoulli_logit_glm_lpmf(const dev_data<int>& y, const dev_data<double>& x,
+                                     const T_alpha& alpha, const T_beta& beta) {
+  return bernoulli_logit_glm_lpmf<false>(y, x, alpha, beta);
+}
+
+/** Host data (uploaded per call, like the reference reading host memory). */
+template <bool propto, typename T_alpha, typename T_beta>
+inline auto bernoulli_logit_glm_lpmf(const std::vector<int>& y, const std::vector<double>& x_colmajor,
+                                     int M, const T_alpha& alpha, const T_beta& beta) {
+  const int R = int(y.size());
+  if ((long long)x_colmajor.size() != (long long)R * M)
+    throw std::invalid_argument("bernoulli_logit_glm_lpmf: x must hold y.size() * M values");
+  dev_data<int> yd = to_dev_data(y);
+  dev_data<double> xd = to_dev_data(x_colmajor.data(), x_colmajor.size(), R, M);
+  return bernoulli_logit_glm_lpmf<propto>(yd, xd, alpha, beta);
+}
+
+template <typename T_alpha, typename T_beta>
+inline auto bernoulli_logit_glm_lpmf(const std::vector<int>& y, const std::vector<double>& x_colmajor,
+                                     int M, const T_alpha& alpha, const T_beta& beta) {
+  return bernoulli_logit_glm_lpmf<false>(y, x_colmajor, M, alpha, beta);
+}
+
+/**
+ * Row-sharded reducer (reduce_sum-style entry point): `shard` holds this
+ * rank's rows with shard.distributed = true and the communicator joined via
+ * amd::comm_init; every rank calls it with the same (alpha, beta) and gets the
+ * full-data log density and gradient.
+ */
+template <bool propto = false, typename T_alpha, typename T_beta>
+inline auto reduce_sum_bernoulli_logit_glm(const glm_shard& shard, const T_alpha& alpha,
+                                           const T_beta& beta) {
+  return bernoulli_logit_glm_lpmf<propto>(shard, alpha, beta);
+}
+
+}  // namespace math
+}  // namespace stan
+#endif

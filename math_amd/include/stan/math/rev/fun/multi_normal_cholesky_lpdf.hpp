@@ -8,7 +8,8 @@
 // device; when L is a cholesky_decompose output (structurally lower) the
 // upper-triangle partials land on the reference's dummy vari and are skipped,
 // which removes the explicit O(n^3) inverse (see math_amd/csrc/mvn.hip).
-// y and mu are data here (double); y or mu as vars go through the host path.
+// y and mu may be data (double / dev_data) or device vectors of vars: the
+// reverse adds -adj sd into y' and +adj sd into mu' (:139-146).
 // With L a var, propto = true drops only the constant NEG_LOG_SQRT_TWO_PI
 // term (include_summand<propto>, :107-109).
 
@@ -30,14 +31,18 @@ class mvn_cholesky_dev_vari : public vari {
   dev_matrix_vari* L_;
   const double* ws_;  // [w, sd] on device
   int n_;
+  dev_matrix_vari* y_;   // null when y is data
+  dev_matrix_vari* mu_;  // null when mu is data
 
-  mvn_cholesky_dev_vari(double lp, dev_matrix_vari* L, const double* ws)
-      : vari(lp), L_(L), ws_(ws), n_(L->rows_) {}
+  mvn_cholesky_dev_vari(double lp, dev_matrix_vari* L, const double* ws,
+                        dev_matrix_vari* y = nullptr, dev_matrix_vari* mu = nullptr)
+      : vari(lp), L_(L), ws_(ws), n_(L->rows_), y_(y), mu_(mu) {}
 
   void chain() override {
     const int lower_only = L_->structure_ == dev_structure::lower ? 1 : 0;
     amd::check(smg_mvn_cholesky_rev(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, adj_, lower_only,
-                                    nullptr, nullptr, L_->adj_, n_),
+                                    y_ ? y_->adj_ : nullptr, mu_ ? mu_->adj_ : nullptr, L_->adj_,
+                                    n_),
                "multi_normal_cholesky_lpdf");
   }
 };
@@ -55,7 +60,8 @@ inline void mvn_check_sizes(int ny, int nmu, const dev_var_matrix& L) {
 }
 
 template <bool propto>
-inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const dev_var_matrix& L) {
+inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const dev_var_matrix& L,
+                            dev_matrix_vari* y_vi = nullptr, dev_matrix_vari* mu_vi = nullptr) {
   const char* fn = "multi_normal_cholesky_lpdf";
   if (n == 0) return var(0.0);
   smg_ctx* c = amd::ctx();
@@ -65,7 +71,7 @@ inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const 
   double lp = 0;
   amd::to_host(&lp, lp_d, 1);
   if (propto) lp -= -std::log(std::sqrt(2.0 * 3.14159265358979323846)) * n;
-  return var(new mvn_cholesky_dev_vari(lp, L.vi_, ws));
+  return var(new mvn_cholesky_dev_vari(lp, L.vi_, ws, y_vi, mu_vi));
 }
 
 inline void mvn_check_data(const std::vector<double>& y, const std::vector<double>* mu) {
@@ -108,6 +114,22 @@ inline var multi_normal_cholesky_lpdf(const dev_data<double>& y, const dev_data<
                                       const dev_var_matrix& L) {
   internal::mvn_check_sizes(int(y.size()), int(mu.size()), L);
   return internal::mvn_cholesky_dev<propto>(y.data(), mu.data(), int(y.size()), L);
+}
+
+/** y and mu as device vectors of vars. */
+template <bool propto = false>
+inline var multi_normal_cholesky_lpdf(const dev_var_matrix& y, const dev_var_matrix& mu,
+                                      const dev_var_matrix& L) {
+  internal::mvn_check_sizes(int(y.size()), int(mu.size()), L);
+  return internal::mvn_cholesky_dev<propto>(y.val_ptr(), mu.val_ptr(), int(y.size()), L, y.vi_,
+                                            mu.vi_);
+}
+template <bool propto = false>
+inline var multi_normal_cholesky_lpdf(const dev_var_matrix& y, const dev_data<double>& mu,
+                                      const dev_var_matrix& L) {
+  internal::mvn_check_sizes(int(y.size()), int(mu.size()), L);
+  return internal::mvn_cholesky_dev<propto>(y.val_ptr(), mu.data(), int(y.size()), L, y.vi_,
+                                            nullptr);
 }
 
 }  // namespace math

@@ -1,0 +1,178 @@
+#ifndef STAN_MATH_REV_FUN_MULTIPLY_HPP
+#define STAN_MATH_REV_FUN_MULTIPLY_HPP
+
+// multiply / transpose / sum on device matrices of vars.
+//
+// multiply (rev/mat/fun/multiply.hpp:619-661, multiply_mat_vari :35-552):
+//   C = A B;  reverse Aadj += Cadj B^T, Badj += A^T Cadj (MFMA fp64 GEMMs,
+//   smg_multiply_*).  var*var, var*double and double*var operand kinds, and
+//   scalar * matrix (:562-600): B = c A, Aadj += c Badj, c' += <Badj, A>.
+// Same size check as :623-625 (check_multiplicable) before the tape is touched.
+//
+// transpose: the reference's transpose(Matrix<var>) shares the varis; here it
+// is a node whose reverse adds Badj^T into Aadj (one tiled copy each way).
+//
+// sum (rev/mat/fun/sum.hpp:18-60): value = deterministic device reduction;
+// reverse Aadj += adj.  On a structurally lower matrix (cholesky_decompose
+// output) the upper entries are the reference's dummy vari and get nothing.
+
+#include <stan/math/amd/matrix.hpp>
+#include <stan/math/rev/core.hpp>
+
+#include <sstream>
+#include <stdexcept>
+
+namespace stan {
+namespace math {
+
+namespace internal {
+
+inline void check_multiplicable(const char* fn, int a_rows, int a_cols, int b_rows, int b_cols) {
+  (void)a_rows;
+  (void)b_cols;
+  if (a_cols != b_rows) {
+    std::ostringstream m;
+    m << fn << ": Columns of m1 (" << a_cols << ") and Rows of m2 (" << b_rows
+      << ") must match in size";
+    throw std::invalid_argument(m.str());
+  }
+}
+
+/** One operand of a matrix functor: a device var node or constant device data. */
+struct dev_operand {
+  dev_matrix_vari* vi = nullptr;  // null for data
+  const double* data = nullptr;
+  int rows = 0, cols = 0;
+  const double* val() const { return vi ? vi->val_ : data; }
+  double* adj() const { return vi ? vi->adj_ : nullptr; }
+};
+inline dev_operand operand(const dev_var_matrix& m) {
+  return dev_operand{m.vi_, nullptr, m.rows(), m.cols()};
+}
+inline dev_operand operand(const dev_data<double>& d) {
+  return dev_operand{nullptr, d.data(), d.rows(), d.cols()};
+}
+
+class multiply_dev_vari : public vari {
+ public:
+  dev_operand A_, B_;
+  dev_matrix_vari* C_;
+  multiply_dev_vari(const dev_operand& A, const dev_operand& B)
+      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A.rows, B.cols)) {
+    amd::check(smg_multiply_fwd(amd::ctx(), A_.val(), A_.rows, B_.val(), B_.rows, A_.rows, A_.cols,
+                                B_.cols, C_->val_, C_->rows_),
+               "multiply");
+  }
+  void chain() override {
+    amd::check(smg_multiply_rev(amd::ctx(), A_.val(), A_.rows, B_.val(), B_.rows, C_->adj_,
+                                C_->rows_, A_.rows, A_.cols, B_.cols, A_.adj(), A_.rows, B_.adj(),
+                                B_.rows),
+               "multiply");
+  }
+};
+
+class scale_dev_vari : public vari {
+ public:
+  dev_operand A_;
+  double c_;
+  vari* c_vi_;   // null when c is data
+  double* cadj_;  // device scalar
+  dev_matrix_vari* B_;
+  scale_dev_vari(const dev_operand& A, double c, vari* c_vi)
+      : vari(0.0), A_(A), c_(c), c_vi_(c_vi), cadj_(c_vi ? amd::alloc_doubles(1) : nullptr),
+        B_(new dev_matrix_vari(A.rows, A.cols)) {
+    smg_ctx* x = amd::ctx();
+    const long long n = (long long)A.rows * A.cols;
+    amd::check(smg_memset(x, B_->val_, 0, size_t(n) * sizeof(double)), "multiply");
+    amd::check(smg_axpy(x, n, c_, A_.val(), 1, B_->val_, 1), "multiply");
+  }
+  void chain() override {
+    smg_ctx* x = amd::ctx();
+    const long long n = (long long)A_.rows * A_.cols;
+    if (A_.adj()) amd::check(smg_axpy(x, n, c_, B_->adj_, 1, A_.adj(), 1), "multiply");
+    if (c_vi_) {
+      amd::check(smg_memset(x, cadj_, 0, sizeof(double)), "multiply");
+      amd::check(smg_dot(x, B_->adj_, A_.val(), n, cadj_), "multiply");
+      add_pending_adjoint(c_vi_, cadj_);
+    }
+  }
+};
+
+class transpose_dev_vari : public vari {
+ public:
+  dev_matrix_vari* A_;
+  dev_matrix_vari* B_;
+  explicit transpose_dev_vari(dev_matrix_vari* A)
+      : vari(0.0), A_(A), B_(new dev_matrix_vari(A->cols_, A->rows_)) {
+    amd::check(smg_transpose(amd::ctx(), A_->rows_, A_->cols_, A_->val_, A_->rows_, B_->val_,
+                             B_->rows_, 0.0),
+               "transpose");
+  }
+  void chain() override {
+    amd::check(smg_transpose(amd::ctx(), B_->rows_, B_->cols_, B_->adj_, B_->rows_, A_->adj_,
+                             A_->rows_, 1.0),
+               "transpose");
+  }
+};
+
+class sum_dev_vari : public vari {
+ public:
+  dev_matrix_vari* A_;
+  sum_dev_vari(double v, dev_matrix_vari* A) : vari(v), A_(A) {}
+  void chain() override {
+    const int uplo = A_->structure_ == dev_structure::lower ? 1 : 0;
+    amd::check(smg_shift(amd::ctx(), A_->rows_, A_->cols_, adj_, A_->adj_, A_->rows_, uplo), "sum");
+  }
+};
+
+inline dev_var_matrix multiply_dev(const dev_operand& A, const dev_operand& B) {
+  check_multiplicable("multiply", A.rows, A.cols, B.rows, B.cols);
+  auto* node = new multiply_dev_vari(A, B);
+  return dev_var_matrix(node->C_);
+}
+
+}  // namespace internal
+
+inline dev_var_matrix multiply(const dev_var_matrix& A, const dev_var_matrix& B) {
+  return internal::multiply_dev(internal::operand(A), internal::operand(B));
+}
+inline dev_var_matrix multiply(const dev_var_matrix& A, const dev_data<double>& B) {
+  return internal::multiply_dev(internal::operand(A), internal::operand(B));
+}
+inline dev_var_matrix multiply(const dev_data<double>& A, const dev_var_matrix& B) {
+  return internal::multiply_dev(internal::operand(A), internal::operand(B));
+}
+inline dev_var_matrix multiply(const var& c, const dev_var_matrix& A) {
+  auto* node = new internal::scale_dev_vari(internal::operand(A), c.val(), c.vi_);
+  return dev_var_matrix(node->B_);
+}
+inline dev_var_matrix multiply(const dev_var_matrix& A, const var& c) { return multiply(c, A); }
+inline dev_var_matrix multiply(double c, const dev_var_matrix& A) {
+  auto* node = new internal::scale_dev_vari(internal::operand(A), c, nullptr);
+  return dev_var_matrix(node->B_);
+}
+inline dev_var_matrix multiply(const dev_var_matrix& A, double c) { return multiply(c, A); }
+inline dev_var_matrix multiply(const var& c, const dev_data<double>& A) {
+  auto* node = new internal::scale_dev_vari(internal::operand(A), c.val(), c.vi_);
+  return dev_var_matrix(node->B_);
+}
+
+inline dev_var_matrix transpose(const dev_var_matrix& A) {
+  auto* node = new internal::transpose_dev_vari(A.vi_);
+  return dev_var_matrix(node->B_);
+}
+
+inline var sum(const dev_var_matrix& A) {
+  if (A.size() == 0) return var(0.0);
+  smg_ctx* c = amd::ctx();
+  double* s = amd::alloc_doubles(1);
+  amd::check(smg_memset(c, s, 0, sizeof(double)), "sum");
+  amd::check(smg_sum(c, A.val_ptr(), (long long)A.size(), s), "sum");
+  double v = 0;
+  amd::to_host(&v, s, 1);
+  return var(new internal::sum_dev_vari(v, A.vi_));
+}
+
+}  // namespace math
+}  // namespace stan
+#endif

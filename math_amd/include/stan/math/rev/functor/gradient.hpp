@@ -10,6 +10,7 @@
 // (Eigen::VectorXd as in the reference, or std::vector<double>); f receives
 // the same container type over var.
 
+#include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/core.hpp>
 
 #include <type_traits>
@@ -39,6 +40,33 @@ void gradient(const F& f, const Vec& x, double& fx, Vec& grad_fx) {
     grad(fx_var.vi_);
     grad_fx.resize(x.size());
     for (size_t i = 0; i < size_t(x.size()); ++i) grad_fx[i] = x_var[i].adj();
+  } catch (const std::exception& e) {
+    recover_memory_nested();
+    throw;
+  }
+  recover_memory_nested();
+}
+
+/**
+ * gradient() with a device-resident independent matrix: x (rows x cols,
+ * column-major, device) becomes ONE dev_matrix_vari leaf, f receives it as a
+ * dev_var_matrix, and the gradient is copied device-to-device into grad_dev
+ * (rows * cols doubles).  Same nesting / recovery contract as above; this is
+ * the form for functions of N^2 parameters (config 2: A -> sum(chol(A A^T + N I)))
+ * where the reference materialises N^2 host varis.
+ */
+template <typename F>
+void gradient(const F& f, const dev_data<double>& x, double& fx, double* grad_dev) {
+  start_nested();
+  try {
+    smg_ctx* c = amd::ctx();
+    auto* leaf = new dev_matrix_vari(x.rows(), x.cols());
+    const size_t n = leaf->size();
+    amd::check(smg_memcpy_d2d(c, leaf->val_, x.data(), n * sizeof(double)), "gradient");
+    var fx_var = f(dev_var_matrix(leaf));
+    fx = fx_var.val();
+    grad(fx_var.vi_);
+    amd::check(smg_memcpy_d2d(c, grad_dev, leaf->adj_, n * sizeof(double)), "gradient");
   } catch (const std::exception& e) {
     recover_memory_nested();
     throw;

@@ -1,0 +1,522 @@
+// Drives every §8 functor of the header-only stan::math layer on the device.
+// Reads one command and its inputs from stdin (written by
+// tests/test_cpp_functors.py from the golden fixtures), prints the values and
+// gradients as %.17g for comparison with the reference's.
+//
+//   mulchol N nsamp idx...        config 2 via the device-leaf gradient
+//   mulchol_eigen N               config 2 via Eigen Matrix<var> (host varis)
+//   multiply kind m k n A B W     f = sum(W .* multiply(A, B))
+//   mdivide lower kind m n A B W  f = sum(W .* mdivide_left_tri<TriView>(A, B))
+//   lse N x                       log_sum_exp(std::vector<var>) and (Matrix<var>)
+//   lse_pair n a b                log_sum_exp(var, var)
+//   special n x                   lgamma(var), digamma(var) values + derivatives
+//   special_vec X(200) W(200)     f = sum(W .* (lgamma(X) + 0.5 digamma(X))), Matrix<var> 10x20
+//   normal N theta                gradient of normal_lpdf(theta | 0, 1)
+//   normal_vec y mu sigma (9)     all var vectors; f, f(propto), gradients
+//   normal_known y mu sigma (4)   double arguments -> values
+//   glm R M nb beta               device-filled (x, y); single call and 32 row shards
+//   glm_data R M x y theta        explicit data (cutoff branches)
+//   mvn N y mu L                  multi_normal_cholesky_lpdf, every argument var (Eigen)
+//   errors                        the reference's exceptions
+#include <stan/math.hpp>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstdio>
+#include <iostream>
+#include <string>
+#include <vector>
+
+using namespace stan::math;
+
+// tokens through strtod so inf / -inf / nan parse like any other value
+static std::vector<double> read_vec(size_t n) {
+  std::vector<double> v(n);
+  std::string t;
+  for (auto& x : v) {
+    std::cin >> t;
+    x = std::strtod(t.c_str(), nullptr);
+  }
+  return v;
+}
+static void print(const char* tag, const std::vector<double>& v) {
+  std::printf("%s", tag);
+  for (double x : v) std::printf(" %.17g", x);
+  std::printf("\n");
+}
+static void print1(const char* tag, double v) { std::printf("%s %.17g\n", tag, v); }
+
+static std::vector<var> vars(const std::vector<double>& v) {
+  return std::vector<var>(v.begin(), v.end());
+}
+static std::vector<double> adjs(const std::vector<var>& v) {
+  std::vector<double> g(v.size());
+  for (size_t i = 0; i < v.size(); ++i) g[i] = v[i].adj();
+  return g;
+}
+// sum_i w_i * c_i over host vars (scalar tape ops)
+static var wdot(const std::vector<double>& w, const std::vector<var>& c) {
+  var s = 0.0;
+  for (size_t i = 0; i < w.size(); ++i) s += w[i] * c[i];
+  return s;
+}
+
+static void cmd_mulchol() {
+  int N, ns;
+  std::cin >> N >> ns;
+  std::vector<long long> idx(ns);
+  for (auto& i : idx) std::cin >> i;
+  smg_ctx* c = amd::ctx();
+  const size_t nn = size_t(N) * N;
+  double* A = amd::alloc_doubles(nn);
+  double* G = amd::alloc_doubles(nn);
+  amd::check(smg_fill_unif(c, A, (long long)nn, 20260101ull + 2, -1.0, 1.0, std::sqrt(3.0 / N)), "fill");
+  auto f = [N](const dev_var_matrix& a) {
+    return sum(cholesky_decompose(add_diag(multiply(a, transpose(a)), double(N))));
+  };
+  for (int rep = 0; rep < 2; ++rep) {
+    double fx;
+    gradient(f, dev_data<double>(A, nn, N, N), fx, G);
+    std::vector<double> g(nn);
+    amd::to_host(g.data(), G, nn);
+    double s = 0, l2 = 0;
+    for (double v : g) {
+      s += v;
+      l2 += v * v;
+    }
+    print1("fx", fx);
+    print1("grad_sum", s);
+    print1("grad_l2", std::sqrt(l2));
+    std::vector<double> samp;
+    if (ns == 0)
+      samp = g;
+    else
+      for (long long i : idx) samp.push_back(g[i]);
+    print("grad", samp);
+  }
+}
+
+static void cmd_mulchol_eigen() {
+  int N;
+  std::cin >> N;
+  std::vector<double> a = read_vec(size_t(N) * N);
+  Eigen::VectorXd x = Eigen::Map<Eigen::VectorXd>(a.data(), a.size()), g;
+  double fx;
+  auto f = [N](const vector_v& v) {
+    matrix_v A(N, N);
+    for (int i = 0; i < N * N; ++i) A(i) = v(i);
+    matrix_v C = multiply(A, transpose(A));
+    matrix_v Cd = add_diag(C, double(N));
+    return sum(cholesky_decompose(Cd));
+  };
+  gradient(f, x, fx, g);
+  print1("fx", fx);
+  print("grad", std::vector<double>(g.data(), g.data() + g.size()));
+}
+
+static void cmd_multiply() {
+  int kind, m, k, n;
+  std::cin >> kind >> m >> k >> n;
+  auto A = read_vec(size_t(m) * k), B = read_vec(size_t(k) * n), W = read_vec(size_t(m) * n);
+  start_nested();
+  std::vector<var> av = vars(A), bv = vars(B);
+  dev_var_matrix C;
+  if (kind == 0) C = multiply(to_dev(av, m, k), to_dev(bv, k, n));
+  if (kind == 1) C = multiply(to_dev(av, m, k), to_dev_data(B.data(), B.size(), k, n));
+  if (kind == 2) C = multiply(to_dev_data(A.data(), A.size(), m, k), to_dev(bv, k, n));
+  var f = wdot(W, to_var_vector(C));
+  f.grad();
+  print1("fx", f.val());
+  print1("fx_C0", C.val()[0]);
+  print("C", C.val());
+  print("grad_A", kind == 2 ? std::vector<double>(A.size(), 0.0) : adjs(av));
+  print("grad_B", kind == 1 ? std::vector<double>(B.size(), 0.0) : adjs(bv));
+  recover_memory_nested();
+  // Eigen signature, var * var
+  if (kind == 0) {
+    start_nested();
+    matrix_v Ae(m, k), Be(k, n);
+    for (int i = 0; i < m * k; ++i) Ae(i) = A[i];
+    for (int i = 0; i < k * n; ++i) Be(i) = B[i];
+    matrix_v Ce = multiply(Ae, Be);
+    var fe = 0.0;
+    for (int i = 0; i < m * n; ++i) fe += W[i] * Ce(i);
+    fe.grad();
+    std::vector<double> ga(m * k);
+    for (int i = 0; i < m * k; ++i) ga[i] = Ae(i).adj();
+    print1("fx_eigen", fe.val());
+    print("grad_A_eigen", ga);
+    recover_memory_nested();
+  }
+}
+
+static void cmd_mdivide() {
+  int lower, kind, m, n;
+  std::cin >> lower >> kind >> m >> n;
+  auto A = read_vec(size_t(m) * m), B = read_vec(size_t(m) * n), W = read_vec(size_t(m) * n);
+  start_nested();
+  std::vector<var> av = vars(A), bv = vars(B);
+  dev_var_matrix C;
+  auto Ad = [&]() { return to_dev(av, m, m); };
+  auto Bd = [&]() { return to_dev(bv, m, n); };
+  auto Ac = to_dev_data(A.data(), A.size(), m, m);
+  auto Bc = to_dev_data(B.data(), B.size(), m, n);
+  if (lower) {
+    if (kind == 0) C = mdivide_left_tri<1>(Ad(), Bd());
+    if (kind == 1) C = mdivide_left_tri<1>(Ac, Bd());
+    if (kind == 2) C = mdivide_left_tri<1>(Ad(), Bc);
+  } else {
+    if (kind == 0) C = mdivide_left_tri<2>(Ad(), Bd());
+    if (kind == 1) C = mdivide_left_tri<2>(Ac, Bd());
+    if (kind == 2) C = mdivide_left_tri<2>(Ad(), Bc);
+  }
+  var f = wdot(W, to_var_vector(C));
+  f.grad();
+  print1("fx", f.val());
+  print("C", C.val());
+  print("grad_A", kind == 1 ? std::vector<double>(A.size(), 0.0) : adjs(av));
+  print("grad_B", kind == 2 ? std::vector<double>(B.size(), 0.0) : adjs(bv));
+  recover_memory_nested();
+}
+
+static void cmd_lse() {
+  int N;
+  std::cin >> N;
+  auto x = read_vec(N);
+  start_nested();
+  std::vector<var> xv = vars(x);
+  var f = log_sum_exp(xv);
+  f.grad();
+  print1("fx", f.val());
+  print("grad", adjs(xv));
+  recover_memory_nested();
+  start_nested();
+  vector_v xe(N);
+  for (int i = 0; i < N; ++i) xe(i) = x[i];
+  var fe = log_sum_exp(xe);
+  fe.grad();
+  std::vector<double> g(N);
+  for (int i = 0; i < N; ++i) g[i] = xe(i).adj();
+  print1("fx_eigen", fe.val());
+  print("grad_eigen", g);
+  recover_memory_nested();
+}
+
+static void cmd_lse_pair() {
+  int n;
+  std::cin >> n;
+  auto a = read_vec(n), b = read_vec(n);
+  std::vector<double> f(n), ga(n), gb(n);
+  for (int i = 0; i < n; ++i) {
+    start_nested();
+    var av = a[i], bv = b[i];
+    var r = log_sum_exp(av, bv);
+    r.grad();
+    f[i] = r.val();
+    ga[i] = av.adj();
+    gb[i] = bv.adj();
+    recover_memory_nested();
+  }
+  print("f", f);
+  print("grad_a", ga);
+  print("grad_b", gb);
+}
+
+static void cmd_special() {
+  int n;
+  std::cin >> n;
+  auto x = read_vec(n);
+  std::vector<double> lg(n), dg(n), glg(n), gdg(n);
+  for (int i = 0; i < n; ++i) {
+    start_nested();
+    var a = x[i];
+    var y = lgamma(a);
+    y.grad();
+    lg[i] = y.val();
+    glg[i] = a.adj();
+    recover_memory_nested();
+    start_nested();
+    var b = x[i];
+    var z = digamma(b);
+    z.grad();
+    dg[i] = z.val();
+    gdg[i] = b.adj();
+    recover_memory_nested();
+  }
+  print("lgamma", lg);
+  print("digamma", dg);
+  print("grad_lgamma", glg);
+  print("grad_digamma", gdg);
+  // vectorised device path over the same inputs (values only)
+  start_nested();
+  std::vector<var> xv = vars(x);
+  std::vector<var> l = lgamma(xv), d = digamma(xv);
+  std::vector<double> lv(n), dv(n);
+  for (int i = 0; i < n; ++i) {
+    lv[i] = l[i].val();
+    dv[i] = d[i].val();
+  }
+  print("lgamma_dev", lv);
+  print("digamma_dev", dv);
+  recover_memory_nested();
+}
+
+static void cmd_special_vec() {
+  auto X = read_vec(200), W = read_vec(200);
+  start_nested();
+  matrix_v Xe(10, 20);
+  for (int i = 0; i < 200; ++i) Xe(i) = X[i];
+  matrix_v L = lgamma(Xe), D = digamma(Xe);
+  var f = 0.0;
+  for (int i = 0; i < 200; ++i) f += W[i] * (L(i) + 0.5 * D(i));
+  f.grad();
+  std::vector<double> g(200);
+  for (int i = 0; i < 200; ++i) g[i] = Xe(i).adj();
+  print1("fx", f.val());
+  print("grad", g);
+  recover_memory_nested();
+}
+
+static void cmd_normal() {
+  int N;
+  std::cin >> N;
+  auto th = read_vec(N);
+  double fx;
+  std::vector<double> g;
+  for (int rep = 0; rep < 2; ++rep) {
+    gradient([](const std::vector<var>& t) { return normal_lpdf(t, 0.0, 1.0); }, th, fx, g);
+    print1("fx", fx);
+    print("grad", g);
+  }
+  // device-resident parameters (dev_var_matrix) through the same functor
+  start_nested();
+  auto d = to_dev_var_matrix(th.data(), N, 1);
+  var f = normal_lpdf(d, 0.0, 1.0);
+  f.grad();
+  print1("fx_dev", f.val());
+  print("grad_dev", d.adj());
+  recover_memory_nested();
+}
+
+static void cmd_normal_vec() {
+  auto y = read_vec(9), mu = read_vec(9), s = read_vec(9);
+  start_nested();
+  std::vector<var> yv = vars(y), mv = vars(mu), sv = vars(s);
+  var f = normal_lpdf(yv, mv, sv);
+  f.grad();
+  print1("fx", f.val());
+  print("grad_y", adjs(yv));
+  print("grad_mu", adjs(mv));
+  print("grad_sigma", adjs(sv));
+  var fp = normal_lpdf<true>(yv, mv, sv);
+  print1("fx_propto", fp.val());
+  recover_memory_nested();
+}
+
+static void cmd_normal_known() {
+  auto y = read_vec(4), mu = read_vec(4), s = read_vec(4);
+  std::vector<double> out(4);
+  for (int i = 0; i < 4; ++i) out[i] = normal_lpdf(y[i], mu[i], s[i]);
+  print("values", out);
+  // propto with all-double arguments drops every term (include_summand)
+  print1("propto_double", normal_lpdf<true>(y[0], mu[0], s[0]));
+}
+
+static void cmd_glm() {
+  long long R;
+  int M;
+  std::cin >> R >> M;
+  auto beta = read_vec(M);
+  smg_ctx* c = amd::ctx();
+  // resident data outside any nested tape (like the MPI data cache)
+  int* y = amd::alloc_ints(size_t(R));
+  double* x = amd::alloc_doubles(size_t(R) * M);
+  amd::check(smg_fill_unif(c, x, R * M, 20260101ull + 41, -1.0, 1.0, std::sqrt(3.0)), "fill");
+  amd::check(smg_fill_bernoulli(c, y, R, 20260101ull + 42, 0.5), "fill");
+  std::vector<double> th(M + 1);
+  th[0] = 0.1;
+  for (int j = 0; j < M; ++j) th[1 + j] = beta[j];
+  dev_data<int> yd(y, size_t(R), int(R), 1);
+  dev_data<double> xd(x, size_t(R) * M, int(R), M);
+  double fx;
+  std::vector<double> g;
+  for (int rep = 0; rep < 2; ++rep) {
+    gradient(
+        [&](const std::vector<var>& t) {
+          std::vector<var> b(t.begin() + 1, t.end());
+          return bernoulli_logit_glm_lpmf(yd, xd, t[0], b);
+        },
+        th, fx, g);
+    print1("fx", fx);
+    print("grad", g);
+  }
+  // 32 contiguous row shards summed on the tape (the map_rect32 decomposition)
+  gradient(
+      [&](const std::vector<var>& t) {
+        std::vector<var> b(t.begin() + 1, t.end());
+        var s = 0.0;
+        for (int k = 0; k < 32; ++k) {
+          long long b0, b1;
+          row_partition(R, 32, k, &b0, &b1);
+          glm_shard sh;
+          sh.y = y + b0;
+          sh.x = x + b0;
+          sh.rows = b1 - b0;
+          sh.M = M;
+          sh.ldx = R;
+          sh.row0 = b0;
+          sh.total_rows = R;
+          s += bernoulli_logit_glm_lpmf<false>(sh, t[0], b);
+        }
+        return s;
+      },
+      th, fx, g);
+  print1("fx_shards32", fx);
+  print("grad_shards32", g);
+}
+
+static void cmd_glm_data() {
+  int R, M;
+  std::cin >> R >> M;
+  auto xv = read_vec(size_t(R) * M), yv = read_vec(R), th = read_vec(M + 1);
+  std::vector<int> y(R);
+  for (int i = 0; i < R; ++i) y[i] = int(yv[i]);
+  double fx;
+  std::vector<double> g;
+  gradient(
+      [&](const std::vector<var>& t) {
+        std::vector<var> b(t.begin() + 1, t.end());
+        return bernoulli_logit_glm_lpmf(y, xv, M, t[0], b);
+      },
+      th, fx, g);
+  print1("fx", fx);
+  print("grad", g);
+  // Eigen signature (x MatrixXd, beta Matrix<var,-1,1>)
+  start_nested();
+  matrix_d xe = Eigen::Map<matrix_d>(xv.data(), R, M);
+  vector_v be(M);
+  for (int j = 0; j < M; ++j) be(j) = th[1 + j];
+  var a = th[0];
+  var f = bernoulli_logit_glm_lpmf(y, xe, a, be);
+  f.grad();
+  std::vector<double> ge(M + 1);
+  ge[0] = a.adj();
+  for (int j = 0; j < M; ++j) ge[1 + j] = be(j).adj();
+  print1("fx_eigen", f.val());
+  print("grad_eigen", ge);
+  recover_memory_nested();
+}
+
+static void cmd_mvn() {
+  int N;
+  std::cin >> N;
+  auto y = read_vec(N), mu = read_vec(N), L = read_vec(size_t(N) * N);
+  start_nested();
+  std::vector<var> yv = vars(y), mv = vars(mu), Lv = vars(L);
+  matrix_v Le(N, N);
+  for (int i = 0; i < N * N; ++i) Le(i) = Lv[i];
+  vector_v ye(N), me(N);
+  for (int i = 0; i < N; ++i) {
+    ye(i) = yv[i];
+    me(i) = mv[i];
+  }
+  var f = multi_normal_cholesky_lpdf(ye, me, Le);
+  f.grad();
+  print1("fx", f.val());
+  print("grad_y", adjs(yv));
+  print("grad_mu", adjs(mv));
+  print("grad_L", adjs(Lv));
+  recover_memory_nested();
+}
+
+template <typename F>
+static void expect_throw(const char* name, F&& f) {
+  start_nested();
+  try {
+    f();
+    std::printf("%s nothrow\n", name);
+  } catch (const std::domain_error& e) {
+    std::printf("%s domain_error %s\n", name, e.what());
+  } catch (const std::invalid_argument& e) {
+    std::printf("%s invalid_argument %s\n", name, e.what());
+  } catch (const std::exception& e) {
+    std::printf("%s other %s\n", name, e.what());
+  }
+  recover_memory_nested();
+}
+
+static void cmd_errors() {
+  const double nan = std::nan("");
+  expect_throw("normal_nan_y", [&] { normal_lpdf(std::vector<var>{1.0, nan}, 0.0, 1.0); });
+  expect_throw("normal_inf_mu", [&] { normal_lpdf(var(1.0), INFINITY, 1.0); });
+  expect_throw("normal_neg_sigma", [&] { normal_lpdf(var(1.0), 0.0, -1.0); });
+  expect_throw("normal_sizes",
+               [&] { normal_lpdf(std::vector<var>{1.0, 2.0}, std::vector<double>{0, 0, 0}, 1.0); });
+  expect_throw("multiply_sizes", [&] {
+    auto A = to_dev_var_matrix(std::vector<double>(6, 1.0).data(), 2, 3);
+    multiply(A, A);
+  });
+  expect_throw("mdivide_square", [&] {
+    auto A = to_dev_var_matrix(std::vector<double>(6, 1.0).data(), 2, 3);
+    mdivide_left_tri<1>(A, A);
+  });
+  expect_throw("chol_not_symmetric", [&] {
+    std::vector<double> a = {2, 1, 0, 2};
+    cholesky_decompose(to_dev_var_matrix(a.data(), 2, 2));
+  });
+  expect_throw("chol_not_pd", [&] {
+    std::vector<double> a = {1, 2, 2, 1};
+    cholesky_decompose(to_dev_var_matrix(a.data(), 2, 2));
+  });
+  expect_throw("glm_y_bounds", [&] {
+    bernoulli_logit_glm_lpmf(std::vector<int>{0, 2}, std::vector<double>{1, 2}, 1, var(0.0),
+                             std::vector<var>{1.0});
+  });
+  expect_throw("glm_beta_size", [&] {
+    bernoulli_logit_glm_lpmf(std::vector<int>{0, 1}, std::vector<double>{1, 2}, 1, var(0.0),
+                             std::vector<var>{1.0, 2.0});
+  });
+  expect_throw("glm_nonfinite_beta", [&] {
+    bernoulli_logit_glm_lpmf(std::vector<int>{0, 1}, std::vector<double>{1, 2}, 1, var(0.0),
+                             std::vector<var>{INFINITY});
+  });
+  // empty containers
+  start_nested();
+  var e1 = log_sum_exp(std::vector<var>{});
+  std::printf("lse_empty %.17g\n", e1.val());
+  var e2 = normal_lpdf(std::vector<var>{}, 0.0, 1.0);
+  std::printf("normal_empty %.17g\n", e2.val());
+  recover_memory_nested();
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
+int main() {
+  std::string cmd;
+  std::cin >> cmd;
+  try {
+    if (cmd == "mulchol") cmd_mulchol();
+    else if (cmd == "mulchol_eigen") cmd_mulchol_eigen();
+    else if (cmd == "multiply") cmd_multiply();
+    else if (cmd == "mdivide") cmd_mdivide();
+    else if (cmd == "lse") cmd_lse();
+    else if (cmd == "lse_pair") cmd_lse_pair();
+    else if (cmd == "special") cmd_special();
+    else if (cmd == "special_vec") cmd_special_vec();
+    else if (cmd == "normal") cmd_normal();
+    else if (cmd == "normal_vec") cmd_normal_vec();
+    else if (cmd == "normal_known") cmd_normal_known();
+    else if (cmd == "glm") cmd_glm();
+    else if (cmd == "glm_data") cmd_glm_data();
+    else if (cmd == "mvn") cmd_mvn();
+    else if (cmd == "errors") cmd_errors();
+    else {
+      std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
+      return 2;
+    }
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "exception: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -39,7 +39,7 @@ def test_python_binding_covers_header():
 
 
 def test_cpp_programs_built():
-    for name in ("test_gp_tape",):
+    for name in ("test_gp_tape", "test_functors"):
         assert os.path.exists(os.path.join(BIN, name)), f"{name} not built (run __graft_entry__.build())"
 
 
