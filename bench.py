@@ -1,22 +1,29 @@
 #!/usr/bin/env python3
-"""bench.py — gradient evals/sec (fp64) of the GP-marginal log-density, N=4096.
+"""bench.py — gradient evals/sec (fp64) of the BASELINE configs on MI355X.
 
-BASELINE.json metric: "gradient evals/sec (fp64), GP-marginal log-density
-N=4096, 1->8 MI355X".  One step = one stan::math::gradient() of
+Default workload (BASELINE.json metric, config 3): the GP-marginal
+log-density at N=4096.  One step = one stan::math::gradient() of
   multi_normal_cholesky_lpdf(y | 0, cholesky_decompose(add_diag(
       gp_exp_quad_cov(x, alpha, rho), sigma^2)))
 wrt (alpha, rho, sigma) through the header-only drop-in layer
 (math_amd/include/stan/...) and libsmg_hip.so, inputs x, y = the reference
 harness's config-3 inputs (tests/golden/gp_N4096.json), resident in HBM.
-
 The GP does not shard (one dense factorisation): with --gpus N every rank runs
-an independent replica on its own GPU ("replicas only"); value =
-total evals over all ranks / max-over-ranks wall time.
+an independent replica ("replicas only"), value = total evals over
+all ranks / max-over-ranks wall time.
 
-Also reports, for the dominant kernel family (the fp64 MFMA GEMM), its
-algorithmic flops / HIP-event time over a profiled copy of the timed region,
-and the reference CPU path (oracle/_ref/ref_harness, the real Stan Math
-3.0.0 compiled from /root/reference) timed on one host core.
+--workload glm (config 4): bernoulli_logit_glm_lpmf gradient, R=1e7 rows x
+M=256 covariates, rows partitioned over the ranks (row_partition), x and y
+generated in HBM before the timed region, ONE RCCL all-reduce of the M+2
+[logp, alpha', beta'] doubles per eval (strong scaling: fixed total work).
+
+--workload mulchol (config 2): gradient of sum(cholesky_decompose(add_diag(
+multiply(A, A^T), N))) wrt all N^2 entries of A, N=2048, A resident in HBM.
+
+Each line also carries the roofline of the dominant kernel family (algorithmic
+work / HIP-event time over a profiled copy of the timed region) and, on rank 0
+at N=1, the reference CPU path (oracle/_ref/ref_harness: the real Stan Math
+3.0.0 compiled from /root/reference) timed on one host core on a bounded sample.
 """
 import argparse
 import ctypes
@@ -31,30 +38,224 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_FP64_TFLOPS = 78.6  # MI355X fp64 (vector = matrix), MI355X_MICROARCH.md / BASELINE.md §3
-N_GP = 4096
+PEAK_FP64_TFLOPS = 78.6  # MI355X fp64 dense (vector = matrix), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0    # MI355X HBM3E, MI355X_MICROARCH.md
+SEED = 20260101
+D = ctypes.POINTER(ctypes.c_double)
 
 
-def load_inputs():
-    with open(os.path.join(ROOT, "tests", "golden", f"gp_N{N_GP}.json")) as f:
-        d = json.load(f)
-    return (np.array(d["x"], dtype=np.float64), np.array(d["y"], dtype=np.float64),
-            np.array(d["theta"], dtype=np.float64), d)
+def ptr(a):
+    return a.ctypes.data_as(D)
 
 
-def cpu_baseline(timeout=300):
+def ref_bench(cfg, n, reps=1, timeout=300):
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(exe):
         return None
-    try:
-        out = subprocess.run([exe, "bench", "gp", str(N_GP), "1"], capture_output=True, text=True,
-                             timeout=timeout, env=dict(os.environ, OMP_NUM_THREADS="1"))
-        r = json.loads(out.stdout.strip().splitlines()[-1])
+    out = subprocess.run([exe, "bench", cfg, str(n), str(reps)], capture_output=True, text=True,
+                         timeout=timeout, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def unif(seed, n, a, b):
+    """oracle/gen.h SplitMix64 uniforms (numpy mirror, tests/gen.py)."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return a + (b - a) * ((z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0))
+
+
+class Workload:
+    """init() puts the data in HBM; step() is one gradient eval; guard() checks parity."""
+
+    def __init__(self, bl, args, rank, world, local, dist):
+        self.bl, self.args, self.rank, self.world, self.local, self.dist = bl, args, rank, world, local, dist
+        self.fx = np.zeros(1)
+
+
+class GP(Workload):
+    N = 4096
+    metric = "gradient evals/sec (fp64), GP-marginal log-density N=4096"
+    scaling = "weak"
+
+    def init(self):
+        bl = self.bl
+        bl.smg_bench_gp_init.argtypes = [ctypes.c_int, ctypes.c_int, D, D]
+        bl.smg_bench_gp_step.argtypes = [D, D, D]
+        with open(os.path.join(ROOT, "tests", "golden", f"gp_N{self.N}.json")) as f:
+            self.gold = json.load(f)
+        self.x = np.array(self.gold["x"], dtype=np.float64)
+        self.y = np.array(self.gold["y"], dtype=np.float64)
+        self.theta = np.array(self.gold["theta"], dtype=np.float64)
+        self.g = np.zeros(3)
+        return bl.smg_bench_gp_init(self.local, self.N, ptr(self.x), ptr(self.y))
+
+    def step(self):
+        return self.bl.smg_bench_gp_step(ptr(self.theta), ptr(self.fx), ptr(self.g))
+
+    def guard(self):
+        want = np.array(self.gold["grad"])
+        rel = np.abs(self.g - want) / np.abs(want)
+        ok = rel.max() < 1e-10 and abs(self.fx[0] - self.gold["fx"]) < 1e-9 * abs(self.gold["fx"])
+        return ok, f"fx={self.fx[0]!r} grad={self.g} vs {self.gold['fx']} {self.gold['grad']}"
+
+    def units_per_step(self):
+        return self.world  # one eval per replica
+
+    def config(self):
+        return {"workload": "gp_marginal_gradient", "N": self.N, "kernel": "exp_quad",
+                "parallelism": f"replicas{self.world}", "path": "stan::math::gradient via header-only layer"}
+
+    data = "synthetic (reference harness config-3 inputs: x~U(-10,10), y=sin(x)+0.3eps; theta=(1,1.5,0.3))"
+
+    def roofline(self, fams, steps, t_prof):
+        ms, n, fl = fams["gemm"]
+        ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
+        ev = self.N ** 3 / (t_prof / steps) / 1e12
+        return {"bound": "mfma", "kernel": "k_gemm (fp64 MFMA, all launches of the family)",
+                "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP64_TFLOPS if ach else None, "traffic": None,
+                "launches_per_step": n / steps, "flops_per_launch": fl / max(n, 1),
+                "avg_launch_ms": ms / max(n, 1), "eval_achieved": ev, "eval_frac": ev / PEAK_FP64_TFLOPS,
+                "eval_flops": "N^3 (chol fwd N^3/3 + Murray adjoint 2N^3/3), SURVEY.md §8(d)"}
+
+    def cpu_baseline(self):
+        r = ref_bench("gp", self.N, 1)
+        if r is None:
+            return None
         return {"value": r["evals_per_sec"], "unit": "gradient evals/s", "cores": 1, "kind": "reference",
-                "sample": f"1 gradient eval of the GP marginal at N={N_GP} (Stan Math 3.0.0 compiled from "
-                          f"/root/reference by oracle/Makefile; {r['seconds_per_eval']:.2f} s)"}
-    except Exception as e:  # noqa: BLE001
-        return {"value": None, "error": str(e)[:200]}
+                "sample": f"1 gradient eval of the GP marginal at N={self.N} (Stan Math 3.0.0 compiled "
+                          f"from /root/reference by oracle/Makefile; {r['seconds_per_eval']:.2f} s)"}
+
+
+class GLM(Workload):
+    M = 256
+    metric = "gradient evals/sec (fp64), bernoulli_logit_glm_lpmf 1e7 rows x 256"
+    scaling = "strong"
+
+    def init(self):
+        bl = self.bl
+        self.R = int(self.args.rows)
+        bl.smg_bench_glm_init.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_char_p]
+        bl.smg_bench_glm_step.argtypes = [D, D, D]
+        bl.smg_bench_glm_local_rows.restype = ctypes.c_longlong
+        comm_id = None
+        if self.world > 1:  # RCCL unique id from rank 0, shared over the gloo group
+            from math_amd import hip
+            buf = ctypes.create_string_buffer(128)
+            obj = [None]
+            if self.rank == 0:
+                if hip.lib().smg_comm_unique_id(buf) != 0:
+                    raise SystemExit("smg_comm_unique_id failed")
+                obj = [bytes(buf.raw)]
+            self.dist.broadcast_object_list(obj, src=0)
+            comm_id = obj[0]
+        beta = unif(SEED + 43, self.M, -1.0, 1.0) * np.sqrt(3.0 / self.M)
+        self.theta = np.concatenate([[0.1], beta])
+        self.g = np.zeros(self.M + 1)
+        rc = bl.smg_bench_glm_init(self.local, self.R, self.M, self.rank, self.world, comm_id)
+        self.rows = bl.smg_bench_glm_local_rows()
+        return rc
+
+    def step(self):
+        return self.bl.smg_bench_glm_step(ptr(self.theta), ptr(self.fx), ptr(self.g))
+
+    def guard(self):
+        # deterministic (fixed-order reductions + one all-reduce): two evals bitwise equal
+        fx0, g0 = self.fx.copy(), self.g.copy()
+        self.step()
+        ok = np.isfinite(fx0[0]) and fx0[0] == self.fx[0] and np.array_equal(g0, self.g)
+        return ok, f"fx {fx0[0]!r} vs {self.fx[0]!r}"
+
+    def units_per_step(self):
+        return 1  # one full-data gradient per step across all ranks
+
+    def config(self):
+        return {"workload": "bernoulli_logit_glm_gradient", "rows": self.R, "covariates": self.M,
+                "rows_per_rank": int(self.rows), "parallelism": f"rows{self.world}+rccl_allreduce",
+                "path": "stan::math::gradient + reduce_sum_bernoulli_logit_glm via header-only layer"}
+
+    data = "synthetic (reference harness config-4 streams: x~U(-sqrt3,sqrt3), y~Bern(0.5), generated in HBM)"
+
+    def roofline(self, fams, steps, t_prof):
+        ms, n, _ = fams["glm"]
+        byts = self.rows * self.M * 8 + self.rows * 4  # one read of x and y (SURVEY.md §8(d))
+        avg = ms / max(n, 1)
+        ach = byts / (avg * 1e-3) / 1e9 if avg > 0 else None
+        return {"bound": "hbm", "kernel": "k_glm_fused (one pass over x)", "achieved": ach,
+                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS if ach else None,
+                "traffic": None, "bytes_per_launch": byts, "avg_launch_ms": avg,
+                "launches_per_step": n / steps}
+
+    def cpu_baseline(self):
+        rs = 1000000
+        r = ref_bench("glm", rs, 1)
+        if r is None:
+            return None
+        per = r["seconds_per_eval"] * self.R / rs  # linear in rows (one pass over x)
+        return {"value": 1.0 / per, "unit": "gradient evals/s", "cores": 1, "kind": "reference",
+                "sample": f"1 gradient eval at {rs} rows x {self.M} (Stan Math 3.0.0, {r['seconds_per_eval']:.2f} s)"
+                          f", scaled x{self.R // rs} to {self.R} rows (linear in rows)"}
+
+
+class MulChol(Workload):
+    N = 2048
+    metric = "gradient evals/sec (fp64), sum(cholesky(A A^T + N I)) N=2048"
+    scaling = "weak"
+
+    def init(self):
+        bl = self.bl
+        bl.smg_bench_mulchol_init.argtypes = [ctypes.c_int, ctypes.c_int]
+        bl.smg_bench_mulchol_step.argtypes = [D, D]
+        with open(os.path.join(ROOT, "tests", "golden", f"mulchol_N{self.N}.json")) as f:
+            self.gold = json.load(f)
+        self.sl = np.zeros(2)
+        return bl.smg_bench_mulchol_init(self.local, self.N)
+
+    def step(self, check=False):
+        return self.bl.smg_bench_mulchol_step(ptr(self.fx), ptr(self.sl) if check else None)
+
+    def guard(self):
+        self.step(check=True)
+        g = self.gold
+        ok = (abs(self.fx[0] - g["fx"]) < 1e-11 * abs(g["fx"])
+              and abs(self.sl[0] - g["grad_sum"]) < 1e-10 * g["grad_l2"] * 10
+              and abs(self.sl[1] - g["grad_l2"]) < 1e-10 * g["grad_l2"])
+        return ok, f"fx={self.fx[0]!r} sum={self.sl[0]!r} l2={self.sl[1]!r} vs {g['fx']} {g['grad_sum']} {g['grad_l2']}"
+
+    def units_per_step(self):
+        return self.world
+
+    def config(self):
+        return {"workload": "multiply_cholesky_gradient", "N": self.N, "parallelism": f"replicas{self.world}",
+                "path": "stan::math::gradient (device-leaf) via header-only layer"}
+
+    data = "synthetic (reference harness config-2 input: A = U(-1,1) sqrt(3/N), generated in HBM)"
+
+    def roofline(self, fams, steps, t_prof):
+        ms, n, fl = fams["gemm"]
+        ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
+        ev = 7 * self.N ** 3 / (t_prof / steps) / 1e12
+        return {"bound": "mfma", "kernel": "k_gemm (fp64 MFMA, all launches of the family)",
+                "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP64_TFLOPS if ach else None, "traffic": None,
+                "launches_per_step": n / steps, "avg_launch_ms": ms / max(n, 1),
+                "eval_achieved": ev, "eval_frac": ev / PEAK_FP64_TFLOPS,
+                "eval_flops": "7N^3 (fwd GEMM 2N^3 + rev 2 GEMM 4N^3 + chol N^3), SURVEY.md §8(d)"}
+
+    def cpu_baseline(self):
+        r = ref_bench("mulchol", self.N, 1)
+        if r is None:
+            return None
+        return {"value": r["evals_per_sec"], "unit": "gradient evals/s", "cores": 1, "kind": "reference",
+                "sample": f"1 gradient eval at N={self.N} (Stan Math 3.0.0, {r['seconds_per_eval']:.2f} s)"}
+
+
+WORKLOADS = {"gp": GP, "glm": GLM, "mulchol": MulChol}
 
 
 def main():
@@ -62,6 +263,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="gp")
+    ap.add_argument("--rows", type=float, default=1e7, help="GLM rows (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -70,28 +273,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch.distributed as dist  # CPU-side barrier/max only (gloo); no data-path collective
+        import torch.distributed as dist  # CPU-side barrier / max / id exchange (gloo)
         dist.init_process_group("gloo")
 
     from math_amd import hip
     bl = ctypes.CDLL(os.path.join(ROOT, "math_amd", "lib", "libsmg_bench.so"))
     bl.smg_bench_ctx.restype = ctypes.c_void_p
     bl.smg_bench_error.restype = ctypes.c_char_p
-    D = ctypes.POINTER(ctypes.c_double)
-    bl.smg_bench_gp_init.argtypes = [ctypes.c_int, ctypes.c_int, D, D]
-    bl.smg_bench_gp_step.argtypes = [D, D, D]
     lib = hip.lib()
-
-    x, y, theta, gold = load_inputs()
-    p = lambda a: a.ctypes.data_as(D)  # noqa: E731
-    if bl.smg_bench_gp_init(local, N_GP, p(x), p(y)) != 0:
+    wl = WORKLOADS[args.workload](bl, args, rank, world, local, dist)
+    if wl.init() != 0:
         raise SystemExit(f"init failed: {bl.smg_bench_error().decode()}")
     ctx = ctypes.c_void_p(bl.smg_bench_ctx())
-    fx = np.zeros(1)
-    g = np.zeros(3)
 
     def step():
-        if bl.smg_bench_gp_step(p(theta), p(fx), p(g)) != 0:
+        if wl.step() != 0:
             raise SystemExit(f"step failed: {bl.smg_bench_error().decode()}")
 
     def barrier():
@@ -116,14 +312,12 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # parity guard on the measured configuration (reference golden values)
-    rel = np.abs(g - np.array(gold["grad"])) / np.abs(np.array(gold["grad"]))
-    if not (rel.max() < 1e-10 and abs(fx[0] - gold["fx"]) < 1e-9 * abs(gold["fx"])):
-        raise SystemExit(f"parity failure: fx={fx[0]!r} grad={g} vs {gold['fx']} {gold['grad']}")
+    ok, msg = wl.guard()  # parity guard on the measured configuration
+    if not ok:
+        raise SystemExit(f"parity failure: {msg}")
 
     t = timed(args.steps)
-    evals = args.steps * world
-    value = evals / t
+    value = args.steps * wl.units_per_step() / t
     ms_per_step = 1e3 * t / args.steps
 
     # profiled copy of the timed region: HIP events on the context stream
@@ -131,11 +325,9 @@ def main():
     tp = timed(args.steps)
     fams = {f: hip.profile_read(lib, ctx, f) for f in hip.FAMILIES}
     lib.smg_profile_enable(ctx, 0)
-    gemm_ms, gemm_n, gemm_fl = fams["gemm"]
-    achieved = gemm_fl / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
 
     line = {
-        "metric": "gradient evals/sec (fp64), GP-marginal log-density N=4096",
+        "metric": wl.metric,
         "value": value,
         "unit": "gradient evals/s",
         "n_gpus": world,
@@ -143,33 +335,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl.scaling,
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (reference harness config-3 inputs: x~U(-10,10), y=sin(x)+0.3eps; theta=(1,1.5,0.3))",
-        "config": {"workload": "gp_marginal_gradient", "N": N_GP, "kernel": "exp_quad",
-                   "parallelism": f"replicas{world}", "path": "stan::math::gradient via header-only layer"},
-        "roofline": {
-            "bound": "mfma",
-            "kernel": "k_gemm (fp64 MFMA, all launches of the family)",
-            "achieved": achieved,
-            "peak": PEAK_FP64_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": (achieved / PEAK_FP64_TFLOPS) if achieved else None,
-            "traffic": None,
-            "launches_per_step": gemm_n / args.steps,
-            "flops_per_launch": gemm_fl / max(gemm_n, 1),
-            "avg_launch_ms": gemm_ms / max(gemm_n, 1),
-            "eval_achieved": (N_GP ** 3) / (tp / args.steps) / 1e12,
-            "eval_frac": (N_GP ** 3) / (tp / args.steps) / 1e12 / PEAK_FP64_TFLOPS,
-            "eval_flops": "N^3 (chol fwd N^3/3 + Murray adjoint 2N^3/3), SURVEY.md §8(d)",
-        },
+        "data": wl.data,
+        "config": wl.config(),
+        "roofline": wl.roofline(fams, args.steps, tp),
         "families_ms_per_step": {f: v[0] / args.steps for f, v in fams.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline()
+        try:
+            line["cpu_baseline"] = wl.cpu_baseline()
+        except Exception as e:  # noqa: BLE001
+            line["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if world > 1 and args.workload == "glm":
+        lib.smg_comm_destroy(ctx)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -4,6 +4,7 @@
 // stan::math::gradient() call (stan/math/rev/mat/functor/gradient.hpp:41-57).
 #include <stan/math.hpp>
 
+#include <cmath>
 #include <cstdio>
 #include <exception>
 #include <vector>
@@ -31,6 +32,19 @@ struct gp_functor {
 dev_data<double> g_x, g_y;
 int g_n = 0;
 char g_err[512];
+
+// config 4: bernoulli_logit_glm_lpmf over this rank's row block, one RCCL
+// all-reduce of [logp, alpha', beta'] when world > 1
+stan::math::glm_shard g_shard;
+
+// config 2: sum(cholesky_decompose(add_diag(multiply(A, A^T), N))), A device-resident
+double* g_A = nullptr;
+double* g_G = nullptr;
+double* g_R = nullptr;  // [sum, sum of squares] of the config-2 gradient
+int g_N2 = 0;
+
+constexpr unsigned long long SEED = 20260101ull;
+constexpr unsigned long long GOLDEN = 0x9E3779B97F4A7C15ull;  // SplitMix64 increment (oracle/gen.h)
 
 int fail(const std::exception& e) {
   std::snprintf(g_err, sizeof g_err, "%s", e.what());
@@ -64,6 +78,115 @@ int smg_bench_gp_step(const double* theta, double* fx, double* grad) {
     std::vector<double> th(theta, theta + 3), g;
     stan::math::gradient(gp_functor{g_x, g_y}, th, *fx, g);
     for (int i = 0; i < 3; ++i) grad[i] = g[i];
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+/* Allocate and fill this rank's rows [b0, b1) of the config-4 data directly in
+ * HBM: x(i, j) = unif(SEED+41)[i + j R] * sqrt(3), y(i) = bern(SEED+42)[i], the
+ * same streams as oracle/gen.h (a SplitMix64 stream started k elements later
+ * is the stream of seed + k * GOLDEN). */
+int smg_bench_glm_init(int device, long long R, int M, int rank, int world, const char* comm_id) {
+  try {
+    using namespace stan::math;
+    amd::set_device(device);
+    smg_ctx* c = amd::ctx();
+    if (world > 1) amd::comm_init(world, rank, comm_id);
+    long long b0, b1;
+    row_partition(R, world, rank, &b0, &b1);
+    const long long rows = b1 - b0;
+    double* x = amd::alloc_doubles(size_t(rows > 0 ? rows : 1) * M);
+    int* y = amd::alloc_ints(size_t(rows > 0 ? rows : 1));
+    for (int j = 0; j < M && rows > 0; ++j)
+      amd::check(smg_fill_unif(c, x + size_t(j) * rows, rows,
+                               SEED + 41 + (unsigned long long)(b0 + (long long)j * R) * GOLDEN, -1.0,
+                               1.0, std::sqrt(3.0)),
+                 "glm_init");
+    if (rows > 0)
+      amd::check(smg_fill_bernoulli(c, y, rows, SEED + 42 + (unsigned long long)b0 * GOLDEN, 0.5),
+                 "glm_init");
+    amd::check(smg_sync(c), "glm_init");
+    g_shard = glm_shard{};
+    g_shard.y = y;
+    g_shard.x = x;
+    g_shard.rows = rows;
+    g_shard.M = M;
+    g_shard.ldx = rows > 0 ? rows : 1;
+    g_shard.row0 = b0;
+    g_shard.total_rows = R;
+    g_shard.distributed = world > 1;
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+int smg_bench_glm_step(const double* theta, double* fx, double* grad) {
+  try {
+    using namespace stan::math;
+    const int M = g_shard.M;
+    std::vector<double> th(theta, theta + M + 1), g;
+    gradient(
+        [](const std::vector<var>& t) {
+          std::vector<var> beta(t.begin() + 1, t.end());
+          return reduce_sum_bernoulli_logit_glm(g_shard, t[0], beta);
+        },
+        th, *fx, g);
+    for (int i = 0; i <= M; ++i) grad[i] = g[i];
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+long long smg_bench_glm_local_rows() { return g_shard.rows; }
+
+/* the row partition every sharded reducer uses (stan::math::row_partition) */
+void smg_bench_row_partition(long long R, int world, int rank, long long* b0, long long* b1) {
+  stan::math::row_partition(R, world, rank, b0, b1);
+}
+
+int smg_bench_mulchol_init(int device, int N) {
+  try {
+    using namespace stan::math;
+    amd::set_device(device);
+    smg_ctx* c = amd::ctx();
+    const size_t nn = size_t(N) * N;
+    g_A = amd::alloc_doubles(nn);
+    g_G = amd::alloc_doubles(nn);
+    g_R = amd::alloc_doubles(2);
+    amd::check(smg_fill_unif(c, g_A, (long long)nn, SEED + 2, -1.0, 1.0, std::sqrt(3.0 / N)),
+               "mulchol_init");
+    g_N2 = N;
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+/* one gradient of config 2 wrt all N^2 entries; the gradient stays in HBM
+ * (g_G); grad_sum_l2 = [sum, l2] of it for the parity guard when requested */
+int smg_bench_mulchol_step(double* fx, double* grad_sum_l2) {
+  try {
+    using namespace stan::math;
+    const int N = g_N2;
+    const size_t nn = size_t(N) * N;
+    gradient(
+        [N](const dev_var_matrix& a) {
+          return sum(cholesky_decompose(add_diag(multiply(a, transpose(a)), double(N))));
+        },
+        dev_data<double>(g_A, nn, N, N), *fx, g_G);
+    if (grad_sum_l2) {
+      smg_ctx* c = amd::ctx();
+      double* r = g_R;
+      amd::check(smg_memset(c, r, 0, 2 * sizeof(double)), "mulchol");
+      amd::check(smg_sum(c, g_G, (long long)nn, r), "mulchol");
+      amd::check(smg_dot(c, g_G, g_G, (long long)nn, r + 1), "mulchol");
+      amd::to_host(grad_sum_l2, r, 2);
+      grad_sum_l2[1] = std::sqrt(grad_sum_l2[1]);
+    }
     return 0;
   } catch (const std::exception& e) {
     return fail(e);
