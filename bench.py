@@ -70,6 +70,7 @@ def unif(seed, n, a, b):
 
 class Workload:
     """init() puts the data in HBM; step() is one gradient eval; guard() checks parity."""
+    unit = "gradient evals/s"
 
     def __init__(self, bl, args, rank, world, local, dist):
         self.bl, self.args, self.rank, self.world, self.local, self.dist = bl, args, rank, world, local, dist
@@ -255,7 +256,56 @@ class MulChol(Workload):
                 "sample": f"1 gradient eval at N={self.N} (Stan Math 3.0.0, {r['seconds_per_eval']:.2f} s)"}
 
 
-WORKLOADS = {"gp": GP, "glm": GLM, "mulchol": MulChol}
+class HVP(GP):
+    """config 5: hessian_times_vector of the GP marginal at N=4096, v = (1, -0.5, 0.25)."""
+    metric = "hessian-vector products/sec (fp64), GP-marginal log-density N=4096"
+    unit = "Hv products/s"
+
+    def init(self):
+        rc = super().init()
+        self.bl.smg_bench_hvp_step.argtypes = [D, D, D, D]
+        self.v = np.array([1.0, -0.5, 0.25])
+        self.hv = np.zeros(3)
+        return rc
+
+    def step(self):
+        return self.bl.smg_bench_hvp_step(ptr(self.theta), ptr(self.v), ptr(self.fx), ptr(self.hv))
+
+    def guard(self):
+        # no reference value at N=4096 (the reference's O(N^3) fvar tape is infeasible there);
+        # parity is pinned at N<=256 (tests/test_cpp_functors.py); here: value = the GP's,
+        # and two products bitwise equal (deterministic)
+        h0 = self.hv.copy()
+        self.step()
+        ok = (abs(self.fx[0] - self.gold["fx"]) < 1e-9 * abs(self.gold["fx"])
+              and np.array_equal(h0, self.hv) and np.all(np.isfinite(h0)))
+        return ok, f"fx={self.fx[0]!r} Hv={h0} / {self.hv}"
+
+    def config(self):
+        c = super().config()
+        c["workload"] = "gp_marginal_hessian_times_vector"
+        c["v"] = [1.0, -0.5, 0.25]
+        return c
+
+    def roofline(self, fams, steps, t_prof):
+        r = super().roofline(fams, steps, t_prof)
+        ev = 4 * self.N ** 3 / (t_prof / steps) / 1e12
+        r.update(eval_achieved=ev, eval_frac=ev / PEAK_FP64_TFLOPS,
+                 eval_flops="4N^3 (primal N^3 + tangent fwd N^3 + its reverse 2N^3), SURVEY.md §8(d)")
+        return r
+
+    def cpu_baseline(self):
+        # the reference's fvar<var> tape is O(N^3) scalar nodes: infeasible at N=4096 (~1.7 h);
+        # the bounded sample is N=256, reported as measured (not extrapolated into `value`)
+        r = ref_bench("hvp", 256, 1)
+        if r is None:
+            return None
+        return {"value": None, "unit": "Hv products/s", "cores": 1, "kind": "reference",
+                "sample": f"N=4096 infeasible on the reference; N=256 sample: {r['seconds_per_eval']:.2f} s "
+                          f"per product ({r['evals_per_sec']:.3f}/s), Stan Math 3.0.0 compiled from /root/reference"}
+
+
+WORKLOADS = {"gp": GP, "glm": GLM, "mulchol": MulChol, "hvp": HVP}
 
 
 def main():
@@ -329,7 +379,7 @@ def main():
     line = {
         "metric": wl.metric,
         "value": value,
-        "unit": "gradient evals/s",
+        "unit": wl.unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

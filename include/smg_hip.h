@@ -117,6 +117,17 @@ int smg_gp_exp_quad_cov_fwd(smg_ctx* ctx, const double* x, int n, double sigma,
 int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma,
                             double l, const double* Kadj, int ldka, double* out2);
 
+/* Tangent of the same covariance along (sigma', l') -- what the fvar<var>
+ * instantiation of gp_exp_quad_cov computes inside hessian_times_vector
+ * (mix/mat/functor/hessian_times_vector.hpp:13-40):
+ *   Kd_ij = 2 sigma sigma' e_ij + sigma^2 l' d_ij^2 e_ij / l^3,  e = exp(-d^2/(2 l^2))
+ * rev: out4 += [d/dsigma, d/dl, d/dsigma', d/dl'] of sum(Kdadj .* Kd). */
+int smg_gp_exp_quad_cov_tangent_fwd(smg_ctx* ctx, const double* x, int n, double sigma,
+                                    double l, double dsigma, double dl, double* Kd, int ldk);
+int smg_gp_exp_quad_cov_tangent_rev(smg_ctx* ctx, const double* x, int n, double sigma,
+                                    double l, double dsigma, double dl, const double* Kdadj,
+                                    int ldka, double* out4);
+
 /* add_diag(A, d) (prim/mat/fun/add_diag.hpp:20-55): B = A + diag(d) where d is
  * the host scalar d_scalar (d_vec == NULL) or the device vector d_vec.
  * rev: Aadj += Badj (NULL skips); dadj (device) += diag(Badj), summed into
@@ -237,6 +248,16 @@ int smg_transpose(smg_ctx* ctx, int m, int n, const double* A, int lda,
 int smg_shift(smg_ctx* ctx, int m, int n, double c, double* Y, int ldy, int uplo);
 /* out += sum_i x_i y_i (deterministic) */
 int smg_dot(smg_ctx* ctx, const double* x, const double* y, long long n, double* out);
+/* Y = Phi(X) (accumulate: Y += Phi(X)): strict lower triangle of X, halved
+ * diagonal, zero upper -- the tangent map of a Cholesky factor; Phi is its own
+ * adjoint, so the reverse is the same call with accumulate = 1 */
+int smg_phi(smg_ctx* ctx, int n, const double* X, int ldx, double* Y, int ldy, int accumulate);
+/* out += sum_i A_ii / B_ii; rev Aadj_ii += adj / B_ii, Badj_ii -= adj A_ii / B_ii^2
+ * (the log-determinant tangent term of multi_normal_cholesky_lpdf) */
+int smg_diag_ratio_fwd(smg_ctx* ctx, int n, const double* A, int lda, const double* B, int ldb,
+                       double* out);
+int smg_diag_ratio_rev(smg_ctx* ctx, int n, const double* A, int lda, const double* B, int ldb,
+                       double adj, double* Aadj, int ldaa, double* Badj, int ldba);
 /* argument checks of the lpdf reducers (prim/scal/err/check_*.hpp): *flag (a
  * device double the caller zeroes) becomes 1.0 if any x_i fails.  kind 0:
  * check_not_nan, 1: check_finite, 2: check_positive, 3: check_positive_finite.

@@ -16,11 +16,12 @@ using stan::math::var;
 
 // config 3: multi_normal_cholesky_lpdf(y | 0, cholesky_decompose(add_diag(
 //           gp_exp_quad_cov(x, alpha, rho), sigma^2)))
+// (T = var for gradient(), T = fvar<var> for hessian_times_vector(), config 5)
 struct gp_functor {
   const dev_data<double>& x;
   const dev_data<double>& y;
   template <typename T>
-  var operator()(const T& th) const {
+  T operator()(const std::vector<T>& th) const {
     using namespace stan::math;
     auto K = gp_exp_quad_cov(x, th[0], th[1]);
     auto Kd = add_diag(K, square(th[2]));
@@ -135,6 +136,18 @@ int smg_bench_glm_step(const double* theta, double* fx, double* grad) {
         },
         th, *fx, g);
     for (int i = 0; i <= M; ++i) grad[i] = g[i];
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+/* config 5: H v of the same GP marginal (fwd-over-rev), data from smg_bench_gp_init */
+int smg_bench_hvp_step(const double* theta, const double* v, double* fx, double* hv) {
+  try {
+    std::vector<double> th(theta, theta + 3), vv(v, v + 3), h;
+    stan::math::hessian_times_vector(gp_functor{g_x, g_y}, th, vv, *fx, h);
+    for (int i = 0; i < 3; ++i) hv[i] = h[i];
     return 0;
   } catch (const std::exception& e) {
     return fail(e);

@@ -118,6 +118,88 @@ __global__ void k_diag_adj(const double* __restrict__ Ba, int ldb, int n, double
   if (threadIdx.x == 0) dadj[0] += s;
 }
 
+// Tangent of K along (sigma', l') -- the fvar<var> instantiation of the same
+// covariance (prim/mat/fun/gp_exp_quad_cov.hpp:40-59 over fvar, used by
+// hessian_times_vector):  Kd_ij = 2 sigma sigma' e + sigma^2 l' d^2 e / l^3,
+// e = exp(-d^2 / (2 l^2)); Kd_ii = 2 sigma sigma'.
+__global__ __launch_bounds__(256) void k_gp_tan_fwd(const double* __restrict__ x, int n, double a,
+                                                    double b, double inv_half_sq_l,
+                                                    double* __restrict__ K, int ldk) {
+  // a = 2 sigma sigma', b = sigma^2 l' / l^3
+  const int j = blockIdx.y;
+  const double xj = x[j];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    double v;
+    if (i == j) {
+      v = a;
+    } else {
+      const double d = (i > j) ? x[i] - xj : xj - x[i];
+      const double d2 = d * d;
+      const double e = exp(-d2 * inv_half_sq_l);
+      v = a * e + b * d2 * e;
+    }
+    K[i + (size_t)j * ldk] = v;
+  }
+}
+
+// per-block partials of S_e = sum A e, S_2 = sum A e d^2, S_4 = sum A e d^4 (all positions)
+__global__ __launch_bounds__(256) void k_gp_tan_partials(const double* __restrict__ x, int n,
+                                                         double inv_half_sq_l,
+                                                         const double* __restrict__ Ka, int lda,
+                                                         double* __restrict__ part) {
+  __shared__ double lds[16];
+  double se = 0.0, s2 = 0.0, s4 = 0.0;
+  const long long tot = (long long)n * n;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < tot;
+       q += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(q / n), i = (int)(q % n);
+    const double a = Ka[i + (size_t)j * lda];
+    if (i == j) {
+      se += a;
+    } else {
+      const double d = (i > j) ? x[i] - x[j] : x[j] - x[i];
+      const double d2 = d * d;
+      const double ae = a * exp(-d2 * inv_half_sq_l);
+      se += ae;
+      s2 += ae * d2;
+      s4 += ae * d2 * d2;
+    }
+  }
+  se = block_sum(se, lds);
+  __syncthreads();
+  s2 = block_sum(s2, lds);
+  __syncthreads();
+  s4 = block_sum(s4, lds);
+  if (threadIdx.x == 0) {
+    part[3 * blockIdx.x + 0] = se;
+    part[3 * blockIdx.x + 1] = s2;
+    part[3 * blockIdx.x + 2] = s4;
+  }
+}
+
+__global__ void k_gp_tan_final(const double* __restrict__ part, int nparts, double sigma, double l,
+                               double ds, double dl, double* out4) {
+  __shared__ double lds[16];
+  double se = 0.0, s2 = 0.0, s4 = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    se += part[3 * i];
+    s2 += part[3 * i + 1];
+    s4 += part[3 * i + 2];
+  }
+  se = block_sum(se, lds);
+  __syncthreads();
+  s2 = block_sum(s2, lds);
+  __syncthreads();
+  s4 = block_sum(s4, lds);
+  if (threadIdx.x == 0) {
+    const double l3 = l * l * l, l4 = l3 * l, l6 = l3 * l3;
+    out4[0] += 2 * ds * se + 2 * sigma * dl * s2 / l3;                                  // d/dsigma
+    out4[1] += 2 * sigma * ds * s2 / l3 + sigma * sigma * dl * (s4 / l6 - 3 * s2 / l4);  // d/dl
+    out4[2] += 2 * sigma * se;                                                          // d/dsigma'
+    out4[3] += sigma * sigma * s2 / l3;                                                 // d/dl'
+  }
+}
+
 inline int grid_for(long long tot) {
   long long g = (tot + 255) / 256;
   if (g > 8192) g = 8192;
@@ -155,6 +237,36 @@ int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma, 
   hipLaunchKernelGGL(k_gp_rev_partials, dim3(nb), dim3(256), 0, ctx->stream, x, n, sigma * sigma,
                      0.5 / (l * l), Kadj, ldka, part);
   hipLaunchKernelGGL(k_gp_rev_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, sigma, l, out2);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_gp_exp_quad_cov_tangent_fwd(smg_ctx* ctx, const double* x, int n, double sigma, double l,
+                                    double dsigma, double dl, double* Kd, int ldk) {
+  if (!ctx || n < 0 || (n > 0 && (!x || !Kd || ldk < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  dim3 grid(smg_ceil_div(n, 256) > 16 ? 16 : smg_ceil_div(n, 256), n);
+  hipLaunchKernelGGL(k_gp_tan_fwd, grid, dim3(256), 0, ctx->stream, x, n, 2 * sigma * dsigma,
+                     sigma * sigma * dl / (l * l * l), 0.5 / (l * l), Kd, ldk);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_gp_exp_quad_cov_tangent_rev(smg_ctx* ctx, const double* x, int n, double sigma, double l,
+                                    double dsigma, double dl, const double* Kdadj, int ldka,
+                                    double* out4) {
+  if (!ctx || n < 0 || (n > 0 && (!x || !Kdadj || !out4 || ldka < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  int nb = grid_for((long long)n * n);
+  if (nb > GP_BLOCKS) nb = GP_BLOCKS;
+  double* part = smg_ws(ctx, SMG_WS_RED, 3 * (size_t)nb);
+  if (!part) return SMG_ERR_OOM;
+  hipLaunchKernelGGL(k_gp_tan_partials, dim3(nb), dim3(256), 0, ctx->stream, x, n, 0.5 / (l * l),
+                     Kdadj, ldka, part);
+  hipLaunchKernelGGL(k_gp_tan_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, sigma, l,
+                     dsigma, dl, out4);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

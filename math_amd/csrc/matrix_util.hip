@@ -84,6 +84,39 @@ __global__ void k_check_bounded_int(const int* __restrict__ y, long long n, int 
   if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1.0;
 }
 
+// Y (+)= Phi(X): strict lower of X, diagonal halved, upper zero (the
+// tangent of a Cholesky factor, L' = L Phi(L^{-1} A' L^{-T}))
+__global__ void k_phi(int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy,
+                      int accumulate) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    const double v = i > j ? X[i + (size_t)j * ldx] : (i == j ? 0.5 * X[i + (size_t)j * ldx] : 0.0);
+    double* y = Y + i + (size_t)j * ldy;
+    *y = accumulate ? *y + v : v;
+  }
+}
+
+__global__ void k_diag_ratio(int n, const double* __restrict__ A, int lda,
+                             const double* __restrict__ B, int ldb, double* out) {
+  __shared__ double lds[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += A[i + (size_t)i * lda] / B[i + (size_t)i * ldb];
+  s = block_sum(s, lds);
+  if (threadIdx.x == 0) out[0] += s;
+}
+
+__global__ void k_diag_ratio_rev(int n, const double* __restrict__ A, int lda,
+                                 const double* __restrict__ B, int ldb, double adj, double* Aa,
+                                 int ldaa, double* Ba, int ldba) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const double b = B[i + (size_t)i * ldb];
+    if (Aa) Aa[i + (size_t)i * ldaa] += adj / b;
+    if (Ba) Ba[i + (size_t)i * ldba] -= adj * A[i + (size_t)i * lda] / (b * b);
+  }
+}
+
 inline int grid_for(long long tot, int cap = 4096) {
   long long g = (tot + 255) / 256;
   if (g > cap) g = cap;
@@ -125,6 +158,37 @@ int smg_dot(smg_ctx* ctx, const double* x, const double* y, long long n, double*
   if (!part) return SMG_ERR_OOM;
   hipLaunchKernelGGL(k_dot_part, dim3(nb), dim3(256), 0, ctx->stream, x, y, n, part);
   smg_reduce_partials(ctx, part, nb, 1, out, 1);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_phi(smg_ctx* ctx, int n, const double* X, int ldx, double* Y, int ldy, int accumulate) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!X || !Y || ldx < n || ldy < n) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_phi, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, n, X, ldx,
+                     Y, ldy, accumulate);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_diag_ratio_fwd(smg_ctx* ctx, int n, const double* A, int lda, const double* B, int ldb,
+                       double* out) {
+  if (!ctx || n < 0 || !out) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!A || !B) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_diag_ratio, dim3(1), dim3(1024), 0, ctx->stream, n, A, lda, B, ldb, out);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_diag_ratio_rev(smg_ctx* ctx, int n, const double* A, int lda, const double* B, int ldb,
+                       double adj, double* Aadj, int ldaa, double* Badj, int ldba) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!A || !B) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_diag_ratio_rev, dim3(smg_ceil_div(n, 256)), dim3(256), 0, ctx->stream, n, A,
+                     lda, B, ldb, adj, Aadj, ldaa, Badj, ldba);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

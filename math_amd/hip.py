@@ -79,6 +79,11 @@ _SIGS = {
     "smg_shift": (_I, [_P, _I, _I, _D, _P, _I, _I]),
     "smg_dot": (_I, [_P, _P, _P, _L, _P]),
     "smg_check_domain": (_I, [_P, _P, _L, _I, _P]),
+    "smg_gp_exp_quad_cov_tangent_fwd": (_I, [_P, _P, _I, _D, _D, _D, _D, _P, _I]),
+    "smg_gp_exp_quad_cov_tangent_rev": (_I, [_P, _P, _I, _D, _D, _D, _D, _P, _I, _P]),
+    "smg_phi": (_I, [_P, _I, _P, _I, _P, _I, _I]),
+    "smg_diag_ratio_fwd": (_I, [_P, _I, _P, _I, _P, _I, _P]),
+    "smg_diag_ratio_rev": (_I, [_P, _I, _P, _I, _P, _I, _D, _P, _I, _P, _I]),
     "smg_check_bounded_int": (_I, [_P, _P, _L, _I, _I, _P]),
     "smg_comm_unique_id": (_I, [ctypes.c_char_p]),
     "smg_comm_init": (_I, [_P, _I, _I, ctypes.c_char_p]),

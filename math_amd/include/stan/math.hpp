@@ -22,5 +22,7 @@
 #include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
 #include <stan/math/rev/functor/gradient.hpp>
 #include <stan/math/eigen/interop.hpp>
+#include <stan/math/mix/fvar_functors.hpp>
+#include <stan/math/mix/hessian_times_vector.hpp>
 
 #endif

@@ -5,6 +5,7 @@
 // Included right after var is defined, before any header whose var
 // arithmetic could make Eigen instantiate the primary template.
 #include <Eigen/Core>
+#include <stan/math/fwd/core/fvar.hpp>
 #include <stan/math/rev/core/var.hpp>
 
 #include <limits>
@@ -26,6 +27,25 @@ struct NumTraits<stan::math::var> : GenericNumTraits<stan::math::var> {
     IsInteger = 0,
     IsSigned = 1,
     RequireInitialization = 0,
+    ReadCost = 1,
+    AddCost = 1,
+    MulCost = 1
+  };
+  static inline int digits10() { return std::numeric_limits<double>::digits10; }
+};
+// NumTraits for fvar<var> (fwd/mat/fun/Eigen_NumTraits.hpp)
+template <>
+struct NumTraits<stan::math::fvar<stan::math::var>>
+    : GenericNumTraits<stan::math::fvar<stan::math::var>> {
+  using Real = stan::math::fvar<stan::math::var>;
+  using NonInteger = Real;
+  using Nested = Real;
+  using Literal = Real;
+  enum {
+    IsComplex = 0,
+    IsInteger = 0,
+    IsSigned = 1,
+    RequireInitialization = 1,
     ReadCost = 1,
     AddCost = 1,
     MulCost = 1

@@ -740,7 +740,7 @@ static void fix_glm() {
 }
 
 static void fix_hvp() {
-  for (int N : {8, 32}) {
+  for (int N : {8, 32, 100, 256}) {
     std::vector<double> x;
     VectorXd y;
     gp_inputs(N, x, y);
@@ -794,6 +794,17 @@ static int bench(const std::string& cfg, int N, int reps) {
     for (int r = 0; r < reps; ++r)
       stan::math::gradient(glm_functor{d}, d.theta, fx, g);
     t1 = now();
+  } else if (cfg == "hvp") {
+    std::vector<double> x;
+    VectorXd y;
+    gp_inputs(N, x, y);
+    VectorXd th(3), v(3), hv;
+    th << 1.0, 1.5, 0.3;
+    v << 1.0, -0.5, 0.25;
+    t0 = now();
+    for (int r = 0; r < reps; ++r)
+      stan::math::hessian_times_vector(gp_functor{x, y}, th, v, fx, hv);
+    t1 = now();
   } else if (cfg == "normal") {
     std::vector<double> th = normals(SEED + 1, N);
     VectorXd x = Eigen::Map<VectorXd>(th.data(), N);
@@ -833,7 +844,7 @@ int main(int argc, char** argv) {
   if (argc >= 5 && std::string(argv[1]) == "bench")
     return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
   std::fprintf(stderr,
-               "usage: %s gen [outdir] [only]\n       %s bench gp|mulchol|glm|normal N reps\n",
+               "usage: %s gen [outdir] [only]\n       %s bench gp|mulchol|glm|normal|hvp N reps\n",
                argv[0], argv[0]);
   return 2;
 }

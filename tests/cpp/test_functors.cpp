@@ -18,6 +18,7 @@
 //   glm_data R M x y theta        explicit data (cutoff branches)
 //   mvn N y mu L                  multi_normal_cholesky_lpdf, every argument var (Eigen)
 //   errors                        the reference's exceptions
+//   hvp N theta v x y             hessian_times_vector of the GP marginal (config 5)
 #include <stan/math.hpp>
 
 #include <cmath>
@@ -429,6 +430,45 @@ static void cmd_mvn() {
   recover_memory_nested();
 }
 
+struct gp_functor {
+  const std::vector<double>& x;
+  const std::vector<double>& y;
+  template <typename T>
+  T operator()(const Eigen::Matrix<T, Eigen::Dynamic, 1>& th) const {
+    std::vector<double> mu(x.size(), 0.0);
+    auto K = gp_exp_quad_cov(x, th(0), th(1));
+    auto Kd = add_diag(K, square(th(2)));
+    auto L = cholesky_decompose(Kd);
+    return multi_normal_cholesky_lpdf(y, mu, L);
+  }
+  template <typename T>
+  T operator()(const std::vector<T>& th) const {
+    Eigen::Matrix<T, Eigen::Dynamic, 1> t(3);
+    t << th[0], th[1], th[2];
+    return (*this)(t);
+  }
+};
+
+// hessian_times_vector on the GP marginal (config 5): Eigen and std::vector signatures
+static void cmd_hvp() {
+  int N;
+  std::cin >> N;
+  auto th = read_vec(3), v = read_vec(3), x = read_vec(N), y = read_vec(N);
+  Eigen::VectorXd te = Eigen::Map<Eigen::VectorXd>(th.data(), 3), ve = Eigen::Map<Eigen::VectorXd>(v.data(), 3), Hv;
+  double fx;
+  for (int rep = 0; rep < 2; ++rep) {
+    hessian_times_vector(gp_functor{x, y}, te, ve, fx, Hv);
+    print1("fx", fx);
+    print("Hv", std::vector<double>(Hv.data(), Hv.data() + 3));
+  }
+  std::vector<double> hv;
+  hessian_times_vector(gp_functor{x, y}, th, v, fx, hv);
+  print1("fx_std", fx);
+  print("Hv_std", hv);
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
 template <typename F>
 static void expect_throw(const char* name, F&& f) {
   start_nested();
@@ -510,6 +550,7 @@ int main() {
     else if (cmd == "glm_data") cmd_glm_data();
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
+    else if (cmd == "hvp") cmd_hvp();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;
