@@ -24,5 +24,6 @@
 #include <stan/math/eigen/interop.hpp>
 #include <stan/math/mix/fvar_functors.hpp>
 #include <stan/math/mix/hessian_times_vector.hpp>
+#include <stan/math/rev/functor/map_rect.hpp>
 
 #endif

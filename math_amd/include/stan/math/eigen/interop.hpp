@@ -214,6 +214,18 @@ inline var multi_normal_cholesky_lpdf(const vector_d& y, const vector_d& mu, con
   std::vector<double> yv(y.data(), y.data() + y.size()), mv(mu.data(), mu.data() + mu.size());
   return multi_normal_cholesky_lpdf<propto>(yv, mv, L);
 }
+template <bool propto = false, int RB>
+inline double bernoulli_logit_glm_lpmf(const std::vector<int>& y, const matrix_d& x, double alpha,
+                                       const Eigen::Matrix<double, RB, 1>& beta) {
+  std::vector<double> b(beta.data(), beta.data() + beta.size());
+  std::vector<double> xv(x.data(), x.data() + x.size());
+  if (y.size() != size_t(x.rows()))
+    throw std::invalid_argument(
+        "bernoulli_logit_glm_lpmf: Vector of dependent variables has dimension = " +
+        std::to_string(y.size()) + ", expecting dimension = " + std::to_string(x.rows()));
+  return bernoulli_logit_glm_lpmf<propto>(y, xv, int(x.cols()), alpha, b);
+}
+
 template <bool propto = false>
 inline var multi_normal_cholesky_lpdf(const vector_v& y, const vector_v& mu, const matrix_v& L) {
   return multi_normal_cholesky_lpdf<propto>(to_dev(y), to_dev(mu), to_dev(L));

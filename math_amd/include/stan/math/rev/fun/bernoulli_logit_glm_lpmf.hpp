@@ -192,12 +192,12 @@ bernoulli_logit_glm_lpmf(const glm_shard& s, const T_alpha& alpha, const T_beta&
   internal::glm_alpha(p, alpha);
   internal::glm_beta(p, beta);
   const internal::glm_result r = internal::glm_eval<propto>(s, p);
-  if (r.node) return typename std::conditional<internal::glm_is_var<T_alpha>::value ||
-                                                   internal::glm_is_var<T_beta>::value,
-                                               var, double>::type(var(r.node));
-  return typename std::conditional<internal::glm_is_var<T_alpha>::value ||
-                                       internal::glm_is_var<T_beta>::value,
-                                   var, double>::type(r.lp);
+  if constexpr (internal::glm_is_var<T_alpha>::value || internal::glm_is_var<T_beta>::value) {
+    if (r.node) return var(r.node);
+    return var(r.lp);
+  } else {
+    return r.lp;
+  }
 }
 
 template <bool propto, typename T_alpha, typename T_beta>

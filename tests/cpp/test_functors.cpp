@@ -19,6 +19,7 @@
 //   mvn N y mu L                  multi_normal_cholesky_lpdf, every argument var (Eigen)
 //   errors                        the reference's exceptions
 //   hvp N theta v x y             hessian_times_vector of the GP marginal (config 5)
+//   map_rect_glm R M shards beta  map_rect over GLM row blocks (vs the reference's map_rect32)
 #include <stan/math.hpp>
 
 #include <cmath>
@@ -430,6 +431,72 @@ static void cmd_mvn() {
   recover_memory_nested();
 }
 
+// map_rect job: one block of GLM rows; x_r = the block of x (column-major), x_i = y
+// (the reference harness's glm_shard_functor, oracle/ref_harness.cpp)
+struct glm_job {
+  template <typename T1, typename T2>
+  Eigen::Matrix<T1, Eigen::Dynamic, 1> operator()(const Eigen::Matrix<T1, Eigen::Dynamic, 1>& eta,
+                                                  const Eigen::Matrix<T2, Eigen::Dynamic, 1>&,
+                                                  const std::vector<double>& x_r,
+                                                  const std::vector<int>& x_i, std::ostream*) const {
+    const int M = int(eta.size()) - 1, r = int(x_i.size());
+    matrix_d xs = Eigen::Map<const matrix_d>(x_r.data(), r, M);
+    Eigen::Matrix<T1, Eigen::Dynamic, 1> beta = eta.tail(M);
+    Eigen::Matrix<T1, Eigen::Dynamic, 1> out(1);
+    out(0) = bernoulli_logit_glm_lpmf(x_i, xs, eta(0), beta);
+    return out;
+  }
+};
+
+// map_rect over `shards` row blocks of the config-4 data (generated on the device)
+static void cmd_map_rect_glm() {
+  long long R;
+  int M, shards;
+  std::cin >> R >> M >> shards;
+  auto beta = read_vec(M);
+  smg_ctx* c = amd::ctx();
+  std::vector<double> x(size_t(R) * M);
+  std::vector<int> y(R);
+  {
+    double* xd = amd::alloc_doubles(x.size());
+    int* yd = amd::alloc_ints(y.size());
+    amd::check(smg_fill_unif(c, xd, R * M, 20260101ull + 41, -1.0, 1.0, std::sqrt(3.0)), "fill");
+    amd::check(smg_fill_bernoulli(c, yd, R, 20260101ull + 42, 0.5), "fill");
+    amd::to_host(x.data(), xd, x.size());
+    amd::check(smg_memcpy_d2h(c, y.data(), yd, y.size() * sizeof(int)), "copy");
+    amd::check(smg_sync(c), "copy");
+  }
+  std::vector<std::vector<double>> xr(shards);
+  std::vector<std::vector<int>> xi(shards);
+  for (int s = 0; s < shards; ++s) {
+    long long r0, r1;
+    row_partition(R, shards, s, &r0, &r1);
+    const long long r = r1 - r0;
+    xr[s].resize(size_t(r) * M);
+    for (int j = 0; j < M; ++j)
+      for (long long i = 0; i < r; ++i) xr[s][size_t(j) * r + i] = x[size_t(j) * R + r0 + i];
+    xi[s].assign(y.begin() + r0, y.begin() + r1);
+  }
+  Eigen::VectorXd th(M + 1), g;
+  th(0) = 0.1;
+  for (int j = 0; j < M; ++j) th(1 + j) = beta[j];
+  double fx;
+  gradient(
+      [&](const vector_v& t) {
+        std::vector<vector_v> job(shards);
+        return sum(map_rect<1, glm_job>(t, job, xr, xi));
+      },
+      th, fx, g);
+  print1("fx", fx);
+  print("grad", std::vector<double>(g.data(), g.data() + g.size()));
+  // double-only instantiation: values
+  std::vector<Eigen::VectorXd> jobd(shards);
+  Eigen::VectorXd vals = map_rect<2, glm_job>(th, jobd, xr, xi);
+  print1("fx_double", vals.sum());
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
 struct gp_functor {
   const std::vector<double>& x;
   const std::vector<double>& y;
@@ -551,6 +618,7 @@ int main() {
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
     else if (cmd == "hvp") cmd_hvp();
+    else if (cmd == "map_rect_glm") cmd_map_rect_glm();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;
