@@ -82,31 +82,32 @@ __global__ __launch_bounds__(512) void k_trtri_diag(const double* __restrict__ L
 // symbolic_rev (cholesky_decompose.hpp:101-111) on one diagonal block:
 //   S = D^T tril(Dadj); S = sym_from_lower(S); S = Dinv^T S Dinv
 // writes Ssym (b x b dense, ld b) and Dadj <- tril(S) with halved diagonal.
-__global__ __launch_bounds__(256) void k_symbolic_rev(const double* __restrict__ L, int ldl,
+__global__ __launch_bounds__(512) void k_symbolic_rev(const double* __restrict__ L, int ldl,
                                                       const double* __restrict__ Dinv, int ldd,
                                                       double* __restrict__ Dadj, int lda,
                                                       int b, double* __restrict__ Ssym) {
-  __shared__ double D[SMG_NB * SMG_NBP];   // D, later Dinv
-  __shared__ double G[SMG_NB * SMG_NBP];   // tril(Dadj), later temp
-  __shared__ double S[SMG_NB * SMG_NBP];
-  // zero padding beyond b keeps every 64x64 product exact on the b x b block
+  __shared__ double D[SMG_NB * SMG_NBP];   // D, later temp
+  __shared__ double G[SMG_NB * SMG_NBP];   // tril(Dadj), later S
+  __shared__ double W[SMG_NB * SMG_NBP];   // Dinv (lower)
+  // zero padding beyond b keeps every 64x64 product exact on the b x b block;
+  // the three block loads are issued back to back (one global-latency exposure)
   lds_load_block0(D, L, ldl, b, true);
   lds_load_block0(G, Dadj, lda, b, true);
+  lds_load_block0(W, Dinv, ldd, b, true);
   __syncthreads();
-  lds_mma64<true, false>(S, D, G, 1.0, 0.0);  // S = D^T tril(Dadj)
+  lds_mma64_8w<true, false>(G, D, G);  // S = D^T tril(Dadj)
   // mirror the lower triangle into the upper (:106-107)
   for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
     const int r = e / SMG_NB, c = e % SMG_NB;
-    if (r < c) S[r * SMG_NBP + c] = S[c * SMG_NBP + r];
+    if (r < c) G[r * SMG_NBP + c] = G[c * SMG_NBP + r];
   }
-  lds_load_block0(D, Dinv, ldd, b, true);  // D <- Dinv (lower)
   __syncthreads();
-  lds_mma64<true, false>(G, D, S, 1.0, 0.0);   // G = Dinv^T S
-  lds_mma64<false, false>(S, G, D, 1.0, 0.0);  // S = G Dinv
+  lds_mma64_8w<true, false>(D, W, G);   // T = Dinv^T S
+  lds_mma64_8w<false, false>(G, D, W);  // S = T Dinv
   // outputs: selfadjointView<Lower> of S, and tril(S) with halved diagonal (:160-161)
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
     const int c = e / b, r = e % b;
-    const double low = (r >= c) ? S[r * SMG_NBP + c] : S[c * SMG_NBP + r];
+    const double low = (r >= c) ? G[r * SMG_NBP + c] : G[c * SMG_NBP + r];
     Ssym[r + (size_t)c * b] = low;
     double v = 0.0;
     if (r > c) v = low;
@@ -200,7 +201,6 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
     double* Radj = La + j;
     const double* R = L + j;
     const double* Bv = L + k;
-    const double* Cv = L + k + (size_t)j * ldl;
     int rc;
     if (m > 0) {
       // C_adj = C_adj D^{-1}
@@ -210,17 +210,15 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
         rc = smg_gemm_impl(ctx, 0, 0, 0, m, j, b, -1.0, Cadj, ldla, R, ldl, 1.0, Badj, ldla);
         if (rc) return rc;
       }
-      // D_adj -= C_adj^T C
-      rc = smg_gemm_impl(ctx, 1, 0, 0, b, b, m, -1.0, Cadj, ldla, Cv, ldl, 1.0, Dadj, ldla);
+      // [R_adj | D_adj] -= C_adj^T [B | C]: both operands are contiguous column
+      // ranges (L[k:, 0:k] and Abar[j:k, 0:k]), so one GEMM (one split-K
+      // reduction) does both updates; R_adj's does not depend on the symbolic step
+      rc = smg_gemm_impl(ctx, 1, 0, 0, b, k, m, -1.0, Cadj, ldla, Bv, ldl, 1.0, Radj, ldla);
       if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_symbolic_rev, dim3(1), dim3(256), 0, ctx->stream,
+    hipLaunchKernelGGL(k_symbolic_rev, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream,
                        L + j + (size_t)j * ldl, ldl, Di, n, Dadj, ldla, b, Ssym);
     if (j > 0) {
-      if (m > 0) {  // R_adj -= C_adj^T B
-        rc = smg_gemm_impl(ctx, 1, 0, 0, b, j, m, -1.0, Cadj, ldla, Bv, ldl, 1.0, Radj, ldla);
-        if (rc) return rc;
-      }
       // R_adj -= sym(D_adj) R
       rc = smg_gemm_impl(ctx, 0, 0, 0, b, j, b, -1.0, Ssym, b, R, ldl, 1.0, Radj, ldla);
       if (rc) return rc;

@@ -102,7 +102,7 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->cur_block = 0;
   ctx->offset = 0;
   ctx->host_status = 0;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < SMG_WS_COUNT; ++i) {
     ctx->ws[i] = nullptr;
     ctx->ws_doubles[i] = 0;
   }
@@ -149,7 +149,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   smg_comm_destroy(ctx);
   for (auto& b : ctx->blocks) hipFree(b.base);
   for (auto e : ctx->prof_pool) hipEventDestroy(e);
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < SMG_WS_COUNT; ++i)
     if (ctx->ws[i]) hipFree(ctx->ws[i]);
   hipFree(ctx->status_d);
   hipHostFree(ctx->status_h);

@@ -103,8 +103,14 @@ __global__ __launch_bounds__(256) void k_gemm(
   constexpr bool BKC = !TB;
   using LA = lds_layout<BM, BK, AK>;
   using LB = lds_layout<BN, BK, BKC>;
-  __shared__ double As[LA::size];
-  __shared__ double Bs[LB::size];
+  // one LDS pool: the K-loop operand tiles, reused by the epilogue to stage
+  // the C tile (column chunks of ECH columns, stride BM + 1) so that C is read
+  // and written in whole column segments (coalesced 8*BM-byte runs)
+  constexpr int ECH = (BM * BN + BN <= LA::size + LB::size) ? BN : 32;
+  constexpr int POOL = (LA::size + LB::size > (BM + 1) * ECH) ? LA::size + LB::size : (BM + 1) * ECH;
+  __shared__ double pool[POOL];
+  double* As = pool;
+  double* Bs = pool + LA::size;
 
   const int tile = blockIdx.x % ntiles;
   const int split = blockIdx.x / ntiles;
@@ -137,19 +143,21 @@ __global__ __launch_bounds__(256) void k_gemm(
     load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg, ra);
     load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg, rb);
   }
-  // epilogue operand in flight during the K loop
-  double cpre[TM][TN][4];
+  // epilogue operand in flight during the K loop (small tiles only: the
+  // 128 x 128 tile would double its register count); coalesced mapping
+  // e = tid + 256 q -> (i = e % BM, j = e / BM), the same as the store
+  constexpr int EPT = BM * BN / 256;
+  constexpr bool PREFETCH_C = EPT <= 16;
   const bool use_c = !slab && beta != 0.0;
+  double cpre[PREFETCH_C ? EPT : 1];
+  if (PREFETCH_C) {
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r;
-        const int j = j0 + wc * (BN / 2) + b * 16 + (lane & 15);
-        cpre[a][b][r] = (use_c && i < m && j < n) ? C[i + (size_t)j * ldc] : 0.0;
-      }
+    for (int q = 0; q < EPT; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      const int i = i0 + e % BM, j = j0 + e / BM;
+      cpre[q] = (use_c && i < m && j < n) ? C[i + (size_t)j * ldc] : 0.0;
+    }
+  }
   const int fr = lane & 15, fk = lane >> 4;
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
@@ -178,25 +186,44 @@ __global__ __launch_bounds__(256) void k_gemm(
   }
 
   // epilogue: D layout of v_mfma_f64_16x16x4_f64: reg r of lane l holds
-  // row (l>>4) + 4r, col l&15 of the 16x16 tile.
+  // row (l>>4) + 4r, col l&15 of the 16x16 tile.  Accumulators go to LDS
+  // (column-major, stride BM + 1), then every thread stores whole column runs.
+  __syncthreads();  // operand tiles no longer needed
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+  for (int c0 = 0; c0 < BN; c0 += ECH) {
 #pragma unroll
-    for (int b = 0; b < TN; ++b)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r;
-        const int j = j0 + wc * (BN / 2) + b * 16 + (lane & 15);
-        if (i >= m || j >= n) continue;
-        if (MODE == 1 && i < j) continue;
-        if (MODE == 2 && i > j) continue;
-        const double v = acc[a][b][r];
-        if (slab) {
-          slab[(size_t)split * m * n + (size_t)j * m + i] = v;
-        } else {
-          C[i + (size_t)j * ldc] = use_c ? alpha * v + beta * cpre[a][b][r] : alpha * v;
-        }
+      for (int b = 0; b < TN; ++b) {
+        const int jl = wc * (BN / 2) + b * 16 + (lane & 15) - c0;
+        if (jl < 0 || jl >= ECH) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pool[jl * (BM + 1) + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r] = acc[a][b][r];
       }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BM * ECH / 256; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      const int il = e % BM, jl = e / BM;
+      const int i = i0 + il, j = j0 + c0 + jl;
+      if (i >= m || j >= n) continue;
+      if (MODE == 1 && i < j) continue;
+      if (MODE == 2 && i > j) continue;
+      const double v = pool[jl * (BM + 1) + il];
+      if (slab) {
+        slab[(size_t)split * m * n + (size_t)j * m + i] = v;
+      } else if (!use_c) {
+        C[i + (size_t)j * ldc] = alpha * v;
+      } else {
+        double cv;
+        if (PREFETCH_C) cv = cpre[(c0 / ECH) * (BM * ECH / 256) + q];
+        else cv = C[i + (size_t)j * ldc];
+        C[i + (size_t)j * ldc] = alpha * v + beta * cv;
+      }
+    }
+    if (c0 + ECH < BN) __syncthreads();
+  }
 }
 
 __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restrict__ slab,
@@ -248,13 +275,59 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   return SMG_OK;
 }
 
+// Do two column-major blocks share an element?  Blocks with the same leading
+// dimension are treated as rectangles of one matrix (the sub-blocks Murray's
+// reverse works on: La[k:, j:k] vs La[j:k, 0:k] are disjoint although their
+// address ranges interleave); otherwise the address ranges are compared.
+inline bool overlaps(const double* X, int ldx, int rows, int cols, const double* C, int ldc, int m,
+                     int n) {
+  if (rows <= 0 || cols <= 0 || m <= 0 || n <= 0) return false;
+  const double* x1 = X + (size_t)(cols - 1) * ldx + rows;
+  const double* c1 = C + (size_t)(n - 1) * ldc + m;
+  if (!(X < c1 && C < x1)) return false;
+  if (ldx != ldc) return true;
+  const double* base = X < C ? X : C;
+  const long long ox = X - base, oc = C - base, ld = ldx;
+  const long long rx = ox % ld, cx = ox / ld, rc = oc % ld, cc = oc / ld;
+  return rx < rc + m && rc < rx + rows && cx < cc + n && cc < cx + cols;
+}
+
 template <bool TA, bool TB, int MODE>
 int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
                   int lda, const double* B, int ldb, double beta, double* C, int ldc) {
+  // In-place products (C aliases an operand: the blocked TRSMs C = C Dinv,
+  // L21 = A21 Dinv^T, X_p = W_p B_p) are race-free only when every workgroup
+  // owns whole rows (C aliases A) or whole columns (C aliases B) of C.
+  const bool alias_a = overlaps(A, lda, TA ? k : m, TA ? m : k, C, ldc, m, n);
+  const bool alias_b = overlaps(B, ldb, TB ? n : k, TB ? k : n, C, ldc, m, n);
+  if (alias_a || alias_b) {
+    if (MODE == 0 && alias_a && !alias_b && n <= 64)
+      return launch<32, 64, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (MODE == 0 && alias_b && !alias_a && m <= 64)
+      return launch<64, 32, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    // general aliasing: out of place through a workspace, then C = T (+ beta C)
+    double* T = smg_ws(ctx, SMG_WS_ALIAS, (size_t)m * n);
+    if (!T) return SMG_ERR_OOM;
+    int rc = dispatch_tile<TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, 0.0, T, m);
+    if (rc) return rc;
+    if (beta == 0.0) return smg_copy_impl(ctx, m, n, T, m, C, ldc, 1.0, 0);
+    if (beta != 1.0) {
+      rc = smg_scale_impl(ctx, m, n, beta, C, ldc, MODE);
+      if (rc) return rc;
+    }
+    return smg_copy_impl(ctx, m, n, T, m, C, ldc, 1.0, 1);
+  }
+  // tile size by how many CUs the output grid can occupy (256 CUs): large
+  // outputs take 128x128 tiles (operand reuse), mid-size 64x64, and the
+  // CU-starved shapes of the blocked Cholesky (one 64-wide block column or
+  // row) 32x32, so the grid spreads over 4x more CUs
   const long long big_tiles = (long long)smg_ceil_div(m, 128) * smg_ceil_div(n, 128);
-  if (big_tiles >= 256)
+  const long long mid_tiles = (long long)smg_ceil_div(m, 64) * smg_ceil_div(n, 64);
+  if (big_tiles >= 256 && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  return launch<64, 64, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  if (mid_tiles >= 192)
+    return launch<64, 64, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
 }
 
 }  // namespace

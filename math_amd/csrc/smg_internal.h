@@ -36,8 +36,8 @@ struct smg_ctx {
   void* host_scratch;
   size_t host_scratch_size;
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[4];
-  size_t ws_doubles[4];
+  double* ws[5];
+  size_t ws_doubles[5];
   // profiling
   int prof_on;
   std::vector<smg_prof_slot> prof_pending;
@@ -80,7 +80,8 @@ struct smg_prof_scope {
 
 // named persistent workspaces (grow on demand; a growth synchronises the
 // stream, so steady-state evaluations never reallocate)
-enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3 };
+enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_ALIAS = 4,
+       SMG_WS_COUNT = 5 };
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 // C = beta C (lower != 0: lower triangle only)
 int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int lower);

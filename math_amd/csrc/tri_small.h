@@ -57,6 +57,35 @@ __device__ inline void lds_mma64(double* C, const double* A, const double* B, do
   __syncthreads();
 }
 
+// C (64x64) = op(A) op(B) (beta = 0) with NW = 8 waves: wave w owns row stripe
+// w & 3 and column tiles 2 (w >> 2) .. +1.  Safe when C aliases A or B.
+template <bool TA, bool TB>
+__device__ inline void lds_mma64_8w(double* C, const double* A, const double* B) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = l & 15, fk = l >> 4;
+  const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
+  d4 acc[2];
+  acc[0] = d4{0.0, 0.0, 0.0, 0.0};
+  acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < SMG_NB; k0 += 4) {
+    const int kk = k0 + fk;
+    const double a = TA ? A[kk * SMG_NBP + i] : A[i * SMG_NBP + kk];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = 16 * (t0 + t) + fr;
+      const double b = TB ? B[j * SMG_NBP + kk] : B[kk * SMG_NBP + j];
+      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[(16 * (w & 3) + fk + 4 * r) * SMG_NBP + 16 * (t0 + t) + fr] = acc[t][r];
+  __syncthreads();
+}
+
 // One wave: Cholesky of the 16x16 leaf p of D (lower), then its inverse into X.
 // Latches SMG_ERR_NOT_PD (check_pos_definite, prim/mat/err/check_pos_definite.hpp:77-81).
 __device__ inline void wave_leaf_potrf_inv(double* D, double* X, int p, int* status) {
@@ -554,6 +583,22 @@ __device__ inline void lds_load_block(double* D, const double* A, int ld, int b,
 
 // zero-padded load (no identity): for adjoint blocks
 __device__ inline void lds_load_block0(double* D, const double* A, int ld, int b, bool lower_only) {
+  constexpr int PER = SMG_NB * SMG_NB / SMG_DIAG_THREADS;
+  if (blockDim.x == SMG_DIAG_THREADS) {  // all global loads in flight at once
+    double v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = threadIdx.x + q * SMG_DIAG_THREADS;
+      const int c = e / SMG_NB, r = e % SMG_NB;
+      v[q] = (r < b && c < b && (!lower_only || r >= c)) ? A[r + (size_t)c * ld] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = threadIdx.x + q * SMG_DIAG_THREADS;
+      D[(e % SMG_NB) * SMG_NBP + e / SMG_NB] = v[q];
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
     const int c = e / SMG_NB, r = e % SMG_NB;
     double v = 0.0;

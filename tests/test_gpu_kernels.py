@@ -70,6 +70,45 @@ def test_gemm_triangle(ctx, uplo):
     assert np.array_equal(out[~mask], C[~mask])  # other triangle untouched
 
 
+@pytest.mark.parametrize("case", ["c_is_a_right", "c_is_b_left", "c_in_a_general", "disjoint_blocks"])
+def test_gemm_in_place(ctx, case):
+    """In-place products of the blocked TRSMs (C = C W, C = W C) and general
+    aliasing must be race-free whatever tile size the dispatcher picks."""
+    rng = np.random.default_rng(11)
+    if case == "c_is_a_right":      # C (2000 x 64) = C W (64 x 64), like C_adj D^{-1}
+        m, n = 2000, 64
+        X = rng.standard_normal((m, n)); W = rng.standard_normal((n, n))
+        dX, dW = ctx.put(F(X)), ctx.put(F(W))
+        ctx.call("smg_gemm", 0, 1, 0, m, n, n, 1.0, dX, m, dW, n, 0.0, dX, m)
+        ref = X @ W.T
+        out = ctx.get(dX, m * n).reshape(n, m).T
+    elif case == "c_is_b_left":     # C (64 x 300) = W^T C, like X_p = W_p^T B_p
+        m, n = 64, 300
+        X = rng.standard_normal((m, n)); W = rng.standard_normal((m, m))
+        dX, dW = ctx.put(F(X)), ctx.put(F(W))
+        ctx.call("smg_gemm", 1, 0, 0, m, n, m, 1.0, dW, m, dX, m, 0.0, dX, m)
+        ref = W.T @ X
+        out = ctx.get(dX, m * n).reshape(n, m).T
+    elif case == "c_in_a_general":  # C (300 x 200) = 2 C B - C, beta != 0: out-of-place fallback
+        m, n = 300, 200
+        X = rng.standard_normal((m, n)); B = rng.standard_normal((n, n))
+        dX, dB = ctx.put(F(X)), ctx.put(F(B))
+        ctx.call("smg_gemm", 0, 0, 0, m, n, n, 2.0, dX, m, dB, n, -1.0, dX, m)
+        ref = 2.0 * X @ B - X
+        out = ctx.get(dX, m * n).reshape(n, m).T
+    else:                            # disjoint sub-blocks of one matrix (Murray's R/D/B/C)
+        N = 400
+        Lm = rng.standard_normal((N, N))
+        dL = ctx.put(F(Lm))
+        j, k = 128, 192                   # La[j:k, 0:k] -= La[k:, j:k]^T La[k:, 0:k]
+        at = lambda r, c: dL + 8 * (r + c * N)  # noqa: E731  (device address of L[r, c])
+        ctx.call("smg_gemm", 1, 0, 0, k - j, k, N - k, -1.0, at(k, j), N, at(k, 0), N, 1.0, at(j, 0), N)
+        ref = Lm.copy()
+        ref[j:k, 0:k] -= Lm[k:, j:k].T @ Lm[k:, 0:k]
+        out = ctx.get(dL, N * N).reshape(N, N).T
+    assert np.abs(out - ref).max() <= 1e-11 * (np.abs(ref).max() + 1.0)
+
+
 def test_mfma_layout_asymmetric(ctx):
     """A = I with an asymmetric B catches a transposed D layout."""
     n = 16

@@ -2,12 +2,14 @@
 // (n = 4096, b = 64, block column j = 2048) plus an empty-kernel floor.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "../include/smg_hip.h"
 
 __global__ void k_empty() {}
 
-int main() {
+int main(int argc, char** argv) {
+  const int only = argc > 1 ? atoi(argv[1]) : -1;
   smg_ctx* ctx = nullptr;
   smg_ctx_create(0, 1ull << 30, &ctx);
   hipStream_t s = (hipStream_t)smg_ctx_stream(ctx);
@@ -43,7 +45,9 @@ int main() {
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   printf("%-34s %8.2f us\n", "empty kernel", ms * 1000 / reps);
-  for (auto& sh : shapes) {
+  for (size_t si = 0; si < shapes.size(); ++si) {
+    auto& sh = shapes[si];
+    if (only >= 0 && int(si) != only) continue;
     const int lda = n, ldb = n, ldc = n;
     for (int w = 0; w < 3; ++w)
       smg_gemm(ctx, sh.ta, sh.tb, sh.uplo, sh.m, sh.nn, sh.k, -1.0, A, lda, B, ldb, 1.0, C, ldc);
