@@ -536,13 +536,228 @@ __device__ inline void lds_trtri64_blocked(const double* D, double* X, double* T
   }
 }
 
+// ---------------------------------------------------------------------------
+// Look-ahead variant of lds_potrf64_blocked (same panels, same arithmetic per
+// element): in iteration p, wave 0 applies panel p's rank-8 update to panel
+// p+1 and factors it, WHILE waves 1..7 apply panel p's update to the columns
+// right of panel p+1.  The serial pivot chain (wave 0) overlaps the bulk of
+// the trailing work; one barrier per panel.
+// wave 0: factor the 8 columns held in a[] (lane i = row i, rows < j0 hold 0)
+__device__ __forceinline__ void wave_factor8_reg(double (&a)[8], int j0, bool& bad) {
+  const int i = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const double piv = bcast(a[t], j0 + t);
+    bad |= !(piv > 0.0 && piv < INFINITY);
+    double r = __builtin_amdgcn_rsq(piv);
+    r = r * (1.5 - 0.5 * piv * r * r);
+    r = r * (1.5 - 0.5 * piv * r * r);
+    const double li = (i == j0 + t) ? piv * r : a[t] * r;
+    a[t] = li;
+#pragma unroll
+    for (int c = t + 1; c < 8; ++c) a[c] -= li * bcast(li, j0 + c);
+  }
+}
+
+// wave 0: factor panel columns j0..j0+7 (rows >= j0) of D in place, with NO
+// cross-lane traffic on the pivot chain: every lane factors the 8x8 diagonal
+// block redundantly in registers (left-looking), then solves its own row
+// against it: x_t = (a_t - sum_{s<t} x_s L_ts) / L_tt.
+__device__ __forceinline__ void wave_panel8_local(double* D, int j0, bool& bad) {
+  const int i = threadIdx.x & 63;
+  double Ld[8][8], inv[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c <= r; ++c) Ld[r][c] = D[(j0 + r) * SMG_NBP + j0 + c];  // LDS broadcast
+  double a[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a[t] = (i >= j0 + 8) ? D[i * SMG_NBP + j0 + t] : 0.0;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    double piv = Ld[t][t];
+#pragma unroll
+    for (int q = 0; q < t; ++q) piv -= Ld[t][q] * Ld[t][q];
+    bad |= !(piv > 0.0 && piv < INFINITY);
+    double r = __builtin_amdgcn_rsq(piv);
+    r = r * (1.5 - 0.5 * piv * r * r);
+    r = r * (1.5 - 0.5 * piv * r * r);
+    inv[t] = r;
+    Ld[t][t] = piv * r;
+#pragma unroll
+    for (int c = t + 1; c < 8; ++c) {
+      double v = Ld[c][t];
+#pragma unroll
+      for (int q = 0; q < t; ++q) v -= Ld[c][q] * Ld[t][q];
+      Ld[c][t] = v * r;
+    }
+  }
+  // own row below the diagonal block: x = a L_dd^{-T}
+  double x[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    double v = a[t];
+#pragma unroll
+    for (int q = 0; q < t; ++q) v -= x[q] * Ld[t][q];
+    x[t] = v * inv[t];
+  }
+  if (i >= j0 + 8) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) D[i * SMG_NBP + j0 + t] = x[t];
+  } else if (i >= j0) {
+    const int r = i - j0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (t <= r) {
+        double v = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr)
+          if (rr == r) v = Ld[rr][t];
+        D[i * SMG_NBP + j0 + t] = v;
+      }
+  }
+}
+
+__device__ __forceinline__ void wave_store8(double* D, const double (&a)[8], int j0) {
+  const int i = threadIdx.x & 63;
+  if (i >= j0)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (i >= j0 + t) D[i * SMG_NBP + j0 + t] = a[t];
+}
+
+// wave 0: load, factor (v_readlane broadcasts), store panel j0..j0+7
+__device__ __forceinline__ void wave_panel8_rl(double* D, int j0, bool& bad) {
+  const int i = threadIdx.x & 63;
+  double a[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a[t] = (i >= j0) ? D[i * SMG_NBP + j0 + t] : 0.0;
+  wave_factor8_reg(a, j0, bad);
+  wave_store8(D, a, j0);
+}
+
+__device__ inline void lds_potrf64_lookahead(double* D, int* status) {
+  const int i = threadIdx.x & 63;
+  const int g = threadIdx.x >> 6;
+  bool bad = false;
+  if (g == 0) wave_panel8_rl(D, 0, bad);
+  __syncthreads();
+  for (int p = 0; p < 7; ++p) {
+    const int j0 = 8 * p, c1 = j0 + 8, c2 = j0 + 16;
+    // (A) waves 1..7: panel p+1 (rows >= c1, 8 columns) -= panel p's rank-8
+    //     update, one element per thread
+    if (g > 0) {
+      const int e = threadIdx.x - 64;
+      const int r = c1 + (e >> 3), c = c1 + (e & 7);
+      if (r < 64 && r >= c) {
+        double v = D[r * SMG_NBP + c];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v -= D[r * SMG_NBP + j0 + t] * D[c * SMG_NBP + j0 + t];
+        D[r * SMG_NBP + c] = v;
+      }
+    }
+    __syncthreads();
+    // (B) wave 0 factors panel p+1 while waves 1..7 update columns >= c2
+    if (g == 0) {
+      wave_panel8_rl(D, c1, bad);
+    } else if (c2 < 64) {
+      // rank-8 trailing update of rows/cols >= c2 on the matrix cores: 16x16
+      // tiles (ti >= tj) from 16-tile t0 = c2/16, 2 MFMAs each (K = 8); only
+      // entries with col >= c2 and row >= col are written back
+      const int t0 = c2 >> 4, nt = 4 - t0, ntiles = nt * (nt + 1) / 2;
+      const int fr = i & 15, fk = i >> 4;
+      for (int q = g - 1; q < ntiles; q += 7) {
+        int ti = 0, rem = q;
+        while (rem > ti) {
+          rem -= ti + 1;
+          ++ti;
+        }
+        const int tj = rem + t0;
+        ti += t0;
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < 8; k0 += 4) {
+          const double av = D[(16 * ti + fr) * SMG_NBP + j0 + k0 + fk];
+          const double bv = D[(16 * tj + fr) * SMG_NBP + j0 + k0 + fk];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        const int col = 16 * tj + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ti + fk + 4 * r;
+          if (col >= c2 && row >= col) D[row * SMG_NBP + col] -= acc[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (bad) atomicOr(status, (int)SMG_ERR_NOT_PD);
+}
+
+// X = L^{-1} (64x64) with 16x16 blocks on the fp64 matrix cores:
+//   leaves: wave w < 4 inverts diagonal block w (lane c < 16 owns column c);
+//   block rows p = 1..3:  T = -L[p, 0:p] X[0:p, 0:p]  (wave q < p: tile (p, q)),
+//                         X[p, 0:p] = X_pp T          (wave q < p)
+// X: LDS [64][SMG_NBP], fully written (upper zeros); T: LDS >= 3 * 256 doubles.
+__device__ inline void lds_trtri64_mfma(const double* D, double* X, double* T) {
+  const int l = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < 64 * SMG_NBP; e += blockDim.x) X[e] = 0.0;
+  __syncthreads();
+  if (w < 4) {
+    const int r0 = 16 * w;
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      double s = (l == r) ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < r; ++t) s -= D[(r0 + r) * SMG_NBP + r0 + t] * x[t];
+      const double dd = D[(r0 + r) * SMG_NBP + r0 + r];
+      double rr = __builtin_amdgcn_rcp(dd);
+      rr = rr * (2.0 - dd * rr);
+      rr = rr * (2.0 - dd * rr);
+      x[r] = s * rr;
+    }
+    if (l < 16)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) X[(r0 + r) * SMG_NBP + r0 + l] = x[r];
+  }
+  __syncthreads();
+  const int fr = l & 15, fk = l >> 4;
+  for (int p = 1; p < 4; ++p) {
+    if (w < p) {  // T_q = -sum_{k < 16p} L[16p + r][k] X[k][16q + c]
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      for (int k0 = 16 * w; k0 < 16 * p; k0 += 4) {  // X[k][16w..] = 0 for k < 16w
+        const double a = D[(16 * p + fr) * SMG_NBP + k0 + fk];
+        const double b = X[(k0 + fk) * SMG_NBP + 16 * w + fr];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[w * 256 + (fk + 4 * r) * 16 + fr] = -acc[r];
+    }
+    __syncthreads();
+    if (w < p) {  // X[16p + r][16w + c] = sum_t Xpp[r][t] T_w[t][c]
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k0 = 0; k0 < 16; k0 += 4) {
+        const double a = X[(16 * p + fr) * SMG_NBP + 16 * p + k0 + fk];
+        const double b = T[w * 256 + (k0 + fk) * 16 + fr];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) X[(16 * p + fk + 4 * r) * SMG_NBP + 16 * w + fr] = acc[r];
+    }
+    __syncthreads();
+  }
+}
+
 // Drop-in for lds_potrf_inv64_v2 built from the blocked pieces: factor (if
 // asked) then invert, then one coalesced write of L (lower) and X = L^{-1}.
 __device__ inline void lds_potrf_inv64_blk(double* D, double* X, int b, double* Lout, int ldl,
                                            double* Xout, int ldx, int* status, bool factor) {
-  __shared__ double T[8 * 64];
-  if (factor) lds_potrf64_blocked(D, status);
-  lds_trtri64_blocked(D, X, T);
+  __shared__ double T[3 * 256];
+  if (factor) lds_potrf64_lookahead(D, status);
+  lds_trtri64_mfma(D, X, T);
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) {
     const int c = e / b, r = e % b;
     if (Lout) Lout[r + (size_t)c * ldl] = (r >= c) ? D[r * SMG_NBP + c] : 0.0;

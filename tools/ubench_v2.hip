@@ -18,6 +18,15 @@ __global__ __launch_bounds__(512) void k_v2(double* g, double* L, double* dinv, 
   if (MODE == 1) lds_potrf_inv64_blk(D, X, 64, L, 64, dinv, 64, st, true);
   if (MODE == 2) { lds_potrf64_blocked(D, st); }
   if (MODE == 3) { lds_potrf64_blocked(D, st); __shared__ double T[512]; lds_trtri64_blocked(D, X, T); }
+  if (MODE == 4) { lds_potrf64_lookahead(D, st); }
+  if (MODE == 5) { lds_potrf64_lookahead(D, st); __shared__ double T2[768]; lds_trtri64_mfma(D, X, T2); }
+  if (MODE == 5 || MODE == 1) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < 4096; e += blockDim.x) {
+      const int c = e / 64, r = e % 64;
+      if (MODE == 5) { L[r + 64 * c] = r >= c ? D[r * SMG_NBP + c] : 0.0; dinv[r + 64 * c] = r >= c ? X[r * SMG_NBP + c] : 0.0; }
+    }
+  }
   __syncthreads();
   long long t2 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = t2 - t1; }
@@ -45,7 +54,8 @@ int main() {
       hipMemcpy(Xr[slot].data(), dinv, 4096 * 8, hipMemcpyDeviceToHost);
     }
   };
-  run(0, "v2 fused", k_v2<0>); run(1, "blocked", k_v2<1>); run(-1, "blk potrf", k_v2<2>); run(-1, "blk potrf+inv", k_v2<3>);
+  run(0, "v2 fused", k_v2<0>); run(-1, "blk potrf", k_v2<2>); run(-1, "blk potrf+inv", k_v2<3>);
+  run(-1, "la potrf", k_v2<4>); run(1, "la+mfma inv", k_v2<5>);
   double dl = 0, dx = 0;
   for (int e = 0; e < 4096; ++e) {
     dl = fmax(dl, fabs(Lr[0][e] - Lr[1][e]) / (fabs(Lr[0][e]) + 1e-300) * (Lr[0][e] != 0));
