@@ -116,11 +116,233 @@ __global__ __launch_bounds__(512) void k_symbolic_rev(const double* __restrict__
   }
 }
 
+// P (n x n dense) = X + X^T from the lower triangle of X with halved diagonal
+__global__ void k_sym_from_half(const double* __restrict__ X, int ldx, int n, double* __restrict__ P) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    P[e] = i > j ? X[i + (size_t)j * ldx] : (i < j ? X[j + (size_t)i * ldx] : 2.0 * X[i + (size_t)i * ldx]);
+  }
+}
+
+// Recursive-doubling step of the block inverses of a lower-triangular L:
+// from the s x s inverses Wi (rows aligned with L, ld ldi, s columns) to the
+// 2s x 2s inverses Wo (ld ldo, 2s columns) of the nb full 2s-blocks:
+// this kernel copies the diagonal s-blocks and zeroes the upper-right one;
+// the lower-left X21 = -X22 (L21 X11) comes from two batched GEMMs.
+__global__ void k_inv_double_diag(int nb, int s2, const double* __restrict__ Wi, int ldi,
+                                  double* __restrict__ Wo, int ldo) {
+  const int s = s2 / 2;
+  const long long tot = (long long)nb * s2 * s2;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(e / ((long long)s2 * s2));
+    const int rem = (int)(e % ((long long)s2 * s2));
+    const int c = rem / s2, r = rem % s2;
+    const int row = q * s2 + r;
+    double v;
+    if (r < s && c < s) v = Wi[row + (size_t)c * ldi];
+    else if (r >= s && c >= s) v = Wi[row + (size_t)(c - s) * ldi];
+    else if (r < s) v = 0.0;
+    else continue;  // lower-left: written by the GEMMs
+    Wo[row + (size_t)c * ldo] = v;
+  }
+}
+
+// G = tril(X) (n x n dense, ld n)
+__global__ void k_tril_copy(const double* __restrict__ X, int ldx, int n, double* __restrict__ G) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    G[e] = i >= j ? X[i + (size_t)j * ldx] : 0.0;
+  }
+}
+
+// S (n x n, ld n): upper triangle <- lower triangle (sym_from_lower)
+__global__ void k_mirror_lower(double* __restrict__ S, int n) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    if (i < j) S[i + (size_t)j * n] = S[j + (size_t)i * n];
+  }
+}
+
+// Dadj (ld lda) <- tril(S) with halved diagonal; strict upper untouched
+__global__ void k_half_lower(const double* __restrict__ S, int n, double* __restrict__ Dadj, int lda) {
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n), i = (int)(e % n);
+    if (i > j) Dadj[i + (size_t)j * lda] = S[e];
+    else if (i == j) Dadj[i + (size_t)j * lda] = 0.5 * S[e];
+  }
+}
+
 inline int grid_for(long long tot) {
   long long g = (tot + 255) / 256;
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   return (int)g;
+}
+
+// Murray's reverse on an n x n (sub)matrix with SMG_NB blocks, in place:
+// on exit the lower triangle of La holds Abar of chol(this block) with the
+// reference's convention (halved diagonal, :160-161).  Dv: the SMG_NB-block
+// inverses of L's diagonal blocks (rows aligned with L, leading dimension ldd).
+int chol_rev_blocks(smg_ctx* ctx, const double* L, int ldl, const double* Dv, int ldd, double* La,
+                    int ldla, int n) {
+  double* Ssym = smg_ws(ctx, SMG_WS_TMP, (size_t)SMG_NB * SMG_NB);
+  if (!Ssym) return SMG_ERR_OOM;
+  const int nblk = (n + SMG_NB - 1) / SMG_NB;
+  for (int p = nblk - 1; p >= 0; --p) {
+    const int j = p * SMG_NB;
+    const int b = min(SMG_NB, n - j);
+    const int k = j + b, m = n - k;
+    const double* Di = Dv + j;
+    double* Cadj = La + k + (size_t)j * ldla;
+    double* Badj = La + k;
+    double* Dadj = La + j + (size_t)j * ldla;
+    double* Radj = La + j;
+    const double* R = L + j;
+    const double* Bv = L + k;
+    int rc;
+    if (m > 0) {
+      // C_adj = C_adj D^{-1}
+      rc = smg_gemm_impl(ctx, 0, 0, 0, m, b, b, 1.0, Cadj, ldla, Di, ldd, 0.0, Cadj, ldla);
+      if (rc) return rc;
+      if (j > 0) {  // B_adj -= C_adj R
+        rc = smg_gemm_impl(ctx, 0, 0, 0, m, j, b, -1.0, Cadj, ldla, R, ldl, 1.0, Badj, ldla);
+        if (rc) return rc;
+      }
+      // [R_adj | D_adj] -= C_adj^T [B | C]: both operands are contiguous column
+      // ranges (L[k:, 0:k] and Abar[j:k, 0:k]), so one GEMM (one split-K
+      // reduction) does both updates; R_adj's does not depend on the symbolic step
+      rc = smg_gemm_impl(ctx, 1, 0, 0, b, k, m, -1.0, Cadj, ldla, Bv, ldl, 1.0, Radj, ldla);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_symbolic_rev, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream,
+                       L + j + (size_t)j * ldl, ldl, Di, ldd, Dadj, ldla, b, Ssym);
+    if (j > 0) {
+      // R_adj -= sym(D_adj) R
+      rc = smg_gemm_impl(ctx, 0, 0, 0, b, j, b, -1.0, Ssym, b, R, ldl, 1.0, Radj, ldla);
+      if (rc) return rc;
+    }
+  }
+  return SMG_OK;
+}
+
+// Inverses of the full SMG_NB2 diagonal blocks of L by two recursive-doubling
+// levels from the SMG_NB-block inverses Dv (ld ldd): W (ld ldw, SMG_NB2 columns).
+int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, const double* Dv, int ldd, int n,
+                        double* W128, double* W, int ldw) {
+  const double* Wi = Dv;
+  int ldi = ldd;
+  for (int s2 = 2 * SMG_NB; s2 <= SMG_NB2; s2 *= 2) {
+    const int s = s2 / 2, nb = n / s2;
+    if (nb == 0) return SMG_OK;
+    double* Wo = s2 == SMG_NB2 ? W : W128;
+    hipLaunchKernelGGL(k_inv_double_diag, dim3(grid_for((long long)nb * s2 * s2)), dim3(256), 0,
+                       ctx->stream, nb, s2, Wi, ldi, Wo, ldw);
+    double* T = smg_ws(ctx, SMG_WS_TMP, (size_t)nb * s * s);
+    if (!T) return SMG_ERR_OOM;
+    // T_q = L21_q X11_q ;  X21_q = -X22_q T_q
+    int rc = smg_gemm_batched_impl(ctx, 0, 0, s, s, s, 1.0, L + s, ldl, (long long)s2 * (ldl + 1),
+                                   Wi, ldi, s2, 0.0, T, s, (long long)s * s, nb);
+    if (rc) return rc;
+    rc = smg_gemm_batched_impl(ctx, 0, 0, s, s, s, -1.0, Wi + s, ldi, s2, T, s, (long long)s * s,
+                               0.0, Wo + s, ldw, s2, nb);
+    if (rc) return rc;
+    Wi = Wo;
+    ldi = ldw;
+  }
+  return SMG_OK;
+}
+
+// Two-level Murray reverse: outer blocks of SMG_NB2 columns make the three
+// big updates rank-SMG_NB2 (compute-bound GEMMs).  The diagonal block's
+// symbolic adjoint (:101-111) is applied in closed form to the whole
+// SMG_NB2 block: P = D^{-T} sym(D^T tril(Dadj)) D^{-1} with the block inverse
+// from chol_block_inverses (a ragged last block falls back to the exact
+// inner recursion chol_rev_blocks); P also feeds R_adj -= P R.
+int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* Dv, int ldd,
+                       double* La, int ldla, int n) {
+  const int nbo = (n + SMG_NB2 - 1) / SMG_NB2;
+  double* Winv = smg_ws(ctx, SMG_WS_INV, (size_t)n * (SMG_NB2 + SMG_NB2 / 2));
+  if (!Winv) return SMG_ERR_OOM;
+  double* W = Winv;                                 // n x SMG_NB2, ld n
+  double* W128 = Winv + (size_t)n * SMG_NB2;        // n x SMG_NB2/2, ld n
+  int rc = chol_block_inverses(ctx, L, ldl, Dv, ldd, n, W128, W, n);
+  if (rc) return rc;
+  const size_t bb = (size_t)SMG_NB2 * SMG_NB2;
+  for (int P = nbo - 1; P >= 0; --P) {
+    const int J = P * SMG_NB2;
+    const int K = min(J + SMG_NB2, n), bs = K - J, m = n - K;
+    const bool full = bs == SMG_NB2;
+    double* Ca = La + K + (size_t)J * ldla;
+    double* Da = La + J + (size_t)J * ldla;
+    const double* Ld = L + J + (size_t)J * ldl;
+    const double* Wp = W + J;  // this block's inverse, ld n
+    if (m > 0) {
+      if (full) {  // C_adj = C_adj D^{-1}
+        rc = smg_gemm_impl(ctx, 0, 0, 0, m, bs, bs, 1.0, Ca, ldla, Wp, n, 0.0, Ca, ldla);
+        if (rc) return rc;
+      } else {  // ragged: blocked right solve with the SMG_NB inverses
+        const int nbi = (bs + SMG_NB - 1) / SMG_NB;
+        for (int q = nbi - 1; q >= 0; --q) {
+          const int jq = q * SMG_NB, bq = min(SMG_NB, bs - jq), rest = bs - jq - bq;
+          if (rest > 0) {
+            rc = smg_gemm_impl(ctx, 0, 0, 0, m, bq, rest, -1.0, Ca + (size_t)(jq + bq) * ldla, ldla,
+                               Ld + (jq + bq) + (size_t)jq * ldl, ldl, 1.0, Ca + (size_t)jq * ldla,
+                               ldla);
+            if (rc) return rc;
+          }
+          rc = smg_gemm_impl(ctx, 0, 0, 0, m, bq, bq, 1.0, Ca + (size_t)jq * ldla, ldla,
+                             Dv + J + jq, ldd, 0.0, Ca + (size_t)jq * ldla, ldla);
+          if (rc) return rc;
+        }
+      }
+      if (J > 0) {  // B_adj -= C_adj R
+        rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Ca, ldla, L + J, ldl, 1.0, La + K, ldla);
+        if (rc) return rc;
+      }
+      // [R_adj | D_adj] -= C_adj^T [B | C]
+      rc = smg_gemm_impl(ctx, 1, 0, 0, bs, K, m, -1.0, Ca, ldla, L + K, ldl, 1.0, La + J, ldla);
+      if (rc) return rc;
+    }
+    double* Pm;
+    if (full) {
+      double* G = smg_ws(ctx, SMG_WS_TMP, 3 * bb);
+      if (!G) return SMG_ERR_OOM;
+      double* S = G + bb;
+      double* T = S + bb;
+      const int gb = grid_for((long long)bb);
+      hipLaunchKernelGGL(k_tril_copy, dim3(gb), dim3(256), 0, ctx->stream, Da, ldla, bs, G);
+      rc = smg_gemm_impl(ctx, 1, 0, 0, bs, bs, bs, 1.0, Ld, ldl, G, bs, 0.0, S, bs);  // D^T tril(Dadj)
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_mirror_lower, dim3(gb), dim3(256), 0, ctx->stream, S, bs);
+      rc = smg_gemm_impl(ctx, 1, 0, 0, bs, bs, bs, 1.0, Wp, n, S, bs, 0.0, T, bs);  // D^{-T} S
+      if (rc) return rc;
+      rc = smg_gemm_impl(ctx, 0, 0, 0, bs, bs, bs, 1.0, T, bs, Wp, n, 0.0, S, bs);  // ... D^{-1}
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_half_lower, dim3(gb), dim3(256), 0, ctx->stream, S, bs, Da, ldla);
+      Pm = S;
+    } else {
+      rc = chol_rev_blocks(ctx, Ld, ldl, Dv + J, ldd, Da, ldla, bs);
+      if (rc) return rc;
+      Pm = smg_ws(ctx, SMG_WS_ALIAS, (size_t)bs * bs);
+      if (!Pm) return SMG_ERR_OOM;
+      hipLaunchKernelGGL(k_sym_from_half, dim3(grid_for((long long)bs * bs)), dim3(256), 0,
+                         ctx->stream, Da, ldla, bs, Pm);
+    }
+    if (J > 0) {  // R_adj -= P R
+      rc = smg_gemm_impl(ctx, 0, 0, 0, bs, J, bs, -1.0, Pm, bs, L + J, ldl, 1.0, La + J, ldla);
+      if (rc) return rc;
+    }
+  }
+  return SMG_OK;
 }
 
 }  // namespace
@@ -150,6 +372,23 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   if (A != L || lda != ldl)
     hipLaunchKernelGGL(k_copy_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
                        A, lda, n, L, ldl);
+  // Right-looking with one-block look-ahead on two streams.  Step p (columns
+  // [j, k)): crit = potrf(p), L21(p), then the WINDOW update of the next
+  // block column [k, k + NB); side = the REST of the trailing update,
+  // columns [k + NB, n).  Hazards: W(p) and R(p-1) both write columns
+  // [k, k + NB) -> crit waits R(p-1) before W(p); R(p) reads L21(p) -> side
+  // waits L21(p); R(p) after R(p-1) by stream order.  R(p) then overlaps
+  // W(p) + potrf(p+1) + L21(p+1), the serial chain.
+  // (measured on MI355X: each cross-queue event costs ~12 us of dependency
+  // latency, more than the overlap it buys at NB = 64, so it is off by default)
+  const bool la = false && n > 2 * SMG_NB && smg_side_begin(ctx) == SMG_OK;
+  hipEvent_t ev_r = nullptr;  // last R(p) recorded on the side stream
+  int evi = 0;
+  if (la) {  // the side stream starts after everything already on the tape's stream
+    hipEvent_t e0 = smg_event(ctx, evi++);
+    hipEventRecord(e0, ctx->stream);
+    hipStreamWaitEvent(ctx->side, e0, 0);
+  }
   for (int j = 0; j < n; j += SMG_NB) {
     const int b = min(SMG_NB, n - j);
     const int m = n - j - b;
@@ -163,10 +402,37 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
       int rc = smg_gemm_impl(ctx, 0, 1, 0, m, b, b, 1.0, L21, ldl, Di, n, 0.0, L21, ldl);
       if (rc) return rc;
       double* L22 = L + (j + b) + (size_t)(j + b) * ldl;
-      rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, b, -1.0, L21, ldl, L21, ldl, 1.0, L22, ldl);
+      if (!la) {
+        rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, b, -1.0, L21, ldl, L21, ldl, 1.0, L22, ldl);
+        if (rc) return rc;
+        continue;
+      }
+      const int w = min(SMG_NB, m);  // window: the next block column
+      hipEvent_t ev_l21 = smg_event(ctx, evi++);
+      hipEventRecord(ev_l21, ctx->stream);
+      if (ev_r) hipStreamWaitEvent(ctx->stream, ev_r, 0);
+      // W(p): A[k:, k:k+w] -= L21 L21[0:w]^T  (lower part of the diagonal sub-block
+      // via a triangle product, the rows below with a plain one)
+      rc = smg_gemm_impl(ctx, 0, 1, 1, w, w, b, -1.0, L21, ldl, L21, ldl, 1.0, L22, ldl);
       if (rc) return rc;
+      if (m > w) {
+        rc = smg_gemm_impl(ctx, 0, 1, 0, m - w, w, b, -1.0, L21 + w, ldl, L21, ldl, 1.0, L22 + w,
+                           ldl);
+        if (rc) return rc;
+        // R(p) on the side stream: columns [k + w, n), lower triangle
+        hipStreamWaitEvent(ctx->side, ev_l21, 0);
+        {
+          smg_on_side on(ctx);
+          rc = smg_gemm_impl(ctx, 0, 1, 1, m - w, m - w, b, -1.0, L21 + w, ldl, L21 + w, ldl, 1.0,
+                             L22 + w + (size_t)w * ldl, ldl);
+        }
+        if (rc) return rc;
+        ev_r = smg_event(ctx, evi++);
+        hipEventRecord(ev_r, ctx->side);
+      }
     }
   }
+  if (ev_r) hipStreamWaitEvent(ctx->stream, ev_r, 0);  // join
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
@@ -187,43 +453,9 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
                          L + j + (size_t)j * ldl, ldl, b, Dv + j, n);
     }
   }
-  double* Ssym = smg_ws(ctx, SMG_WS_TMP, (size_t)SMG_NB * SMG_NB);
-  if (!Ssym) return SMG_ERR_OOM;
-  const int nblk = (n + SMG_NB - 1) / SMG_NB;
-  for (int p = nblk - 1; p >= 0; --p) {
-    const int j = p * SMG_NB;
-    const int b = min(SMG_NB, n - j);
-    const int k = j + b, m = n - k;
-    const double* Di = Dv + j;
-    double* Cadj = La + k + (size_t)j * ldla;
-    double* Badj = La + k;
-    double* Dadj = La + j + (size_t)j * ldla;
-    double* Radj = La + j;
-    const double* R = L + j;
-    const double* Bv = L + k;
-    int rc;
-    if (m > 0) {
-      // C_adj = C_adj D^{-1}
-      rc = smg_gemm_impl(ctx, 0, 0, 0, m, b, b, 1.0, Cadj, ldla, Di, n, 0.0, Cadj, ldla);
-      if (rc) return rc;
-      if (j > 0) {  // B_adj -= C_adj R
-        rc = smg_gemm_impl(ctx, 0, 0, 0, m, j, b, -1.0, Cadj, ldla, R, ldl, 1.0, Badj, ldla);
-        if (rc) return rc;
-      }
-      // [R_adj | D_adj] -= C_adj^T [B | C]: both operands are contiguous column
-      // ranges (L[k:, 0:k] and Abar[j:k, 0:k]), so one GEMM (one split-K
-      // reduction) does both updates; R_adj's does not depend on the symbolic step
-      rc = smg_gemm_impl(ctx, 1, 0, 0, b, k, m, -1.0, Cadj, ldla, Bv, ldl, 1.0, Radj, ldla);
-      if (rc) return rc;
-    }
-    hipLaunchKernelGGL(k_symbolic_rev, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream,
-                       L + j + (size_t)j * ldl, ldl, Di, n, Dadj, ldla, b, Ssym);
-    if (j > 0) {
-      // R_adj -= sym(D_adj) R
-      rc = smg_gemm_impl(ctx, 0, 0, 0, b, j, b, -1.0, Ssym, b, R, ldl, 1.0, Radj, ldla);
-      if (rc) return rc;
-    }
-  }
+  int rc = n > 2 * SMG_NB2 ? chol_rev_two_level(ctx, L, ldl, Dv, n, La, ldla, n)
+                           : chol_rev_blocks(ctx, L, ldl, Dv, n, La, ldla, n);
+  if (rc) return rc;
   hipLaunchKernelGGL(k_add_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
                      La, ldla, n, Aadj, ldaa);
   SMG_LAUNCH_CHECK();

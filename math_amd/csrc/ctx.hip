@@ -63,6 +63,8 @@ double* smg_ws(smg_ctx* ctx, int id, size_t doubles) {
   if (doubles > ctx->ws_doubles[id]) {
     if (ctx->ws[id]) {
       hipStreamSynchronize(ctx->stream);
+      if (ctx->side) hipStreamSynchronize(ctx->side);
+      if (ctx->main_stream) hipStreamSynchronize(ctx->main_stream);
       hipFree(ctx->ws[id]);
     }
     size_t n = doubles < (1u << 18) ? (1u << 18) : doubles + doubles / 4;
@@ -76,6 +78,28 @@ double* smg_ws(smg_ctx* ctx, int id, size_t doubles) {
     ctx->ws_doubles[id] = n;
   }
   return ctx->ws[id];
+}
+
+int smg_side_begin(smg_ctx* ctx) {
+  if (ctx->side) return SMG_OK;
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+    ctx->side = nullptr;
+    ctx->host_status |= SMG_ERR_HIP;
+    return SMG_ERR_HIP;
+  }
+  return SMG_OK;
+}
+
+hipEvent_t smg_event(smg_ctx* ctx, int i) {
+  while ((int)ctx->ev_pool.size() <= i) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      ctx->host_status |= SMG_ERR_HIP;
+      return nullptr;
+    }
+    ctx->ev_pool.push_back(e);
+  }
+  return ctx->ev_pool[i];
 }
 
 void smg_reduce_partials(smg_ctx* ctx, const double* partials, int nparts,
@@ -108,6 +132,8 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   }
   ctx->prof_on = 0;
   ctx->comm = nullptr;
+  ctx->side = nullptr;
+  ctx->main_stream = nullptr;
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
     ctx->prof_ms[i] = 0;
     ctx->prof_count[i] = 0;
@@ -149,6 +175,11 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   smg_comm_destroy(ctx);
   for (auto& b : ctx->blocks) hipFree(b.base);
   for (auto e : ctx->prof_pool) hipEventDestroy(e);
+  for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  if (ctx->side) {
+    hipStreamSynchronize(ctx->side);
+    hipStreamDestroy(ctx->side);
+  }
   for (int i = 0; i < SMG_WS_COUNT; ++i)
     if (ctx->ws[i]) hipFree(ctx->ws[i]);
   hipFree(ctx->status_d);

@@ -96,7 +96,12 @@ template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
 __global__ __launch_bounds__(256) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
-    int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab) {
+    int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab, long long sA,
+    long long sB, long long sC) {
+  // strided batch over blockIdx.y (sA = sB = sC = 0 for a single product)
+  A += blockIdx.y * sA;
+  B += blockIdx.y * sB;
+  C += blockIdx.y * sC;
   // A-side contiguity: no-trans A is m-contiguous; trans A is k-contiguous.
   // B-side as an (n x k) operand: no-trans B is k-contiguous; trans B is n-contiguous.
   constexpr bool AK = TA;
@@ -242,14 +247,15 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
 
 template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
 int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
-           int lda, const double* B, int ldb, double beta, double* C, int ldc) {
+           int lda, const double* B, int ldb, double beta, double* C, int ldc, int batch = 1,
+           long long sA = 0, long long sB = 0, long long sC = 0) {
   const int tm = smg_ceil_div(m, BM), tn = smg_ceil_div(n, BN);
   const int ntiles = MODE != 0 ? tm * (tm + 1) / 2 : tm * tn;
   // split K when the tile grid cannot fill the 256 CUs and K is long
   int splits = 1;
   const int target = 512;
   constexpr int KMIN = 64;  // shortest K chunk of a split
-  if (ntiles < target && k >= 2 * KMIN) {
+  if (batch == 1 && ntiles < target && k >= 2 * KMIN) {
     splits = smg_ceil_div(target, ntiles);
     const int maxs = k / KMIN;
     if (splits > maxs) splits = maxs;
@@ -260,12 +266,14 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   splits = smg_ceil_div(k, kchunk);
   double* slab = nullptr;
   if (splits > 1) {
-    slab = smg_ws(ctx, SMG_WS_GEMM, (size_t)splits * m * n);
+    // the side stream has its own slab so concurrent split-K GEMMs never share one
+    slab = smg_ws(ctx, ctx->stream == ctx->side ? SMG_WS_GEMM_SIDE : SMG_WS_GEMM,
+                  (size_t)splits * m * n);
     if (!slab) return SMG_ERR_OOM;
   }
-  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntiles * splits), dim3(256), 0,
+  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntiles * splits, batch), dim3(256), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
-                     ntiles, kchunk, slab);
+                     ntiles, kchunk, slab, sA, sB, sC);
   if (splits > 1) {
     const long long tot = (long long)m * n;
     hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
@@ -331,6 +339,28 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
 }
 
 }  // namespace
+
+// batch x (C_i = alpha op(A_i) op(B_i) + beta C_i), operand i at base + i * stride
+// (doubles); full C only, no split-K, operands must not alias
+int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha,
+                          const double* A, int lda, long long sA, const double* B, int ldb,
+                          long long sB, double beta, double* C, int ldc, long long sC, int batch) {
+  if (m <= 0 || n <= 0 || batch <= 0) return SMG_OK;
+  if (k <= 0 || alpha == 0.0) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GEMM);
+  if (ctx->prof_on) ctx->prof_flops[SMG_FAM_GEMM] += 2.0 * m * n * k * batch;
+  const bool big = (long long)smg_ceil_div(m, 64) * smg_ceil_div(n, 64) * batch >= 192;
+#define SMG_BATCHED(TA_, TB_)                                                                    \
+  return big ? launch<64, 64, 32, TA_, TB_, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, \
+                                               batch, sA, sB, sC)                                 \
+             : launch<32, 32, 32, TA_, TB_, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, \
+                                               batch, sA, sB, sC);
+  if (!ta && !tb) SMG_BATCHED(false, false)
+  if (!ta && tb) SMG_BATCHED(false, true)
+  if (ta && !tb) SMG_BATCHED(true, false)
+  SMG_BATCHED(true, true)
+#undef SMG_BATCHED
+}
 
 int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
                   double alpha, const double* A, int lda, const double* B, int ldb,

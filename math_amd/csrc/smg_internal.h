@@ -23,7 +23,12 @@ struct smg_prof_slot {
 
 struct smg_ctx {
   int device;
-  hipStream_t stream;
+  hipStream_t stream;       // the tape's stream: every entry point's work is ordered on it
+  // look-ahead side stream of the blocked factorizations (created lazily);
+  // work issued there is joined back into `stream` before the entry returns
+  hipStream_t side;
+  hipStream_t main_stream;  // saved while `stream` temporarily points at `side`
+  std::vector<hipEvent_t> ev_pool;
   // device bump arena: blocks double in size (memory/stack_alloc.hpp:94-119)
   std::vector<smg_arena_block> blocks;
   size_t cur_block;
@@ -36,8 +41,8 @@ struct smg_ctx {
   void* host_scratch;
   size_t host_scratch_size;
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[5];
-  size_t ws_doubles[5];
+  double* ws[7];
+  size_t ws_doubles[7];
   // profiling
   int prof_on;
   std::vector<smg_prof_slot> prof_pending;
@@ -81,8 +86,21 @@ struct smg_prof_scope {
 // named persistent workspaces (grow on demand; a growth synchronises the
 // stream, so steady-state evaluations never reallocate)
 enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_ALIAS = 4,
-       SMG_WS_COUNT = 5 };
+       SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_COUNT = 7 };
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
+
+// side-stream helpers (ctx.hip): events come from a per-context pool
+int smg_side_begin(smg_ctx* ctx);          // ensure `side` exists
+hipEvent_t smg_event(smg_ctx* ctx, int i); // i-th pooled event (grown on demand)
+// RAII: issue the enclosed launches on the side stream
+struct smg_on_side {
+  smg_ctx* ctx;
+  explicit smg_on_side(smg_ctx* c) : ctx(c) {
+    ctx->main_stream = ctx->stream;
+    ctx->stream = ctx->side;
+  }
+  ~smg_on_side() { ctx->stream = ctx->main_stream; }
+};
 // C = beta C (lower != 0: lower triangle only)
 int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int lower);
 
@@ -99,6 +117,10 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
 int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
                   int k, double alpha, const double* A, int lda, const double* B,
                   int ldb, double beta, double* C, int ldc);
+
+int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha,
+                          const double* A, int lda, long long sA, const double* B, int ldb,
+                          long long sB, double beta, double* C, int ldc, long long sC, int batch);
 
 // deterministic device reductions: out[0] (+)= sum of per-block partials
 // partial layout: nparts doubles (or nparts x width for vector partials)

@@ -13,6 +13,7 @@
 #include "smg_internal.h"
 
 constexpr int SMG_NB = 64;           // diagonal block size of every blocked kernel
+constexpr int SMG_NB2 = 256;         // outer block of the two-level Cholesky reverse
 constexpr int SMG_NBP = SMG_NB + 1;  // padded LDS row stride
 constexpr int SMG_DIAG_THREADS = 512;  // threads of the fused diagonal-block kernels
 
