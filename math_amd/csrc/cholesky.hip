@@ -372,67 +372,40 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   if (A != L || lda != ldl)
     hipLaunchKernelGGL(k_copy_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
                        A, lda, n, L, ldl);
-  // Right-looking with one-block look-ahead on two streams.  Step p (columns
-  // [j, k)): crit = potrf(p), L21(p), then the WINDOW update of the next
-  // block column [k, k + NB); side = the REST of the trailing update,
-  // columns [k + NB, n).  Hazards: W(p) and R(p-1) both write columns
-  // [k, k + NB) -> crit waits R(p-1) before W(p); R(p) reads L21(p) -> side
-  // waits L21(p); R(p) after R(p-1) by stream order.  R(p) then overlaps
-  // W(p) + potrf(p+1) + L21(p+1), the serial chain.
-  // (measured on MI355X: each cross-queue event costs ~12 us of dependency
-  // latency, more than the overlap it buys at NB = 64, so it is off by default)
-  const bool la = false && n > 2 * SMG_NB && smg_side_begin(ctx) == SMG_OK;
-  hipEvent_t ev_r = nullptr;  // last R(p) recorded on the side stream
-  int evi = 0;
-  if (la) {  // the side stream starts after everything already on the tape's stream
-    hipEvent_t e0 = smg_event(ctx, evi++);
-    hipEventRecord(e0, ctx->stream);
-    hipStreamWaitEvent(ctx->side, e0, 0);
-  }
-  for (int j = 0; j < n; j += SMG_NB) {
-    const int b = min(SMG_NB, n - j);
-    const int m = n - j - b;
-    double* L11 = L + j + (size_t)j * ldl;
-    double* Di = Dinv + j;  // rows j..j+b, columns 0..b, ld n
-    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L11, ldl, b, Di, n,
-                       ctx->status_d);
-    if (m > 0) {
+  // Two-level right-looking: panels of SMG_NB2 columns factored with SMG_NB
+  // steps whose updates stay inside the panel (all rows below), then ONE
+  // rank-SMG_NB2 SYRK of the trailing matrix per panel (compute-bound, vs a
+  // memory-bound rank-SMG_NB update per step).  n <= 2 SMG_NB2: one level.
+  const int NB2 = n > 2 * SMG_NB2 ? SMG_NB2 : n;
+  for (int J = 0; J < n; J += NB2) {
+    const int K = min(J + NB2, n);
+    for (int j = J; j < K; j += SMG_NB) {
+      const int b = min(SMG_NB, n - j);
+      const int mall = n - j - b;       // rows below this diagonal block
+      const int rcols = K - (j + b);    // panel columns right of it
+      double* L11 = L + j + (size_t)j * ldl;
+      double* Di = Dinv + j;  // rows j..j+b, columns 0..b, ld n
+      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L11, ldl,
+                         b, Di, n, ctx->status_d);
+      if (mall == 0) continue;
       double* L21 = L + (j + b) + (size_t)j * ldl;
       // L21 = A21 * Dinv^T  (in place: one column tile, reads finish before writes)
-      int rc = smg_gemm_impl(ctx, 0, 1, 0, m, b, b, 1.0, L21, ldl, Di, n, 0.0, L21, ldl);
+      int rc = smg_gemm_impl(ctx, 0, 1, 0, mall, b, b, 1.0, L21, ldl, Di, n, 0.0, L21, ldl);
       if (rc) return rc;
-      double* L22 = L + (j + b) + (size_t)(j + b) * ldl;
-      if (!la) {
-        rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, b, -1.0, L21, ldl, L21, ldl, 1.0, L22, ldl);
+      if (rcols > 0) {  // panel columns [j+b, K), lower trapezoid, all rows below
+        rc = smg_gemm_impl(ctx, 0, 1, 1, mall, rcols, b, -1.0, L21, ldl, L21, ldl, 1.0,
+                           L + (j + b) + (size_t)(j + b) * ldl, ldl);
         if (rc) return rc;
-        continue;
-      }
-      const int w = min(SMG_NB, m);  // window: the next block column
-      hipEvent_t ev_l21 = smg_event(ctx, evi++);
-      hipEventRecord(ev_l21, ctx->stream);
-      if (ev_r) hipStreamWaitEvent(ctx->stream, ev_r, 0);
-      // W(p): A[k:, k:k+w] -= L21 L21[0:w]^T  (lower part of the diagonal sub-block
-      // via a triangle product, the rows below with a plain one)
-      rc = smg_gemm_impl(ctx, 0, 1, 1, w, w, b, -1.0, L21, ldl, L21, ldl, 1.0, L22, ldl);
-      if (rc) return rc;
-      if (m > w) {
-        rc = smg_gemm_impl(ctx, 0, 1, 0, m - w, w, b, -1.0, L21 + w, ldl, L21, ldl, 1.0, L22 + w,
-                           ldl);
-        if (rc) return rc;
-        // R(p) on the side stream: columns [k + w, n), lower triangle
-        hipStreamWaitEvent(ctx->side, ev_l21, 0);
-        {
-          smg_on_side on(ctx);
-          rc = smg_gemm_impl(ctx, 0, 1, 1, m - w, m - w, b, -1.0, L21 + w, ldl, L21 + w, ldl, 1.0,
-                             L22 + w + (size_t)w * ldl, ldl);
-        }
-        if (rc) return rc;
-        ev_r = smg_event(ctx, evi++);
-        hipEventRecord(ev_r, ctx->side);
       }
     }
+    if (K < n) {  // trailing A[K:, K:] -= L[K:, J:K] L[K:, J:K]^T (lower)
+      const int m = n - K;
+      const double* P = L + K + (size_t)J * ldl;
+      int rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, K - J, -1.0, P, ldl, P, ldl, 1.0,
+                             L + K + (size_t)K * ldl, ldl);
+      if (rc) return rc;
+    }
   }
-  if (ev_r) hipStreamWaitEvent(ctx->stream, ev_r, 0);  // join
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

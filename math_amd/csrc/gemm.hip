@@ -120,14 +120,20 @@ __global__ __launch_bounds__(256) void k_gemm(
   const int tile = blockIdx.x % ntiles;
   const int split = blockIdx.x / ntiles;
   int bi, bj;
-  if (MODE == 1) {
+  // triangle modes: square C -> only the tiles of the triangle are launched
+  // (tri_decode); trapezoidal C (m != n, the panel updates of the two-level
+  // Cholesky) -> the full grid, tiles wholly outside the triangle exit
+  const bool tri_sq = MODE != 0 && m == n && BM == BN;
+  if (MODE == 1 && tri_sq) {
     tri_decode(tile, bi, bj);
-  } else if (MODE == 2) {
+  } else if (MODE == 2 && tri_sq) {
     tri_decode(tile, bj, bi);
   } else {
     bi = tile % tiles_m;
     bj = tile / tiles_m;
   }
+  if (MODE == 1 && !tri_sq && bj * BN > bi * BM + BM - 1) return;
+  if (MODE == 2 && !tri_sq && bi * BM > bj * BN + BN - 1) return;
   const int i0 = bi * BM, j0 = bj * BN;
   const int kbeg = split * kchunk;
   const int kend = min(k, kbeg + kchunk);
@@ -250,7 +256,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
            int lda, const double* B, int ldb, double beta, double* C, int ldc, int batch = 1,
            long long sA = 0, long long sB = 0, long long sC = 0) {
   const int tm = smg_ceil_div(m, BM), tn = smg_ceil_div(n, BN);
-  const int ntiles = MODE != 0 ? tm * (tm + 1) / 2 : tm * tn;
+  const int ntiles = (MODE != 0 && m == n && BM == BN) ? tm * (tm + 1) / 2 : tm * tn;
   // split K when the tile grid cannot fill the 256 CUs and K is long
   int splits = 1;
   const int target = 512;
@@ -330,8 +336,12 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   // CU-starved shapes of the blocked Cholesky (one 64-wide block column or
   // row) 32x32, so the grid spreads over 4x more CUs
   const long long big_tiles = (long long)smg_ceil_div(m, 128) * smg_ceil_div(n, 128);
-  const long long mid_tiles = (long long)smg_ceil_div(m, 64) * smg_ceil_div(n, 64);
-  if (big_tiles >= 256 && k > 128)
+  const long long t64 = smg_ceil_div(m, 64);
+  const long long mid_tiles =
+      (MODE != 0 && m == n) ? t64 * (t64 + 1) / 2 : t64 * smg_ceil_div(n, 64);
+  // (triangle modes keep 64 x 64 tiles: half the 128-tile grid would sit on
+  // the diagonal, and the split-K those few tiles need costs a reduction)
+  if (MODE == 0 && big_tiles >= 256 && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
   if (mid_tiles >= 192)
     return launch<64, 64, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
@@ -372,16 +382,15 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
   }
   smg_prof_scope prof(ctx, SMG_FAM_GEMM);
   if (ctx->prof_on)
-    ctx->prof_flops[SMG_FAM_GEMM] += uplo ? (double)k * m * (m + 1) : 2.0 * m * n * k;
+    ctx->prof_flops[SMG_FAM_GEMM] +=
+        uplo ? 2.0 * k * ((double)m * n - (double)n * (n - 1) / 2) : 2.0 * m * n * k;
   if (uplo == 1) {
-    if (m != n) return SMG_ERR_ARG;
     if (!ta && tb) return dispatch_tile<false, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
     if (ta && !tb) return dispatch_tile<true, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
     if (!ta && !tb) return dispatch_tile<false, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
     return dispatch_tile<true, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
   }
   if (uplo == 2) {
-    if (m != n) return SMG_ERR_ARG;
     if (!ta && tb) return dispatch_tile<false, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
     if (ta && !tb) return dispatch_tile<true, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
     if (!ta && !tb) return dispatch_tile<false, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);

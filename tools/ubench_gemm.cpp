@@ -32,6 +32,12 @@ int main(int argc, char** argv) {
       {"rev fused TN (64,2112,2048)", 1, 0, 0, 64, 2112, 2048},
       {"rev Radj sym NN (64,2048,64)", 0, 0, 0, 64, 2048, 64},
       {"big NN (4096,4096,4096)", 0, 0, 0, 4096, 4096, 4096},
+      {"SYRK256 (2048,2048,256)", 0, 1, 1, 2048, 2048, 256},
+      {"SYRK256 (1024,1024,256)", 0, 1, 1, 1024, 1024, 256},
+      {"SYRK256 (3584,3584,256)", 0, 1, 1, 3584, 3584, 256},
+      {"rev B NN (1792,2048,256)", 0, 0, 0, 1792, 2048, 256},
+      {"rev TN (256,2304,1792)", 1, 0, 0, 256, 2304, 1792},
+      {"sym256 TN (256,256,256)", 1, 0, 0, 256, 256, 256},
   };
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -51,7 +57,7 @@ int main(int argc, char** argv) {
     const int lda = n, ldb = n, ldc = n;
     for (int w = 0; w < 3; ++w)
       smg_gemm(ctx, sh.ta, sh.tb, sh.uplo, sh.m, sh.nn, sh.k, -1.0, A, lda, B, ldb, 1.0, C, ldc);
-    const int rr = sh.m == 4096 ? 5 : reps;
+    const int rr = sh.k == 4096 ? 5 : reps;
     hipEventRecord(e0, s);
     for (int r = 0; r < rr; ++r)
       smg_gemm(ctx, sh.ta, sh.tb, sh.uplo, sh.m, sh.nn, sh.k, -1.0, A, lda, B, ldb, 1.0, C, ldc);
