@@ -140,15 +140,19 @@ int smg_add_diag_rev(smg_ctx* ctx, const double* Badj, int ldb, int n,
 /* cholesky_decompose(Matrix<var>) (rev/mat/fun/cholesky_decompose.hpp:378-427)
  *   check: latches SMG_ERR_NOT_SYMMETRIC when |A_ij - A_ji| > 1e-8 (:383)
  *   fwd:   L = lower Cholesky factor (upper zeroed); latches SMG_ERR_NOT_PD.
- *          Dinv (n x nb per diagonal block, may be NULL) receives the inverse
- *          diagonal blocks for reuse by the reverse pass and by TRSV.
+ *          aux (smg_cholesky_aux_doubles(n) doubles, may be NULL) receives the
+ *          inverses of L's diagonal blocks at 64, 128 and 256 granularity
+ *          (n x 64 | n x 128 | n x 256, each leading dimension n), reused by
+ *          the reverse pass and by the triangular solves (TRSV / MVN).
  *   rev:   Murray's blocked adjoint (:118-165): Aadj(lower) += f(L, Ladj);
- *          Ladj (lower) is used as workspace and overwritten. */
+ *          Ladj (lower) is used as workspace and overwritten; aux as written
+ *          by the forward, or NULL (recomputed). */
+long long smg_cholesky_aux_doubles(int n);
 int smg_cholesky_block_size(int n);
 int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n);
 int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L,
-                     int ldl, double* Dinv);
-int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
+                     int ldl, double* aux);
+int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux,
                      double* Ladj, int ldla, int n, double* Aadj, int ldaa);
 
 /* mdivide_left_tri<TriView>(A, B) (rev/mat/fun/mdivide_left_tri.hpp:16-373)
@@ -174,7 +178,7 @@ int smg_multiply_rev(smg_ctx* ctx, const double* A, int lda, const double* B,
 /* multi_normal_cholesky_lpdf<false>(y | mu, L)
  * (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:40-160).
  *   fwd: out3 = [lp, -, -]; w = L^{-1}(y - mu), sd = L^{-T} w kept in ws
- *        (ws >= 2n doubles); Dinv optional (from smg_cholesky_fwd).
+ *        (ws >= 2n doubles); aux optional (smg_cholesky_fwd's block inverses).
  *   rev: with adj = d(root)/d(lp) (host scalar):
  *        yadj -= adj sd, muadj += adj sd  (NULL skips)
  *        lower_only != 0: Ladj(lower) += adj (tril(sd w^T) - diag(1/L_ii))
@@ -183,10 +187,10 @@ int smg_multiply_rev(smg_ctx* ctx, const double* A, int lda, const double* B,
  *        lower_only == 0: Ladj += adj (sd w^T - L^{-T}) over all n^2 entries,
  *          the reference's full partials (:147,155). */
 int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu,
-                         const double* L, int ldl, const double* Dinv, int n,
+                         const double* L, int ldl, const double* aux, int n,
                          double* ws, double* out_lp);
 int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
-                         const double* Dinv, int n, const double* ws, double adj,
+                         const double* aux, int n, const double* ws, double adj,
                          int lower_only, double* yadj, double* muadj,
                          double* Ladj, int ldla);
 

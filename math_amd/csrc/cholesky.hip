@@ -267,15 +267,13 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, const double* Dv
 // SMG_NB2 block: P = D^{-T} sym(D^T tril(Dadj)) D^{-1} with the block inverse
 // from chol_block_inverses (a ragged last block falls back to the exact
 // inner recursion chol_rev_blocks); P also feeds R_adj -= P R.
-int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* Dv, int ldd,
-                       double* La, int ldla, int n) {
+int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
+                       double* La, int ldla) {
   const int nbo = (n + SMG_NB2 - 1) / SMG_NB2;
-  double* Winv = smg_ws(ctx, SMG_WS_INV, (size_t)n * (SMG_NB2 + SMG_NB2 / 2));
-  if (!Winv) return SMG_ERR_OOM;
-  double* W = Winv;                                 // n x SMG_NB2, ld n
-  double* W128 = Winv + (size_t)n * SMG_NB2;        // n x SMG_NB2/2, ld n
-  int rc = chol_block_inverses(ctx, L, ldl, Dv, ldd, n, W128, W, n);
-  if (rc) return rc;
+  const double* Dv = aux;                           // SMG_NB-block inverses, ld n
+  const int ldd = n;
+  const double* W = aux + (size_t)n * (SMG_NB + SMG_NB2 / 2);  // SMG_NB2-block inverses, ld n
+  int rc;
   const size_t bb = (size_t)SMG_NB2 * SMG_NB2;
   for (int P = nbo - 1; P >= 0; --P) {
     const int J = P * SMG_NB2;
@@ -351,6 +349,11 @@ extern "C" {
 
 int smg_cholesky_block_size(int n) { return SMG_NB; }
 
+// aux = [SMG_NB inverses | SMG_NB2/2 inverses | SMG_NB2 inverses], each n rows, ld n
+long long smg_cholesky_aux_doubles(int n) {
+  return (long long)(n > 0 ? n : 0) * (SMG_NB + SMG_NB2 / 2 + SMG_NB2);
+}
+
 int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n) {
   if (!ctx || n < 0 || (n > 0 && (!A || lda < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
@@ -365,10 +368,12 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   if (!ctx || n < 0 || (n > 0 && (!A || !L || lda < n || ldl < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_FWD);
-  if (!Dinv) {
-    Dinv = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_NB);
-    if (!Dinv) return SMG_ERR_OOM;
+  double* aux = Dinv;
+  if (!aux) {
+    aux = smg_ws(ctx, SMG_WS_TMP2, (size_t)smg_cholesky_aux_doubles(n));
+    if (!aux) return SMG_ERR_OOM;
   }
+  Dinv = aux;  // the SMG_NB level comes first
   if (A != L || lda != ldl)
     hipLaunchKernelGGL(k_copy_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
                        A, lda, n, L, ldl);
@@ -406,6 +411,10 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
       if (rc) return rc;
     }
   }
+  // the 128- and 256-block inverses (reverse pass, triangular solves)
+  int rc = chol_block_inverses(ctx, L, ldl, aux, n, n, aux + (size_t)n * SMG_NB,
+                               aux + (size_t)n * (SMG_NB + SMG_NB2 / 2), n);
+  if (rc) return rc;
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
@@ -416,18 +425,22 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
     return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
-  double* Dv = const_cast<double*>(Dinv);
-  if (!Dv) {
-    Dv = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_NB);
-    if (!Dv) return SMG_ERR_OOM;
+  const double* aux = Dinv;
+  if (!aux) {  // no forward aux: rebuild the block inverses from L
+    double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)smg_cholesky_aux_doubles(n));
+    if (!w) return SMG_ERR_OOM;
     for (int j = 0; j < n; j += SMG_NB) {
       const int b = min(SMG_NB, n - j);
       hipLaunchKernelGGL(k_trtri_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream,
-                         L + j + (size_t)j * ldl, ldl, b, Dv + j, n);
+                         L + j + (size_t)j * ldl, ldl, b, w + j, n);
     }
+    int rc = chol_block_inverses(ctx, L, ldl, w, n, n, w + (size_t)n * SMG_NB,
+                                 w + (size_t)n * (SMG_NB + SMG_NB2 / 2), n);
+    if (rc) return rc;
+    aux = w;
   }
-  int rc = n > 2 * SMG_NB2 ? chol_rev_two_level(ctx, L, ldl, Dv, n, La, ldla, n)
-                           : chol_rev_blocks(ctx, L, ldl, Dv, n, La, ldla, n);
+  int rc = n > 2 * SMG_NB2 ? chol_rev_two_level(ctx, L, ldl, aux, n, La, ldla)
+                           : chol_rev_blocks(ctx, L, ldl, aux, n, La, ldla, n);
   if (rc) return rc;
   hipLaunchKernelGGL(k_add_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
                      La, ldla, n, Aadj, ldaa);

@@ -113,17 +113,22 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
   if (!r) return SMG_ERR_OOM;
   double* res = r + n;
   int rc;
-  if (!Dinv) {  // diagonal-block inverses of L (the Cholesky forward normally provides them)
+  // the Cholesky forward's aux holds the 64- and 256-row diagonal-block
+  // inverses (smg_cholesky_aux_doubles); without it, build the 64-row level
+  const double* W256 = nullptr;
+  if (!Dinv) {
     double* W = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_NB);
     if (!W) return SMG_ERR_OOM;
     rc = smg_trtri_blocks_impl(ctx, L, ldl, n, W);
     if (rc) return rc;
     Dinv = W;
+  } else {
+    W256 = Dinv + (size_t)n * (SMG_NB + SMG_NB2 / 2);
   }
   hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(256), 0, ctx->stream, y, mu, n, res);
-  rc = smg_trsv_lower_impl(ctx, 0, L, ldl, Dinv, n, res, w, r, n);  // w = L^{-1}(y - mu)
+  rc = smg_trsv_lower_impl(ctx, 0, L, ldl, Dinv, W256, n, res, w, r, n);  // w = L^{-1}(y - mu)
   if (rc) return rc;
-  rc = smg_trsv_lower_impl(ctx, 1, L, ldl, Dinv, n, w, sd, r, n);  // sd = L^{-T} w
+  rc = smg_trsv_lower_impl(ctx, 1, L, ldl, Dinv, W256, n, w, sd, r, n);  // sd = L^{-T} w
   if (rc) return rc;
   hipLaunchKernelGGL(k_mvn_lp, dim3(1), dim3(1024), 0, ctx->stream, w, L, ldl, n, out_lp);
   SMG_LAUNCH_CHECK();

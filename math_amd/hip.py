@@ -79,6 +79,7 @@ _SIGS = {
     "smg_shift": (_I, [_P, _I, _I, _D, _P, _I, _I]),
     "smg_dot": (_I, [_P, _P, _P, _L, _P]),
     "smg_check_domain": (_I, [_P, _P, _L, _I, _P]),
+    "smg_cholesky_aux_doubles": (_L, [_I]),
     "smg_gp_exp_quad_cov_tangent_fwd": (_I, [_P, _P, _I, _D, _D, _D, _D, _P, _I]),
     "smg_gp_exp_quad_cov_tangent_rev": (_I, [_P, _P, _I, _D, _D, _D, _D, _P, _I, _P]),
     "smg_phi": (_I, [_P, _I, _P, _I, _P, _I, _I]),

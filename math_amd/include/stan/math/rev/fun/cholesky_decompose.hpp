@@ -98,7 +98,7 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   if (n == 0) return dev_var_matrix(new dev_matrix_vari(0, 0, dev_structure::lower));
   amd::check(smg_check_symmetric(c, A.val_ptr(), n, n), fn);
   auto* L = new dev_matrix_vari(n, n, dev_structure::lower);
-  L->aux_ = amd::alloc_doubles(size_t(n) * smg_cholesky_block_size(n));
+  L->aux_ = amd::alloc_doubles(size_t(smg_cholesky_aux_doubles(n)));
   amd::check(smg_cholesky_fwd(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
   int st = 0;
   amd::check(smg_status(c, &st), fn);

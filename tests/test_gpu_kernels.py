@@ -143,8 +143,7 @@ def test_gp_cov(ctx, n):
 def test_cholesky_golden(ctx, path):
     d = golden(os.path.basename(path)[:-5])
     N = int(d["N"])
-    nb = 64
-    dA, dL, dD = ctx.put(f64(d["A"])), ctx.zeros(N * N), ctx.zeros(N * nb)
+    dA, dL, dD = ctx.put(f64(d["A"])), ctx.zeros(N * N), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(N))
     ctx.call("smg_check_symmetric", dA, N, N)
     ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
     assert ctx.status() == 0
@@ -164,7 +163,7 @@ def test_cholesky_vs_oracle(ctx, N):
     A = 0.5 * (A + A.T)
     Lref = np.zeros(N * N)
     assert oracle().oracle_cholesky(ptr(F(A)), N, ptr(Lref)) == 0
-    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(N * 64)
+    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(N))
     ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
     L = ctx.get(dL, N * N)
     near_rel(L, Lref, 1e-11, atol=1e-11 * np.abs(Lref).max(), what="L")
@@ -182,7 +181,7 @@ def test_cholesky_not_pd_and_not_symmetric(ctx):
     A = np.eye(N)
     A[40, 40] = -1.0
     dA, dL = ctx.put(F(A)), ctx.zeros(N * N)
-    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, ctx.zeros(N * 64))
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(N)))
     assert ctx.status() & 2
     A = np.eye(N)
     A[5, 3] = 1e-7
@@ -391,7 +390,8 @@ def gp_gradient_abi(ctx, x, y, theta):
     n = len(x)
     a, r, s = theta
     dx, dy = ctx.put(f64(x)), ctx.put(f64(y))
-    K, Kd, L, Dinv = ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * 64)
+    K, Kd, L = ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * n)
+    Dinv = ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(n))
     ws, lp = ctx.zeros(2 * n), ctx.zeros(1)
     ctx.call("smg_gp_exp_quad_cov_fwd", dx, n, a, r, K, n)
     ctx.call("smg_add_diag_fwd", K, n, n, s * s, None, Kd, n)
