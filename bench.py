@@ -57,6 +57,20 @@ def ref_bench(cfg, n, reps=1, timeout=300):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+def pmc_traffic(workload):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (tools/pmc_traffic.sh + tools/pmc_traffic.py: separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes, calibrated on a known 8 B/lane
+    stream), or None when absent."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d[workload]["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def unif(seed, n, a, b):
     """oracle/gen.h SplitMix64 uniforms (numpy mirror, tests/gen.py)."""
     with np.errstate(over="ignore"):
@@ -116,9 +130,11 @@ class GP(Workload):
         ms, n, fl = fams["gemm"]
         ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
         ev = self.N ** 3 / (t_prof / steps) / 1e12
+        traffic, src = pmc_traffic("gp")
         return {"bound": "mfma", "kernel": "k_gemm (fp64 MFMA, all launches of the family)",
                 "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_FP64_TFLOPS if ach else None, "traffic": None,
+                "frac": ach / PEAK_FP64_TFLOPS if ach else None, "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
                 "launches_per_step": n / steps, "flops_per_launch": fl / max(n, 1),
                 "avg_launch_ms": ms / max(n, 1), "eval_achieved": ev, "eval_frac": ev / PEAK_FP64_TFLOPS,
                 "eval_flops": "N^3 (chol fwd N^3/3 + Murray adjoint 2N^3/3), SURVEY.md §8(d)"}
@@ -187,9 +203,11 @@ class GLM(Workload):
         byts = self.rows * self.M * 8 + self.rows * 4  # one read of x and y
         avg = ms / max(n, 1)
         ach = byts / (avg * 1e-3) / 1e9 if avg > 0 else None
+        traffic, src = pmc_traffic("glm")
         return {"bound": "hbm", "kernel": "k_glm_fused (one pass over x)", "achieved": ach,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS if ach else None,
-                "traffic": None, "bytes_per_launch": byts, "avg_launch_ms": avg,
+                "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
+                "bytes_per_launch": byts, "avg_launch_ms": avg,
                 "launches_per_step": n / steps}
 
     def cpu_baseline(self):
