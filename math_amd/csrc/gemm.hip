@@ -111,8 +111,12 @@ __global__ __launch_bounds__(256) void k_gemm(
   // one LDS pool: the K-loop operand tiles, reused by the epilogue to stage
   // the C tile (column chunks of ECH columns, stride BM + 1) so that C is read
   // and written in whole column segments (coalesced 8*BM-byte runs)
-  constexpr int ECH = (BM * BN + BN <= LA::size + LB::size) ? BN : 32;
-  constexpr int POOL = (LA::size + LB::size > (BM + 1) * ECH) ? LA::size + LB::size : (BM + 1) * ECH;
+  // 128 x 128 tiles double-buffer the operand tiles (one barrier per K stage)
+  constexpr bool DB = BM == 128;
+  constexpr int STAGE = LA::size + LB::size;
+  constexpr int OPS = DB ? 2 * STAGE : STAGE;
+  constexpr int ECH = (BM * BN + BN <= OPS) ? BN : 32;
+  constexpr int POOL = (OPS > (BM + 1) * ECH) ? OPS : (BM + 1) * ECH;
   __shared__ double pool[POOL];
   double* As = pool;
   double* Bs = pool + LA::size;
@@ -170,29 +174,60 @@ __global__ __launch_bounds__(256) void k_gemm(
     }
   }
   const int fr = lane & 15, fk = lane >> 4;
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    store_tile<BM, BK, AK>(As, ra);
-    store_tile<BN, BK, BKC>(Bs, rb);
-    __syncthreads();
-    if (k0 + BK < kend) {
-      load_tile<BM, BK, AK>(A, lda, m, kend, i0, k0 + BK, ra);
-      load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, k0 + BK, rb);
-    }
+  auto mma_stage = [&](const double* Ab, const double* Bb) {
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       double af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
-        af[a] = As[LA::at(wr * (BM / 2) + a * 16 + fr, ks * 4 + fk)];
+        af[a] = Ab[LA::at(wr * (BM / 2) + a * 16 + fr, ks * 4 + fk)];
 #pragma unroll
       for (int b = 0; b < TN; ++b)
-        bf[b] = Bs[LB::at(wc * (BN / 2) + b * 16 + fr, ks * 4 + fk)];
+        bf[b] = Bb[LB::at(wc * (BN / 2) + b * 16 + fr, ks * 4 + fk)];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+  };
+  if (DB) {
+    // stage s computes from buffer s & 1 while stage s + 1 is stored into the
+    // other buffer and stage s + 2 is in flight from global memory
+    if (kq > 0) {
+      store_tile<BM, BK, AK>(As, ra);
+      store_tile<BN, BK, BKC>(Bs, rb);
+      if (kbeg + BK < kend) {
+        load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + BK, ra);
+        load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + BK, rb);
+      }
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      mma_stage(pool + cur * STAGE, pool + cur * STAGE + LA::size);
+      if (k0 + BK < kend) {
+        store_tile<BM, BK, AK>(pool + (cur ^ 1) * STAGE, ra);
+        store_tile<BN, BK, BKC>(pool + (cur ^ 1) * STAGE + LA::size, rb);
+        if (k0 + 2 * BK < kend) {
+          load_tile<BM, BK, AK>(A, lda, m, kend, i0, k0 + 2 * BK, ra);
+          load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, k0 + 2 * BK, rb);
+        }
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      __syncthreads();
+      store_tile<BM, BK, AK>(As, ra);
+      store_tile<BN, BK, BKC>(Bs, rb);
+      __syncthreads();
+      if (k0 + BK < kend) {
+        load_tile<BM, BK, AK>(A, lda, m, kend, i0, k0 + BK, ra);
+        load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, k0 + BK, rb);
+      }
+      mma_stage(As, Bs);
     }
   }
 
