@@ -39,7 +39,8 @@ enum smg_status_code {
   SMG_ERR_NONFINITE = 8,      /* check_finite / not_nan family */
   SMG_ERR_ARG = 16,           /* bad sizes / null pointers (host-side check) */
   SMG_ERR_OOM = 32,           /* device arena exhausted */
-  SMG_ERR_NOT_POSITIVE = 64   /* check_positive */
+  SMG_ERR_NOT_POSITIVE = 64,  /* check_positive */
+  SMG_ERR_SYNC = 128          /* a cross-workgroup wait of a device kernel timed out */
 };
 
 typedef struct smg_ctx smg_ctx;

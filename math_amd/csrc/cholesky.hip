@@ -69,6 +69,230 @@ __global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int 
   lds_potrf_inv64_blk(D, X, b, L, ldl, Dinv, ldd, status, true);
 }
 
+// ---------------------------------------------------------------------------
+// Persistent panel factorisation: ONE launch factors a panel of up to
+// PANEL_MAX_STEPS diagonal blocks (columns [J, K), all rows below), where the
+// blocked loop above would issue potrf / TRSM / trapezoid-update launches
+// per 64-column step.  Row tile t (64 rows from J + 64 t) belongs to
+// workgroup t mod gridDim.x, which applies every step's update to it, so the
+// only cross-workgroup dependencies are
+//   * the factored diagonal block j (L_jj, Dinv_j): flag diag[j];
+//   * the panel-region rows L_cj (c < nb) that update tile t's column block c:
+//     flag row[j][c].
+// A workgroup only ever waits on tiles c < nb <= 8 owned by workgroups
+// 0 .. 7, which are dispatched first, so the grid needs no co-residency.  The
+// critical path per step is the next diagonal tile's own L_tj + A_tt update
+// (two 64^3 LDS products) and its factorisation; the other tiles' updates
+// overlap it.  Flags carry the launch's epoch (no reset launch); every wait
+// gives up after ~4 s and latches SMG_ERR_SYNC so a protocol fault can never
+// hang the device.
+constexpr int PANEL_MAX_STEPS = 8;
+constexpr int PANEL_MAX_GRID = 256;
+
+// dev instrumentation (tools/ubench_panel.hip): per-workgroup event log of
+// (s_memrealtime, code); compiled out of the library
+#ifdef SMG_PANEL_TRACE
+__device__ unsigned long long g_panel_trace[PANEL_MAX_GRID * 128];
+__device__ int g_panel_trace_n[PANEL_MAX_GRID];
+#define PANEL_EV(code)                                                              \
+  if (threadIdx.x == 0) {                                                           \
+    const int k_ = g_panel_trace_n[blockIdx.x]++;                                   \
+    if (k_ < 64) {                                                                  \
+      g_panel_trace[blockIdx.x * 128 + 2 * k_] = __builtin_amdgcn_s_memrealtime(); \
+      g_panel_trace[blockIdx.x * 128 + 2 * k_ + 1] = (code);                        \
+    }                                                                               \
+  }
+#else
+#define PANEL_EV(code)
+#endif
+
+// Every global store of the panel kernel is a device-scope (sc1) store, so
+// no XCD's L2 holds dirty panel data and the release fence before a flag has
+// nothing to write back.  Waiters spin on a relaxed device-scope load (no L2
+// invalidation per poll, which would evict every resident operand of the
+// XCD) and take ONE acquire fence once the flag is seen.
+__device__ __forceinline__ void st_dev(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void panel_publish(int* flag, int epoch) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void panel_wait(const int* flag, int epoch, int* status) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        atomicOr(status, (int)SMG_ERR_SYNC);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// rows x cols block of a col-major matrix -> registers (8 per thread, 512
+// threads); branch-free: clamped addresses, out-of-range (and, with lower,
+// strict-upper) elements masked at the LDS store
+struct panel_regs {
+  double v[8];
+  unsigned ok;
+};
+__device__ inline void panel_gload(panel_regs& R, const double* A, int ld, int rows, int cols,
+                                   bool lower) {
+  R.ok = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    const int c = e >> 6, r = e & 63;
+    R.v[q] = A[min(r, rows - 1) + (size_t)min(c, cols - 1) * ld];
+    R.ok |= (r < rows && c < cols && (!lower || r >= c)) ? (1u << q) : 0u;
+  }
+}
+__device__ inline void panel_lstore(double* D, const panel_regs& R) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    D[(e & 63) * SMG_NBP + (e >> 6)] = ((R.ok >> q) & 1u) ? R.v[q] : 0.0;
+  }
+}
+__device__ inline void panel_gstore(const double* D, double* A, int ld, int rows, int cols,
+                                    bool lower) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    const int c = e >> 6, r = e & 63;
+    if (r < rows && c < cols && (!lower || r >= c)) st_dev(&A[r + (size_t)c * ld], D[r * SMG_NBP + c]);
+  }
+}
+// b x b lower triangle of D with zeros above (the factored block / inverse)
+__device__ inline void panel_gstore_tri(const double* D, double* A, int ld, int b) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    const int c = e >> 6, r = e & 63;
+    if (r < b && c < b) st_dev(&A[r + (size_t)c * ld], r >= c ? D[r * SMG_NBP + c] : 0.0);
+  }
+}
+
+__global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
+                                                    int K, double* __restrict__ Dinv, int ldd,
+                                                    int* flags, int epoch, int* status) {
+  __shared__ double D[SMG_NB * SMG_NBP];
+  __shared__ double X[SMG_NB * SMG_NBP];
+  __shared__ double Y[SMG_NB * SMG_NBP];
+  __shared__ double Z[SMG_NB * SMG_NBP];
+  constexpr int S = PANEL_MAX_STEPS;
+  int* diag = flags;           // diag[j]: L_jj, Dinv_j stored
+  int* row = flags + S;        // row[j S + t]: L_tj stored (panel tiles t < nb)
+  int* done = flags + S + S * S;  // done[j S + t]: tile t's step-j updates stored
+  const int nb = (K - J + SMG_NB - 1) / SMG_NB;
+  const int T = (n - J + SMG_NB - 1) / SMG_NB;
+
+  if (blockIdx.x == 0) {
+    // the diagonal chain: factor block j, then apply step j to tile j + 1
+    // (L_{j+1,j} and the A_{j+1,j+1} update) so that block j + 1 is ready
+    // in LDS without a hand-off to another workgroup
+    double* Dc = D;  // current diagonal block (LDS)
+    double* Zn = Z;  // next one
+    lds_load_block(Dc, L + J + (size_t)J * ldl, ldl, min(SMG_NB, K - J), true);
+    __syncthreads();
+    for (int j = 0; j < nb; ++j) {
+      const int cj = J + SMG_NB * j;
+      const int bj = min(SMG_NB, K - cj);
+      PANEL_EV((j << 16) | (j << 8) | 2);
+      lds_potrf_inv64_blk(Dc, X, bj, nullptr, 0, nullptr, 0, status, true);
+      __syncthreads();
+      PANEL_EV((j << 16) | (j << 8) | 10);
+      panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
+      panel_gstore_tri(X, Dinv + cj, ldd, bj);
+      PANEL_EV((j << 16) | (j << 8) | 3);
+      panel_publish(&diag[j], epoch);
+      PANEL_EV((j << 16) | (j << 8) | 4);
+      if (j + 1 >= nb) break;
+      const int t = j + 1, rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
+      const int bt = min(SMG_NB, K - rt0);
+      if (j >= 1) panel_wait(&done[(j - 1) * S + t], epoch, status);
+      panel_regs Ra, Rz;
+      panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+      panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
+      panel_lstore(Y, Ra);
+      panel_lstore(Zn, Rz);
+      __syncthreads();
+      lds_mma64_8w<false, true>(Y, Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T
+      panel_gstore(Y, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+      panel_publish(&row[j * S + t], epoch);
+      lds_mma64_8w<false, true>(Zn, Y, Y, -1.0, 1.0);  // A_tt -= L_tj L_tj^T
+      // the factorisation's input: lower triangle, zero strict upper (the
+      // symmetric update filled it), identity padding beyond bt
+      for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
+        const int r = e >> 6, c = e & 63;
+        if (c > r) Zn[r * SMG_NBP + c] = 0.0;
+        else if (r == c && r >= bt) Zn[r * SMG_NBP + c] = 1.0;
+      }
+      __syncthreads();
+      double* tmp = Dc;
+      Dc = Zn;
+      Zn = tmp;
+      PANEL_EV((j << 16) | (t << 8) | 9);
+    }
+    return;
+  }
+
+  // the other workgroups: tiles t >= 2, owner(t) = 1 + (t - 2) mod (grid - 1);
+  // every step of tile t here except step t - 1 of a panel tile (t < nb),
+  // which the chain applies
+  for (int j = 0; j < nb; ++j) {
+    const int cj = J + SMG_NB * j;
+    const int bj = min(SMG_NB, K - cj);
+    for (int t = 2 + (blockIdx.x - 1); t < T; t += gridDim.x - 1) {
+      if (t <= j || (t == j + 1 && t < nb)) continue;  // done / the chain's
+      const int rt0 = J + SMG_NB * t;
+      const int rt = min(SMG_NB, n - rt0);
+      __syncthreads();  // LDS of the previous item fully consumed
+      PANEL_EV((j << 16) | (t << 8) | 5);
+      panel_regs Ra, Rd;
+      panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);  // own data, final
+      panel_wait(&diag[j], epoch, status);
+      PANEL_EV((j << 16) | (t << 8) | 6);
+      panel_gload(Rd, Dinv + cj, ldd, bj, bj, true);
+      panel_lstore(D, Ra);
+      panel_lstore(X, Rd);
+      __syncthreads();
+      lds_mma64_8w<false, true>(D, D, X);  // L_tj = A_tj Dinv_j^T
+      panel_gstore(D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+      PANEL_EV((j << 16) | (t << 8) | 7);
+      if (t < nb) panel_publish(&row[j * S + t], epoch);
+      // A_tc -= L_tj L_cj^T for the panel's later column blocks c <= t
+      const int clast = min(t, nb - 1);
+      for (int c = j + 1; c <= clast; ++c) {
+        const int cc = J + SMG_NB * c;
+        const int bc = min(SMG_NB, K - cc);
+        const bool own = c == t;  // L_cj is L_tj itself; A_tt: lower triangle
+        panel_regs Ry, Rz;
+        panel_gload(Rz, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
+        if (!own) {
+          panel_wait(&row[j * S + c], epoch, status);
+          panel_gload(Ry, L + cc + (size_t)cj * ldl, ldl, bc, bj, false);
+        }
+        __syncthreads();  // previous product's Y / Z consumed
+        if (!own) panel_lstore(Y, Ry);
+        panel_lstore(Z, Rz);
+        __syncthreads();
+        lds_mma64_8w<false, true>(Z, D, own ? D : Y, -1.0, 1.0);
+        panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
+        PANEL_EV((j << 16) | (t << 8) | (16 + c));
+      }
+      if (t == j + 2 && t < nb) panel_publish(&done[j * S + t], epoch);
+    }
+  }
+}
+
 // inverse of a lower-triangular diagonal block (no factorisation)
 __global__ __launch_bounds__(512) void k_trtri_diag(const double* __restrict__ L, int ldl,
                                                     int b, double* __restrict__ Dinv, int ldd) {
@@ -384,24 +608,13 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   const int NB2 = n > 2 * SMG_NB2 ? SMG_NB2 : n;
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
-    for (int j = J; j < K; j += SMG_NB) {
-      const int b = min(SMG_NB, n - j);
-      const int mall = n - j - b;       // rows below this diagonal block
-      const int rcols = K - (j + b);    // panel columns right of it
-      double* L11 = L + j + (size_t)j * ldl;
-      double* Di = Dinv + j;  // rows j..j+b, columns 0..b, ld n
-      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L11, ldl,
-                         b, Di, n, ctx->status_d);
-      if (mall == 0) continue;
-      double* L21 = L + (j + b) + (size_t)j * ldl;
-      // L21 = A21 * Dinv^T  (in place: one column tile, reads finish before writes)
-      int rc = smg_gemm_impl(ctx, 0, 1, 0, mall, b, b, 1.0, L21, ldl, Di, n, 0.0, L21, ldl);
-      if (rc) return rc;
-      if (rcols > 0) {  // panel columns [j+b, K), lower trapezoid, all rows below
-        rc = smg_gemm_impl(ctx, 0, 1, 1, mall, rcols, b, -1.0, L21, ldl, L21, ldl, 1.0,
-                           L + (j + b) + (size_t)(j + b) * ldl, ldl);
-        if (rc) return rc;
-      }
+    {  // the whole panel in one persistent launch (k_chol_panel)
+      // workgroup 0 = diagonal chain; tiles 2 .. T-1 over the others
+      const int T = smg_ceil_div(n - J, SMG_NB);
+      const int grid = T <= 2 ? 1 : (T - 1 < PANEL_MAX_GRID ? T - 1 : PANEL_MAX_GRID);
+      const int epoch = ++ctx->flag_epoch;
+      hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);
     }
     if (K < n) {  // trailing A[K:, K:] -= L[K:, J:K] L[K:, J:K]^T (lower)
       const int m = n - K;

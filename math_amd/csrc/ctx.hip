@@ -151,12 +151,15 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
     return SMG_ERR_OOM;
   }
   ctx->blocks.push_back({base, initial});
-  if (hipMalloc(&ctx->status_d, 256) != hipSuccess ||
+  // status word at [0]; the panel-kernel flags from byte 256 on
+  if (hipMalloc(&ctx->status_d, SMG_STATUS_BYTES) != hipSuccess ||
       hipHostMalloc(&ctx->status_h, 256, hipHostMallocDefault) != hipSuccess) {
     delete ctx;
     return SMG_ERR_HIP;
   }
-  hipMemset(ctx->status_d, 0, 256);
+  hipMemset(ctx->status_d, 0, SMG_STATUS_BYTES);
+  ctx->flags_d = ctx->status_d + 64;
+  ctx->flag_epoch = 0;
   ctx->host_scratch_size = 1u << 20;
   if (hipHostMalloc(&ctx->host_scratch, ctx->host_scratch_size, hipHostMallocDefault) != hipSuccess) {
     delete ctx;

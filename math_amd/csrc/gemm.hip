@@ -7,14 +7,12 @@
 //
 // Tiling: a 256-thread workgroup (4 waves, 2x2) owns a BM x BN tile of C;
 // each wave owns (BM/2) x (BN/2) = TM x TN MFMA tiles of 16x16 held in
-// accumulators.  K advances in stages of BK (16 for 128x128 tiles, 32 for
-// 64x64 tiles, whose GEMMs in the blocked Cholesky have K = 64: two stages,
-// one exposed global-load latency) staged through LDS:
-//   operand contiguous along the output dim (A no-trans, B trans): LDS [k][dim+16]
-//   operand contiguous along k (A trans, B no-trans):               LDS [dim][k+BK/2+1 (BK=16: +1)]
-// Both make the MFMA fragment reads (16 consecutive rows/cols x 4 k) bank-
-// conflict free for ds_read_b64 (row stride = 16 mod 32 doubles, resp. 17).
-// Global->LDS staging goes through registers with one stage of prefetch; the
+// accumulators.  K advances in stages of BK (16 for the 128 x 128 and
+// 64 x 64 tiles, 32 for the 32-wide ones) staged through LDS in unpadded,
+// XOR-swizzled images (lds_layout): conflict-free ds_read_b64 fragment reads
+// (16 consecutive rows/cols x 4 k) and staging stores.
+// Global->LDS staging goes through registers (one stage of prefetch for the
+// 128 x 128 tile, two for the small tiles) into double-buffered LDS; the
 // beta * C operand of the epilogue is fetched before the K loop.
 // Split-K writes fixed-order partial slabs reduced by a second kernel, so the
 // result is bitwise deterministic run to run.
@@ -22,19 +20,25 @@
 
 namespace {
 
+// LDS images of the operand tiles, unpadded and XOR-swizzled so that both
+// the staging stores (32 consecutive elements along the contiguous dim per
+// half-wave) and the MFMA fragment reads (16 consecutive rows x 2 k per
+// half-wave, ds_read_b64) hit 32 distinct bank pairs.
 template <int BM, int BK, bool KCONTIG>
 struct lds_layout;
 template <int BM, int BK>
-struct lds_layout<BM, BK, false> {  // [k][BM + 16]
-  static constexpr int S = BM + 16;
-  static constexpr int size = BK * S;
-  __device__ static int at(int i, int kk) { return kk * S + i; }
+struct lds_layout<BM, BK, false> {  // [k][BM], row index ^ 16 on odd k
+  static_assert(BM % 32 == 0, "BM");
+  static constexpr int size = BK * BM;
+  __device__ static int at(int i, int kk) { return kk * BM + (i ^ ((kk & 1) << 4)); }
 };
 template <int BM, int BK>
-struct lds_layout<BM, BK, true> {  // [BM][S], S = 17 mod 32
-  static constexpr int S = BK == 16 ? 17 : BK + 17;
-  static constexpr int size = BM * S;
-  __device__ static int at(int i, int kk) { return i * S + kk; }
+struct lds_layout<BM, BK, true> {  // [BM][BK], k index ^ f(row)
+  static_assert(BK == 16 || BK == 32, "BK");
+  static constexpr int size = BM * BK;
+  __device__ static int at(int i, int kk) {
+    return i * BK + (kk ^ (BK == 16 ? (i & 14) : ((i & 15) << 1)));
+  }
 };
 
 // Operand X viewed as a (rows x k) matrix in the kernel's orientation:
@@ -43,8 +47,9 @@ struct lds_layout<BM, BK, true> {  // [BM][S], S = 17 mod 32
 template <int BM, int BK, bool KCONTIG>
 __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
                                           int rows, int k, int i0, int k0,
-                                          double (&r)[BM * BK / 256]) {
+                                          double (&r)[BM * BK / 256], unsigned& ok) {
   constexpr int PER = BM * BK / 256;
+  ok = 0;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int e = threadIdx.x + 256 * q;
@@ -56,16 +61,21 @@ __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
       kk = e / BM;
       i = e % BM;
     }
+    // branch-free edges: every lane loads from a clamped in-range address
+    // (i0 < rows and k0 < k hold for every launched tile and stage) and the
+    // out-of-range values are zeroed when the tile is stored to LDS.  A
+    // select right after the load would make the wave wait for it here and
+    // serialise the prefetch behind the K loop's MFMAs.
     const int gi = i0 + i, gk = k0 + kk;
-    double v = 0.0;
-    if (gi < rows && gk < k)
-      v = KCONTIG ? X[(size_t)gi * ld + gk] : X[gi + (size_t)gk * ld];
-    r[q] = v;
+    const int ci = min(gi, rows - 1), ck = min(gk, k - 1);
+    r[q] = KCONTIG ? X[(size_t)ci * ld + ck] : X[ci + (size_t)ck * ld];
+    ok |= (gi < rows && gk < k) ? (1u << q) : 0u;
   }
 }
 
 template <int BM, int BK, bool KCONTIG>
-__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256]) {
+__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256],
+                                           unsigned ok) {
   constexpr int PER = BM * BK / 256;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -78,7 +88,7 @@ __device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * B
       kk = e / BM;
       i = e % BM;
     }
-    lds[lds_layout<BM, BK, KCONTIG>::at(i, kk)] = r[q];
+    lds[lds_layout<BM, BK, KCONTIG>::at(i, kk)] = ((ok >> q) & 1u) ? r[q] : 0.0;
   }
 }
 
@@ -111,15 +121,13 @@ __global__ __launch_bounds__(256) void k_gemm(
   // one LDS pool: the K-loop operand tiles, reused by the epilogue to stage
   // the C tile (column chunks of ECH columns, stride BM + 1) so that C is read
   // and written in whole column segments (coalesced 8*BM-byte runs)
-  // 128 x 128 tiles double-buffer the operand tiles (one barrier per K stage)
-  constexpr bool DB = BM == 128;
+  // operand tiles are double-buffered in LDS (one barrier per K stage)
+  constexpr int NR = BM == 128 ? 1 : 2;
   constexpr int STAGE = LA::size + LB::size;
-  constexpr int OPS = DB ? 2 * STAGE : STAGE;
+  constexpr int OPS = 2 * STAGE;
   constexpr int ECH = (BM * BN + BN <= OPS) ? BN : 32;
   constexpr int POOL = (OPS > (BM + 1) * ECH) ? OPS : (BM + 1) * ECH;
   __shared__ double pool[POOL];
-  double* As = pool;
-  double* Bs = pool + LA::size;
 
   const int tile = blockIdx.x % ntiles;
   const int split = blockIdx.x / ntiles;
@@ -151,13 +159,25 @@ __global__ __launch_bounds__(256) void k_gemm(
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
-  double ra[BM * BK / 256], rb[BN * BK / 256];
-  const int kq = kend - kbeg;
-  // A as (m x k) operand; B as (n x k) operand
-  if (kq > 0) {
-    load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg, ra);
-    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg, rb);
-  }
+  // operand tiles in registers between global memory and LDS: NR sets, so
+  // that the load of stage s + NR is in flight while stages s .. s + NR - 1
+  // are consumed (NR = 2 for the small tiles, whose grids leave only two or
+  // three waves per SIMD to hide the load latency behind)
+  constexpr int PA = BM * BK / 256, PB = BN * BK / 256;
+  double ra[NR][PA], rb[NR][PB];
+  unsigned oka[NR], okb[NR];
+  const int nst = (kend - kbeg + BK - 1) / BK;  // K stages of this split
+  auto gload = [&](int set, int st) {
+    load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + st * BK, ra[set], oka[set]);
+    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set], okb[set]);
+  };
+  auto lstore = [&](int set, int buf) {
+    store_tile<BM, BK, AK>(pool + buf * STAGE, ra[set], oka[set]);
+    store_tile<BN, BK, BKC>(pool + buf * STAGE + LA::size, rb[set], okb[set]);
+  };
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+    if (j < nst) gload(j, j);
   // epilogue operand in flight during the K loop (small tiles only: the
   // 128 x 128 tile would double its register count); coalesced mapping
   // e = tid + 256 q -> (i = e % BM, j = e / BM), the same as the store
@@ -191,43 +211,27 @@ __global__ __launch_bounds__(256) void k_gemm(
           acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
     }
   };
-  if (DB) {
-    // stage s computes from buffer s & 1 while stage s + 1 is stored into the
-    // other buffer and stage s + 2 is in flight from global memory
-    if (kq > 0) {
-      store_tile<BM, BK, AK>(As, ra);
-      store_tile<BN, BK, BKC>(Bs, rb);
-      if (kbeg + BK < kend) {
-        load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + BK, ra);
-        load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + BK, rb);
-      }
-    }
-    __syncthreads();
-    int cur = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-      mma_stage(pool + cur * STAGE, pool + cur * STAGE + LA::size);
-      if (k0 + BK < kend) {
-        store_tile<BM, BK, AK>(pool + (cur ^ 1) * STAGE, ra);
-        store_tile<BN, BK, BKC>(pool + (cur ^ 1) * STAGE + LA::size, rb);
-        if (k0 + 2 * BK < kend) {
-          load_tile<BM, BK, AK>(A, lda, m, kend, i0, k0 + 2 * BK, ra);
-          load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, k0 + 2 * BK, rb);
+  // stage s computes from LDS buffer s & 1 while stage s + 1 is stored into
+  // the other buffer and stage s + 1 + NR is issued into the freed registers
+  // (one barrier per stage); the loop is unrolled by two so that every
+  // register-set index is a compile-time constant
+  if (nst > 0) {
+    lstore(0, 0);
+    if (NR < nst) gload(0, NR);
+  }
+  __syncthreads();
+  for (int s0 = 0; s0 < nst; s0 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int st = s0 + u;
+      if (st < nst) {
+        mma_stage(pool + u * STAGE, pool + u * STAGE + LA::size);
+        if (st + 1 < nst) {
+          lstore((u + 1) % NR, u ^ 1);
+          if (st + 1 + NR < nst) gload((u + 1) % NR, st + 1 + NR);
         }
+        __syncthreads();
       }
-      __syncthreads();
-      cur ^= 1;
-    }
-  } else {
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-      __syncthreads();
-      store_tile<BM, BK, AK>(As, ra);
-      store_tile<BN, BK, BKC>(Bs, rb);
-      __syncthreads();
-      if (k0 + BK < kend) {
-        load_tile<BM, BK, AK>(A, lda, m, kend, i0, k0 + BK, ra);
-        load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, k0 + BK, rb);
-      }
-      mma_stage(As, Bs);
     }
   }
 
@@ -341,6 +345,10 @@ inline bool overlaps(const double* X, int ldx, int rows, int cols, const double*
   return rx < rc + m && rc < rx + rows && cx < cc + n && cc < cx + cols;
 }
 
+// K stage of the 64 x 64 tile: 16 keeps two stages of registers and two LDS
+// buffers within 32 KB per workgroup (four or more workgroups per CU)
+constexpr int BK64 = 16;
+
 template <bool TA, bool TB, int MODE>
 int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
                   int lda, const double* B, int ldb, double beta, double* C, int ldc) {
@@ -379,7 +387,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   if (MODE == 0 && big_tiles >= 256 && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
   if (mid_tiles >= 192)
-    return launch<64, 64, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
   return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
 }
 
@@ -396,7 +404,7 @@ int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, dou
   if (ctx->prof_on) ctx->prof_flops[SMG_FAM_GEMM] += 2.0 * m * n * k * batch;
   const bool big = (long long)smg_ceil_div(m, 64) * smg_ceil_div(n, 64) * batch >= 192;
 #define SMG_BATCHED(TA_, TB_)                                                                    \
-  return big ? launch<64, 64, 32, TA_, TB_, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, \
+  return big ? launch<64, 64, BK64, TA_, TB_, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, \
                                                batch, sA, sB, sC)                                 \
              : launch<32, 32, 32, TA_, TB_, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, \
                                                batch, sA, sB, sC);

@@ -21,6 +21,9 @@ struct smg_prof_slot {
   int family;
 };
 
+// device status allocation: the status word, then the panel-kernel flags
+constexpr size_t SMG_STATUS_BYTES = 256 + 4096 * sizeof(int);
+
 struct smg_ctx {
   int device;
   hipStream_t stream;       // the tape's stream: every entry point's work is ordered on it
@@ -37,6 +40,10 @@ struct smg_ctx {
   int* status_d;
   int* status_h;
   int host_status;  // host-detected errors (OOM, HIP)
+  // cross-workgroup flags of the persistent panel kernels (device, zeroed at
+  // creation; a launch's flags count as set when they hold its epoch)
+  int* flags_d;
+  int flag_epoch;
   // pinned host scratch
   void* host_scratch;
   size_t host_scratch_size;

@@ -58,10 +58,11 @@ __device__ inline void lds_mma64(double* C, const double* A, const double* B, do
   __syncthreads();
 }
 
-// C (64x64) = op(A) op(B) (beta = 0) with NW = 8 waves: wave w owns row stripe
-// w & 3 and column tiles 2 (w >> 2) .. +1.  Safe when C aliases A or B.
+// C (64x64) = alpha op(A) op(B) + beta C with NW = 8 waves: wave w owns row
+// stripe w & 3 and column tiles 2 (w >> 2) .. +1.  Safe when C aliases A or B.
 template <bool TA, bool TB>
-__device__ inline void lds_mma64_8w(double* C, const double* A, const double* B) {
+__device__ inline void lds_mma64_8w(double* C, const double* A, const double* B,
+                                    double alpha = 1.0, double beta = 0.0) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int fr = l & 15, fk = l >> 4;
   const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
@@ -83,7 +84,10 @@ __device__ inline void lds_mma64_8w(double* C, const double* A, const double* B)
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) C[(16 * (w & 3) + fk + 4 * r) * SMG_NBP + 16 * (t0 + t) + fr] = acc[t][r];
+    for (int r = 0; r < 4; ++r) {
+      double* c = &C[(16 * (w & 3) + fk + 4 * r) * SMG_NBP + 16 * (t0 + t) + fr];
+      *c = beta == 0.0 ? alpha * acc[t][r] : alpha * acc[t][r] + beta * *c;
+    }
   __syncthreads();
 }
 

@@ -74,6 +74,10 @@ inline void throw_status(int st, const char* function, const char* what = "") {
     throw std::domain_error(m.str());
   }
   if (st & SMG_ERR_OOM) throw std::bad_alloc();
+  if (st & SMG_ERR_SYNC) {
+    m << "device synchronisation timed out in " << what;
+    throw std::runtime_error(m.str());
+  }
   if (st & SMG_ERR_ARG) {
     m << "invalid argument " << what;
     throw std::invalid_argument(m.str());
