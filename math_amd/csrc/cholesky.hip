@@ -20,6 +20,7 @@
 // partition, so results agree to round-off.  Aadj(lower) += L_adj(lower).
 #include "smg_internal.h"
 #include "tri_small.h"
+#include <cstdlib>
 
 namespace {
 
@@ -458,16 +459,18 @@ int chol_rev_blocks(smg_ctx* ctx, const double* L, int ldl, const double* Dv, in
   return SMG_OK;
 }
 
-// Inverses of the full SMG_NB2 diagonal blocks of L by two recursive-doubling
-// levels from the SMG_NB-block inverses Dv (ld ldd): W (ld ldw, SMG_NB2 columns).
-int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, const double* Dv, int ldd, int n,
-                        double* W128, double* W, int ldw) {
-  const double* Wi = Dv;
-  int ldi = ldd;
-  for (int s2 = 2 * SMG_NB; s2 <= SMG_NB2; s2 *= 2) {
+// Inverses of the full 128-, 256- and 512-row diagonal blocks of L by
+// recursive doubling from the SMG_NB-block inverses: aux (ld n) holds the
+// levels at the SMG_AUX_W* column offsets (smg_cholesky_aux_doubles).
+int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int n) {
+  const double* Wi = aux;
+  int ldi = n;
+  for (int s2 = 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
     const int s = s2 / 2, nb = n / s2;
     if (nb == 0) return SMG_OK;
-    double* Wo = s2 == SMG_NB2 ? W : W128;
+    const int off = s2 == 128 ? SMG_AUX_W128 : (s2 == 256 ? SMG_AUX_W256 : SMG_AUX_W512);
+    double* Wo = aux + (size_t)n * off;
+    const int ldw = n;
     hipLaunchKernelGGL(k_inv_double_diag, dim3(grid_for((long long)nb * s2 * s2)), dim3(256), 0,
                        ctx->stream, nb, s2, Wi, ldi, Wo, ldw);
     double* T = smg_ws(ctx, SMG_WS_TMP, (size_t)nb * s * s);
@@ -485,24 +488,36 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, const double* Dv
   return SMG_OK;
 }
 
-// Two-level Murray reverse: outer blocks of SMG_NB2 columns make the three
-// big updates rank-SMG_NB2 (compute-bound GEMMs).  The diagonal block's
+// Two-level Murray reverse: outer blocks of SMG_NBR columns make the three
+// big updates rank-SMG_NBR (compute-bound GEMMs).  The diagonal block's
 // symbolic adjoint (:101-111) is applied in closed form to the whole
-// SMG_NB2 block: P = D^{-T} sym(D^T tril(Dadj)) D^{-1} with the block inverse
+// SMG_NBR block: P = D^{-T} sym(D^T tril(Dadj)) D^{-1} with the block inverse
 // from chol_block_inverses (a ragged last block falls back to the exact
 // inner recursion chol_rev_blocks); P also feeds R_adj -= P R.
 int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                        double* La, int ldla) {
-  const int nbo = (n + SMG_NB2 - 1) / SMG_NB2;
+  const int nbo = (n + SMG_NBR - 1) / SMG_NBR;
   const double* Dv = aux;                           // SMG_NB-block inverses, ld n
   const int ldd = n;
-  const double* W = aux + (size_t)n * (SMG_NB + SMG_NB2 / 2);  // SMG_NB2-block inverses, ld n
+  const double* W = aux + (size_t)n * SMG_AUX_W512;  // SMG_NBR-block inverses, ld n
   int rc;
-  const size_t bb = (size_t)SMG_NB2 * SMG_NB2;
+  const size_t bb = (size_t)SMG_NBR * SMG_NBR;
+  // B_adj -= C_adj R (rows K:, columns 0:J) runs on the side stream, in
+  // parallel with [R_adj | D_adj] -= C_adj^T [B | C], the symbolic step and
+  // R_adj -= P R (rows J:K) on the main stream: disjoint outputs, and neither
+  // reads what the other writes.  The next block's C_adj (rows J:, columns
+  // J-NB2:J) includes B_adj's rows, hence the wait at the top of each step.
+  const bool side = smg_side_begin(ctx) == SMG_OK;
+  int nev = 0;
+  hipEvent_t F = nullptr;
   for (int P = nbo - 1; P >= 0; --P) {
-    const int J = P * SMG_NB2;
-    const int K = min(J + SMG_NB2, n), bs = K - J, m = n - K;
-    const bool full = bs == SMG_NB2;
+    if (F) {
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
+      F = nullptr;
+    }
+    const int J = P * SMG_NBR;
+    const int K = min(J + SMG_NBR, n), bs = K - J, m = n - K;
+    const bool full = bs == SMG_NBR;
     double* Ca = La + K + (size_t)J * ldla;
     double* Da = La + J + (size_t)J * ldla;
     const double* Ld = L + J + (size_t)J * ldl;
@@ -527,8 +542,23 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
         }
       }
       if (J > 0) {  // B_adj -= C_adj R
-        rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Ca, ldla, L + J, ldl, 1.0, La + K, ldla);
-        if (rc) return rc;
+        if (side) {
+          hipEvent_t E = smg_event(ctx, nev++);
+          if (!E) return SMG_ERR_HIP;
+          SMG_HIP_TRY(hipEventRecord(E, ctx->stream));
+          SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
+          {
+            smg_on_side on(ctx);
+            rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Ca, ldla, L + J, ldl, 1.0, La + K, ldla);
+          }
+          if (rc) return rc;
+          F = smg_event(ctx, nev++);
+          if (!F) return SMG_ERR_HIP;
+          SMG_HIP_TRY(hipEventRecord(F, ctx->side));
+        } else {
+          rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Ca, ldla, L + J, ldl, 1.0, La + K, ldla);
+          if (rc) return rc;
+        }
       }
       // [R_adj | D_adj] -= C_adj^T [B | C]
       rc = smg_gemm_impl(ctx, 1, 0, 0, bs, K, m, -1.0, Ca, ldla, L + K, ldl, 1.0, La + J, ldla);
@@ -564,6 +594,7 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
       if (rc) return rc;
     }
   }
+  if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
   return SMG_OK;
 }
 
@@ -573,9 +604,9 @@ extern "C" {
 
 int smg_cholesky_block_size(int n) { return SMG_NB; }
 
-// aux = [SMG_NB inverses | SMG_NB2/2 inverses | SMG_NB2 inverses], each n rows, ld n
+// aux = the 64-, 128-, 256- and 512-row diagonal-block inverses, n rows each, ld n
 long long smg_cholesky_aux_doubles(int n) {
-  return (long long)(n > 0 ? n : 0) * (SMG_NB + SMG_NB2 / 2 + SMG_NB2);
+  return (long long)(n > 0 ? n : 0) * SMG_AUX_COLS;
 }
 
 int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n) {
@@ -601,11 +632,25 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   if (A != L || lda != ldl)
     hipLaunchKernelGGL(k_copy_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
                        A, lda, n, L, ldl);
-  // Two-level right-looking: panels of SMG_NB2 columns factored with SMG_NB
+  // Two-level right-looking: panels of SMG_NBF columns factored with SMG_NB
   // steps whose updates stay inside the panel (all rows below), then ONE
-  // rank-SMG_NB2 SYRK of the trailing matrix per panel (compute-bound, vs a
-  // memory-bound rank-SMG_NB update per step).  n <= 2 SMG_NB2: one level.
-  const int NB2 = n > 2 * SMG_NB2 ? SMG_NB2 : n;
+  // rank-SMG_NBF update of the trailing matrix per panel (compute-bound, vs a
+  // memory-bound rank-SMG_NB update per step).  n <= 2 SMG_NBF: one level.
+  //
+  // Look-ahead: panel p's trailing update is split into
+  //   (a) the next panel's columns  A[K:, K:K2] -= P P[0:K2-K]^T  (main stream)
+  //   (b) the rest                  A[K2:, K2:] -= P2 P2^T        (side stream)
+  // so that (b), the bulk of the rank-NB2 work, runs on the CUs the next
+  // panel's chain leaves idle while (a), on the chain's critical path, runs
+  // alone.  Ordering (E = (a) done, F = (b) done):
+  //   main: panel_p, wait F_{p-1}, (a)_p, rec E_p, panel_{p+1} ...
+  //   side: wait E_p, (b)_p, rec F_p
+  // (a)_p and (b)_{p-1} both update columns K_p:K_{p+1}, hence the wait;
+  // (b)_p is disjoint from panel p+1's columns.
+  const int NB2 = n > 2 * SMG_NBF ? SMG_NBF : n;
+  const bool look = NB2 < n && smg_side_begin(ctx) == SMG_OK;
+  int nev = 0;       // pooled events used
+  hipEvent_t F = nullptr;  // the pending (b) on the side stream
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
@@ -616,17 +661,43 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
       hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);
     }
-    if (K < n) {  // trailing A[K:, K:] -= L[K:, J:K] L[K:, J:K]^T (lower)
-      const int m = n - K;
-      const double* P = L + K + (size_t)J * ldl;
+    if (K >= n) break;
+    const int m = n - K;
+    const double* P = L + K + (size_t)J * ldl;
+    if (!look) {  // trailing A[K:, K:] -= L[K:, J:K] L[K:, J:K]^T (lower)
       int rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, K - J, -1.0, P, ldl, P, ldl, 1.0,
                              L + K + (size_t)K * ldl, ldl);
       if (rc) return rc;
+      continue;
+    }
+    const int K2 = min(K + NB2, n);
+    hipEvent_t E = smg_event(ctx, nev++);
+    if (!E) return SMG_ERR_HIP;
+    if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
+    // (a) the next panel's columns (lower trapezoid), main stream
+    int rc = smg_gemm_impl(ctx, 0, 1, 1, m, K2 - K, K - J, -1.0, P, ldl, P, ldl, 1.0,
+                           L + K + (size_t)K * ldl, ldl);
+    if (rc) return rc;
+    SMG_HIP_TRY(hipEventRecord(E, ctx->stream));
+    F = nullptr;
+    if (K2 < n) {  // (b) the rest, side stream
+      const int m2 = n - K2;
+      const double* P2 = L + K2 + (size_t)J * ldl;
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
+      {
+        smg_on_side on(ctx);
+        rc = smg_gemm_impl(ctx, 0, 1, 1, m2, m2, K - J, -1.0, P2, ldl, P2, ldl, 1.0,
+                           L + K2 + (size_t)K2 * ldl, ldl);
+      }
+      if (rc) return rc;
+      F = smg_event(ctx, nev++);
+      if (!F) return SMG_ERR_HIP;
+      SMG_HIP_TRY(hipEventRecord(F, ctx->side));
     }
   }
+  if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
   // the 128- and 256-block inverses (reverse pass, triangular solves)
-  int rc = chol_block_inverses(ctx, L, ldl, aux, n, n, aux + (size_t)n * SMG_NB,
-                               aux + (size_t)n * (SMG_NB + SMG_NB2 / 2), n);
+  int rc = chol_block_inverses(ctx, L, ldl, aux, n);
   if (rc) return rc;
   SMG_LAUNCH_CHECK();
   return SMG_OK;
@@ -647,12 +718,11 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
       hipLaunchKernelGGL(k_trtri_diag, dim3(1), dim3(SMG_DIAG_THREADS), 0, ctx->stream,
                          L + j + (size_t)j * ldl, ldl, b, w + j, n);
     }
-    int rc = chol_block_inverses(ctx, L, ldl, w, n, n, w + (size_t)n * SMG_NB,
-                                 w + (size_t)n * (SMG_NB + SMG_NB2 / 2), n);
+    int rc = chol_block_inverses(ctx, L, ldl, w, n);
     if (rc) return rc;
     aux = w;
   }
-  int rc = n > 2 * SMG_NB2 ? chol_rev_two_level(ctx, L, ldl, aux, n, La, ldla)
+  int rc = n > 2 * SMG_NBR ? chol_rev_two_level(ctx, L, ldl, aux, n, La, ldla)
                            : chol_rev_blocks(ctx, L, ldl, aux, n, La, ldla, n);
   if (rc) return rc;
   hipLaunchKernelGGL(k_add_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,

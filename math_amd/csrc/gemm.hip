@@ -17,6 +17,8 @@
 // Split-K writes fixed-order partial slabs reduced by a second kernel, so the
 // result is bitwise deterministic run to run.
 #include "smg_internal.h"
+#include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -41,15 +43,36 @@ struct lds_layout<BM, BK, true> {  // [BM][BK], k index ^ f(row)
   }
 };
 
+// compile-time unrolled loop: f(std::integral_constant<int, 0>) .. f(<N - 1>)
+template <int I, int N, typename F>
+__device__ __forceinline__ void smg_static_for_impl(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    smg_static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void smg_static_for(F&& f) {
+  smg_static_for_impl<0, N>(f);
+}
+
+// every out-of-range operand element is loaded from this zero instead of
+// being masked after the load (see load_tile)
+__device__ double g_gemm_zero[2] = {0.0, 0.0};  // global (not constant) address space: keeps the operand loads global_load, not flat_load
+
 // Operand X viewed as a (rows x k) matrix in the kernel's orientation:
 //   KCONTIG == false : element (i, kk) at X[i + kk*ld]
 //   KCONTIG == true  : element (i, kk) at X[kk + i*ld]
+// Branch- and select-free on the loaded data: an out-of-range element's
+// ADDRESS is redirected to g_gemm_zero, so the loaded register goes straight
+// to its LDS store.  (A select on the loaded value lets the scheduler hoist
+// the select -- and with it a wait for that load -- ahead of the previous
+// stage's MFMAs, which serialises the prefetch.)
 template <int BM, int BK, bool KCONTIG>
 __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
                                           int rows, int k, int i0, int k0,
-                                          double (&r)[BM * BK / 256], unsigned& ok) {
+                                          double (&r)[BM * BK / 256]) {
   constexpr int PER = BM * BK / 256;
-  ok = 0;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int e = threadIdx.x + 256 * q;
@@ -61,21 +84,14 @@ __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
       kk = e / BM;
       i = e % BM;
     }
-    // branch-free edges: every lane loads from a clamped in-range address
-    // (i0 < rows and k0 < k hold for every launched tile and stage) and the
-    // out-of-range values are zeroed when the tile is stored to LDS.  A
-    // select right after the load would make the wave wait for it here and
-    // serialise the prefetch behind the K loop's MFMAs.
     const int gi = i0 + i, gk = k0 + kk;
-    const int ci = min(gi, rows - 1), ck = min(gk, k - 1);
-    r[q] = KCONTIG ? X[(size_t)ci * ld + ck] : X[ci + (size_t)ck * ld];
-    ok |= (gi < rows && gk < k) ? (1u << q) : 0u;
+    const double* p = KCONTIG ? X + ((size_t)gi * ld + gk) : X + (gi + (size_t)gk * ld);
+    r[q] = *((gi < rows && gk < k) ? p : g_gemm_zero);
   }
 }
 
 template <int BM, int BK, bool KCONTIG>
-__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256],
-                                           unsigned ok) {
+__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256]) {
   constexpr int PER = BM * BK / 256;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -88,7 +104,7 @@ __device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * B
       kk = e / BM;
       i = e % BM;
     }
-    lds[lds_layout<BM, BK, KCONTIG>::at(i, kk)] = ((ok >> q) & 1u) ? r[q] : 0.0;
+    lds[lds_layout<BM, BK, KCONTIG>::at(i, kk)] = r[q];
   }
 }
 
@@ -107,7 +123,7 @@ __global__ __launch_bounds__(256) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
     int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab, long long sA,
-    long long sB, long long sC) {
+    long long sB, long long sC, int px, int ntp) {
   // strided batch over blockIdx.y (sA = sB = sC = 0 for a single product)
   A += blockIdx.y * sA;
   B += blockIdx.y * sB;
@@ -129,9 +145,28 @@ __global__ __launch_bounds__(256) void k_gemm(
   constexpr int POOL = (OPS > (BM + 1) * ECH) ? OPS : (BM + 1) * ECH;
   __shared__ double pool[POOL];
 
-  const int tile = blockIdx.x % ntiles;
-  const int split = blockIdx.x / ntiles;
-  int bi, bj;
+  int bi, bj, tile, split;
+  if (px > 0) {
+    // XCD-aware placement (full / trapezoidal grids): workgroups b and b + 8
+    // share an XCD (round-robin dispatch), so XCD slot x = b % 8 takes one
+    // rectangle of a px x (8 / px) partition of the tile grid, column-major
+    // inside it; each XCD's L2 then holds 1/px of A's rows and px/8 of B's
+    // columns instead of all of both.  Grid: ntp = 8 x the largest rectangle
+    // per split; surplus workgroups exit.
+    split = blockIdx.x / ntp;
+    const int tb = blockIdx.x - split * ntp;
+    const int x = tb & 7, l = tb >> 3, py = 8 / px;
+    const int tiles_n = ntiles / tiles_m;
+    const int rx = x % px, ry = x / px;
+    const int r0 = rx * tiles_m / px, r1 = (rx + 1) * tiles_m / px;
+    const int c0 = ry * tiles_n / py, c1 = (ry + 1) * tiles_n / py;
+    const int rm = r1 - r0;
+    if (rm <= 0 || l >= rm * (c1 - c0)) return;
+    tile = (r0 + l % rm) + (c0 + l / rm) * tiles_m;
+  } else {
+    tile = blockIdx.x % ntiles;
+    split = blockIdx.x / ntiles;
+  }
   // triangle modes: square C -> only the tiles of the triangle are launched
   // (tri_decode); trapezoidal C (m != n, the panel updates of the two-level
   // Cholesky) -> the full grid, tiles wholly outside the triangle exit
@@ -165,19 +200,21 @@ __global__ __launch_bounds__(256) void k_gemm(
   // three waves per SIMD to hide the load latency behind)
   constexpr int PA = BM * BK / 256, PB = BN * BK / 256;
   double ra[NR][PA], rb[NR][PB];
-  unsigned oka[NR], okb[NR];
   const int nst = (kend - kbeg + BK - 1) / BK;  // K stages of this split
   auto gload = [&](int set, int st) {
-    load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + st * BK, ra[set], oka[set]);
-    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set], okb[set]);
+    load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + st * BK, ra[set]);
+    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set]);
   };
   auto lstore = [&](int set, int buf) {
-    store_tile<BM, BK, AK>(pool + buf * STAGE, ra[set], oka[set]);
-    store_tile<BN, BK, BKC>(pool + buf * STAGE + LA::size, rb[set], okb[set]);
+    store_tile<BM, BK, AK>(pool + buf * STAGE, ra[set]);
+    store_tile<BN, BK, BKC>(pool + buf * STAGE + LA::size, rb[set]);
   };
+  // every stage load is unconditional (addresses are clamped in range and
+  // stages past the end are masked to zero): a conditional load would make
+  // the waitcnt pass assume the worst on the loop back-edge and wait for ALL
+  // outstanding loads at each LDS store, i.e. no prefetch at all
 #pragma unroll
-  for (int j = 0; j < NR; ++j)
-    if (j < nst) gload(j, j);
+  for (int j = 0; j < NR; ++j) gload(j, j);
   // epilogue operand in flight during the K loop (small tiles only: the
   // 128 x 128 tile would double its register count); coalesced mapping
   // e = tid + 256 q -> (i = e % BM, j = e / BM), the same as the store
@@ -215,25 +252,30 @@ __global__ __launch_bounds__(256) void k_gemm(
   // the other buffer and stage s + 1 + NR is issued into the freed registers
   // (one barrier per stage); the loop is unrolled by two so that every
   // register-set index is a compile-time constant
-  if (nst > 0) {
-    lstore(0, 0);
-    if (NR < nst) gload(0, NR);
-  }
+  // (an odd stage count runs one all-zero stage: the loop body has no
+  // conditional memory operations)
+  lstore(0, 0);
+  gload(0, NR);
   __syncthreads();
-  for (int s0 = 0; s0 < nst; s0 += 2) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int st = s0 + u;
-      if (st < nst) {
-        mma_stage(pool + u * STAGE, pool + u * STAGE + LA::size);
-        if (st + 1 < nst) {
-          lstore((u + 1) % NR, u ^ 1);
-          if (st + 1 + NR < nst) gload((u + 1) % NR, st + 1 + NR);
-        }
-        __syncthreads();
-      }
-    }
-  }
+  // stage st: MMA from LDS buffer st & 1, store stage st + 1 (register set
+  // (st + 1) % NR) into the other buffer, refill that set with stage
+  // st + 1 + NR.  Unrolled by U = lcm(2, NR) so every set / buffer index is a
+  // compile-time constant; the main loop has no conditional memory operation
+  // (the tail's guards only cost precision of its own waits).
+  constexpr int U = NR % 2 == 0 ? NR : 2 * NR;
+  auto body = [&](int st, auto uc) {
+    constexpr int u = decltype(uc)::value;
+    mma_stage(pool + (u & 1) * STAGE, pool + (u & 1) * STAGE + LA::size);
+    lstore((u + 1) % NR, (u & 1) ^ 1);
+    gload((u + 1) % NR, st + 1 + NR);
+    __syncthreads();
+  };
+  int s0 = 0;
+  for (; s0 + U <= nst; s0 += U)
+    smg_static_for<U>([&](auto uc) { body(s0 + decltype(uc)::value, uc); });
+  smg_static_for<U - 1>([&](auto uc) {
+    if (s0 + decltype(uc)::value < nst) body(s0 + decltype(uc)::value, uc);
+  });
 
   // epilogue: D layout of v_mfma_f64_16x16x4_f64: reg r of lane l holds
   // row (l>>4) + 4r, col l&15 of the 16x16 tile.  Accumulators go to LDS
@@ -300,7 +342,8 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   int splits = 1;
   const int target = 512;
   constexpr int KMIN = 64;  // shortest K chunk of a split
-  if (batch == 1 && ntiles < target && k >= 2 * KMIN) {
+  static const bool nosplit = getenv("SMG_GEMM_NOSPLIT") != nullptr;  // dev (tools/ubench_gemm)
+  if (!nosplit && batch == 1 && ntiles < target && k >= 2 * KMIN) {
     splits = smg_ceil_div(target, ntiles);
     const int maxs = k / KMIN;
     if (splits > maxs) splits = maxs;
@@ -316,9 +359,27 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
                   (size_t)splits * m * n);
     if (!slab) return SMG_ERR_OOM;
   }
-  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntiles * splits, batch), dim3(256), 0,
+  // XCD partition px x (8 / px) of a full tile grid minimising the per-XCD
+  // operand footprint (rows of A + columns of B, in tiles); triangle grids
+  // (tri_decode order) and grids too small to split keep the linear order
+  int px = 0, ntp = ntiles;
+  if (!(MODE != 0 && m == n && BM == BN) && ntiles >= 64) {
+    long long best = -1;
+    for (int p = 1; p <= 8; p *= 2) {
+      const int q = 8 / p;
+      if (p > tm || q > tn) continue;
+      const long long rr = smg_ceil_div(tm, p), cc = smg_ceil_div(tn, q);
+      const long long foot = rr * BM + cc * BN;
+      if (best < 0 || foot < best) {
+        best = foot;
+        px = p;
+        ntp = 8 * (int)(rr * cc);
+      }
+    }
+  }
+  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntp * splits, batch), dim3(256), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
-                     ntiles, kchunk, slab, sA, sB, sC);
+                     ntiles, kchunk, slab, sA, sB, sC, px, ntp);
   if (splits > 1) {
     const long long tot = (long long)m * n;
     hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
@@ -382,11 +443,28 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   const long long t64 = smg_ceil_div(m, 64);
   const long long mid_tiles =
       (MODE != 0 && m == n) ? t64 * (t64 + 1) / 2 : t64 * smg_ceil_div(n, 64);
+  {  // dev override for tile studies (tools/ubench_gemm): SMG_GEMM_TILE=128|12864|64|32
+    static const int forced = [] {
+      const char* e = getenv("SMG_GEMM_TILE");
+      return e ? atoi(e) : 0;
+    }();
+    if (forced == 128)
+      return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (forced == 12864)
+      return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (forced == 64)
+      return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (forced == 32)
+      return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  }
   // (triangle modes keep 64 x 64 tiles: half the 128-tile grid would sit on
   // the diagonal, and the split-K those few tiles need costs a reduction)
   if (MODE == 0 && big_tiles >= 256 && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  if (mid_tiles >= 192)
+  // 64 x 64 only when its grid fills two workgroups per CU without split-K:
+  // below that, 32 x 32 tiles (4x the workgroups) beat a split 64 x 64 grid
+  // (tools/ubench_gemm: (3584,256,256) 18.6 vs 28 us)
+  if (mid_tiles >= 512)
     return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
   return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
 }

@@ -123,7 +123,7 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
     if (rc) return rc;
     Dinv = W;
   } else {
-    W256 = Dinv + (size_t)n * (SMG_NB + SMG_NB2 / 2);
+    W256 = Dinv + (size_t)n * SMG_AUX_W256;
   }
   hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(256), 0, ctx->stream, y, mu, n, res);
   rc = smg_trsv_lower_impl(ctx, 0, L, ldl, Dinv, W256, n, res, w, r, n);  // w = L^{-1}(y - mu)

@@ -13,7 +13,15 @@
 #include "smg_internal.h"
 
 constexpr int SMG_NB = 64;           // diagonal block size of every blocked kernel
-constexpr int SMG_NB2 = 256;         // outer block of the two-level Cholesky reverse
+constexpr int SMG_NB2 = 256;         // outer block of the blocked triangular solves
+constexpr int SMG_NBR = 512;         // outer block of the two-level Cholesky reverse
+constexpr int SMG_NBF = 512;         // panel width of the two-level Cholesky forward
+// cholesky aux layout (n rows each, ld n): inverses of the 64-, 128-, 256-
+// and 512-row diagonal blocks of L
+constexpr int SMG_AUX_W128 = SMG_NB;
+constexpr int SMG_AUX_W256 = SMG_NB + 128;
+constexpr int SMG_AUX_W512 = SMG_NB + 128 + 256;
+constexpr int SMG_AUX_COLS = SMG_NB + 128 + 256 + 512;
 constexpr int SMG_NBP = SMG_NB + 1;  // padded LDS row stride
 constexpr int SMG_DIAG_THREADS = 512;  // threads of the fused diagonal-block kernels
 

@@ -38,6 +38,12 @@ int main(int argc, char** argv) {
       {"rev B NN (1792,2048,256)", 0, 0, 0, 1792, 2048, 256},
       {"rev TN (256,2304,1792)", 1, 0, 0, 256, 2304, 1792},
       {"sym256 TN (256,256,256)", 1, 0, 0, 256, 256, 256},
+      {"rev TN (256,256,3840)", 1, 0, 0, 256, 256, 3840},
+      {"rev TN (256,3840,256)", 1, 0, 0, 256, 3840, 256},
+      {"rev TN (256,2048,2048)", 1, 0, 0, 256, 2048, 2048},
+      {"rev NN Cadj W (3584,256,256)", 0, 0, 0, 3584, 256, 256},
+      {"rev NN B (3584,256,256)", 0, 0, 0, 3584, 256, 256},
+      {"rev NN PR (256,3584,256)", 0, 0, 0, 256, 3584, 256},
   };
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
