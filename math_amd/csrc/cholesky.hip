@@ -20,6 +20,7 @@
 // partition, so results agree to round-off.  Aadj(lower) += L_adj(lower).
 #include "smg_internal.h"
 #include "tri_small.h"
+#include "smg_sync.h"
 #include <cstdlib>
 
 namespace {
@@ -107,35 +108,7 @@ __device__ int g_panel_trace_n[PANEL_MAX_GRID];
 #define PANEL_EV(code)
 #endif
 
-// Every global store of the panel kernel is a device-scope (sc1) store, so
-// no XCD's L2 holds dirty panel data and the release fence before a flag has
-// nothing to write back.  Waiters spin on a relaxed device-scope load (no L2
-// invalidation per poll, which would evict every resident operand of the
-// XCD) and take ONE acquire fence once the flag is seen.
-__device__ __forceinline__ void st_dev(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ inline void panel_publish(int* flag, int epoch) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ inline void panel_wait(const int* flag, int epoch, int* status) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
-        atomicOr(status, (int)SMG_ERR_SYNC);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
+// hand-off primitives (st_dev / panel_publish / panel_wait): smg_sync.h
 
 // rows x cols block of a col-major matrix -> registers (8 per thread, 512
 // threads); branch-free: clamped addresses, out-of-range (and, with lower,

@@ -14,6 +14,7 @@
 // latency-bound launches, so the count is what matters); a ragged tail uses
 // the 64-row level.
 #include "smg_internal.h"
+#include "smg_sync.h"
 #include "tri_small.h"
 
 namespace {
@@ -247,6 +248,158 @@ struct trsv_step {
   int j, b, big;
 };
 
+// ---- persistent solve: ONE launch per solve (n % 256 == 0) ----------------
+// Workgroup s owns the 64-row strip s (rows, forward; columns of L = rows of
+// L^T, backward) of 256-row block p = s / 4.  It accumulates its residual
+// from every published block of y it depends on (forward: blocks < p, in
+// order; backward: blocks > p, from the last), publishes the residual strip
+// (rf[s]), then -- once the four strips of block p have -- computes its 64
+// entries of y_p = W_p r_p (W_p^T r_p) from the 256-row inverse and
+// publishes them (yf[s]).  The critical path per block is one 64 x 256
+// residual product and one 64 x 256 diagonal product, with two hand-offs;
+// everything else overlaps.  All n / 64 workgroups must be co-resident
+// (n / 64 <= 256 CUs; SMG_ERR_SYNC otherwise).
+__device__ inline void wait_strips(const int* f, int s0, int cnt, int epoch, int* status) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < cnt; ++k)
+      while (__hip_atomic_load(&f[s0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+          atomicOr(status, (int)SMG_ERR_SYNC);
+          k = cnt;
+          break;
+        }
+      }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+template <bool TRANS>
+__global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__ L, int ldl,
+                                                      const double* __restrict__ W, int ldw,
+                                                      const double* __restrict__ x,
+                                                      double* __restrict__ y,
+                                                      double* __restrict__ r, int n, int* flags,
+                                                      int epoch, int* status) {
+  // Operand reads never wait on a flag: this strip's W_p slice is loaded into
+  // registers at entry, and each block of L is loaded before the wait for
+  // the y block it multiplies, so only LDS traffic and FMAs follow a flag.
+  __shared__ double vp[256];
+  __shared__ double part[256];
+  const int s = blockIdx.x, p = s >> 2, sub = s & 3, nb = n >> 8, ns = n >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int* yf = flags;
+  int* rf = flags + ns;
+  double wv[64], lv[64];
+  if (!TRANS) {
+    // thread (row 64 s + lane, quarter w of each 256-column block)
+    const int i = 64 * s + lane;
+    const double* Wr = W + (256 * p + 64 * sub + lane) + (size_t)(64 * w) * ldw;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) wv[k] = Wr[(size_t)k * ldw];
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int q = 0; q < p; ++q) {
+      const double* Lc = L + i + (size_t)(256 * q + 64 * w) * ldl;
+#pragma unroll
+      for (int k = 0; k < 64; ++k) lv[k] = Lc[(size_t)k * ldl];
+      wait_strips(yf, 4 * q, 4, epoch, status);
+      vp[t] = y[256 * q + t];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 64; k += 2) {
+        acc0 += lv[k] * vp[64 * w + k];
+        acc1 += lv[k + 1] * vp[64 * w + k + 1];
+      }
+      __syncthreads();  // vp consumed
+    }
+    part[t] = acc0 + acc1;
+    __syncthreads();
+    if (w == 0)
+      st_dev(&r[i], x[i] - ((part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane])));
+    panel_publish(&rf[s], epoch);
+    // y rows 256 p + 64 sub + lane = W_p[64 sub + lane, :] r_p
+    wait_strips(rf, 4 * p, 4, epoch, status);
+    vp[t] = r[256 * p + t];
+    __syncthreads();
+    acc0 = 0.0;
+    acc1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 64; k += 2) {
+      acc0 += wv[k] * vp[64 * w + k];
+      acc1 += wv[k + 1] * vp[64 * w + k + 1];
+    }
+    part[t] = acc0 + acc1;
+    __syncthreads();
+    if (w == 0)
+      st_dev(&y[i], (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]));
+    panel_publish(&yf[s], epoch);
+  } else {
+    // wave w: 16 columns j = 64 s + 16 w + cc of L (rows of L^T); lanes run
+    // down the contiguous column segments (rows lane + 64 k of a block);
+    // one wave reduction per column at the end
+    const int c0 = 64 * sub + 16 * w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc)
+        wv[16 * k + cc] = W[(256 * p + lane + 64 * k) + (size_t)(c0 + cc) * ldw];
+    double acc[16];
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) acc[cc] = 0.0;
+    const int j0 = 64 * s + 16 * w;
+    for (int q = nb - 1; q > p; --q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc)
+          lv[16 * k + cc] = L[(256 * q + lane + 64 * k) + (size_t)(j0 + cc) * ldl];
+      wait_strips(yf, 4 * q, 4, epoch, status);
+      vp[t] = y[256 * q + t];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double v = vp[lane + 64 * k];
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) acc[cc] += lv[16 * k + cc] * v;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      const double v = wave_sum(acc[cc]);
+      if (lane == cc) part[16 * w + cc] = v;
+    }
+    __syncthreads();
+    if (t < 64) st_dev(&r[64 * s + t], x[64 * s + t] - part[t]);
+    panel_publish(&rf[s], epoch);
+    // y entries 256 p + 64 sub + 16 w + cc = (W_p^T r_p)[..] = W_p[:, col] . r_p
+    wait_strips(rf, 4 * p, 4, epoch, status);
+    vp[t] = r[256 * p + t];
+    __syncthreads();
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) acc[cc] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double v = vp[lane + 64 * k];
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) acc[cc] += wv[16 * k + cc] * v;
+    }
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      const double v = wave_sum(acc[cc]);
+      if (lane == cc) part[16 * w + cc] = v;
+    }
+    __syncthreads();
+    if (t < 64) st_dev(&y[256 * p + 64 * sub + t], part[t]);
+    panel_publish(&yf[s], epoch);
+  }
+}
+
+// flags region of the persistent solves (after the panel kernel's)
+constexpr int TRSV_FLAG_OFFSET = 256;
+
 }  // namespace
 
 // y = L^{-1} x (trans = 0) or L^{-T} x (trans = 1); L lower.  W64: the 64-row
@@ -255,6 +408,19 @@ struct trsv_step {
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,
                         const double* W256, int ldw, const double* x, double* y, double* r, int n) {
   if (n <= 0) return SMG_OK;
+  if (W256 && n % 256 == 0 && n >= 512 && n / 64 <= 256 &&
+      TRSV_FLAG_OFFSET + 2 * (n / 64) <= 4096) {
+    const int epoch = ++ctx->flag_epoch;
+    int* f = ctx->flags_d + TRSV_FLAG_OFFSET;
+    if (trans)
+      hipLaunchKernelGGL(k_trsv_persist<true>, dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl, W256,
+                         ldw, x, y, r, n, f, epoch, ctx->status_d);
+    else
+      hipLaunchKernelGGL(k_trsv_persist<false>, dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl,
+                         W256, ldw, x, y, r, n, f, epoch, ctx->status_d);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
   hipMemcpyAsync(r, x, sizeof(double) * n, hipMemcpyDeviceToDevice, ctx->stream);
   // block schedule: full 256-row blocks from the top, then 64-row blocks
   trsv_step steps[1024];
