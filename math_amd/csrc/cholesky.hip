@@ -25,36 +25,54 @@
 
 namespace {
 
-__global__ void k_check_symmetric(const double* __restrict__ A, int lda, int n, int* status) {
+// one 64 x 64 tile pair per workgroup: tile (bi, bj) of the lower triangle
+// and its mirror (bj, bi), both read coalesced (column segments), the mirror
+// transposed through LDS; every element is read once
+__global__ __launch_bounds__(256) void k_check_symmetric(const double* __restrict__ A, int lda,
+                                                         int n, int* status) {
   // CONSTRAINT_TOLERANCE = 1e-8 absolute (prim/mat/err/constraint_tolerance.hpp:12)
-  const long long tot = (long long)n * n;
-  bool bad = false;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
-    if (i <= j) continue;
-    // !(|d| <= tol) so that NaN entries fail too (check_symmetric.hpp:45-46)
-    if (!(fabs(A[i + (size_t)j * lda] - A[j + (size_t)i * lda]) <= 1e-8)) bad = true;
+  __shared__ double T[64][65];
+  int bi, bj;
+  {  // blockIdx.x -> (bi, bj), bj <= bi, row-major over the lower triangle
+    const int t = blockIdx.x;
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    bi = r;
+    bj = t - r * (r + 1) / 2;
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
+  const int i0 = 64 * bi, j0 = 64 * bj;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // mirror tile: rows j0.., cols i0.. -> T[c][r] = A(j0 + r, i0 + c)
+  for (int c = w; c < 64; c += 4) {
+    const int gr = j0 + lane, gc = i0 + c;
+    T[c][lane] = (gr < n && gc < n) ? A[gr + (size_t)gc * lda] : 0.0;
+  }
+  __syncthreads();
+  bool bad = false;
+  for (int c = w; c < 64; c += 4) {  // A(i0 + lane, j0 + c) vs A(j0 + c, i0 + lane) = T[lane][c]
+    const int gr = i0 + lane, gc = j0 + c;
+    if (gr < n && gc < n && gr > gc)
+      // !(|d| <= tol) so that NaN entries fail too (check_symmetric.hpp:45-46)
+      bad |= !(fabs(A[gr + (size_t)gc * lda] - T[lane][c]) <= 1e-8);
+  }
+  if (__any(bad) && lane == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
 }
 
 __global__ void k_copy_lower(const double* __restrict__ A, int lda, int n,
                              double* __restrict__ L, int ldl) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     L[i + (size_t)j * ldl] = (i >= j) ? A[i + (size_t)j * lda] : 0.0;
   }
 }
 
 __global__ void k_add_lower(const double* __restrict__ X, int ldx, int n,
                             double* __restrict__ Y, int ldy) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     if (i >= j) Y[i + (size_t)j * ldy] += X[i + (size_t)j * ldx];
   }
 }
@@ -316,10 +334,9 @@ __global__ __launch_bounds__(512) void k_symbolic_rev(const double* __restrict__
 
 // P (n x n dense) = X + X^T from the lower triangle of X with halved diagonal
 __global__ void k_sym_from_half(const double* __restrict__ X, int ldx, int n, double* __restrict__ P) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     P[e] = i > j ? X[i + (size_t)j * ldx] : (i < j ? X[j + (size_t)i * ldx] : 2.0 * X[i + (size_t)i * ldx]);
   }
 }
@@ -350,30 +367,27 @@ __global__ void k_inv_double_diag(int nb, int s2, const double* __restrict__ Wi,
 
 // G = tril(X) (n x n dense, ld n)
 __global__ void k_tril_copy(const double* __restrict__ X, int ldx, int n, double* __restrict__ G) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     G[e] = i >= j ? X[i + (size_t)j * ldx] : 0.0;
   }
 }
 
 // S (n x n, ld n): upper triangle <- lower triangle (sym_from_lower)
 __global__ void k_mirror_lower(double* __restrict__ S, int n) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     if (i < j) S[i + (size_t)j * n] = S[j + (size_t)i * n];
   }
 }
 
 // Dadj (ld lda) <- tril(S) with halved diagonal; strict upper untouched
 __global__ void k_half_lower(const double* __restrict__ S, int n, double* __restrict__ Dadj, int lda) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     if (i > j) Dadj[i + (size_t)j * lda] = S[e];
     else if (i == j) Dadj[i + (size_t)j * lda] = 0.5 * S[e];
   }
@@ -585,8 +599,9 @@ long long smg_cholesky_aux_doubles(int n) {
 int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n) {
   if (!ctx || n < 0 || (n > 0 && (!A || lda < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
-  hipLaunchKernelGGL(k_check_symmetric, dim3(grid_for((long long)n * n)), dim3(256), 0,
-                     ctx->stream, A, lda, n, ctx->status_d);
+  const int tb = smg_ceil_div(n, 64);
+  hipLaunchKernelGGL(k_check_symmetric, dim3(tb * (tb + 1) / 2), dim3(256), 0, ctx->stream, A, lda,
+                     n, ctx->status_d);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -43,10 +43,9 @@ __global__ __launch_bounds__(256) void k_gp_rev_partials(const double* __restric
                                                          double* __restrict__ part) {
   __shared__ double lds[16];
   double al = 0.0, as = 0.0;
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     const double a = Ka[i + (size_t)j * lda];
     if (i == j) {
       as += a * s2;
@@ -86,10 +85,9 @@ __global__ void k_gp_rev_final(const double* __restrict__ part, int nparts, doub
 
 __global__ void k_add_diag_fwd(const double* __restrict__ A, int lda, int n, double d,
                                const double* __restrict__ dv, double* __restrict__ B, int ldb) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     double v = A[i + (size_t)j * lda];
     if (i == j) v += dv ? dv[i] : d;
     B[i + (size_t)j * ldb] = v;
@@ -98,10 +96,9 @@ __global__ void k_add_diag_fwd(const double* __restrict__ A, int lda, int n, dou
 
 __global__ void k_add_full(const double* __restrict__ X, int ldx, int n, double* __restrict__ Y,
                            int ldy) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     Y[i + (size_t)j * ldy] += X[i + (size_t)j * ldx];
   }
 }

@@ -38,10 +38,9 @@ __global__ __launch_bounds__(256) void k_transpose(int m, int n, const double* _
 }
 
 __global__ void k_shift(int m, int n, double c, double* __restrict__ Y, int ldy, int uplo) {
-  const long long tot = (long long)m * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / m), i = (int)(e % m);
+  for (smg_mn it(m, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     if (uplo == 1 && i < j) continue;
     Y[i + (size_t)j * ldy] += c;
   }
@@ -88,10 +87,9 @@ __global__ void k_check_bounded_int(const int* __restrict__ y, long long n, int 
 // tangent of a Cholesky factor, L' = L Phi(L^{-1} A' L^{-T}))
 __global__ void k_phi(int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy,
                       int accumulate) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     const double v = i > j ? X[i + (size_t)j * ldx] : (i == j ? 0.5 * X[i + (size_t)j * ldx] : 0.0);
     double* y = Y + i + (size_t)j * ldy;
     *y = accumulate ? *y + v : v;

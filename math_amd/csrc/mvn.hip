@@ -55,10 +55,9 @@ __global__ void k_mvn_lp(const double* __restrict__ w, const double* __restrict_
 __global__ void k_mvn_rev_lower(const double* __restrict__ L, int ldl, int n,
                                 const double* __restrict__ w, const double* __restrict__ sd,
                                 double adj, double* __restrict__ La, int ldla) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     if (i < j) continue;
     double g = sd[i] * w[j];
     if (i == j) g -= 1.0 / L[i + (size_t)i * ldl];
@@ -70,10 +69,9 @@ __global__ void k_mvn_rev_lower(const double* __restrict__ L, int ldl, int n,
 __global__ void k_mvn_rev_full(const double* __restrict__ Linv, int n, const double* __restrict__ w,
                                const double* __restrict__ sd, double adj, double* __restrict__ La,
                                int ldla) {
-  const long long tot = (long long)n * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / n), i = (int)(e % n);
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     const double g = sd[i] * w[j] - Linv[j + (size_t)i * n];
     La[i + (size_t)j * ldla] += adj * g;
   }

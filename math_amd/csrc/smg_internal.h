@@ -162,3 +162,30 @@ __device__ __forceinline__ double block_sum(double v, double* lds /* >= 16 */) {
     for (int i = 0; i < nw; ++i) s += lds[i];
   return s;  // valid in thread 0 only
 }
+
+// grid-stride walk over a column-major m x n index space: (i, j) advance by
+// the grid stride with one compare instead of a 64-bit division per element
+// (a division per element cost element-wise passes ~40% of their bandwidth)
+struct smg_mn {
+  long long e, tot;
+  int i, j, m, si, sj, st;
+  __device__ __forceinline__ smg_mn(int m_, int n_) : m(m_) {
+    tot = (long long)m_ * n_;
+    e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    st = gridDim.x * blockDim.x;
+    j = m_ > 0 ? (int)(e / m_) : 0;
+    i = m_ > 0 ? (int)(e - (long long)j * m_) : 0;
+    sj = m_ > 0 ? st / m_ : 0;
+    si = st - sj * m_;
+  }
+  __device__ __forceinline__ bool ok() const { return e < tot; }
+  __device__ __forceinline__ void next() {
+    e += st;
+    i += si;
+    j += sj;
+    if (i >= m) {
+      i -= m;
+      ++j;
+    }
+  }
+};

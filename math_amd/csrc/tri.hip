@@ -32,10 +32,9 @@ __global__ __launch_bounds__(512) void k_trtri_blocks(const double* __restrict__
 
 __global__ void k_copy(int m, int n, const double* __restrict__ A, int lda,
                        double* __restrict__ B, int ldb, double alpha, int accumulate) {
-  const long long tot = (long long)m * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / m), i = (int)(e % m);
+  for (smg_mn it(m, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     const double v = alpha * A[i + (size_t)j * lda];
     double* d = B + i + (size_t)j * ldb;
     *d = accumulate ? *d + v : v;
@@ -43,10 +42,9 @@ __global__ void k_copy(int m, int n, const double* __restrict__ A, int lda,
 }
 
 __global__ void k_scale(int m, int n, double beta, double* C, int ldc, int tri) {
-  const long long tot = (long long)m * n;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / m), i = (int)(e % m);
+  for (smg_mn it(m, n); it.ok(); it.next()) {
+    const long long e = it.e;
+    const int i = it.i, j = it.j;
     if (tri == 1 && i < j) continue;
     if (tri == 2 && i > j) continue;
     if (tri == 3 && i >= j) continue;

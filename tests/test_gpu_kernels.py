@@ -194,6 +194,20 @@ def test_cholesky_not_pd_and_not_symmetric(ctx):
     assert ctx.status() == 0
 
 
+@pytest.mark.parametrize("N,i,j,v,bad", [(200, 150, 10, 1e-7, True), (200, 10, 150, 1e-7, True),
+                                         (200, 130, 129, -2e-8, True), (200, 63, 64, 1e-9, False),
+                                         (129, 128, 0, float("nan"), True), (64, 63, 62, 0.0, False)])
+def test_check_symmetric_tiles(ctx, N, i, j, v, bad):
+    """Tile-pair symmetric check: one perturbed entry anywhere (either
+    triangle, across tile boundaries, ragged last tile, NaN)."""
+    rng = np.random.default_rng(N + i + j)
+    B = rng.standard_normal((N, N))
+    A = B + B.T
+    A[i, j] += v
+    ctx.call("smg_check_symmetric", ctx.put(F(A)), N, N)
+    assert bool(ctx.status() & 4) == bad
+
+
 # ------------------------------------------------------ mdivide_left_tri
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "mdivide_left_tri_*.json"))))
 def test_mdivide_golden(ctx, path):
