@@ -93,12 +93,15 @@ __global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int 
 // Persistent panel factorisation: ONE launch factors a panel of up to
 // PANEL_MAX_STEPS diagonal blocks (columns [J, K), all rows below), where the
 // blocked loop above would issue potrf / TRSM / trapezoid-update launches
-// per 64-column step.  Row tile t (64 rows from J + 64 t) belongs to
-// workgroup t mod gridDim.x, which applies every step's update to it, so the
-// only cross-workgroup dependencies are
-//   * the factored diagonal block j (L_jj, Dinv_j): flag diag[j];
+// per 64-column step.  Workgroup 0 is the diagonal chain; row tile t >= 1
+// (64 rows from J + 64 t) belongs to workgroup 1 + (t - 1) mod (gridDim.x - 1),
+// which applies every step's update to it, so the only cross-workgroup
+// dependencies are
+//   * the factored diagonal block j (Dinv_j): flag diag[j];
 //   * the panel-region rows L_cj (c < nb) that update tile t's column block c:
-//     flag row[j][c].
+//     flag row[j][c];
+//   * tile j + 2's step-j updates, which the chain's step j + 1 reads:
+//     flag done[j][j + 2].
 // A workgroup only ever waits on tiles c < nb <= 8 owned by workgroups
 // 0 .. 7, which are dispatched first, so the grid needs no co-residency.  The
 // critical path per step is the next diagonal tile's own L_tj + A_tt update
@@ -188,8 +191,12 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
 
   if (blockIdx.x == 0) {
     // the diagonal chain: factor block j, then apply step j to tile j + 1
-    // (L_{j+1,j} and the A_{j+1,j+1} update) so that block j + 1 is ready
-    // in LDS without a hand-off to another workgroup
+    // (a private L_{j+1,j} and the A_{j+1,j+1} update) so that block j + 1 is
+    // ready in LDS without a hand-off.  Tile j + 1's owner computes the same
+    // L_{j+1,j} (same inputs, same code: the same bits) and stores /
+    // publishes it, so no store or publish of it sits on the chain.  The
+    // chain reads A_{j+1,j} before publishing diag[j]; the owner overwrites
+    // it with L_{j+1,j} only after seeing diag[j].
     double* Dc = D;  // current diagonal block (LDS)
     double* Zn = Z;  // next one
     lds_load_block(Dc, L + J + (size_t)J * ldl, ldl, min(SMG_NB, K - J), true);
@@ -201,24 +208,30 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       lds_potrf_inv64_blk(Dc, X, bj, nullptr, 0, nullptr, 0, status, true);
       __syncthreads();
       PANEL_EV((j << 16) | (j << 8) | 10);
-      panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
+      const bool more = j + 1 < nb;
+      const int t = j + 1, rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
+      const int bt = min(SMG_NB, K - rt0);
+      panel_regs Ra, Rz;
+      if (more) {
+        if (j >= 1) panel_wait(&done[(j - 1) * S + t], epoch, status);
+        PANEL_EV((j << 16) | (t << 8) | 11);
+        panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+        panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
+      }
+      // Dinv_j is what the other tiles wait for; L_jj is read by no one in
+      // the launch, so it is stored after the publish (off the chain)
       panel_gstore_tri(X, Dinv + cj, ldd, bj);
       PANEL_EV((j << 16) | (j << 8) | 3);
       panel_publish(&diag[j], epoch);
       PANEL_EV((j << 16) | (j << 8) | 4);
-      if (j + 1 >= nb) break;
-      const int t = j + 1, rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
-      const int bt = min(SMG_NB, K - rt0);
-      if (j >= 1) panel_wait(&done[(j - 1) * S + t], epoch, status);
-      panel_regs Ra, Rz;
-      panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
-      panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
+      panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
+      if (!more) break;
       panel_lstore(Y, Ra);
       panel_lstore(Zn, Rz);
       __syncthreads();
-      lds_mma64_8w<false, true>(Y, Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T
-      panel_gstore(Y, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
-      panel_publish(&row[j * S + t], epoch);
+      PANEL_EV((j << 16) | (t << 8) | 12);
+      lds_mma64_8w<false, true>(Y, Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T (private)
+      PANEL_EV((j << 16) | (t << 8) | 13);
       lds_mma64_8w<false, true>(Zn, Y, Y, -1.0, 1.0);  // A_tt -= L_tj L_tj^T
       // the factorisation's input: lower triangle, zero strict upper (the
       // symmetric update filled it), identity padding beyond bt
@@ -236,14 +249,16 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     return;
   }
 
-  // the other workgroups: tiles t >= 2, owner(t) = 1 + (t - 2) mod (grid - 1);
-  // every step of tile t here except step t - 1 of a panel tile (t < nb),
-  // which the chain applies
+  // the other workgroups: tiles t >= 1, owner(t) = 1 + (t - 1) mod (grid - 1);
+  // every step of tile t.  At step t - 1 of a panel tile (t < nb) the owner
+  // only computes, stores and publishes L_{t,t-1}: the chain applies the
+  // A_tt update privately
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
-    for (int t = 2 + (blockIdx.x - 1); t < T; t += gridDim.x - 1) {
-      if (t <= j || (t == j + 1 && t < nb)) continue;  // done / the chain's
+    for (int t = 1 + (blockIdx.x - 1); t < T; t += gridDim.x - 1) {
+      if (t <= j) continue;  // done
+      const bool next = t == j + 1 && t < nb;  // the chain's next diagonal tile
       const int rt0 = J + SMG_NB * t;
       const int rt = min(SMG_NB, n - rt0);
       __syncthreads();  // LDS of the previous item fully consumed
@@ -260,6 +275,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       panel_gstore(D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
       PANEL_EV((j << 16) | (t << 8) | 7);
       if (t < nb) panel_publish(&row[j * S + t], epoch);
+      if (next) continue;
       // A_tc -= L_tj L_cj^T for the panel's later column blocks c <= t
       const int clast = min(t, nb - 1);
       for (int c = j + 1; c <= clast; ++c) {
@@ -635,16 +651,19 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   //   side: wait E_p, (b)_p, rec F_p
   // (a)_p and (b)_{p-1} both update columns K_p:K_{p+1}, hence the wait;
   // (b)_p is disjoint from panel p+1's columns.
-  const int NB2 = n > 2 * SMG_NBF ? SMG_NBF : n;
+  // (panels never exceed SMG_NBF = PANEL_MAX_STEPS x SMG_NB columns: the
+  // flag arrays of k_chol_panel hold PANEL_MAX_STEPS steps)
+  static_assert(SMG_NBF <= PANEL_MAX_STEPS * SMG_NB, "panel width");
+  const int NB2 = n > SMG_NBF ? SMG_NBF : n;
   const bool look = NB2 < n && smg_side_begin(ctx) == SMG_OK;
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
-      // workgroup 0 = diagonal chain; tiles 2 .. T-1 over the others
+      // workgroup 0 = diagonal chain; tiles 1 .. T-1 over the others
       const int T = smg_ceil_div(n - J, SMG_NB);
-      const int grid = T <= 2 ? 1 : (T - 1 < PANEL_MAX_GRID ? T - 1 : PANEL_MAX_GRID);
+      const int grid = T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID;  // chain + owners of tiles 1..T-1
       const int epoch = ++ctx->flag_epoch;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);

@@ -8,7 +8,7 @@
 #include <cmath>
 
 int main() {
-  const int n = 4096, J = 0, K = 256;
+  const int n = 4096, J = 0, K = 512;
   std::vector<double> A((size_t)n * n);
   for (int j = 0; j < n; ++j)
     for (int i = 0; i < n; ++i) A[i + (size_t)j * n] = (i == j ? n : 0.0) + 1.0 / (1.0 + i + j);
@@ -46,7 +46,7 @@ int main() {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    hipLaunchKernelGGL(k_chol_panel, dim3(T - 1), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
+    hipLaunchKernelGGL(k_chol_panel, dim3(T), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
                        status);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
