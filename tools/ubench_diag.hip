@@ -32,7 +32,7 @@ __global__ __launch_bounds__(512) void k_diag(const double* A, int* status, unsi
     lds_potrf64_blocked(D, status);
     __syncthreads();
     unsigned long long t5 = __builtin_amdgcn_s_memrealtime();
-    lds_trtri64_blocked(D, X, Tt);
+    if (threadIdx.x < 64) wave_potrf64_reg(A, 64, 64, false, nullptr, 0, Tt, D, status, true);
     __syncthreads();
     unsigned long long t6 = __builtin_amdgcn_s_memrealtime();
     lds_load_block((r & 1) ? D : Y, A, 64, 64, true);
@@ -67,7 +67,7 @@ int main() {
   unsigned long long h[NPH];
   (void)hipMemcpy(h, dt, 8 * NPH, hipMemcpyDeviceToHost);
   const char* nm[NPH] = {"potrf64_lookahead", "trtri64_mfma", "mma64_8w", "potrf64_blocked",
-                         "trtri64_blocked", "barrier", "potrf_inv64_blk", "load_block"};
+                         "potrf64_reg(1 wave)", "barrier", "potrf_inv64_blk", "load_block"};
   for (int p = 0; p < NPH; ++p) printf("%-20s %8.2f us\n", nm[p], h[p] / 100.0 / reps);
   return 0;
 }
