@@ -113,7 +113,12 @@ __global__ __launch_bounds__(256) void k_glm_fused(const int* __restrict__ y,
   if (t < M) p[2 + t] = gacc;
 }
 
-constexpr int GLM_RB = 32;  // rows per tile (measured on MI355X: 16 rows 4.3 TB/s, 32 rows 5.1, 64 rows 4.0)
+// rows per tile (measured on MI355X: 16 rows 4.3 TB/s, 32 rows 5.1, 64 rows 4.0).
+// Also measured and rejected: 16-byte loads (two rows per lane) 4.8 TB/s vs
+// 5.0 for 8-byte loads; contiguous per-workgroup tile ranges 3.9 TB/s (the
+// interleaved order keeps concurrently running workgroups on adjacent
+// segments of every column)
+constexpr int GLM_RB = 32;
 
 int glm_blocks(long long R) {
   const long long ntiles = (R + GLM_RB - 1) / GLM_RB;
