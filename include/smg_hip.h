@@ -233,6 +233,27 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x,
                             long long R, int M, long long ldx,
                             const double* alpha_beta, double* ws, double* out);
 
+/* normal_id_glm_lpdf<false>(y | x, alpha, beta, sigma), scalar alpha and
+ * sigma (prim/mat/prob/normal_id_glm_lpdf.hpp:40-150), ONE fused pass over x:
+ *   abs = [alpha, beta(M), sigma] (device);
+ *   out[0] = sum y_scaled^2, out[1] = sum mu', out[2..M+1] = x^T mu'
+ *   with y_scaled = (y - x beta - alpha)/sigma, mu' = y_scaled/sigma.
+ * M <= 256.  ws: >= smg_glm_ws_doubles(R, M). */
+int smg_normal_id_glm(smg_ctx* ctx, const double* y, const double* x,
+                      long long R, int M, long long ldx,
+                      const double* alpha_beta_sigma, double* ws, double* out);
+
+/* poisson_log_glm_lpmf<false>(y | x, alpha, beta), scalar alpha
+ * (prim/mat/prob/poisson_log_glm_lpmf.hpp:37-123), ONE fused pass over x:
+ *   out[0] = sum(y theta - exp theta), out[1] = sum theta',
+ *   out[2..M+1] = x^T theta', out[M+2] = sum lgamma(y + 1)
+ *   with theta = x beta + alpha, theta' = y - exp(theta).
+ * M <= 256.  ws: >= smg_glm_ws_doubles(R, M).  y >= 0 is checked by the
+ * caller (smg_check_bounded_int). */
+int smg_poisson_log_glm(smg_ctx* ctx, const int* y, const double* x,
+                        long long R, int M, long long ldx,
+                        const double* alpha_beta, double* ws, double* out);
+
 /* generic helpers used by the host layer's reverse sweep */
 /* y[i*incy] += alpha * x[i*incx] with alpha read from host */
 int smg_axpy(smg_ctx* ctx, long long n, double alpha, const double* x, int incx,

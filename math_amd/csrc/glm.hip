@@ -1,6 +1,22 @@
-// bernoulli_logit_glm_lpmf<false>(y | x, alpha, beta), scalar alpha, in ONE
-// pass over x.
+// The GLM reducers over rows, each in ONE pass over x (scalar intercept):
+//   KIND 0  bernoulli_logit_glm_lpmf  (y int in {0,1})
+//   KIND 1  normal_id_glm_lpdf        (y double, scalar sigma)
+//   KIND 2  poisson_log_glm_lpmf      (y int >= 0)
+// They differ only in the per-row function of the linear predictor; the
+// x-streaming, the x^T theta' product and the deterministic reductions are
+// shared.
 //
+// KIND 1: prim/mat/prob/normal_id_glm_lpdf.hpp:84-150
+//   y_scaled = (y - x beta - alpha) / sigma;  mu' = y_scaled / sigma
+//   partials: beta' = x^T mu', alpha' = sum mu', sigma' = (sum y_scaled^2 - N)/sigma
+//   logp = -N log sqrt(2 pi) - N log sigma - sum y_scaled^2 / 2
+//   (device: out = [sum y_scaled^2, sum mu', x^T mu'])
+// KIND 2: prim/mat/prob/poisson_log_glm_lpmf.hpp:81-123
+//   theta = x beta + alpha;  theta' = y - exp(theta)
+//   logp = -sum lgamma(y + 1) + sum(y theta - exp(theta))
+//   (device: out = [sum(y theta - exp theta), sum theta', x^T theta', sum lgamma(y + 1)])
+//
+// KIND 0:
 // Reference: prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138
 //   ytheta = sign .* (x beta + alpha), sign = 2y - 1            (:92-94)
 //   logp   = sum( ytheta > 20 ? -exp(-ytheta)
@@ -22,12 +38,14 @@ namespace {
 
 constexpr int MMAX = 256;         // fused path: M <= 256
 
-template <int RB>
-__global__ __launch_bounds__(256) void k_glm_fused(const int* __restrict__ y,
+template <int RB, int KIND>
+__global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
                                                    const double* __restrict__ x, long long R,
                                                    int M, long long ldx,
                                                    const double* __restrict__ ab,
                                                    double* __restrict__ part) {
+  const int* __restrict__ y = static_cast<const int*>(yv);
+  const double* __restrict__ yd = static_cast<const double*>(yv);
   constexpr int XS = RB + 1;  // LDS column stride (bank-conflict free)
   constexpr int PER = RB * MMAX / 256;
   constexpr int G = 256 / RB;  // column groups of the eta pass
@@ -39,9 +57,11 @@ __global__ __launch_bounds__(256) void k_glm_fused(const int* __restrict__ y,
   const int t = threadIdx.x;
   if (t < M) beta[t] = ab[1 + t];
   const double alpha = ab[0];
+  const double inv_sigma = KIND == 1 ? 1.0 / ab[1 + M] : 0.0;  // ab = [alpha, beta(M), sigma]
   const long long ntiles = (R + RB - 1) / RB;
   double gacc = 0.0;                 // column t's beta' accumulator (t < M)
   double lp_acc = 0.0, ga_acc = 0.0; // rows' logp / alpha' (threads < RB)
+  double c_acc = 0.0;                // KIND 2: rows' lgamma(y + 1)
   double reg[PER];
 
   auto load = [&](long long tile) {
@@ -82,11 +102,24 @@ __global__ __launch_bounds__(256) void k_glm_fused(const int* __restrict__ y,
         double eta = 0.0;
 #pragma unroll
         for (int g = 0; g < G; ++g) eta += etap[g * RB + t];
-        const double sgn = 2.0 * y[gr] - 1.0;
-        const double yt = sgn * (eta + alpha);
-        const double e = exp(-yt);
-        lp_acc += yt > 20.0 ? -e : (yt < -20.0 ? yt : -log1p(e));
-        th = yt > 20.0 ? -e : (yt < -20.0 ? sgn : sgn * e / (e + 1));
+        if (KIND == 0) {
+          const double sgn = 2.0 * y[gr] - 1.0;
+          const double yt = sgn * (eta + alpha);
+          const double e = exp(-yt);
+          lp_acc += yt > 20.0 ? -e : (yt < -20.0 ? yt : -log1p(e));
+          th = yt > 20.0 ? -e : (yt < -20.0 ? sgn : sgn * e / (e + 1));
+        } else if (KIND == 1) {
+          const double ys = (yd[gr] - eta - alpha) * inv_sigma;
+          lp_acc += ys * ys;
+          th = ys * inv_sigma;
+        } else {
+          const double yi = (double)y[gr];
+          const double theta = eta + alpha;
+          const double e = exp(theta);
+          lp_acc += yi * theta - e;
+          th = yi - e;
+          c_acc += lgamma(yi + 1.0);
+        }
         ga_acc += th;
       }
       thd[t] = th;
@@ -99,16 +132,22 @@ __global__ __launch_bounds__(256) void k_glm_fused(const int* __restrict__ y,
       gacc += s;
     }
   }
-  // per-block partial [logp, alpha', beta'(M)]
-  const int W = M + 2;
+  // per-block partial [logp, alpha', beta'(M) (, lgamma sum)]
+  const int W = M + 2 + (KIND == 2);
   double* p = part + (size_t)blockIdx.x * W;
   __syncthreads();
   const double lp = block_sum(lp_acc, lds);
   __syncthreads();
   const double ga = block_sum(ga_acc, lds);
+  double cs = 0.0;
+  if (KIND == 2) {
+    __syncthreads();
+    cs = block_sum(c_acc, lds);
+  }
   if (t == 0) {
     p[0] = lp;
     p[1] = ga;
+    if (KIND == 2) p[M + 2] = cs;
   }
   if (t < M) p[2 + t] = gacc;
 }
@@ -158,7 +197,7 @@ __global__ void k_glm_rows(const int* __restrict__ y, const double* __restrict__
 extern "C" {
 
 long long smg_glm_ws_doubles(long long R, int M) {
-  if (M <= MMAX) return (long long)glm_blocks(R) * (M + 2);
+  if (M <= MMAX) return (long long)glm_blocks(R) * (M + 3);
   return 2 * R + 2 * 1024;
 }
 
@@ -169,7 +208,8 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x, long lo
   smg_prof_scope prof(ctx, SMG_FAM_GLM);
   if (M <= MMAX) {
     const int nb = glm_blocks(R);
-    hipLaunchKernelGGL(k_glm_fused<GLM_RB>, dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx, ab, ws);
+    hipLaunchKernelGGL((k_glm_fused<GLM_RB, 0>), dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx,
+                       ab, ws);
     smg_reduce_partials(ctx, ws, nb, M + 2, out, 0);
     SMG_LAUNCH_CHECK();
     return SMG_OK;
@@ -190,6 +230,33 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x, long lo
   rc = smg_gemm_impl(ctx, 1, 0, 0, M, 1, (int)R, 1.0, x, (int)ldx, th, (int)R, 0.0, out + 2, M);
   SMG_LAUNCH_CHECK();
   return rc;
+}
+
+// normal_id_glm_lpdf / poisson_log_glm_lpmf: the fused pass (M <= 256)
+int smg_normal_id_glm(smg_ctx* ctx, const double* y, const double* x, long long R, int M,
+                      long long ldx, const double* abs, double* ws, double* out) {
+  if (!ctx || R < 0 || M < 0 || M > MMAX || !abs || !ws || !out) return SMG_ERR_ARG;
+  if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GLM);
+  const int nb = glm_blocks(R);
+  hipLaunchKernelGGL((k_glm_fused<GLM_RB, 1>), dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx,
+                     abs, ws);
+  smg_reduce_partials(ctx, ws, nb, M + 2, out, 0);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_poisson_log_glm(smg_ctx* ctx, const int* y, const double* x, long long R, int M,
+                        long long ldx, const double* ab, double* ws, double* out) {
+  if (!ctx || R < 0 || M < 0 || M > MMAX || !ab || !ws || !out) return SMG_ERR_ARG;
+  if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GLM);
+  const int nb = glm_blocks(R);
+  hipLaunchKernelGGL((k_glm_fused<GLM_RB, 2>), dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx,
+                     ab, ws);
+  smg_reduce_partials(ctx, ws, nb, M + 3, out, 0);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
 }
 
 }  // extern "C"

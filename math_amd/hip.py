@@ -71,6 +71,8 @@ _SIGS = {
     "smg_normal_lpdf": (_I, [_P, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _P, _P]),
     "smg_glm_ws_doubles": (_L, [_L, _I]),
     "smg_bernoulli_logit_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
+    "smg_normal_id_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
+    "smg_poisson_log_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_axpy": (_I, [_P, _L, _D, _P, _I, _P, _I]),
     "smg_axpy_dev": (_I, [_P, _L, _P, _P, _P]),
     "smg_sum": (_I, [_P, _P, _L, _P]),

@@ -47,6 +47,7 @@ inline void comm_destroy() {
  * x: rows x M column-major with leading dimension ldx (ldx >= rows). */
 struct glm_shard {
   const int* y = nullptr;
+  const double* yd = nullptr;  // real-valued y (normal_id_glm_lpdf)
   const double* x = nullptr;
   long long rows = 0;
   int M = 0;

@@ -473,6 +473,69 @@ double oracle_glm(const int* y, const double* x, long long R, int M,
   return logp;
 }
 
+// x beta over the rows (column by column, like Eigen's col-major GEMV)
+static std::vector<double> glm_eta(const double* x, long long R, int M, const double* beta) {
+  std::vector<double> eta((size_t)R, 0.0);
+  for (int j = 0; j < M; ++j) {
+    const double b = beta[j];
+    const double* col = x + (size_t)j * R;
+    for (long long i = 0; i < R; ++i) eta[i] += col[i] * b;
+  }
+  return eta;
+}
+
+// g[1 + j] = x_j . d
+static void glm_xt(const double* x, long long R, int M, const double* d, double* g) {
+  for (int j = 0; j < M; ++j) {
+    const double* col = x + (size_t)j * R;
+    double s = 0;
+    for (long long i = 0; i < R; ++i) s += col[i] * d[i];
+    g[1 + j] = s;
+  }
+}
+
+double oracle_normal_id_glm(const double* y, const double* x, long long R, int M,
+                            double alpha, const double* beta, double sigma, double* g) {
+  // normal_id_glm_lpdf.hpp:84-86: y_scaled = (y - x beta - alpha) * inv_sigma
+  const double inv_sigma = 1.0 / sigma;
+  std::vector<double> ys = glm_eta(x, R, M, beta), mu((size_t)R);
+  double sq = 0, sa = 0;
+  for (long long i = 0; i < R; ++i) {
+    ys[i] = (y[i] - ys[i] - alpha) * inv_sigma;
+    mu[i] = inv_sigma * ys[i];  // :92 mu_derivative
+    sq += ys[i] * ys[i];
+    sa += mu[i];
+  }
+  if (g) {
+    g[0] = sa;                                // :104-109 alpha
+    glm_xt(x, R, M, mu.data(), g);            // :101-103 beta
+    g[M + 1] = (sq - (double)R) * inv_sigma;  // :116-118 sigma
+  }
+  // :131-142
+  const double NEG_LOG_SQRT_TWO_PI = -0.91893853320467274178;
+  return NEG_LOG_SQRT_TWO_PI * (double)R - (double)R * std::log(sigma) - 0.5 * sq;
+}
+
+double oracle_poisson_log_glm(const int* y, const double* x, long long R, int M,
+                              double alpha, const double* beta, double* g) {
+  // poisson_log_glm_lpmf.hpp:81-106
+  std::vector<double> th = glm_eta(x, R, M, beta), d((size_t)R);
+  double sd = 0, lg = 0, s2 = 0;
+  for (long long i = 0; i < R; ++i) {
+    th[i] += alpha;
+    const double e = std::exp(th[i]);
+    d[i] = y[i] - e;
+    sd += d[i];
+    lg += std::lgamma(y[i] + 1.0);
+    s2 += y[i] * th[i] - e;
+  }
+  if (g) {
+    g[0] = sd;
+    glm_xt(x, R, M, d.data(), g);
+  }
+  return -lg + s2;
+}
+
 void oracle_gp_marginal(const double* x, const double* y, int n,
                         const double* theta, double* fx, double* grad) {
   const double alpha = theta[0], rho = theta[1], sigma = theta[2];

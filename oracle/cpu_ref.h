@@ -82,6 +82,18 @@ double oracle_glm(const int* y, const double* x, long long R, int M,
                   double alpha, const double* beta, double* galpha,
                   double* gbeta);
 
+/* normal_id_glm_lpdf<false>(y | x, alpha, beta, sigma), scalar alpha and
+ * sigma.  prim/mat/prob/normal_id_glm_lpdf.hpp:84-150.  Returns logp; the
+ * gradient wrt (alpha, beta, sigma) into g (M + 2). */
+double oracle_normal_id_glm(const double* y, const double* x, long long R, int M,
+                            double alpha, const double* beta, double sigma, double* g);
+
+/* poisson_log_glm_lpmf<false>(y | x, alpha, beta), scalar alpha.
+ * prim/mat/prob/poisson_log_glm_lpmf.hpp:81-123.  Returns logp (lgamma terms
+ * included); the gradient wrt (alpha, beta) into g (M + 1). */
+double oracle_poisson_log_glm(const int* y, const double* x, long long R, int M,
+                              double alpha, const double* beta, double* g);
+
 /* GP marginal gradient (config 3) through the restated functors. */
 void oracle_gp_marginal(const double* x, const double* y, int n,
                         const double* theta, double* fx, double* grad);

@@ -29,6 +29,8 @@
  *   trigamma (double)        stan/math/prim/scal/fun/trigamma.hpp:33-125
  *   normal_lpdf              stan/math/prim/scal/prob/normal_lpdf.hpp:36-119
  *   bernoulli_logit_glm_lpmf stan/math/prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138
+ *   normal_id_glm_lpdf       stan/math/prim/mat/prob/normal_id_glm_lpdf.hpp:40-150
+ *   poisson_log_glm_lpmf     stan/math/prim/mat/prob/poisson_log_glm_lpmf.hpp:37-123
  *   map_rect                 stan/math/prim/mat/functor/map_rect.hpp:120-177
  *   hessian_times_vector     stan/math/mix/mat/functor/hessian_times_vector.hpp:13-40
  */
@@ -739,6 +741,74 @@ static void fix_glm() {
   }
 }
 
+// normal_id / poisson_log GLM inputs (tests/gen.py glm2_inputs)
+static void glm2_inputs(int R, int M, bool normal, glm_data& d, VectorXd& yd) {
+  d = glm_inputs(R, M);
+  if (normal) {
+    std::vector<double> y = unif(SEED + 51, R, -2.0, 2.0);
+    yd = Eigen::Map<VectorXd>(y.data(), R);
+    d.theta.conservativeResize(M + 2);
+    d.theta(M + 1) = 1.3;
+  } else {
+    std::vector<double> u = unif(SEED + 52, R, 0.0, 6.0);
+    for (int i = 0; i < R; ++i) d.y[i] = (int)u[i];
+    for (int j = 0; j < M; ++j) d.theta(j + 1) *= 0.5;
+  }
+}
+template <bool propto>
+struct normal_glm_functor {
+  const glm_data& d;
+  const VectorXd& y;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, 1> beta = th.segment(1, d.M);
+    return stan::math::normal_id_glm_lpdf<propto>(y, d.x, th(0), beta, th(d.M + 1));
+  }
+};
+template <bool propto>
+struct poisson_glm_functor {
+  const glm_data& d;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, 1> beta = th.tail(d.M);
+    return stan::math::poisson_log_glm_lpmf<propto>(d.y, d.x, th(0), beta);
+  }
+};
+
+static void fix_glm2() {
+  struct Case {
+    int R, M;
+  };
+  for (Case c : {Case{1000, 8}, Case{20000, 64}}) {
+    for (int normal = 1; normal >= 0; --normal) {
+      glm_data d;
+      VectorXd yd;
+      glm2_inputs(c.R, c.M, normal, d, yd);
+      double fx, fxp;
+      VectorXd g, gp;
+      Json j;
+      if (normal) {
+        stan::math::gradient(normal_glm_functor<false>{d, yd}, d.theta, fx, g);
+        stan::math::gradient(normal_glm_functor<true>{d, yd}, d.theta, fxp, gp);
+        j.put_str("what", "gradient of normal_id_glm_lpdf(y|x,alpha,beta,sigma) wrt (alpha,beta,sigma); inputs: tests/gen.py glm2_inputs");
+      } else {
+        stan::math::gradient(poisson_glm_functor<false>{d}, d.theta, fx, g);
+        stan::math::gradient(poisson_glm_functor<true>{d}, d.theta, fxp, gp);
+        j.put_str("what", "gradient of poisson_log_glm_lpmf(y|x,alpha,beta) wrt (alpha,beta); inputs: tests/gen.py glm2_inputs");
+      }
+      j.put_int("R", c.R);
+      j.put_int("M", c.M);
+      j.put("fx", fx);
+      j.put_vec("grad", g);
+      j.put("fx_propto", fxp);
+      j.put_vec("grad_propto", gp);
+      write_fixture(std::string(normal ? "normal_id_glm" : "poisson_log_glm") + "_R" +
+                        std::to_string(c.R) + "_M" + std::to_string(c.M),
+                    j);
+    }
+  }
+}
+
 static void fix_hvp() {
   for (int N : {8, 32, 100, 256}) {
     std::vector<double> x;
@@ -836,6 +906,7 @@ int main(int argc, char** argv) {
     if (want("cholesky")) fix_cholesky();
     if (want("mvn")) fix_mvn();
     if (want("glm")) fix_glm();
+    if (want("glm2")) fix_glm2();
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();
     if (want("gp")) fix_gp();

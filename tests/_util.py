@@ -99,6 +99,8 @@ def oracle():
             "oracle_trigamma": (dd, [dd]),
             "oracle_normal_lpdf": (dd, [_D, ii, _D, ii, _D, ii, ii, _D, _D, _D]),
             "oracle_glm": (dd, [_I, _D, ctypes.c_longlong, ii, dd, _D, _D, _D]),
+            "oracle_normal_id_glm": (dd, [_D, _D, ctypes.c_longlong, ii, dd, _D, dd, _D]),
+            "oracle_poisson_log_glm": (dd, [_I, _D, ctypes.c_longlong, ii, dd, _D, _D]),
             "oracle_gp_marginal": (None, [_D, _D, ii, _D, _D, _D]),
             "oracle_mulchol": (None, [_D, ii, _D, _D]),
         }
@@ -112,3 +114,16 @@ def oracle():
 
 def f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def glm2_oracle(kind, x, y, th, M):
+    """(logp, gradient) of the restated normal_id / poisson_log GLM."""
+    R = len(y)
+    g = np.zeros(M + 2 if kind == "normal" else M + 1)
+    xf = f64(x.ravel(order="F"))
+    if kind == "normal":
+        lp = oracle().oracle_normal_id_glm(ptr(f64(y)), ptr(xf), R, M, th[0], ptr(f64(th[1:M + 1])), th[M + 1], ptr(g))
+    else:
+        lp = oracle().oracle_poisson_log_glm(ptr(np.ascontiguousarray(y, dtype=np.int32)), ptr(xf), R, M, th[0],
+                                             ptr(f64(th[1:])), ptr(g))
+    return lp, g

@@ -20,6 +20,8 @@
 //   errors                        the reference's exceptions
 //   hvp N theta v x y             hessian_times_vector of the GP marginal (config 5)
 //   map_rect_glm R M shards beta  map_rect over GLM row blocks (vs the reference's map_rect32)
+//   glm2 kind R M y theta         normal_id_glm_lpdf (kind 0) / poisson_log_glm_lpmf (kind 1):
+//                                 device x, single call, 7 row shards, propto
 #include <stan/math.hpp>
 
 #include <cmath>
@@ -377,6 +379,67 @@ static void cmd_glm() {
   print("grad_shards32", g);
 }
 
+static void cmd_glm2() {
+  int kind, M;
+  long long R;
+  std::cin >> kind >> R >> M;
+  auto yv = read_vec(size_t(R));
+  auto th = read_vec(size_t(kind == 0 ? M + 2 : M + 1));
+  smg_ctx* c = amd::ctx();
+  double* x = amd::alloc_doubles(size_t(R) * M);
+  amd::check(smg_fill_unif(c, x, R * M, 20260101ull + 41, -1.0, 1.0, std::sqrt(3.0)), "fill");
+  std::vector<int> yi(yv.begin(), yv.end());
+  dev_data<double> yd = to_dev_data(yv);
+  dev_data<int> ydi = to_dev_data(yi);
+  dev_data<double> xd(x, size_t(R) * M, int(R), M);
+  auto f = [&](const std::vector<var>& t, auto propto_tag) {
+    constexpr bool P = decltype(propto_tag)::value;
+    std::vector<var> b(t.begin() + 1, t.begin() + 1 + M);
+    if (kind == 0) return normal_id_glm_lpdf<P>(yd, xd, t[0], b, t[M + 1]);
+    return poisson_log_glm_lpmf<P>(ydi, xd, t[0], b);
+  };
+  double fx;
+  std::vector<double> g;
+  gradient([&](const std::vector<var>& t) { return f(t, std::false_type{}); }, th, fx, g);
+  print1("fx", fx);
+  print("grad", g);
+  gradient([&](const std::vector<var>& t) { return f(t, std::true_type{}); }, th, fx, g);
+  print1("fx_propto", fx);
+  print("grad_propto", g);
+  // 7 contiguous row shards summed on the tape (each shard: its own N)
+  gradient(
+      [&](const std::vector<var>& t) {
+        std::vector<var> b(t.begin() + 1, t.begin() + 1 + M);
+        var s = 0.0;
+        for (int k = 0; k < 7; ++k) {
+          long long b0, b1;
+          row_partition(R, 7, k, &b0, &b1);
+          glm_shard sh;
+          sh.y = ydi.data() + b0;
+          sh.yd = yd.data() + b0;
+          sh.x = x + b0;
+          sh.rows = b1 - b0;
+          sh.M = M;
+          sh.ldx = R;
+          sh.row0 = b0;
+          sh.total_rows = b1 - b0;
+          if (kind == 0) s += normal_id_glm_lpdf<false>(sh, t[0], b, t[M + 1]);
+          else s += poisson_log_glm_lpmf<false>(sh, t[0], b);
+        }
+        return s;
+      },
+      th, fx, g);
+  print1("fx_shards7", fx);
+  print("grad_shards7", g);
+  // all-double arguments: a plain double, no tape
+  std::vector<double> bd(th.begin() + 1, th.begin() + 1 + M);
+  start_nested();
+  const double v = kind == 0 ? normal_id_glm_lpdf<false>(yd, xd, th[0], bd, th[M + 1])
+                             : poisson_log_glm_lpmf<false>(ydi, xd, th[0], bd);
+  recover_memory_nested();
+  print1("fx_double", v);
+}
+
 static void cmd_glm_data() {
   int R, M;
   std::cin >> R >> M;
@@ -575,6 +638,26 @@ static void cmd_errors() {
     std::vector<double> a = {1, 2, 2, 1};
     cholesky_decompose(to_dev_var_matrix(a.data(), 2, 2));
   });
+  expect_throw("normal_glm_sigma", [&] {
+    normal_id_glm_lpdf(std::vector<double>{0.5, 1.0}, std::vector<double>{1, 2}, 1, var(0.0),
+                       std::vector<var>{var(1.0)}, var(-1.0));
+  });
+  expect_throw("normal_glm_beta_size", [&] {
+    normal_id_glm_lpdf(std::vector<double>{0.5, 1.0}, std::vector<double>{1, 2}, 1, var(0.0),
+                       std::vector<var>{var(1.0), var(2.0)}, var(1.0));
+  });
+  expect_throw("normal_glm_nonfinite_y", [&] {
+    normal_id_glm_lpdf(std::vector<double>{0.5, INFINITY}, std::vector<double>{1, 2}, 1, var(0.0),
+                       std::vector<var>{var(1.0)}, var(1.0));
+  });
+  expect_throw("poisson_glm_negative_y", [&] {
+    poisson_log_glm_lpmf(std::vector<int>{0, 3, -2}, std::vector<double>{1, 2, 3}, 1, var(0.0),
+                         std::vector<var>{var(1.0)});
+  });
+  expect_throw("poisson_glm_nonfinite_beta", [&] {
+    poisson_log_glm_lpmf(std::vector<int>{0, 3}, std::vector<double>{1, 2}, 1, var(0.0),
+                         std::vector<var>{var(INFINITY)});
+  });
   expect_throw("glm_y_bounds", [&] {
     bernoulli_logit_glm_lpmf(std::vector<int>{0, 2}, std::vector<double>{1, 2}, 1, var(0.0),
                              std::vector<var>{1.0});
@@ -615,6 +698,7 @@ int main() {
     else if (cmd == "normal_known") cmd_normal_known();
     else if (cmd == "glm") cmd_glm();
     else if (cmd == "glm_data") cmd_glm_data();
+    else if (cmd == "glm2") cmd_glm2();
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
     else if (cmd == "hvp") cmd_hvp();

@@ -44,3 +44,17 @@ def glm_inputs(R: int, M: int):
     b = unif(SEED + 43, M, -1.0, 1.0) * np.sqrt(3.0 / M)
     theta = np.concatenate([[0.1], b])
     return x.reshape(M, R).T.copy(order="F"), y, theta
+
+
+def glm2_inputs(R: int, M: int, kind: str):
+    """normal_id / poisson_log GLM inputs, ref_harness.cpp glm2_inputs: x and
+    beta as glm_inputs; y uniform on [-2, 2) (normal) or floor(U[0, 6))
+    counts (poisson); theta = (alpha, beta(M)[, sigma])."""
+    x, _, th = glm_inputs(R, M)
+    if kind == "normal":
+        y = unif(SEED + 51, R, -2.0, 2.0)
+        theta = np.concatenate([th, [1.3]])
+    else:
+        y = np.floor(unif(SEED + 52, R, 0.0, 6.0)).astype(np.int32)
+        theta = np.concatenate([[th[0]], 0.5 * th[1:]])
+    return x, y, theta

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import gen
-from _util import GOLDEN, f64, golden, near_rel, oracle, ptr
+from _util import GOLDEN, f64, glm2_oracle, golden, near_rel, oracle, ptr
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-10
@@ -374,6 +374,48 @@ def test_glm_golden(ctx, name):
     out = _glm(ctx, x, y, th, R, M)
     near_rel(out[0], d["fx"], 1e-12, what="fx")
     near_rel(out[1:], d["grad"], RTOL, what="grad")
+
+
+def _glm2(ctx, kind, x, y, th, R, M):
+    """Device normal_id / poisson_log GLM -> (logp, gradient) assembled as the
+    host layer does (normal: logp = -N log sqrt(2 pi) - N log sigma - sq/2,
+    sigma' = (sq - N)/sigma; poisson: logp = sum(y theta - e^theta) - sum lgamma(y+1))."""
+    dx, dab = ctx.put(F(x)), ctx.put(f64(th))
+    ws = ctx.zeros(int(ctx.lib.smg_glm_ws_doubles(R, M)))
+    out = ctx.zeros(M + 3)
+    if kind == "normal":
+        ctx.call("smg_normal_id_glm", ctx.put(f64(y)), dx, R, M, R, dab, ws, out)
+        o = ctx.get(out, M + 2)
+        sig = th[M + 1]
+        lp = -0.91893853320467274178 * R - R * np.log(sig) - 0.5 * o[0]
+        return lp, np.concatenate([o[1:], [(o[0] - R) / sig]])
+    ctx.call("smg_poisson_log_glm", ctx.put(np.ascontiguousarray(y, dtype=np.int32)), dx, R, M, R, dab, ws, out)
+    o = ctx.get(out, M + 3)
+    return o[0] - o[M + 2], o[1:M + 2]
+
+
+@pytest.mark.parametrize("name", ["normal_id_glm_R1000_M8", "normal_id_glm_R20000_M64",
+                                  "poisson_log_glm_R1000_M8", "poisson_log_glm_R20000_M64"])
+def test_glm2_golden(ctx, name):
+    d = golden(name)
+    R, M = int(d["R"]), int(d["M"])
+    kind = "normal" if name.startswith("normal") else "poisson"
+    x, y, th = gen.glm2_inputs(R, M, kind)
+    lp, g = _glm2(ctx, kind, x, y, th, R, M)
+    near_rel(lp, d["fx"], 1e-12, what="fx")
+    near_rel(g, d["grad"], RTOL, what="grad")
+
+
+@pytest.mark.parametrize("kind", ["normal", "poisson"])
+def test_glm2_vs_oracle_ragged(ctx, kind):
+    """Beyond the fixtures: 200003 rows (ragged last tile, odd R) x 200
+    covariates against the reference-pinned restatement."""
+    R, M = 200003, 200
+    x, y, th = gen.glm2_inputs(R, M, kind)
+    lp, g = _glm2(ctx, kind, x, y, th, R, M)
+    lpo, go = glm2_oracle(kind, x, y, th, M)
+    near_rel(lp, lpo, 1e-12, what="fx")
+    near_rel(g, go, RTOL, what="grad")
 
 
 def test_glm_extreme(ctx):
