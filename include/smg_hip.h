@@ -142,9 +142,10 @@ int smg_add_diag_rev(smg_ctx* ctx, const double* Badj, int ldb, int n,
  *   check: latches SMG_ERR_NOT_SYMMETRIC when |A_ij - A_ji| > 1e-8 (:383)
  *   fwd:   L = lower Cholesky factor (upper zeroed); latches SMG_ERR_NOT_PD.
  *          aux (smg_cholesky_aux_doubles(n) doubles, may be NULL) receives the
- *          inverses of L's diagonal blocks at 64, 128 and 256 granularity
- *          (n x 64 | n x 128 | n x 256, each leading dimension n), reused by
- *          the reverse pass and by the triangular solves (TRSV / MVN).
+ *          inverses of L's diagonal blocks at 64, 128, 256 and 512
+ *          granularity (n x 64 | n x 128 | n x 256 | n x 512, each leading
+ *          dimension n), reused by the reverse pass and by the triangular
+ *          solves (TRSV / MVN / TRSM).
  *   rev:   Murray's blocked adjoint (:118-165): Aadj(lower) += f(L, Ladj);
  *          Ladj (lower) is used as workspace and overwritten; aux as written
  *          by the forward, or NULL (recomputed). */
@@ -167,6 +168,57 @@ int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda,
                              const double* C, int ldc, const double* Cadj,
                              int ldca, int m, int n, double* Aadj, int ldaa,
                              double* Badj, int ldba, double* ws);
+
+/* mdivide_left_spd(A, B) (rev/mat/fun/mdivide_left_spd.hpp:20-150)
+ *   fwd: L = chol(lower(A)) into L (m x m, ld m) and aux
+ *        (smg_cholesky_aux_doubles(m)); C = A^{-1} B via two blocked TRSMs.
+ *        Latches SMG_ERR_NOT_PD.
+ *   rev: W = A^{-1} Cadj; Aadj -= W C^T (every entry); Badj += W.
+ *        Aadj / Badj may be NULL.  ws: >= m*n doubles. */
+int smg_mdivide_left_spd_fwd(smg_ctx* ctx, const double* A, int lda,
+                             const double* B, int ldb, int m, int n, double* L,
+                             double* aux, double* C, int ldc);
+int smg_mdivide_left_spd_rev(smg_ctx* ctx, const double* L, const double* aux,
+                             int m, int n, const double* C, int ldc,
+                             const double* Cadj, int ldca, double* Aadj,
+                             int ldaa, double* Badj, int ldba, double* ws);
+
+/* log_determinant_spd(A) (rev/mat/fun/log_determinant_spd.hpp:16-57)
+ *   fwd: L = chol(lower(A)) (+aux), out[0] = 2 sum log L_ii; latches
+ *        SMG_ERR_NOT_PD.
+ *   rev: Aadj += adj * A^{-1} (every entry).  ws: >= n*n doubles. */
+int smg_log_determinant_spd_fwd(smg_ctx* ctx, const double* A, int lda, int n,
+                                double* L, double* aux, double* out);
+int smg_log_determinant_spd_rev(smg_ctx* ctx, const double* L,
+                                const double* aux, int n, double adj,
+                                double* Aadj, int ldaa, double* ws);
+
+/* multiply_lower_tri_self_transpose(L), L: K x J
+ * (rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44)
+ *   fwd: C (K x K) = T T^T, T = lower trapezoid of L.  ws: >= K*J.
+ *   rev: Ladj (lower trapezoid) += (Cadj + Cadj^T) T.  ws: >= 2 K*J + K*K. */
+int smg_multiply_lower_tri_self_transpose_fwd(smg_ctx* ctx, const double* L,
+                                              int ldl, int K, int J, double* C,
+                                              int ldc, double* ws);
+int smg_multiply_lower_tri_self_transpose_rev(smg_ctx* ctx, const double* L,
+                                              int ldl, int K, int J,
+                                              const double* Cadj, int ldca,
+                                              double* Ladj, int ldla, double* ws);
+
+/* quad_form_sym(A, B), A: M x M symmetric, B: M x N
+ * (rev/mat/fun/quad_form_sym.hpp:15-40, quad_form.hpp:17-100)
+ *   fwd: C (N x N) = (Cd + Cd^T)/2, Cd = B^T A B.  ws: >= M*N + N*N.
+ *   rev: Aadj += B S B^T; Badj += A B S^T + A^T B S (NULL skips), with
+ *        S = Cadj, or (Cadj + Cadj^T)/2 when sym_adj (A and B both var: the
+ *        prim template, prim/mat/fun/quad_form_sym.hpp:11-18).
+ *        ws: >= M*N + N*N. */
+int smg_quad_form_sym_fwd(smg_ctx* ctx, const double* A, int lda,
+                          const double* B, int ldb, int M, int N, double* C,
+                          int ldc, double* ws);
+int smg_quad_form_sym_rev(smg_ctx* ctx, const double* A, int lda,
+                          const double* B, int ldb, int M, int N,
+                          const double* Cadj, int ldca, int sym_adj, double* Aadj,
+                          int ldaa, double* Badj, int ldba, double* ws);
 
 /* multiply(A, B) (rev/mat/fun/multiply.hpp:65-135): fwd C = A B;
  * rev Aadj += Cadj B^T, Badj += A^T Cadj (NULL skips an operand). */

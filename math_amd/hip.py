@@ -73,6 +73,14 @@ _SIGS = {
     "smg_bernoulli_logit_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_normal_id_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_poisson_log_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
+    "smg_mdivide_left_spd_fwd": (_I, [_P, _P, _I, _P, _I, _I, _I, _P, _P, _P, _I]),
+    "smg_mdivide_left_spd_rev": (_I, [_P, _P, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P]),
+    "smg_log_determinant_spd_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P]),
+    "smg_log_determinant_spd_rev": (_I, [_P, _P, _P, _I, _D, _P, _I, _P]),
+    "smg_multiply_lower_tri_self_transpose_fwd": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
+    "smg_multiply_lower_tri_self_transpose_rev": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
+    "smg_quad_form_sym_fwd": (_I, [_P, _P, _I, _P, _I, _I, _I, _P, _I, _P]),
+    "smg_quad_form_sym_rev": (_I, [_P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
     "smg_axpy": (_I, [_P, _L, _D, _P, _I, _P, _I]),
     "smg_axpy_dev": (_I, [_P, _L, _P, _P, _P]),
     "smg_sum": (_I, [_P, _P, _L, _P]),

@@ -25,6 +25,7 @@
 #include <stan/math/rev/fun/cholesky_decompose.hpp>
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
 #include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
+#include <stan/math/rev/fun/spd_functors.hpp>
 #include <stan/math/rev/fun/lgamma.hpp>
 #include <stan/math/rev/fun/log_sum_exp.hpp>
 #include <stan/math/rev/fun/mdivide_left_tri.hpp>
@@ -194,6 +195,58 @@ inline Eigen::Matrix<var, Eigen::Dynamic, C2> mdivide_left_tri(
 template <int TriView>
 inline matrix_v mdivide_left_tri(const matrix_v& A) {
   return to_host_matrix(mdivide_left_tri<TriView>(to_dev(A)));
+}
+
+// ------------------------------------------------ §8(f) row 3 (spd_functors.hpp)
+/** rev/mat/fun/mdivide_left_spd.hpp:232-260 signatures. */
+template <int R1, int C1, int R2, int C2>
+inline matrix_v mdivide_left_spd(const Eigen::Matrix<var, R1, C1>& A, const Eigen::Matrix<var, R2, C2>& b) {
+  internal::check_square("mdivide_left_spd", "A", int(A.rows()), int(A.cols()));
+  internal::check_multiplicable_named("mdivide_left_spd", "A", int(A.cols()), "b", int(b.rows()));
+  return to_host_matrix(mdivide_left_spd(to_dev(A), to_dev(b)));
+}
+template <int R1, int C1, int R2, int C2>
+inline matrix_v mdivide_left_spd(const Eigen::Matrix<double, R1, C1>& A, const Eigen::Matrix<var, R2, C2>& b) {
+  internal::check_square("mdivide_left_spd", "A", int(A.rows()), int(A.cols()));
+  internal::check_multiplicable_named("mdivide_left_spd", "A", int(A.cols()), "b", int(b.rows()));
+  const matrix_d Ad = A;
+  return to_host_matrix(mdivide_left_spd(to_dev_data(Ad.data(), size_t(Ad.size()), int(Ad.rows()), int(Ad.cols())),
+                                         to_dev(b)));
+}
+template <int R1, int C1, int R2, int C2>
+inline matrix_v mdivide_left_spd(const Eigen::Matrix<var, R1, C1>& A, const Eigen::Matrix<double, R2, C2>& b) {
+  internal::check_square("mdivide_left_spd", "A", int(A.rows()), int(A.cols()));
+  internal::check_multiplicable_named("mdivide_left_spd", "A", int(A.cols()), "b", int(b.rows()));
+  const matrix_d bd = b;
+  return to_host_matrix(mdivide_left_spd(to_dev(A), to_dev_data(bd.data(), size_t(bd.size()), int(bd.rows()),
+                                                               int(bd.cols()))));
+}
+/** rev/mat/fun/log_determinant_spd.hpp:16 signature. */
+template <int R, int C>
+inline var log_determinant_spd(const Eigen::Matrix<var, R, C>& m) {
+  internal::check_square("log_determinant_spd", "m", int(m.rows()), int(m.cols()));
+  return log_determinant_spd(to_dev(m));
+}
+/** rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14 signature. */
+inline matrix_v multiply_lower_tri_self_transpose(const matrix_v& L) {
+  if (L.rows() == 0) return matrix_v(0, 0);
+  return to_host_matrix(multiply_lower_tri_self_transpose(to_dev(L)));
+}
+/** rev/mat/fun/quad_form_sym.hpp:15-40 signatures (matrix B -> matrix, vector b -> var). */
+template <int Ra, int Ca, int Rb, int Cb>
+inline matrix_v quad_form_sym(const Eigen::Matrix<var, Ra, Ca>& A, const Eigen::Matrix<var, Rb, Cb>& B) {
+  return to_host_matrix(quad_form_sym(to_dev(A), to_dev(B)));
+}
+template <int Ra, int Ca, int Rb, int Cb>
+inline matrix_v quad_form_sym(const Eigen::Matrix<double, Ra, Ca>& A, const Eigen::Matrix<var, Rb, Cb>& B) {
+  const matrix_d Ad = A;
+  return to_host_matrix(quad_form_sym(to_dev_data(Ad.data(), size_t(Ad.size()), int(Ad.rows()), int(Ad.cols())),
+                                      to_dev(B)));
+}
+template <int Ra, int Ca, int Rb>
+inline var quad_form_sym(const Eigen::Matrix<var, Ra, Ca>& A, const Eigen::Matrix<var, Rb, 1>& b) {
+  matrix_v B = b;
+  return quad_form_sym(A, B)(0, 0);
 }
 
 /** bernoulli_logit_glm_lpmf(y, x, alpha, beta) with Eigen x / beta (:46-144). */

@@ -536,6 +536,122 @@ double oracle_poisson_log_glm(const int* y, const double* x, long long R, int M,
   return -lg + s2;
 }
 
+// X (n x k) <- A^{-1} X through L = chol(A): forward then backward substitution
+static void spd_solve(const double* L, int n, double* X, int k) {
+  for (int c = 0; c < k; ++c) {
+    double* x = X + (size_t)c * n;
+    for (int i = 0; i < n; ++i) {
+      double s = x[i];
+      for (int j = 0; j < i; ++j) s -= L[i + (size_t)j * n] * x[j];
+      x[i] = s / L[i + (size_t)i * n];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double s = x[i];
+      for (int j = i + 1; j < n; ++j) s -= L[j + (size_t)i * n] * x[j];
+      x[i] = s / L[i + (size_t)i * n];
+    }
+  }
+}
+
+int oracle_mdivide_left_spd(const double* A, const double* B, int n, int k, const double* W,
+                            double* fx, double* gA, double* gB) {
+  std::vector<double> L((size_t)n * n);
+  if (oracle_cholesky(A, n, L.data()) != 0) return -1;
+  std::vector<double> C(B, B + (size_t)n * k), Wa(W, W + (size_t)n * k);
+  spd_solve(L.data(), n, C.data(), k);  // C = A^{-1} B (:57-62)
+  double f = 0;
+  for (size_t e = 0; e < (size_t)n * k; ++e) f += W[e] * C[e];
+  *fx = f;
+  spd_solve(L.data(), n, Wa.data(), k);  // adjB = A^{-1} Cadj (:95-96)
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int c = 0; c < k; ++c) s += Wa[i + (size_t)c * n] * C[j + (size_t)c * n];
+      gA[i + (size_t)j * n] = -s;  // Aadj -= adjB C^T (:97-98)
+    }
+  for (size_t e = 0; e < (size_t)n * k; ++e) gB[e] = Wa[e];
+  return 0;
+}
+
+int oracle_log_determinant_spd(const double* A, int n, double* fx, double* gA) {
+  std::vector<double> L((size_t)n * n);
+  if (oracle_cholesky(A, n, L.data()) != 0) return -1;
+  double s = 0;
+  for (int i = 0; i < n; ++i) s += std::log(L[i + (size_t)i * n]);
+  *fx = 2 * s;
+  std::fill(gA, gA + (size_t)n * n, 0.0);
+  for (int i = 0; i < n; ++i) gA[i + (size_t)i * n] = 1.0;
+  spd_solve(L.data(), n, gA, n);  // A^{-1} (:46-53)
+  return 0;
+}
+
+void oracle_mlt_self_transpose(const double* L, int K, int J, const double* W, double* fx,
+                               double* gL) {
+  auto T = [&](int i, int j) { return i >= j ? L[i + (size_t)j * K] : 0.0; };
+  double f = 0;
+  for (int m = 0; m < K; ++m)
+    for (int q = 0; q < K; ++q) {
+      double c = 0;
+      for (int j = 0; j < J; ++j) c += T(m, j) * T(q, j);
+      f += W[m + (size_t)q * K] * c;
+    }
+  *fx = f;
+  for (int j = 0; j < J; ++j)
+    for (int i = 0; i < K; ++i) {
+      double s = 0;
+      if (i >= j)
+        for (int q = 0; q < K; ++q) s += (W[i + (size_t)q * K] + W[q + (size_t)i * K]) * T(q, j);
+      gL[i + (size_t)j * K] = s;
+    }
+}
+
+void oracle_quad_form_sym(const double* A, const double* B, int M, int N, const double* Win,
+                          int sym, double* fx, double* gA, double* gB) {
+  // sym: both operands var -> the prim template autodiffs 0.5 (Cd + Cd^T), so
+  // the adjoint reaching Cd is sym(W) (prim/mat/fun/quad_form_sym.hpp:11-18)
+  std::vector<double> Ws(Win, Win + (size_t)N * N);
+  if (sym)
+    for (int c = 0; c < N; ++c)
+      for (int r = 0; r < N; ++r) Ws[r + (size_t)c * N] = 0.5 * (Win[r + (size_t)c * N] + Win[c + (size_t)r * N]);
+  const double* W = Ws.data();
+  std::vector<double> AB((size_t)M * N, 0.0), Cd((size_t)N * N, 0.0);
+  for (int c = 0; c < N; ++c)
+    for (int k2 = 0; k2 < M; ++k2)
+      for (int i = 0; i < M; ++i) AB[i + (size_t)c * M] += A[i + (size_t)k2 * M] * B[k2 + (size_t)c * M];
+  for (int c = 0; c < N; ++c)
+    for (int r = 0; r < N; ++r) {
+      double s = 0;
+      for (int i = 0; i < M; ++i) s += B[i + (size_t)r * M] * AB[i + (size_t)c * M];
+      Cd[r + (size_t)c * N] = s;
+    }
+  double f = 0;
+  for (int c = 0; c < N; ++c)
+    for (int r = 0; r < N; ++r)
+      f += Win[r + (size_t)c * N] * 0.5 * (Cd[r + (size_t)c * N] + Cd[c + (size_t)r * N]);
+  *fx = f;
+  // Aadj = B W B^T ; Badj = A B W^T + A^T B W  (quad_form.hpp chainA / chainB)
+  std::vector<double> BW((size_t)M * N, 0.0), BWt((size_t)M * N, 0.0);
+  for (int c = 0; c < N; ++c)
+    for (int q = 0; q < N; ++q)
+      for (int i = 0; i < M; ++i) {
+        BW[i + (size_t)c * M] += B[i + (size_t)q * M] * W[q + (size_t)c * N];
+        BWt[i + (size_t)c * M] += B[i + (size_t)q * M] * W[c + (size_t)q * N];
+      }
+  for (int j = 0; j < M; ++j)
+    for (int i = 0; i < M; ++i) {
+      double s = 0;
+      for (int c = 0; c < N; ++c) s += BW[i + (size_t)c * M] * B[j + (size_t)c * M];
+      gA[i + (size_t)j * M] = s;
+    }
+  for (int c = 0; c < N; ++c)
+    for (int i = 0; i < M; ++i) {
+      double s = 0;
+      for (int k2 = 0; k2 < M; ++k2)
+        s += A[i + (size_t)k2 * M] * BWt[k2 + (size_t)c * M] + A[k2 + (size_t)i * M] * BW[k2 + (size_t)c * M];
+      gB[i + (size_t)c * M] = s;
+    }
+}
+
 void oracle_gp_marginal(const double* x, const double* y, int n,
                         const double* theta, double* fx, double* grad) {
   const double alpha = theta[0], rho = theta[1], sigma = theta[2];

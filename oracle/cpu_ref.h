@@ -94,6 +94,22 @@ double oracle_normal_id_glm(const double* y, const double* x, long long R, int M
 double oracle_poisson_log_glm(const int* y, const double* x, long long R, int M,
                               double alpha, const double* beta, double* g);
 
+/* SURVEY.md 8(f) row 3, value of f = sum(W .* F(args)) and the gradients
+ * wrt every argument entry (all col-major).
+ *   mdivide_left_spd       rev/mat/fun/mdivide_left_spd.hpp:57-63 (A n x n, B n x k)
+ *   log_determinant_spd    rev/mat/fun/log_determinant_spd.hpp:16-57 (f = the value)
+ *   mlt_self_transpose     rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44 (L K x J)
+ *   quad_form_sym          rev/mat/fun/quad_form.hpp:17-100 (A M x M, B M x N);
+ *                          sym = 1: both operands var (prim/mat/fun/quad_form_sym.hpp:11-18)
+ * Returns 0, or -1 when the Cholesky factorisation fails. */
+int oracle_mdivide_left_spd(const double* A, const double* B, int n, int k, const double* W,
+                            double* fx, double* gA, double* gB);
+int oracle_log_determinant_spd(const double* A, int n, double* fx, double* gA);
+void oracle_mlt_self_transpose(const double* L, int K, int J, const double* W, double* fx,
+                               double* gL);
+void oracle_quad_form_sym(const double* A, const double* B, int M, int N, const double* W,
+                          int sym, double* fx, double* gA, double* gB);
+
 /* GP marginal gradient (config 3) through the restated functors. */
 void oracle_gp_marginal(const double* x, const double* y, int n,
                         const double* theta, double* fx, double* grad);

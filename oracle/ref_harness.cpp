@@ -31,6 +31,10 @@
  *   bernoulli_logit_glm_lpmf stan/math/prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138
  *   normal_id_glm_lpdf       stan/math/prim/mat/prob/normal_id_glm_lpdf.hpp:40-150
  *   poisson_log_glm_lpmf     stan/math/prim/mat/prob/poisson_log_glm_lpmf.hpp:37-123
+ *   mdivide_left_spd         stan/math/rev/mat/fun/mdivide_left_spd.hpp:232-260
+ *   log_determinant_spd      stan/math/rev/mat/fun/log_determinant_spd.hpp:16-57
+ *   multiply_lower_tri_self_transpose  stan/math/rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44
+ *   quad_form_sym            stan/math/rev/mat/fun/quad_form_sym.hpp:15-27
  *   map_rect                 stan/math/prim/mat/functor/map_rect.hpp:120-177
  *   hessian_times_vector     stan/math/mix/mat/functor/hessian_times_vector.hpp:13-40
  */
@@ -809,6 +813,110 @@ static void fix_glm2() {
   }
 }
 
+// ---- mdivide_left_spd, log_determinant_spd,
+// multiply_lower_tri_self_transpose, quad_form_sym.  Inputs are exact
+// element-wise constructions (tests/gen.py spd_inputs mirrors them bit for
+// bit): S_ij = S_ji = u_ij (i > j), S_ii = n + u_ii (diagonally dominant,
+// so SPD); B, L, W uniform on [-1, 1).  f = sum(W .* F(args)); the gradient
+// runs over every entry of every argument (col-major, args concatenated).
+static MatrixXd spd_exact(int n, uint64_t seed) {
+  std::vector<double> u = unif(seed, (size_t)n * n, -1.0, 1.0);
+  MatrixXd S(n, n);
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      const int a = i > j ? i : j, b = i > j ? j : i;  // lower-triangle source
+      S(i, j) = u[(size_t)b * n + a];
+    }
+  for (int i = 0; i < n; ++i) S(i, i) = n + u[(size_t)i * n + i];
+  return S;
+}
+static MatrixXd unif_mat(int r, int c, uint64_t seed) {
+  std::vector<double> u = unif(seed, (size_t)r * c, -1.0, 1.0);
+  return Eigen::Map<MatrixXd>(u.data(), r, c);
+}
+static Matrix<var, Dynamic, Dynamic> take(const Matrix<var, Dynamic, 1>& th, size_t off, int r, int c) {
+  Matrix<var, Dynamic, Dynamic> m(r, c);
+  for (int i = 0; i < r * c; ++i) m(i) = th((Eigen::Index)(off + i));
+  return m;
+}
+struct spd_functor {
+  int kind, n, k;  // kind 0 mdivide_left_spd(A n x n, B n x k); 1 log_determinant_spd(A);
+                   // 2 multiply_lower_tri_self_transpose(L n x k); 3 quad_form_sym(A, B n x k)
+  MatrixXd W;
+  var operator()(const Matrix<var, Dynamic, 1>& th) const {
+    using stan::math::sum;
+    if (kind == 0) {
+      auto A = take(th, 0, n, n), B = take(th, (size_t)n * n, n, k);
+      Matrix<var, Dynamic, Dynamic> C = stan::math::mdivide_left_spd(A, B);
+      return sum(stan::math::elt_multiply(C, W));
+    }
+    if (kind == 1) return stan::math::log_determinant_spd(take(th, 0, n, n));
+    if (kind == 2) {
+      Matrix<var, Dynamic, Dynamic> C = stan::math::multiply_lower_tri_self_transpose(take(th, 0, n, k));
+      return sum(stan::math::elt_multiply(C, W));
+    }
+    auto A = take(th, 0, n, n), B = take(th, (size_t)n * n, n, k);
+    Matrix<var, Dynamic, Dynamic> C = stan::math::quad_form_sym(A, B);
+    return sum(stan::math::elt_multiply(C, W));
+  }
+};
+static void fix_spd() {
+  struct Case {
+    int kind, n, k;
+  };
+  const char* names[] = {"mdivide_left_spd", "log_determinant_spd", "multiply_lower_tri_self_transpose",
+                         "quad_form_sym"};
+  for (Case c : {Case{0, 5, 3}, Case{0, 40, 7}, Case{0, 130, 17}, Case{1, 5, 0}, Case{1, 40, 0},
+                 Case{1, 130, 0}, Case{2, 5, 5}, Case{2, 40, 25}, Case{2, 25, 40}, Case{2, 130, 130},
+                 Case{3, 5, 3}, Case{3, 40, 12}, Case{3, 130, 60}}) {
+    const uint64_t s0 = SEED + 60 + 10 * c.kind;
+    VectorXd th;
+    int wr = 0, wc = 0;
+    if (c.kind == 0 || c.kind == 3) {
+      MatrixXd A = spd_exact(c.n, s0), B = unif_mat(c.n, c.k, s0 + 1);
+      th.resize((Eigen::Index)c.n * c.n + (Eigen::Index)c.n * c.k);
+      th << Eigen::Map<VectorXd>(A.data(), A.size()), Eigen::Map<VectorXd>(B.data(), B.size());
+      wr = c.kind == 0 ? c.n : c.k;
+      wc = c.k;
+    } else if (c.kind == 1) {
+      MatrixXd A = spd_exact(c.n, s0);
+      th = Eigen::Map<VectorXd>(A.data(), A.size());
+    } else {
+      MatrixXd L = unif_mat(c.n, c.k, s0 + 1);
+      th = Eigen::Map<VectorXd>(L.data(), L.size());
+      wr = wc = c.n;
+    }
+    spd_functor f{c.kind, c.n, c.k, unif_mat(wr, wc, s0 + 2)};
+    double fx;
+    VectorXd g;
+    stan::math::gradient(f, th, fx, g);
+    Json j;
+    j.put_str("what", std::string("gradient of sum(W .* ") + names[c.kind] +
+                          "(...)) (log_determinant_spd: the value itself) wrt every argument entry; "
+                          "inputs: tests/gen.py spd_inputs");
+    j.put_int("kind", c.kind);
+    j.put_int("n", c.n);
+    j.put_int("k", c.k);
+    j.put("fx", fx);
+    j.put("grad_sum", g.sum());
+    j.put("grad_l2", g.norm());
+    if (g.size() <= 4000) {
+      j.put_vec("grad", g);
+    } else {
+      smg_rng r = smg_rng_make(SEED + 223);
+      std::vector<double> idx, val;
+      for (int q = 0; q < 512; ++q) {
+        size_t kk = smg_rng_next(&r) % (size_t)g.size();
+        idx.push_back((double)kk);
+        val.push_back(g((Eigen::Index)kk));
+      }
+      j.put_vec("sample_index", idx);
+      j.put_vec("sample_grad", val);
+    }
+    write_fixture(std::string(names[c.kind]) + "_n" + std::to_string(c.n) + "_k" + std::to_string(c.k), j);
+  }
+}
+
 static void fix_hvp() {
   for (int N : {8, 32, 100, 256}) {
     std::vector<double> x;
@@ -907,6 +1015,7 @@ int main(int argc, char** argv) {
     if (want("mvn")) fix_mvn();
     if (want("glm")) fix_glm();
     if (want("glm2")) fix_glm2();
+    if (want("spd")) fix_spd();
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();
     if (want("gp")) fix_gp();

@@ -102,6 +102,10 @@ def oracle():
             "oracle_normal_id_glm": (dd, [_D, _D, ctypes.c_longlong, ii, dd, _D, dd, _D]),
             "oracle_poisson_log_glm": (dd, [_I, _D, ctypes.c_longlong, ii, dd, _D, _D]),
             "oracle_gp_marginal": (None, [_D, _D, ii, _D, _D, _D]),
+            "oracle_mdivide_left_spd": (ii, [_D, _D, ii, ii, _D, _D, _D, _D]),
+            "oracle_log_determinant_spd": (ii, [_D, ii, _D, _D]),
+            "oracle_mlt_self_transpose": (None, [_D, ii, ii, _D, _D, _D]),
+            "oracle_quad_form_sym": (None, [_D, _D, ii, ii, _D, ii, _D, _D, _D]),
             "oracle_mulchol": (None, [_D, ii, _D, _D]),
         }
         for name, (res, args) in sig.items():
@@ -127,3 +131,41 @@ def glm2_oracle(kind, x, y, th, M):
         lp = oracle().oracle_poisson_log_glm(ptr(np.ascontiguousarray(y, dtype=np.int32)), ptr(xf), R, M, th[0],
                                              ptr(f64(th[1:])), ptr(g))
     return lp, g
+
+
+def spd_oracle(kind, args, n, k, sym=1):
+    """(f, gradient over every argument entry, col-major, concatenated) of the
+    restated SURVEY 8(f) row-3 functor `kind` (gen.spd_inputs order)."""
+    fx = np.zeros(1)
+    F = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64).ravel(order="F"))  # noqa: E731
+    if kind == 0:
+        A, B, W = args
+        gA, gB = np.zeros(n * n), np.zeros(n * k)
+        assert oracle().oracle_mdivide_left_spd(ptr(F(A)), ptr(F(B)), n, k, ptr(F(W)), ptr(fx), ptr(gA), ptr(gB)) == 0
+        return fx[0], np.concatenate([gA, gB])
+    if kind == 1:
+        (A,) = args
+        gA = np.zeros(n * n)
+        assert oracle().oracle_log_determinant_spd(ptr(F(A)), n, ptr(fx), ptr(gA)) == 0
+        return fx[0], gA
+    if kind == 2:
+        L, W = args
+        gL = np.zeros(n * k)
+        oracle().oracle_mlt_self_transpose(ptr(F(L)), n, k, ptr(F(W)), ptr(fx), ptr(gL))
+        return fx[0], gL
+    A, B, W = args
+    gA, gB = np.zeros(n * n), np.zeros(n * k)
+    oracle().oracle_quad_form_sym(ptr(F(A)), ptr(F(B)), n, k, ptr(F(W)), sym, ptr(fx), ptr(gA), ptr(gB))
+    return fx[0], np.concatenate([gA, gB])
+
+
+def check_against_fixture(d, fx, g, rtol, what=""):
+    """fx and the gradient (full, or its sum / L2 / sampled entries)."""
+    near_rel(fx, d["fx"], 1e-12, what=what + " fx")
+    if "grad" in d:
+        near_rel(g, d["grad"], rtol, what=what + " grad")
+    else:
+        idx = np.array(d["sample_index"], dtype=np.int64)
+        near_rel(g[idx], d["sample_grad"], rtol, what=what + " sampled grad")
+    near_rel(np.sum(g), d["grad_sum"], 1e-9, atol=1e-9 * np.abs(g).sum(), what=what + " grad sum")
+    near_rel(np.linalg.norm(g), d["grad_l2"], 1e-11, what=what + " grad l2")

@@ -20,6 +20,9 @@
 //   errors                        the reference's exceptions
 //   hvp N theta v x y             hessian_times_vector of the GP marginal (config 5)
 //   map_rect_glm R M shards beta  map_rect over GLM row blocks (vs the reference's map_rect32)
+//   spd kind n k args... W        mdivide_left_spd / log_determinant_spd /
+//                                 multiply_lower_tri_self_transpose / quad_form_sym through the
+//                                 Eigen signatures; f = sum(W .* F(args)), gradient over all entries
 //   glm2 kind R M y theta         normal_id_glm_lpdf (kind 0) / poisson_log_glm_lpmf (kind 1):
 //                                 device x, single call, 7 row shards, propto
 #include <stan/math.hpp>
@@ -379,6 +382,38 @@ static void cmd_glm() {
   print("grad_shards32", g);
 }
 
+static void cmd_spd() {
+  int kind, n, k;
+  std::cin >> kind >> n >> k;
+  size_t na = kind == 2 ? size_t(n) * k : size_t(n) * n;
+  size_t nb = (kind == 0 || kind == 3) ? size_t(n) * k : 0;
+  auto th = read_vec(na + nb);
+  const int wr = kind == 0 ? n : (kind == 3 ? k : n), wc = kind == 0 ? k : (kind == 3 ? k : n);
+  std::vector<double> W = kind == 1 ? std::vector<double>() : read_vec(size_t(wr) * wc);
+  auto take = [](const std::vector<var>& t, size_t off, int r, int c) {
+    matrix_v m(r, c);
+    for (int i = 0; i < r * c; ++i) m(i) = t[off + size_t(i)];
+    return m;
+  };
+  auto wsum = [&](const matrix_v& C) {
+    var s = 0.0;
+    for (int i = 0; i < C.size(); ++i) s += W[size_t(i)] * C(i);
+    return s;
+  };
+  double fx;
+  std::vector<double> g;
+  gradient(
+      [&](const std::vector<var>& t) -> var {
+        if (kind == 0) return wsum(mdivide_left_spd(take(t, 0, n, n), take(t, na, n, k)));
+        if (kind == 1) return log_determinant_spd(take(t, 0, n, n));
+        if (kind == 2) return wsum(multiply_lower_tri_self_transpose(take(t, 0, n, k)));
+        return wsum(quad_form_sym(take(t, 0, n, n), take(t, na, n, k)));
+      },
+      th, fx, g);
+  print1("fx", fx);
+  print("grad", g);
+}
+
 static void cmd_glm2() {
   int kind, M;
   long long R;
@@ -658,6 +693,32 @@ static void cmd_errors() {
     poisson_log_glm_lpmf(std::vector<int>{0, 3}, std::vector<double>{1, 2}, 1, var(0.0),
                          std::vector<var>{var(INFINITY)});
   });
+  expect_throw("spd_mdivide_sizes", [&] {
+    mdivide_left_spd(matrix_v(matrix_d::Identity(3, 3).cast<var>()), matrix_v(matrix_d::Ones(2, 1).cast<var>()));
+  });
+  expect_throw("spd_mdivide_not_pd", [&] {
+    matrix_d A = matrix_d::Identity(3, 3);
+    A(1, 1) = -1.0;
+    mdivide_left_spd(matrix_v(A.cast<var>()), matrix_v(matrix_d::Ones(3, 1).cast<var>()));
+  });
+  expect_throw("spd_logdet_not_symmetric", [&] {
+    matrix_d A = matrix_d::Identity(3, 3);
+    A(2, 0) = 0.5;
+    log_determinant_spd(matrix_v(A.cast<var>()));
+  });
+  expect_throw("spd_logdet_negative", [&] {
+    matrix_d A = matrix_d::Identity(3, 3);
+    A(1, 1) = -1.0;
+    log_determinant_spd(matrix_v(A.cast<var>()));
+  });
+  expect_throw("spd_quad_form_sizes", [&] {
+    quad_form_sym(matrix_v(matrix_d::Identity(3, 3).cast<var>()), matrix_v(matrix_d::Ones(2, 2).cast<var>()));
+  });
+  expect_throw("spd_quad_form_not_symmetric", [&] {
+    matrix_d A = matrix_d::Identity(3, 3);
+    A(2, 0) = 0.5;
+    quad_form_sym(matrix_v(A.cast<var>()), matrix_v(matrix_d::Ones(3, 2).cast<var>()));
+  });
   expect_throw("glm_y_bounds", [&] {
     bernoulli_logit_glm_lpmf(std::vector<int>{0, 2}, std::vector<double>{1, 2}, 1, var(0.0),
                              std::vector<var>{1.0});
@@ -699,6 +760,7 @@ int main() {
     else if (cmd == "glm") cmd_glm();
     else if (cmd == "glm_data") cmd_glm_data();
     else if (cmd == "glm2") cmd_glm2();
+    else if (cmd == "spd") cmd_spd();
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
     else if (cmd == "hvp") cmd_hvp();

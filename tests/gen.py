@@ -58,3 +58,30 @@ def glm2_inputs(R: int, M: int, kind: str):
         y = np.floor(unif(SEED + 52, R, 0.0, 6.0)).astype(np.int32)
         theta = np.concatenate([[th[0]], 0.5 * th[1:]])
     return x, y, theta
+
+
+def spd_exact(n: int, seed: int) -> np.ndarray:
+    """ref_harness.cpp spd_exact: S_ij = S_ji = u (lower source), S_ii = n + u_ii."""
+    u = unif(seed, n * n, -1.0, 1.0).reshape(n, n).T  # u[i, j] = element i + j n (col-major)
+    low = np.tril(u)
+    S = low + np.tril(u, -1).T
+    S[np.diag_indices(n)] = n + np.diag(u)
+    return S
+
+
+def unif_mat(r: int, c: int, seed: int) -> np.ndarray:
+    return unif(seed, r * c, -1.0, 1.0).reshape(c, r).T.copy()
+
+
+def spd_inputs(kind: int, n: int, k: int):
+    """ref_harness.cpp fix_spd inputs: (args..., W) for kind 0 mdivide_left_spd,
+    1 log_determinant_spd, 2 multiply_lower_tri_self_transpose, 3 quad_form_sym."""
+    s0 = SEED + 60 + 10 * kind
+    if kind in (0, 3):
+        A, B = spd_exact(n, s0), unif_mat(n, k, s0 + 1)
+        W = unif_mat(n if kind == 0 else k, k, s0 + 2)
+        return A, B, W
+    if kind == 1:
+        return (spd_exact(n, s0),)
+    L = unif_mat(n, k, s0 + 1)
+    return L, unif_mat(n, n, s0 + 2)

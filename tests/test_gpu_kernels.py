@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import gen
-from _util import GOLDEN, f64, glm2_oracle, golden, near_rel, oracle, ptr
+from _util import GOLDEN, check_against_fixture, f64, glm2_oracle, golden, near_rel, oracle, ptr, spd_oracle
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-10
@@ -241,7 +241,7 @@ def test_mdivide_large_vs_oracle(ctx):
 
 
 # ------------------------------------------------------------- multiply
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "multiply_*.json"))))
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "multiply_[0-9]*.json"))))
 def test_multiply_golden(ctx, path):
     d = golden(os.path.basename(path)[:-5])
     m, k, n, kind = (int(d[s]) for s in ("m", "k", "n", "kind"))
@@ -416,6 +416,86 @@ def test_glm2_vs_oracle_ragged(ctx, kind):
     lpo, go = glm2_oracle(kind, x, y, th, M)
     near_rel(lp, lpo, 1e-12, what="fx")
     near_rel(g, go, RTOL, what="grad")
+
+
+# ------------------------------------------ SURVEY 8(f) row 3 (spd.hip)
+def _spd_device(ctx, kind, args, n, k, sym=1):
+    """f = sum(W .* F(args)) and the gradient over every argument entry through
+    the C-ABI (forward, then the reverse with Cadj = W)."""
+    if kind == 0:
+        A, B, W = args
+        dA, dB, dW = ctx.put(F(A)), ctx.put(F(B)), ctx.put(F(W))
+        L, aux, C = ctx.zeros(n * n), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(n)), ctx.zeros(n * k)
+        ctx.call("smg_mdivide_left_spd_fwd", dA, n, dB, n, n, k, L, aux, C, n)
+        gA, gB, ws = ctx.zeros(n * n), ctx.zeros(n * k), ctx.zeros(n * k)
+        ctx.call("smg_mdivide_left_spd_rev", L, aux, n, k, C, n, dW, n, gA, n, gB, n, ws)
+        f = float(np.sum(F(W) * ctx.get(C, n * k)))
+        return f, np.concatenate([ctx.get(gA, n * n), ctx.get(gB, n * k)])
+    if kind == 1:
+        (A,) = args
+        L, aux, out = ctx.zeros(n * n), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(n)), ctx.zeros(1)
+        ctx.call("smg_log_determinant_spd_fwd", ctx.put(F(A)), n, n, L, aux, out)
+        gA, ws = ctx.zeros(n * n), ctx.zeros(n * n)
+        ctx.call("smg_log_determinant_spd_rev", L, aux, n, 1.0, gA, n, ws)
+        return ctx.get(out, 1)[0], ctx.get(gA, n * n)
+    if kind == 2:
+        Lm, W = args
+        dL, C, ws = ctx.put(F(Lm)), ctx.zeros(n * n), ctx.zeros(2 * n * k + n * n)
+        ctx.call("smg_multiply_lower_tri_self_transpose_fwd", dL, n, n, k, C, n, ws)
+        gL = ctx.zeros(n * k)
+        ctx.call("smg_multiply_lower_tri_self_transpose_rev", dL, n, n, k, ctx.put(F(W)), n, gL, n, ws)
+        return float(np.sum(F(W) * ctx.get(C, n * n))), ctx.get(gL, n * k)
+    A, B, W = args
+    dA, dB, C, ws = ctx.put(F(A)), ctx.put(F(B)), ctx.zeros(k * k), ctx.zeros(n * k + k * k)
+    ctx.call("smg_quad_form_sym_fwd", dA, n, dB, n, n, k, C, k, ws)
+    gA, gB = ctx.zeros(n * n), ctx.zeros(n * k)
+    ctx.call("smg_quad_form_sym_rev", dA, n, dB, n, n, k, ctx.put(F(W)), k, sym, gA, n, gB, n, ws)
+    return float(np.sum(F(W) * ctx.get(C, k * k))), np.concatenate([ctx.get(gA, n * n), ctx.get(gB, n * k)])
+
+
+SPD_CASES = sorted(os.path.basename(p)[:-5] for pat in ("mdivide_left_spd_*", "log_determinant_spd_*",
+                                                         "multiply_lower_tri_self_transpose_*", "quad_form_sym_*")
+                   for p in glob.glob(os.path.join(GOLDEN, pat + ".json")))
+
+
+@pytest.mark.parametrize("name", SPD_CASES)
+def test_spd_golden(ctx, name):
+    d = golden(name)
+    kind, n, k = int(d["kind"]), int(d["n"]), int(d["k"])
+    fx, g = _spd_device(ctx, kind, gen.spd_inputs(kind, n, k), n, k)
+    assert ctx.status() == 0
+    check_against_fixture(d, fx, g, RTOL, what=name)
+
+
+@pytest.mark.parametrize("kind,n,k", [(0, 700, 33), (1, 600, 0), (2, 300, 200), (2, 200, 300),
+                                      (3, 300, 150)])
+def test_spd_vs_oracle_large(ctx, kind, n, k):
+    """Beyond the fixtures (two-level Cholesky, multi-block TRSMs, ragged tiles)
+    against the reference-pinned restatement."""
+    args = gen.spd_inputs(kind, n, k)
+    fx, g = _spd_device(ctx, kind, args, n, k)
+    fo, go = spd_oracle(kind, args, n, k)
+    near_rel(fx, fo, 1e-11, what="fx")
+    near_rel(g, go, RTOL, atol=RTOL * np.abs(go).max(), what="grad")
+
+
+def test_quad_form_sym_mixed_operands(ctx):
+    """A data, B var: the rev vari's unsymmetrised adjoint (sym_adj = 0)."""
+    n, k = 40, 12
+    args = gen.spd_inputs(3, n, k)
+    fx, g = _spd_device(ctx, 3, args, n, k, sym=0)
+    fo, go = spd_oracle(3, args, n, k, sym=0)
+    near_rel(fx, fo, 1e-12, what="fx")
+    near_rel(g, go, RTOL, what="grad")
+
+
+def test_spd_not_pd(ctx):
+    n = 80
+    A = np.eye(n)
+    A[50, 50] = -2.0
+    L, aux, out = ctx.zeros(n * n), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(n)), ctx.zeros(1)
+    ctx.call("smg_log_determinant_spd_fwd", ctx.put(F(A)), n, n, L, aux, out)
+    assert ctx.status() & 2
 
 
 def test_glm_extreme(ctx):
