@@ -2,7 +2,8 @@
 #define STAN_MATH_MIX_HESSIAN_TIMES_VECTOR_HPP
 
 // gradient_dot_vector (mix/mat/functor/gradient_dot_vector.hpp:12-25) and
-// hessian_times_vector (mix/mat/functor/hessian_times_vector.hpp:13-40):
+// hessian_times_vector (mix/mat/functor/hessian_times_vector.hpp:13-40) and
+// hessian (mix/mat/functor/hessian.hpp:39-72):
 // fwd-over-rev.  x becomes vars, each seeded as fvar<var>(x_i, v_i); f runs at
 // fvar<var>; grad() of the tangent (= grad f . v, a var) leaves H v in the
 // adjoints of x.  Nested tape, recovered also when f throws.
@@ -70,6 +71,55 @@ void hessian_times_vector(const F& f, const Eigen::Matrix<double, Eigen::Dynamic
     throw;
   }
   recover_memory_nested();
+}
+
+/**
+ * hessian(f, x, fx, grad, H) (mix/mat/functor/hessian.hpp:39-72): one
+ * fwd-over-rev sweep per coordinate i -- x_j seeded as fvar<var>(x_j, i == j),
+ * grad(i) = the tangent's value, H(i, :) = the adjoints of x after grad() of
+ * the tangent; each sweep on its own nested tape (recovered also on throw).
+ * With device functors underneath, every sweep is one forward + one reverse
+ * of the tangent network on the GPU.
+ */
+template <typename F>
+void hessian(const F& f, const Eigen::Matrix<double, Eigen::Dynamic, 1>& x, double& fx,
+             Eigen::Matrix<double, Eigen::Dynamic, 1>& grad_out,
+             Eigen::Matrix<double, Eigen::Dynamic, Eigen::Dynamic>& H) {
+  const Eigen::Index n = x.size();
+  H.resize(n, n);
+  grad_out.resize(n);
+  if (n == 0) {  // (:45-48): the value at the empty input (evaluated at fvar<var>,
+                 // so functors need not instantiate at double)
+    start_nested();
+    try {
+      fx = f(Eigen::Matrix<fvar<var>, Eigen::Dynamic, 1>(0)).val_.val();
+    } catch (const std::exception&) {
+      recover_memory_nested();
+      throw;
+    }
+    recover_memory_nested();
+    return;
+  }
+  for (Eigen::Index i = 0; i < n; ++i) {
+    start_nested();
+    try {
+      Eigen::Matrix<var, Eigen::Dynamic, 1> x_var(n);
+      Eigen::Matrix<fvar<var>, Eigen::Dynamic, 1> x_fvar(n);
+      for (Eigen::Index j = 0; j < n; ++j) {
+        x_var(j) = x(j);
+        x_fvar(j) = fvar<var>(x_var(j), var(i == j ? 1.0 : 0.0));
+      }
+      fvar<var> fx_fvar = f(x_fvar);
+      grad_out(i) = fx_fvar.d_.val();
+      if (i == 0) fx = fx_fvar.val_.val();
+      grad(fx_fvar.d_.vi_);
+      for (Eigen::Index j = 0; j < n; ++j) H(i, j) = x_var(j).adj();
+    } catch (const std::exception&) {
+      recover_memory_nested();
+      throw;
+    }
+    recover_memory_nested();
+  }
 }
 #endif
 

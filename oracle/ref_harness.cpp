@@ -37,6 +37,7 @@
  *   quad_form_sym            stan/math/rev/mat/fun/quad_form_sym.hpp:15-27
  *   map_rect                 stan/math/prim/mat/functor/map_rect.hpp:120-177
  *   hessian_times_vector     stan/math/mix/mat/functor/hessian_times_vector.hpp:13-40
+ *   hessian                  stan/math/mix/mat/functor/hessian.hpp:39-72
  */
 #define STAN_MATH_REV_CORE_INIT_CHAINABLESTACK_HPP
 #include <stan/math/mix/mat.hpp>
@@ -917,6 +918,29 @@ static void fix_spd() {
   }
 }
 
+static void fix_hessian() {  // mix/mat/functor/hessian.hpp on the GP marginal
+  for (int N : {8, 32, 100}) {
+    std::vector<double> x;
+    VectorXd y;
+    gp_inputs(N, x, y);
+    VectorXd th(3), g;
+    th << 1.0, 1.5, 0.3;
+    double fx;
+    MatrixXd H;
+    stan::math::hessian(gp_functor{x, y}, th, fx, g, H);
+    Json j;
+    j.put_str("what", "hessian (fwd-over-rev, mix/mat/functor/hessian.hpp) of the GP marginal log density");
+    j.put_int("N", N);
+    j.put_vec("theta", th);
+    j.put_vec("x", x);
+    j.put_vec("y", y);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    j.put_mat("H", H);
+    write_fixture("hessian_gp_N" + std::to_string(N), j);
+  }
+}
+
 static void fix_hvp() {
   for (int N : {8, 32, 100, 256}) {
     std::vector<double> x;
@@ -1016,6 +1040,7 @@ int main(int argc, char** argv) {
     if (want("glm")) fix_glm();
     if (want("glm2")) fix_glm2();
     if (want("spd")) fix_spd();
+    if (want("hessian")) fix_hessian();
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();
     if (want("gp")) fix_gp();

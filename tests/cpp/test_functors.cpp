@@ -19,6 +19,7 @@
 //   mvn N y mu L                  multi_normal_cholesky_lpdf, every argument var (Eigen)
 //   errors                        the reference's exceptions
 //   hvp N theta v x y             hessian_times_vector of the GP marginal (config 5)
+//   hessian N theta x y           hessian() of the GP marginal (3 fwd-over-rev sweeps)
 //   map_rect_glm R M shards beta  map_rect over GLM row blocks (vs the reference's map_rect32)
 //   spd kind n k args... W        mdivide_left_spd / log_determinant_spd /
 //                                 multiply_lower_tri_self_transpose / quad_form_sym through the
@@ -634,6 +635,21 @@ static void cmd_hvp() {
               ChainableStack::instance_->dev_adj_stack_.size());
 }
 
+static void cmd_hessian() {
+  int N;
+  std::cin >> N;
+  auto th = read_vec(3), x = read_vec(N), y = read_vec(N);
+  Eigen::VectorXd te = Eigen::Map<Eigen::VectorXd>(th.data(), 3), g;
+  Eigen::MatrixXd H;
+  double fx;
+  hessian(gp_functor{x, y}, te, fx, g, H);
+  print1("fx", fx);
+  print("grad", std::vector<double>(g.data(), g.data() + 3));
+  print("H", std::vector<double>(H.data(), H.data() + 9));
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
 template <typename F>
 static void expect_throw(const char* name, F&& f) {
   start_nested();
@@ -764,6 +780,7 @@ int main() {
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
     else if (cmd == "hvp") cmd_hvp();
+    else if (cmd == "hessian") cmd_hessian();
     else if (cmd == "map_rect_glm") cmd_map_rect_glm();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
