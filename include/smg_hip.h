@@ -306,6 +306,19 @@ int smg_poisson_log_glm(smg_ctx* ctx, const int* y, const double* x,
                         long long R, int M, long long ldx,
                         const double* alpha_beta, double* ws, double* out);
 
+/* categorical_logit_glm_lpmf<false>(y | x, alpha, beta)
+ * (prim/mat/prob/categorical_logit_glm_lpmf.hpp:38-146): x R x M
+ * (column-major, ld ldx), alpha_beta = [alpha(C), beta(M x C column-major)],
+ * y in 1..C (checked by the caller), ONE fused pass over x:
+ *   out[0] = logp, out[1..C] = alpha', out[C+1 ..] = beta' (M x C).
+ * M <= 256 and C <= 16: one fused pass; otherwise lin = x beta by GEMM, a
+ * row softmax pass, alpha' / beta' by GEMM (R, M C < 2^31).
+ * ws: >= smg_glm_categorical_ws_doubles(R, M, C). */
+long long smg_glm_categorical_ws_doubles(long long R, int M, int C);
+int smg_categorical_logit_glm(smg_ctx* ctx, const int* y, const double* x,
+                              long long R, int M, long long ldx, int C,
+                              const double* alpha_beta, double* ws, double* out);
+
 /* generic helpers used by the host layer's reverse sweep */
 /* y[i*incy] += alpha * x[i*incx] with alpha read from host */
 int smg_axpy(smg_ctx* ctx, long long n, double alpha, const double* x, int incx,

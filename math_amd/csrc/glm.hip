@@ -38,6 +38,10 @@ namespace {
 
 constexpr int MMAX = 256;         // fused path: M <= 256
 
+// zero page (global address space) for out-of-range loads: the address is
+// redirected, no select on the loaded value
+__device__ double g_glm_zero[2] = {0.0, 0.0};
+
 template <int RB, int KIND>
 __global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
                                                    const double* __restrict__ x, long long R,
@@ -168,6 +172,121 @@ int glm_blocks(long long R) {
   return (int)nb;
 }
 
+// ------------------------------------------------ categorical_logit_glm_lpmf
+// prim/mat/prob/categorical_logit_glm_lpmf.hpp:38-146 (x an N x M matrix,
+// alpha C, beta M x C, y in 1..C), ONE pass over x in 16-row tiles:
+//   lin = x beta + alpha;  logp = sum_i lin(i, y_i - 1) - max_i - log sum exp(lin_i - max_i)
+//   theta'(i, c) = [c == y_i - 1] - softmax(lin_i)_c
+//   alpha' = sum_i theta'(i, :),  beta' = x^T theta'
+// (the reference's neg_softmax_lin plus the one-hot terms, :117-143).
+// Per-workgroup partial [logp, alpha'(C), beta'(M x C col-major)], reduced in
+// fixed order.  M <= 256, C <= CAT_CMAX.
+constexpr int CAT_RB = 16;
+constexpr int CAT_CMAX = 16;
+
+__global__ __launch_bounds__(256) void k_glm_categorical(const int* __restrict__ y,
+                                                         const double* __restrict__ x, long long R,
+                                                         int M, long long ldx, int C,
+                                                         const double* __restrict__ ab,
+                                                         double* __restrict__ part) {
+  constexpr int RB = CAT_RB, XS = RB + 1;
+  constexpr int PER = RB * MMAX / 256;
+  __shared__ double X[MMAX * XS];
+  __shared__ double beta[MMAX * CAT_CMAX];  // beta[m * CAT_CMAX + c]
+  __shared__ double alpha[CAT_CMAX];
+  __shared__ double lin[RB * CAT_CMAX];     // then theta'
+  __shared__ double lds[16];
+  const int t = threadIdx.x;
+  for (int e = t; e < M * C; e += 256) beta[(e % M) * CAT_CMAX + e / M] = ab[C + e];  // ab = [alpha(C), beta(M x C)]
+  if (t < C) alpha[t] = ab[t];
+  const long long ntiles = (R + RB - 1) / RB;
+  double gacc[CAT_CMAX];  // column t of beta': one accumulator per class
+#pragma unroll
+  for (int c = 0; c < CAT_CMAX; ++c) gacc[c] = 0.0;
+  double lp_acc = 0.0, ga_acc = 0.0;  // rows' logp (t < RB) / class t's alpha' (t < C)
+  double reg[PER];
+  auto load = [&](long long tile) {
+    const long long r0 = tile * RB;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      const int r = e % RB, c = e / RB;
+      const long long gr = r0 + r;
+      reg[q] = *((c < M && gr < R) ? x + gr + (size_t)c * ldx : g_glm_zero);
+    }
+  };
+  long long tile = blockIdx.x;
+  if (tile < ntiles) load(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // previous tile fully consumed
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      X[(e / RB) * XS + (e % RB)] = reg[q];
+    }
+    __syncthreads();
+    const long long next = tile + gridDim.x;
+    if (next < ntiles) load(next);  // in flight during the compute below
+    if (t < RB * C) {  // lin(r, c)
+      const int r = t % RB, c = t / RB;
+      double s = 0.0;
+      for (int m = 0; m < M; ++m) s += X[m * XS + r] * beta[m * CAT_CMAX + c];
+      lin[r * CAT_CMAX + c] = s + alpha[c];
+    }
+    __syncthreads();
+    if (t < RB) {  // the row's softmax, logp and theta'
+      const long long gr = tile * RB + t;
+      if (gr < R) {
+        double mx = lin[t * CAT_CMAX];
+        for (int c = 1; c < C; ++c) mx = fmax(mx, lin[t * CAT_CMAX + c]);
+        double se = 0.0;
+        for (int c = 0; c < C; ++c) se += exp(lin[t * CAT_CMAX + c] - mx);
+        const double inv = 1.0 / se;
+        const int yc = y[gr] - 1;
+        lp_acc += log(inv) - mx + lin[t * CAT_CMAX + yc];
+        for (int c = 0; c < C; ++c)
+          lin[t * CAT_CMAX + c] = (c == yc ? 1.0 : 0.0) - exp(lin[t * CAT_CMAX + c] - mx) * inv;
+      } else {
+        for (int c = 0; c < C; ++c) lin[t * CAT_CMAX + c] = 0.0;
+      }
+    }
+    __syncthreads();
+    if (t < C) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) s += lin[r * CAT_CMAX + t];
+      ga_acc += s;
+    }
+    if (t < M) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const double xv = X[t * XS + r];
+#pragma unroll
+        for (int c = 0; c < CAT_CMAX; ++c)
+          if (c < C) gacc[c] += xv * lin[r * CAT_CMAX + c];
+      }
+    }
+  }
+  const int W = 1 + C + M * C;
+  double* p = part + (size_t)blockIdx.x * W;
+  __syncthreads();
+  const double lp = block_sum(lp_acc, lds);
+  if (t == 0) p[0] = lp;
+  if (t < C) p[1 + t] = ga_acc;
+  if (t < M)
+#pragma unroll
+    for (int c = 0; c < CAT_CMAX; ++c)
+      if (c < C) p[1 + C + (size_t)c * M + t] = gacc[c];
+}
+
+int glm_cat_blocks(long long R) {
+  const long long ntiles = (R + CAT_RB - 1) / CAT_RB;
+  long long nb = 512;
+  if (nb > ntiles) nb = ntiles;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
 // ------------------------------------------------ generic path (M > 256)
 __global__ void k_glm_rows(const int* __restrict__ y, const double* __restrict__ eta, long long R,
                            double alpha, double* __restrict__ th, double* part) {
@@ -190,6 +309,37 @@ __global__ void k_glm_rows(const int* __restrict__ y, const double* __restrict__
     part[2 * blockIdx.x] = lp;
     part[2 * blockIdx.x + 1] = ga;
   }
+}
+
+// categorical generic path (M > 256 or C > 16): lin = x beta by GEMM, then one
+// thread per row turns lin(i, :) (column-major, ld R) into theta'(i, :) in
+// place and accumulates the row's logp; alpha' and beta' by GEMM.
+__global__ void k_glm_cat_rows(const int* __restrict__ y, double* __restrict__ lin, long long R, int C,
+                               const double* __restrict__ alpha, double* __restrict__ ones,
+                               double* __restrict__ part) {
+  __shared__ double lds[16];
+  double lp = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < R;
+       i += (long long)gridDim.x * blockDim.x) {
+    double mx = -INFINITY;
+    for (int c = 0; c < C; ++c) {
+      const double v = lin[i + (size_t)c * R] + alpha[c];
+      lin[i + (size_t)c * R] = v;
+      mx = fmax(mx, v);
+    }
+    double se = 0.0;
+    for (int c = 0; c < C; ++c) se += exp(lin[i + (size_t)c * R] - mx);
+    const double inv = 1.0 / se;
+    const int yc = y[i] - 1;
+    lp += log(inv) - mx + lin[i + (size_t)yc * R];
+    for (int c = 0; c < C; ++c) {
+      const double v = lin[i + (size_t)c * R];
+      lin[i + (size_t)c * R] = (c == yc ? 1.0 : 0.0) - exp(v - mx) * inv;
+    }
+    ones[i] = 1.0;
+  }
+  lp = block_sum(lp, lds);
+  if (threadIdx.x == 0) part[blockIdx.x] = lp;
 }
 
 }  // namespace
@@ -228,6 +378,43 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x, long lo
   hipLaunchKernelGGL(k_glm_rows, dim3(1024), dim3(256), 0, ctx->stream, y, eta, R, alpha_h, th, part);
   smg_reduce_partials(ctx, part, 1024, 2, out, 0);
   rc = smg_gemm_impl(ctx, 1, 0, 0, M, 1, (int)R, 1.0, x, (int)ldx, th, (int)R, 0.0, out + 2, M);
+  SMG_LAUNCH_CHECK();
+  return rc;
+}
+
+long long smg_glm_categorical_ws_doubles(long long R, int M, int C) {
+  if (M <= MMAX && C <= CAT_CMAX) return (long long)glm_cat_blocks(R) * (1 + C + (long long)M * C);
+  return R * ((long long)C + 1) + 1024;
+}
+
+int smg_categorical_logit_glm(smg_ctx* ctx, const int* y, const double* x, long long R, int M,
+                              long long ldx, int C, const double* alpha_beta, double* ws,
+                              double* out) {
+  if (!ctx || R < 0 || M < 0 || C < 1 || !alpha_beta || !ws || !out) return SMG_ERR_ARG;
+  if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GLM);
+  if (M <= MMAX && C <= CAT_CMAX) {
+    const int nb = glm_cat_blocks(R);
+    hipLaunchKernelGGL(k_glm_categorical, dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx, C,
+                       alpha_beta, ws);
+    smg_reduce_partials(ctx, ws, nb, 1 + C + M * C, out, 0);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
+  if (R > INT_MAX || (long long)M * C > INT_MAX) return SMG_ERR_ARG;  // GEMM dimensions
+  if (R == 0) return smg_memset(ctx, out, 0, sizeof(double) * (1 + C + (size_t)M * C));
+  double* lin = ws;                         // R x C
+  double* ones = ws + R * (long long)C;     // R
+  double* part = ones + R;                  // 1024
+  int rc = smg_gemm_impl(ctx, 0, 0, 0, (int)R, C, M, 1.0, x, (int)ldx, alpha_beta + C, M > 0 ? M : 1,
+                         0.0, lin, (int)R);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_glm_cat_rows, dim3(1024), dim3(256), 0, ctx->stream, y, lin, R, C, alpha_beta,
+                     ones, part);
+  smg_reduce_partials(ctx, part, 1024, 1, out, 0);
+  rc = smg_gemm_impl(ctx, 1, 0, 0, C, 1, (int)R, 1.0, lin, (int)R, ones, (int)R, 0.0, out + 1, C);
+  if (rc) return rc;
+  if (M > 0) rc = smg_gemm_impl(ctx, 1, 0, 0, M, C, (int)R, 1.0, x, (int)ldx, lin, (int)R, 0.0, out + 1 + C, M);
   SMG_LAUNCH_CHECK();
   return rc;
 }

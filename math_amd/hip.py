@@ -73,6 +73,8 @@ _SIGS = {
     "smg_bernoulli_logit_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_normal_id_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_poisson_log_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
+    "smg_glm_categorical_ws_doubles": (_L, [_L, _I, _I]),
+    "smg_categorical_logit_glm": (_I, [_P, _P, _P, _L, _I, _L, _I, _P, _P, _P]),
     "smg_mdivide_left_spd_fwd": (_I, [_P, _P, _I, _P, _I, _I, _I, _P, _P, _P, _I]),
     "smg_mdivide_left_spd_rev": (_I, [_P, _P, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P]),
     "smg_log_determinant_spd_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P]),

@@ -22,6 +22,7 @@
 #include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
 #include <stan/math/rev/fun/normal_id_glm_lpdf.hpp>
 #include <stan/math/rev/fun/poisson_log_glm_lpmf.hpp>
+#include <stan/math/rev/fun/categorical_logit_glm_lpmf.hpp>
 #include <stan/math/rev/fun/spd_functors.hpp>
 #include <stan/math/rev/functor/gradient.hpp>
 #include <stan/math/eigen/interop.hpp>

@@ -25,6 +25,7 @@
 #include <stan/math/rev/fun/cholesky_decompose.hpp>
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
 #include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
+#include <stan/math/rev/fun/categorical_logit_glm_lpmf.hpp>
 #include <stan/math/rev/fun/spd_functors.hpp>
 #include <stan/math/rev/fun/lgamma.hpp>
 #include <stan/math/rev/fun/log_sum_exp.hpp>
@@ -260,6 +261,53 @@ inline var bernoulli_logit_glm_lpmf(const std::vector<int>& y, const matrix_d& x
         "bernoulli_logit_glm_lpmf: Vector of dependent variables has dimension = " +
         std::to_string(y.size()) + ", expecting dimension = " + std::to_string(x.rows()));
   return bernoulli_logit_glm_lpmf<propto>(y, xv, int(x.cols()), alpha, b);
+}
+
+namespace internal {
+template <int R, int C>
+inline dev_var_matrix glm_cat_operand(const Eigen::Matrix<var, R, C>& m) { return to_dev(m); }
+template <int R, int C>
+inline dev_data<double> glm_cat_operand(const Eigen::Matrix<double, R, C>& m) {
+  const matrix_d d = m;
+  return to_dev_data(d);
+}
+}  // namespace internal
+
+/** categorical_logit_glm_lpmf(y, x, alpha, beta) with Eigen x / alpha / beta
+ * (prim/mat/prob/categorical_logit_glm_lpmf.hpp:38-43); var or double alpha
+ * and beta in any combination. */
+template <bool propto = false, typename T_a, typename T_b>
+inline typename std::conditional<std::is_same<T_a, var>::value || std::is_same<T_b, var>::value, var,
+                                 double>::type
+categorical_logit_glm_lpmf(const std::vector<int>& y, const matrix_d& x,
+                           const Eigen::Matrix<T_a, Eigen::Dynamic, 1>& alpha,
+                           const Eigen::Matrix<T_b, Eigen::Dynamic, Eigen::Dynamic>& beta) {
+  if (y.size() != size_t(x.rows()))
+    internal::glm_size_mismatch("categorical_logit_glm_lpmf", "Vector of dependent variables",
+                                (long long)y.size(), x.rows());
+  return categorical_logit_glm_lpmf<propto>(to_dev_data(y), to_dev_data(x), internal::glm_cat_operand(alpha),
+                                            internal::glm_cat_operand(beta));
+}
+
+/** The reference's scalar-y overload: y broadcast to every row. */
+template <bool propto = false, typename T_a, typename T_b>
+inline auto categorical_logit_glm_lpmf(int y, const matrix_d& x, const Eigen::Matrix<T_a, Eigen::Dynamic, 1>& alpha,
+                                       const Eigen::Matrix<T_b, Eigen::Dynamic, Eigen::Dynamic>& beta) {
+  static const char* fn = "categorical_logit_glm_lpmf";
+  if (alpha.size() != beta.cols())
+    internal::glm_size_mismatch(fn, "Intercept vector", (long long)alpha.size(), beta.cols());
+  if (x.cols() != beta.rows()) {
+    std::ostringstream m;
+    m << fn << ": x.cols() (" << x.cols() << ") and beta.rows() (" << beta.rows() << ") must match in size";
+    throw std::invalid_argument(m.str());
+  }
+  if (y < 1 || y > beta.cols()) {
+    std::ostringstream m;
+    m << fn << ": categorical outcome out of support is " << y << ", but must be in the interval [1, "
+      << beta.cols() << "]";
+    throw std::domain_error(m.str());
+  }
+  return categorical_logit_glm_lpmf<propto>(std::vector<int>(size_t(x.rows()), y), x, alpha, beta);
 }
 
 template <bool propto = false>

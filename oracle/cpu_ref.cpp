@@ -536,6 +536,45 @@ double oracle_poisson_log_glm(const int* y, const double* x, long long R, int M,
   return -lg + s2;
 }
 
+double oracle_categorical_logit_glm(const int* y, const double* x, long long R, int M, int C,
+                                    const double* alpha, const double* beta, double* g) {
+  // categorical_logit_glm_lpmf.hpp:84-183 (x an R x M matrix, beta M x C):
+  // lin = x beta + alpha; logp = sum log(1 / sum exp(lin - max)) - sum max
+  // + sum lin(i, y_i - 1); alpha' = colsum(-softmax) + counts; beta' = x^T (-softmax)
+  // + the one-hot rows of x
+  if (R == 0 || C == 1) {
+    if (g)
+      for (long long e = 0; e < C + (long long)M * C; ++e) g[e] = 0.0;
+    return 0.0;
+  }
+  std::vector<double> lin((size_t)C);
+  double lsum = 0, msum = 0, ysum = 0;
+  if (g)
+    for (long long e = 0; e < C + (long long)M * C; ++e) g[e] = 0.0;
+  for (long long i = 0; i < R; ++i) {
+    for (int c = 0; c < C; ++c) {
+      double s = 0;
+      for (int m = 0; m < M; ++m) s += x[i + (size_t)m * R] * beta[m + (size_t)c * M];
+      lin[c] = s + alpha[c];
+    }
+    double mx = lin[0];
+    for (int c = 1; c < C; ++c) mx = std::max(mx, lin[c]);
+    double se = 0;
+    for (int c = 0; c < C; ++c) se += std::exp(lin[c] - mx);
+    const double inv = 1.0 / se;
+    lsum += std::log(inv);
+    msum += mx;
+    ysum += lin[y[i] - 1];
+    if (g)
+      for (int c = 0; c < C; ++c) {
+        const double d = (c == y[i] - 1 ? 1.0 : 0.0) - std::exp(lin[c] - mx) * inv;
+        g[c] += d;
+        for (int m = 0; m < M; ++m) g[C + m + (size_t)c * M] += x[i + (size_t)m * R] * d;
+      }
+  }
+  return lsum - msum + ysum;
+}
+
 // X (n x k) <- A^{-1} X through L = chol(A): forward then backward substitution
 static void spd_solve(const double* L, int n, double* X, int k) {
   for (int c = 0; c < k; ++c) {

@@ -88,6 +88,13 @@ double oracle_glm(const int* y, const double* x, long long R, int M,
 double oracle_normal_id_glm(const double* y, const double* x, long long R, int M,
                             double alpha, const double* beta, double sigma, double* g);
 
+/* categorical_logit_glm_lpmf<false>(y | x, alpha, beta)
+ * prim/mat/prob/categorical_logit_glm_lpmf.hpp:84-183.  x R x M col-major,
+ * alpha C, beta M x C col-major, y in 1..C.  g (optional): [alpha'(C),
+ * beta'(M x C)]. */
+double oracle_categorical_logit_glm(const int* y, const double* x, long long R, int M, int C,
+                                    const double* alpha, const double* beta, double* g);
+
 /* poisson_log_glm_lpmf<false>(y | x, alpha, beta), scalar alpha.
  * prim/mat/prob/poisson_log_glm_lpmf.hpp:81-123.  Returns logp (lgamma terms
  * included); the gradient wrt (alpha, beta) into g (M + 1). */

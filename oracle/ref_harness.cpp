@@ -31,6 +31,7 @@
  *   bernoulli_logit_glm_lpmf stan/math/prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138
  *   normal_id_glm_lpdf       stan/math/prim/mat/prob/normal_id_glm_lpdf.hpp:40-150
  *   poisson_log_glm_lpmf     stan/math/prim/mat/prob/poisson_log_glm_lpmf.hpp:37-123
+ *   categorical_logit_glm_lpmf stan/math/prim/mat/prob/categorical_logit_glm_lpmf.hpp:38-183
  *   mdivide_left_spd         stan/math/rev/mat/fun/mdivide_left_spd.hpp:232-260
  *   log_determinant_spd      stan/math/rev/mat/fun/log_determinant_spd.hpp:16-57
  *   multiply_lower_tri_self_transpose  stan/math/rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44
@@ -814,6 +815,130 @@ static void fix_glm2() {
   }
 }
 
+// categorical_logit_glm inputs (tests/gen.py glm_cat_inputs): x R x M
+// col-major U[-1,1) sqrt 3, alpha U[-1,1) (C), beta U[-1,1) sqrt(3/M) (M x C
+// col-major), y = floor(U[0, C)) + 1; theta = (alpha, beta).
+struct glm_cat_data {
+  int R, M, C;
+  MatrixXd x;
+  std::vector<int> y;
+  VectorXd theta;
+};
+static glm_cat_data glm_cat_inputs(int R, int M, int C) {
+  glm_cat_data d;
+  d.R = R, d.M = M, d.C = C;
+  std::vector<double> x = unif(SEED + 81, (size_t)R * M, -1.0, 1.0);
+  for (double& v : x) v *= std::sqrt(3.0);
+  d.x = Eigen::Map<MatrixXd>(x.data(), R, M);
+  std::vector<double> a = unif(SEED + 82, C, -1.0, 1.0);
+  std::vector<double> b = unif(SEED + 83, (size_t)M * C, -1.0, 1.0);
+  d.theta.resize(C + (Eigen::Index)M * C);
+  for (int c = 0; c < C; ++c) d.theta(c) = a[c];
+  for (int e = 0; e < M * C; ++e) d.theta(C + e) = b[e] * std::sqrt(3.0 / M);
+  std::vector<double> u = unif(SEED + 84, R, 0.0, (double)C);
+  d.y.resize(R);
+  for (int i = 0; i < R; ++i) d.y[i] = (int)u[i] + 1;
+  return d;
+}
+template <bool propto>
+struct glm_cat_functor {
+  const glm_cat_data& d;
+  int y_scalar;  // > 0: the broadcast-scalar overload
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, 1> alpha = th.head(d.C);
+    Matrix<T, Dynamic, Dynamic> beta(d.M, d.C);
+    for (int e = 0; e < d.M * d.C; ++e) beta(e) = th(d.C + e);
+    if (y_scalar > 0) return stan::math::categorical_logit_glm_lpmf<propto>(y_scalar, d.x, alpha, beta);
+    return stan::math::categorical_logit_glm_lpmf<propto>(d.y, d.x, alpha, beta);
+  }
+};
+static void fix_glm_cat() {
+  struct Case {
+    int R, M, C, ys;
+  };
+  for (Case c : {Case{1000, 8, 5, 0}, Case{20000, 64, 16, 0}, Case{3000, 200, 3, 0}, Case{50, 6, 4, 3}}) {
+    glm_cat_data d = glm_cat_inputs(c.R, c.M, c.C);
+    double fx, fxp;
+    VectorXd g, gp;
+    stan::math::gradient(glm_cat_functor<false>{d, c.ys}, d.theta, fx, g);
+    stan::math::gradient(glm_cat_functor<true>{d, c.ys}, d.theta, fxp, gp);
+    Json j;
+    j.put_str("what", "gradient of categorical_logit_glm_lpmf(y|x,alpha,beta) wrt (alpha, beta col-major); inputs: tests/gen.py glm_cat_inputs");
+    j.put_int("R", c.R);
+    j.put_int("M", c.M);
+    j.put_int("C", c.C);
+    j.put_int("y_scalar", c.ys);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    j.put("fx_propto", fxp);
+    j.put_vec("grad_propto", gp);
+    write_fixture("categorical_logit_glm_R" + std::to_string(c.R) + "_M" + std::to_string(c.M) + "_C" +
+                      std::to_string(c.C) + (c.ys ? "_yscalar" : ""),
+                  j);
+  }
+}
+
+// The reference's exceptions (and early returns) for categorical_logit_glm on
+// small hand-made inputs; tests/cpp/test_functors.cpp "glm_cat_errors" runs
+// the same cases through the layer and the test compares the strings.
+static void fix_glm_cat_errors() {
+  using stan::math::var;
+  using VV = Matrix<var, Dynamic, 1>;
+  using MV = Matrix<var, Dynamic, Dynamic>;
+  Json j;
+  auto run = [&](const char* name, auto&& f) {
+    std::string out;
+    try {
+      const double v = stan::math::value_of(f());
+      std::ostringstream o;
+      o.precision(17);
+      o << "value " << v;
+      out = o.str();
+    } catch (const std::domain_error& e) {
+      out = std::string("domain_error ") + e.what();
+    } catch (const std::invalid_argument& e) {
+      out = std::string("invalid_argument ") + e.what();
+    }
+    stan::math::recover_memory();
+    j.put_str(name, out.c_str());
+  };
+  auto X = [](std::initializer_list<double> v, int r, int c) {
+    MatrixXd m(r, c);
+    int i = 0;
+    for (double t : v) m(i++) = t;
+    return m;
+  };
+  auto A = [](std::initializer_list<double> v) {
+    VV a((Eigen::Index)v.size());
+    int i = 0;
+    for (double t : v) a(i++) = t;
+    return a;
+  };
+  auto B = [](std::initializer_list<double> v, int r, int c) {
+    MV m(r, c);
+    int i = 0;
+    for (double t : v) m(i++) = t;
+    return m;
+  };
+  const MatrixXd x = X({1, 2}, 2, 1);
+  using stan::math::categorical_logit_glm_lpmf;
+  run("cat_y_support", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 4}, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_y_zero", [&] { return categorical_logit_glm_lpmf(std::vector<int>{0, 1}, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_y_size", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2, 3}, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_alpha_size", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1}), B({1, 2, 3}, 1, 3)); });
+  run("cat_x_beta", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1, 2}), B({1, 2, 3, 4, 5, 6}, 2, 3)); });
+  run("cat_nonfinite_beta", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1, 2}), B({1, INFINITY, 3}, 1, 3)); });
+  run("cat_nonfinite_alpha", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1, NAN}), B({1, 2, 3}, 1, 3)); });
+  run("cat_nonfinite_x", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, X({1, INFINITY}, 2, 1), A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_y_scalar_support", [&] { return categorical_logit_glm_lpmf(5, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_one_class", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 1}, x, A({0.5}), B({2}, 1, 1)); });
+  run("cat_one_class_y2", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0.5}), B({2}, 1, 1)); });
+  run("cat_empty", [&] { return categorical_logit_glm_lpmf(std::vector<int>{}, MatrixXd(0, 1), A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_small", [&] { return categorical_logit_glm_lpmf(std::vector<int>{3, 1}, x, A({0, 1, 2}), B({1, -2, 0.5}, 1, 3)); });
+  write_fixture("categorical_logit_glm_errors", j);
+}
+
 // ---- mdivide_left_spd, log_determinant_spd,
 // multiply_lower_tri_self_transpose, quad_form_sym.  Inputs are exact
 // element-wise constructions (tests/gen.py spd_inputs mirrors them bit for
@@ -1039,6 +1164,10 @@ int main(int argc, char** argv) {
     if (want("mvn")) fix_mvn();
     if (want("glm")) fix_glm();
     if (want("glm2")) fix_glm2();
+    if (want("glm_cat")) {
+      fix_glm_cat();
+      fix_glm_cat_errors();
+    }
     if (want("spd")) fix_spd();
     if (want("hessian")) fix_hessian();
     if (want("hvp")) fix_hvp();

@@ -101,6 +101,7 @@ def oracle():
             "oracle_glm": (dd, [_I, _D, ctypes.c_longlong, ii, dd, _D, _D, _D]),
             "oracle_normal_id_glm": (dd, [_D, _D, ctypes.c_longlong, ii, dd, _D, dd, _D]),
             "oracle_poisson_log_glm": (dd, [_I, _D, ctypes.c_longlong, ii, dd, _D, _D]),
+            "oracle_categorical_logit_glm": (dd, [_I, _D, ctypes.c_longlong, ii, ii, _D, _D, _D]),
             "oracle_gp_marginal": (None, [_D, _D, ii, _D, _D, _D]),
             "oracle_mdivide_left_spd": (ii, [_D, _D, ii, ii, _D, _D, _D, _D]),
             "oracle_log_determinant_spd": (ii, [_D, ii, _D, _D]),
@@ -130,6 +131,16 @@ def glm2_oracle(kind, x, y, th, M):
     else:
         lp = oracle().oracle_poisson_log_glm(ptr(np.ascontiguousarray(y, dtype=np.int32)), ptr(xf), R, M, th[0],
                                              ptr(f64(th[1:])), ptr(g))
+    return lp, g
+
+
+def glm_cat_oracle(x, y, th, M, C):
+    """(logp, [alpha'(C), beta'(M x C col-major)]) of the restated categorical GLM."""
+    R = len(y)
+    g = np.zeros(C + M * C)
+    xf = f64(x.ravel(order="F"))
+    lp = oracle().oracle_categorical_logit_glm(ptr(np.ascontiguousarray(y, dtype=np.int32)), ptr(xf), R, M, C,
+                                               ptr(f64(th[:C])), ptr(f64(th[C:])), ptr(g))
     return lp, g
 
 

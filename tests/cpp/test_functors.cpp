@@ -26,6 +26,10 @@
 //                                 Eigen signatures; f = sum(W .* F(args)), gradient over all entries
 //   glm2 kind R M y theta         normal_id_glm_lpdf (kind 0) / poisson_log_glm_lpmf (kind 1):
 //                                 device x, single call, 7 row shards, propto
+//   glm_cat R M C ys y theta      categorical_logit_glm_lpmf: device path (dev_var_matrix alpha /
+//                                 beta, 5 row shards), Eigen path (Matrix<var>), mixed and
+//                                 all-double operands; x filled on the device (gen.glm_cat_inputs)
+//   glm_cat_errors                the reference's exceptions / early returns on small inputs
 #include <stan/math.hpp>
 
 #include <cmath>
@@ -758,6 +762,157 @@ static void cmd_errors() {
               ChainableStack::instance_->dev_adj_stack_.size());
 }
 
+static void cmd_glm_cat() {
+  int M, C, ys;
+  long long R;
+  std::cin >> R >> M >> C >> ys;
+  auto yv = read_vec(size_t(R));
+  auto th = read_vec(size_t(C + M * C));
+  smg_ctx* c = amd::ctx();
+  double* x = amd::alloc_doubles(size_t(R) * M);
+  amd::check(smg_fill_unif(c, x, R * M, 20260101ull + 81, -1.0, 1.0, std::sqrt(3.0)), "fill");
+  std::vector<int> yi(yv.begin(), yv.end());
+  dev_data<int> ydi = to_dev_data(yi);
+  dev_data<double> xd(x, size_t(R) * M, int(R), M);
+  std::vector<double> xh(size_t(R) * M);
+  amd::to_host(xh.data(), x, xh.size());
+  const matrix_d xm = Eigen::Map<matrix_d>(xh.data(), R, M);
+  auto split = [&](const std::vector<var>& t, dev_var_matrix& a, dev_var_matrix& b) {
+    a = to_dev(std::vector<var>(t.begin(), t.begin() + C), C, 1);
+    b = to_dev(std::vector<var>(t.begin() + C, t.end()), M, C);
+  };
+  double fx;
+  std::vector<double> g;
+  // device operands, one call
+  gradient(
+      [&](const std::vector<var>& t) {
+        dev_var_matrix a, b;
+        split(t, a, b);
+        return categorical_logit_glm_lpmf<false>(ydi, xd, a, b);
+      },
+      th, fx, g);
+  print1("fx", fx);
+  print("grad", g);
+  gradient(
+      [&](const std::vector<var>& t) {
+        dev_var_matrix a, b;
+        split(t, a, b);
+        return categorical_logit_glm_lpmf<true>(ydi, xd, a, b);
+      },
+      th, fx, g);
+  print1("fx_propto", fx);
+  print("grad_propto", g);
+  // 5 contiguous row shards summed on the tape
+  gradient(
+      [&](const std::vector<var>& t) {
+        dev_var_matrix a, b;
+        split(t, a, b);
+        var s = 0.0;
+        for (int k = 0; k < 5; ++k) {
+          long long b0, b1;
+          row_partition(R, 5, k, &b0, &b1);
+          glm_shard sh;
+          sh.y = ydi.data() + b0;
+          sh.x = x + b0;
+          sh.rows = b1 - b0;
+          sh.M = M;
+          sh.ldx = R;
+          sh.row0 = b0;
+          sh.total_rows = b1 - b0;
+          s += categorical_logit_glm_lpmf<false>(sh, a, b);
+        }
+        return s;
+      },
+      th, fx, g);
+  print1("fx_shards5", fx);
+  print("grad_shards5", g);
+  // Eigen signature, Matrix<var> alpha and beta (scalar y when ys > 0)
+  gradient(
+      [&](const std::vector<var>& t) {
+        Eigen::Matrix<var, Eigen::Dynamic, 1> a(C);
+        Eigen::Matrix<var, Eigen::Dynamic, Eigen::Dynamic> b(M, C);
+        for (int k = 0; k < C; ++k) a(k) = t[k];
+        for (int k = 0; k < M * C; ++k) b(k) = t[C + k];
+        if (ys > 0) return categorical_logit_glm_lpmf(ys, xm, a, b);
+        return categorical_logit_glm_lpmf(yi, xm, a, b);
+      },
+      th, fx, g);
+  print1("fx_eigen", fx);
+  print("grad_eigen", g);
+  // double alpha, var beta: the beta block of the gradient
+  std::vector<double> tb(th.begin() + C, th.end());
+  gradient(
+      [&](const std::vector<var>& t) {
+        Eigen::VectorXd a = Eigen::Map<const Eigen::VectorXd>(th.data(), C);
+        Eigen::Matrix<var, Eigen::Dynamic, Eigen::Dynamic> b(M, C);
+        for (int k = 0; k < M * C; ++k) b(k) = t[k];
+        return categorical_logit_glm_lpmf(yi, xm, a, b);
+      },
+      tb, fx, g);
+  print1("fx_mixed", fx);
+  print("grad_mixed", g);
+  // all double: a plain double; with propto: 0
+  const Eigen::VectorXd a = Eigen::Map<const Eigen::VectorXd>(th.data(), C);
+  const matrix_d b = Eigen::Map<const matrix_d>(th.data() + C, M, C);
+  print1("fx_double", categorical_logit_glm_lpmf(yi, xm, a, b));
+  print1("fx_double_propto", categorical_logit_glm_lpmf<true>(yi, xm, a, b));
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
+static void cmd_glm_cat_errors() {
+  using VV = Eigen::Matrix<var, Eigen::Dynamic, 1>;
+  using MV = Eigen::Matrix<var, Eigen::Dynamic, Eigen::Dynamic>;
+  auto X = [](std::initializer_list<double> v, int r, int c) {
+    matrix_d m(r, c);
+    int i = 0;
+    for (double t : v) m(i++) = t;
+    return m;
+  };
+  auto A = [](std::initializer_list<double> v) {
+    VV a((Eigen::Index)v.size());
+    int i = 0;
+    for (double t : v) a(i++) = t;
+    return a;
+  };
+  auto B = [](std::initializer_list<double> v, int r, int c) {
+    MV m(r, c);
+    int i = 0;
+    for (double t : v) m(i++) = t;
+    return m;
+  };
+  auto run = [&](const char* name, auto&& f) {
+    start_nested();
+    try {
+      const var v = f();
+      std::printf("%s value %.17g\n", name, v.val());
+    } catch (const std::domain_error& e) {
+      std::printf("%s domain_error %s\n", name, e.what());
+    } catch (const std::invalid_argument& e) {
+      std::printf("%s invalid_argument %s\n", name, e.what());
+    } catch (const std::exception& e) {
+      std::printf("%s other %s\n", name, e.what());
+    }
+    recover_memory_nested();
+  };
+  const matrix_d x = X({1, 2}, 2, 1);
+  run("cat_y_support", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 4}, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_y_zero", [&] { return categorical_logit_glm_lpmf(std::vector<int>{0, 1}, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_y_size", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2, 3}, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_alpha_size", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1}), B({1, 2, 3}, 1, 3)); });
+  run("cat_x_beta", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1, 2}), B({1, 2, 3, 4, 5, 6}, 2, 3)); });
+  run("cat_nonfinite_beta", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1, 2}), B({1, INFINITY, 3}, 1, 3)); });
+  run("cat_nonfinite_alpha", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0, 1, NAN}), B({1, 2, 3}, 1, 3)); });
+  run("cat_nonfinite_x", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, X({1, INFINITY}, 2, 1), A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_y_scalar_support", [&] { return categorical_logit_glm_lpmf(5, x, A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_one_class", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 1}, x, A({0.5}), B({2}, 1, 1)); });
+  run("cat_one_class_y2", [&] { return categorical_logit_glm_lpmf(std::vector<int>{1, 2}, x, A({0.5}), B({2}, 1, 1)); });
+  run("cat_empty", [&] { return categorical_logit_glm_lpmf(std::vector<int>{}, matrix_d(0, 1), A({0, 1, 2}), B({1, 2, 3}, 1, 3)); });
+  run("cat_small", [&] { return categorical_logit_glm_lpmf(std::vector<int>{3, 1}, x, A({0, 1, 2}), B({1, -2, 0.5}, 1, 3)); });
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
 int main() {
   std::string cmd;
   std::cin >> cmd;
@@ -776,6 +931,8 @@ int main() {
     else if (cmd == "glm") cmd_glm();
     else if (cmd == "glm_data") cmd_glm_data();
     else if (cmd == "glm2") cmd_glm2();
+    else if (cmd == "glm_cat") cmd_glm_cat();
+    else if (cmd == "glm_cat_errors") cmd_glm_cat_errors();
     else if (cmd == "spd") cmd_spd();
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();

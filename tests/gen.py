@@ -60,6 +60,17 @@ def glm2_inputs(R: int, M: int, kind: str):
     return x, y, theta
 
 
+def glm_cat_inputs(R: int, M: int, C: int):
+    """ref_harness.cpp glm_cat_inputs: x (R x M col-major) U[-1,1) sqrt 3,
+    theta = (alpha U[-1,1) (C), beta U[-1,1) sqrt(3/M) (M x C col-major)),
+    y = floor(U[0, C)) + 1."""
+    x = unif(SEED + 81, R * M, -1.0, 1.0) * np.sqrt(3.0)
+    a = unif(SEED + 82, C, -1.0, 1.0)
+    b = unif(SEED + 83, M * C, -1.0, 1.0) * np.sqrt(3.0 / max(M, 1))
+    y = (np.floor(unif(SEED + 84, R, 0.0, float(C))) + 1).astype(np.int32)
+    return x.reshape(M, R).T.copy(order="F"), y, np.concatenate([a, b])
+
+
 def spd_exact(n: int, seed: int) -> np.ndarray:
     """ref_harness.cpp spd_exact: S_ij = S_ji = u (lower source), S_ii = n + u_ii."""
     u = unif(seed, n * n, -1.0, 1.0).reshape(n, n).T  # u[i, j] = element i + j n (col-major)

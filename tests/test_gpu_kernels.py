@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import gen
-from _util import GOLDEN, check_against_fixture, f64, glm2_oracle, golden, near_rel, oracle, ptr, spd_oracle
+from _util import GOLDEN, check_against_fixture, f64, glm2_oracle, glm_cat_oracle, golden, near_rel, oracle, ptr, spd_oracle
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-10
@@ -416,6 +416,61 @@ def test_glm2_vs_oracle_ragged(ctx, kind):
     lpo, go = glm2_oracle(kind, x, y, th, M)
     near_rel(lp, lpo, 1e-12, what="fx")
     near_rel(g, go, RTOL, what="grad")
+
+
+def _glm_cat(ctx, x, y, th, R, M, C, ldx=None):
+    """Device categorical_logit_glm -> (logp, [alpha', beta'])."""
+    ldx = R if ldx is None else ldx
+    xf = np.zeros((ldx, M))
+    xf[:R] = x
+    ws = ctx.zeros(int(ctx.lib.smg_glm_categorical_ws_doubles(R, M, C)))
+    out = ctx.zeros(1 + C + M * C)
+    ctx.call("smg_categorical_logit_glm", ctx.put(np.ascontiguousarray(y, dtype=np.int32)), ctx.put(F(xf)), R, M,
+             ldx, C, ctx.put(f64(th)), ws, out)
+    o = ctx.get(out, 1 + C + M * C)
+    return o[0], o[1:]
+
+
+GLM_CAT_CASES = sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "categorical_logit_glm_R*.json")))
+
+
+@pytest.mark.parametrize("name", GLM_CAT_CASES)
+def test_glm_cat_golden(ctx, name):
+    d = golden(name)
+    R, M, C, ys = int(d["R"]), int(d["M"]), int(d["C"]), int(d["y_scalar"])
+    x, y, th = gen.glm_cat_inputs(R, M, C)
+    if ys:
+        y = np.full(R, ys, dtype=np.int32)
+    lp, g = _glm_cat(ctx, x, y, th, R, M, C)
+    near_rel(lp, d["fx"], 1e-12, what="fx")
+    near_rel(g, d["grad"], RTOL, what="grad")
+
+
+@pytest.mark.parametrize("R,M,C,ldx", [(200003, 256, 16, 200011), (17, 1, 2, 17), (33, 0, 7, 33), (1, 5, 16, 4),
+                                       (5003, 300, 5, 5003), (4001, 20, 40, 4010), (999, 0, 17, 999)])
+def test_glm_cat_vs_oracle(ctx, R, M, C, ldx):
+    """Beyond the fixtures: ragged last tile, the fused path's M / C limits,
+    M = 0 (intercept only), a leading dimension > R, one row; M > 256 or
+    C > 16 take the GEMM path."""
+    x, y, th = gen.glm_cat_inputs(R, M, C)
+    lp, g = _glm_cat(ctx, x, y, th, R, M, C, ldx)
+    lpo, go = glm_cat_oracle(x, y, th, M, C)
+    near_rel(lp, lpo, 1e-12, what="fx")
+    near_rel(g, go, RTOL, atol=1e-12 * max(1.0, np.abs(go).max()), what="grad")
+
+
+@pytest.mark.parametrize("M,C", [(2, 3), (300, 20)])
+def test_glm_cat_empty_and_args(ctx, M, C):
+    """R = 0 -> zeros on both paths; C < 1, R < 0 or a short ldx -> SMG_ERR_ARG."""
+    n = 1 + C + M * C
+    out = ctx.put(np.full(n, 7.0))
+    ws = ctx.zeros(max(64, int(ctx.lib.smg_glm_categorical_ws_doubles(0, M, C))))
+    ab = ctx.put(np.ones(C + M * C))
+    ctx.call("smg_categorical_logit_glm", 0, 0, 0, M, 0, C, ab, ws, out)
+    assert np.all(ctx.get(out, n) == 0.0)
+    assert ctx.lib.smg_categorical_logit_glm(ctx.ptr, 0, 0, 0, M, 0, 0, ab, ws, out) != 0
+    assert ctx.lib.smg_categorical_logit_glm(ctx.ptr, 0, 0, -1, M, 0, C, ab, ws, out) != 0
+    assert ctx.lib.smg_categorical_logit_glm(ctx.ptr, ws, ws, 10, M, 9, C, ab, ws, out) != 0
 
 
 # ------------------------------------------ SURVEY 8(f) row 3 (spd.hip)
