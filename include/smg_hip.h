@@ -365,6 +365,11 @@ int smg_check_bounded_int(smg_ctx* ctx, const int* y, long long n, int lo, int h
 int smg_comm_unique_id(char* id_host /* 128 bytes */);
 int smg_comm_init(smg_ctx* ctx, int nranks, int rank, const char* id_host);
 int smg_comm_allreduce_sum(smg_ctx* ctx, double* buf, long long count);
+/* recv (device, nranks * count doubles) <- every rank's count doubles of send
+ * (device), rank order; the distributed map_rect executor's exchange of
+ * per-job [value; partials] columns (replaces the gatherv of
+ * prim/mat/functor/mpi_parallel_call.hpp:374-382). */
+int smg_comm_allgather(smg_ctx* ctx, const double* send, long long count, double* recv);
 int smg_comm_destroy(smg_ctx* ctx);
 
 #ifdef __cplusplus

@@ -1,8 +1,9 @@
 // RCCL (xGMI) communicator for the row-sharded reducers.
-// One communicator per process/device; the only collective on the hot path is
-// a single fp64 sum all-reduce of [logp, alpha', beta'(M)] per gradient.
-// Replaces map_rect's Boost.MPI reduce/gather
-// (prim/mat/functor/mpi_parallel_call.hpp:332-392).
+// One communicator per process/device.  The row-sharded reducers' one
+// collective is a single fp64 sum all-reduce of [logp, alpha', beta'(M)] per
+// gradient; the distributed map_rect executor all-gathers per-job results.
+// Replaces map_rect's Boost.MPI reduce/gatherv
+// (prim/mat/functor/mpi_parallel_call.hpp:320-392).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -38,6 +39,14 @@ int smg_comm_allreduce_sum(smg_ctx* ctx, double* buf, long long count) {
   if (count == 0) return SMG_OK;
   if (ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, (ncclComm_t)ctx->comm,
                     ctx->stream) != ncclSuccess)
+    return SMG_ERR_HIP;
+  return SMG_OK;
+}
+
+int smg_comm_allgather(smg_ctx* ctx, const double* send, long long count, double* recv) {
+  if (!ctx || !ctx->comm || count < 0 || (count > 0 && (!send || !recv))) return SMG_ERR_ARG;
+  if (count == 0) return SMG_OK;
+  if (ncclAllGather(send, recv, (size_t)count, ncclDouble, (ncclComm_t)ctx->comm, ctx->stream) != ncclSuccess)
     return SMG_ERR_HIP;
   return SMG_OK;
 }

@@ -101,6 +101,7 @@ _SIGS = {
     "smg_comm_unique_id": (_I, [ctypes.c_char_p]),
     "smg_comm_init": (_I, [_P, _I, _I, ctypes.c_char_p]),
     "smg_comm_allreduce_sum": (_I, [_P, _P, _L]),
+    "smg_comm_allgather": (_I, [_P, _P, _L, _P]),
     "smg_comm_destroy": (_I, [_P]),
 }
 

@@ -18,6 +18,7 @@
 // builds the same node.  Replaces map_rect's MPI/TBB gather
 // (prim/mat/functor/map_rect.hpp:120-177, map_rect_combine.hpp:36-92).
 
+#include <stan/math/amd/comm.hpp>
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/core.hpp>
 #include <stan/math/rev/fun/normal_lpdf.hpp>
@@ -31,17 +32,6 @@
 
 namespace stan {
 namespace math {
-
-namespace amd {
-/** Join this process to an RCCL communicator (one per process / GPU).
- * id: 128 bytes from smg_comm_unique_id on rank 0, shared by the launcher. */
-inline void comm_init(int nranks, int rank, const char* id) {
-  check(smg_comm_init(ctx(), nranks, rank, id), "comm_init");
-}
-inline void comm_destroy() {
-  if (has_ctx()) check(smg_comm_destroy(ctx()), "comm_destroy");
-}
-}  // namespace amd
 
 /** Device-resident GLM data: a row block [row0, row0 + rows) of y and x.
  * x: rows x M column-major with leading dimension ldx (ldx >= rows). */

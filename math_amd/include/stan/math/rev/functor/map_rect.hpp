@@ -11,15 +11,32 @@
 //   * one precomputed-gradients var per output over the outer operands
 //     (map_rect_combine, prim/mat/functor/map_rect_combine.hpp:36-92).
 // Jobs run in order on this thread's tape and device stream; F may use any
-// device functor (e.g. bernoulli_logit_glm_lpmf over the job's rows).  The
-// reference's TBB / MPI executors are replaced by one HIP stream per tape; the
-// row-sharded multi-GPU form of the GLM reducer is glm_shard +
-// reduce_sum_bernoulli_logit_glm (bernoulli_logit_glm_lpmf.hpp).
+// device functor (e.g. bernoulli_logit_glm_lpmf over the job's rows).
+//
+// Multi-GPU (replaces the reference's MPI executor,
+// prim/mat/functor/mpi_parallel_call.hpp:268-392): once the process has joined
+// an RCCL job (amd::comm_init, one process per GPU, W >= 1) or W > 1 ranks of
+// a host collective (amd::set_host_collective), every rank calls
+// map_rect with the same arguments (SPMD -- there is no listening worker
+// loop), evaluates only its chunk of jobs (the reference's mpi_map_chunks
+// split, prim/arr/functor/mpi_cluster.hpp:84-100: J / W each, the remainder
+// to ranks 1, 2, ...) on its own GPU, and two all-gathers exchange
+//   (1) [status, outputs per job] of every rank, then
+//   (2) every job's [value; d/d shared; d/d job] columns,
+// after which every rank combines the same full result.  The per-job values
+// and partials are the ones a single process computes, so the result is
+// bit-identical to the serial path.  A job that throws on any rank makes
+// every rank throw std::domain_error("Error during MPI evaluation."), as the
+// reference's root does (:384-389), so no rank is left waiting in a
+// collective.  The row-sharded GLM reducers keep their own one all-reduce
+// (glm_shard + reduce_sum_bernoulli_logit_glm).
 
+#include <stan/math/amd/comm.hpp>
 #include <stan/math/rev/core.hpp>
 
 #include <Eigen/Dense>
 
+#include <algorithm>
 #include <ostream>
 #include <sstream>
 #include <stdexcept>
@@ -86,6 +103,85 @@ Eigen::MatrixXd map_rect_reduce_job(const Eigen::VectorXd& shared, const Eigen::
   return out;
 }
 
+/** Jobs per rank: J / W each, the remainder one by one to ranks 1, 2, ...
+ * (from rank 0 when J < W) -- mpi_map_chunks. */
+inline std::vector<int> map_rect_chunks(size_t J, int W) {
+  std::vector<int> c(size_t(W), int(J / size_t(W)));
+  const size_t delta = c[0] == 0 ? 0 : 1;
+  for (size_t r = 0; r != J % size_t(W); ++r) ++c[r + delta];
+  return c;
+}
+
+/** Evaluate this rank's chunk of jobs, then all-gather every job's output
+ * columns (rows = 1 + shared partials + job partials, or 1 for values). */
+template <typename F, bool SV, bool JV, typename T_job>
+std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_d,
+                                                  const std::vector<Eigen::Matrix<T_job, Eigen::Dynamic, 1>>& job_params,
+                                                  const std::vector<std::vector<double>>& x_r,
+                                                  const std::vector<std::vector<int>>& x_i, std::ostream* msgs,
+                                                  Eigen::Index rows) {
+  const int W = amd::world_size(), rank = amd::world_rank();
+  const size_t J = job_params.size();
+  const std::vector<int> chunks = map_rect_chunks(J, W);
+  int first = 0, maxc = 0;
+  for (int r = 0; r < W; ++r) {
+    if (r < rank) first += chunks[size_t(r)];
+    maxc = std::max(maxc, chunks[size_t(r)]);
+  }
+  const int mine = chunks[size_t(rank)];
+  std::vector<Eigen::MatrixXd> local(static_cast<size_t>(mine));
+  double ok = 1.0;
+  try {
+    for (int i = 0; i < mine; ++i) {
+      const size_t j = size_t(first + i);
+      const Eigen::VectorXd job_d = map_rect_values(job_params[j]);
+      if constexpr (SV || JV) {
+        local[size_t(i)] = map_rect_reduce_job<F, SV, JV>(shared_d, job_d, x_r[j], x_i[j], msgs);
+      } else {
+        Eigen::VectorXd v = F()(shared_d, job_d, x_r[j], x_i[j], msgs);
+        local[size_t(i)] = v.transpose();
+      }
+    }
+  } catch (const std::exception&) {
+    ok = 0.0;  // flagged, not rethrown: every rank must reach the exchange
+  }
+  // (1) status and the number of outputs of each local job
+  const long long hn = 1 + maxc;
+  std::vector<double> hdr(size_t(hn), 0.0), all_hdr(size_t(hn) * W);
+  hdr[0] = ok;
+  if (ok != 0.0)
+    for (int i = 0; i < mine; ++i) hdr[size_t(1 + i)] = double(local[size_t(i)].cols());
+  amd::allgather(hdr.data(), hn, all_hdr.data());
+  for (int r = 0; r < W; ++r)
+    if (all_hdr[size_t(r) * hn] != 1.0) throw std::domain_error("Error during MPI evaluation.");
+  long long max_pay = 0;
+  for (int r = 0; r < W; ++r) {
+    long long p = 0;
+    for (int i = 0; i < chunks[size_t(r)]; ++i) p += rows * (long long)all_hdr[size_t(r) * hn + 1 + i];
+    max_pay = std::max(max_pay, p);
+  }
+  // (2) every job's columns, rank r's block at r * max_pay
+  std::vector<double> pay(size_t(max_pay), 0.0), all(size_t(max_pay) * W);
+  long long off = 0;
+  for (int i = 0; i < mine; ++i) {
+    const Eigen::MatrixXd& o = local[size_t(i)];
+    std::copy(o.data(), o.data() + o.size(), pay.begin() + off);
+    off += o.size();
+  }
+  amd::allgather(pay.data(), max_pay, all.data());
+  std::vector<Eigen::MatrixXd> outs(J);
+  size_t j = 0;
+  for (int r = 0; r < W; ++r) {
+    const double* base = all.data() + size_t(r) * max_pay;
+    for (int i = 0; i < chunks[size_t(r)]; ++i, ++j) {
+      const Eigen::Index cols = Eigen::Index(all_hdr[size_t(r) * hn + 1 + i]);
+      outs[j] = Eigen::Map<const Eigen::MatrixXd>(base, rows, cols);
+      base += rows * cols;
+    }
+  }
+  return outs;
+}
+
 }  // namespace internal
 
 template <int call_id, typename F, typename T_shared, typename T_job>
@@ -121,17 +217,22 @@ map_rect(const Eigen::Matrix<T_shared, Eigen::Dynamic, 1>& shared_params,
 
   const Eigen::VectorXd shared_d = internal::map_rect_values(shared_params);
   std::vector<Eigen::MatrixXd> outs(J);
-  size_t total = 0;
-  for (size_t j = 0; j < J; ++j) {
-    const Eigen::VectorXd job_d = internal::map_rect_values(job_params[j]);
-    if constexpr (SV || JV) {
-      outs[j] = internal::map_rect_reduce_job<F, SV, JV>(shared_d, job_d, x_r[j], x_i[j], msgs);
-    } else {
-      Eigen::VectorXd v = F()(shared_d, job_d, x_r[j], x_i[j], msgs);
-      outs[j] = v.transpose();
+  if (amd::distributed()) {
+    const Eigen::Index rows = 1 + (SV ? shared_params.size() : 0) + (JV ? job_params[0].size() : 0);
+    outs = internal::map_rect_distributed<F, SV, JV>(shared_d, job_params, x_r, x_i, msgs, rows);
+  } else {
+    for (size_t j = 0; j < J; ++j) {
+      const Eigen::VectorXd job_d = internal::map_rect_values(job_params[j]);
+      if constexpr (SV || JV) {
+        outs[j] = internal::map_rect_reduce_job<F, SV, JV>(shared_d, job_d, x_r[j], x_i[j], msgs);
+      } else {
+        Eigen::VectorXd v = F()(shared_d, job_d, x_r[j], x_i[j], msgs);
+        outs[j] = v.transpose();
+      }
     }
-    total += size_t(outs[j].cols());
   }
+  size_t total = 0;
+  for (size_t j = 0; j < J; ++j) total += size_t(outs[j].cols());
 
   // map_rect_combine: one precomputed-gradients var per output over the outer operands
   result_t result(total);

@@ -939,6 +939,81 @@ static void fix_glm_cat_errors() {
   write_fixture("categorical_logit_glm_errors", j);
 }
 
+// ---- map_rect with a generic user functor whose jobs
+// return different numbers of outputs (x_i[0] = outputs of the job).  Host
+// scalar arithmetic only; the same functor is written out in
+// tests/cpp/maprect_dist.cpp.  f = sum_i (1 + 0.1 i) out_i over the
+// concatenated outputs; gradient over (phi(2), theta(J)).
+struct hier_job {
+  template <typename T1, typename T2>
+  Matrix<stan::return_type_t<T1, T2>, Dynamic, 1> operator()(
+      const Matrix<T1, Dynamic, 1>& phi, const Matrix<T2, Dynamic, 1>& theta,
+      const std::vector<double>& x_r, const std::vector<int>& x_i, std::ostream*) const {
+    using stan::math::exp;
+    using stan::math::log;
+    using stan::math::square;
+    const int nout = x_i[0];
+    Matrix<stan::return_type_t<T1, T2>, Dynamic, 1> out(nout);
+    const auto sigma = exp(phi(1));
+    for (int k = 0; k < nout; ++k) {
+      stan::return_type_t<T1, T2> acc = 0.0;
+      for (size_t i = k; i < x_r.size(); i += nout)
+        acc += -0.5 * square((x_r[i] - (phi(0) + theta(0))) / sigma) - log(sigma);
+      out(k) = acc;
+    }
+    return out;
+  }
+};
+static void maprect_inputs(int J, std::vector<std::vector<double>>& xr, std::vector<std::vector<int>>& xi,
+                           VectorXd& th) {
+  std::vector<double> u = unif(SEED + 91, (size_t)J * 6, -2.0, 2.0);
+  xr.assign(J, std::vector<double>(6));
+  xi.assign(J, std::vector<int>(2, 0));
+  for (int j = 0; j < J; ++j) {
+    for (int i = 0; i < 6; ++i) xr[j][i] = u[(size_t)j * 6 + i];
+    xi[j][0] = 1 + j % 3;
+  }
+  th.resize(2 + J);
+  th(0) = 0.3;
+  th(1) = -0.2;
+  for (int j = 0; j < J; ++j) th(2 + j) = 0.1 * j - 0.25;
+}
+struct hier_maprect_functor {
+  int J;
+  const std::vector<std::vector<double>>& xr;
+  const std::vector<std::vector<int>>& xi;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, 1> phi = th.head(2);
+    std::vector<Matrix<T, Dynamic, 1>> job(J, Matrix<T, Dynamic, 1>(1));
+    for (int j = 0; j < J; ++j) job[j](0) = th(2 + j);
+    Matrix<T, Dynamic, 1> out = stan::math::map_rect<3, hier_job>(phi, job, xr, xi);
+    T f = 0.0;
+    for (int i = 0; i < out.size(); ++i) f += (1.0 + 0.1 * i) * out(i);
+    return f;
+  }
+};
+static void fix_maprect() {
+  for (int J : {7, 1, 16}) {
+    std::vector<std::vector<double>> xr;
+    std::vector<std::vector<int>> xi;
+    VectorXd th, g;
+    maprect_inputs(J, xr, xi, th);
+    double fx;
+    stan::math::gradient(hier_maprect_functor{J, xr, xi}, th, fx, g);
+    std::vector<Matrix<double, Dynamic, 1>> jobd(J, Matrix<double, Dynamic, 1>(1));
+    for (int j = 0; j < J; ++j) jobd[j](0) = th(2 + j);
+    VectorXd vals = stan::math::map_rect<4, hier_job>(VectorXd(th.head(2)), jobd, xr, xi);
+    Json j;
+    j.put_str("what", "map_rect<hier_job>: f = sum_i (1 + 0.1 i) out_i, gradient over (phi(2), theta(J)); inputs: tests/gen.py maprect_inputs");
+    j.put_int("J", J);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    j.put_vec("values", vals);
+    write_fixture("map_rect_hier_J" + std::to_string(J), j);
+  }
+}
+
 // ---- mdivide_left_spd, log_determinant_spd,
 // multiply_lower_tri_self_transpose, quad_form_sym.  Inputs are exact
 // element-wise constructions (tests/gen.py spd_inputs mirrors them bit for
@@ -1169,6 +1244,7 @@ int main(int argc, char** argv) {
       fix_glm_cat_errors();
     }
     if (want("spd")) fix_spd();
+    if (want("maprect")) fix_maprect();
     if (want("hessian")) fix_hessian();
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();

@@ -71,6 +71,16 @@ def glm_cat_inputs(R: int, M: int, C: int):
     return x.reshape(M, R).T.copy(order="F"), y, np.concatenate([a, b])
 
 
+def maprect_inputs(J: int):
+    """ref_harness.cpp maprect_inputs: x_r (J x 6, U[-2, 2)), x_i = (1 + j % 3
+    outputs, fail flag 0), theta = (phi = (0.3, -0.2), theta_j = 0.1 j - 0.25)."""
+    xr = unif(SEED + 91, J * 6, -2.0, 2.0).reshape(J, 6)
+    xi = np.zeros((J, 2), dtype=np.int32)
+    xi[:, 0] = 1 + np.arange(J) % 3
+    th = np.concatenate([[0.3, -0.2], 0.1 * np.arange(J) - 0.25])
+    return xr, xi, th
+
+
 def spd_exact(n: int, seed: int) -> np.ndarray:
     """ref_harness.cpp spd_exact: S_ij = S_ji = u (lower source), S_ii = n + u_ii."""
     u = unif(seed, n * n, -1.0, 1.0).reshape(n, n).T  # u[i, j] = element i + j n (col-major)

@@ -1,4 +1,5 @@
-"""Row sharding of the GLM reducer on CPU, world_size 2, gloo.
+"""Row sharding of the GLM reducer and the multi-rank
+map_rect executor (§8(f) row 1) on CPU, world_size 2 and 3, gloo.
 
 The multi-GPU path partitions the R rows with stan::math::row_partition (the
 C++ header function, called here through libsmg_bench.so), generates each
@@ -102,3 +103,114 @@ def test_glm_two_ranks_gloo_matches_reference(tmp_path):
     res = np.load(out)
     near_rel(res[0], d["fx"], 1e-12, what="fx")
     near_rel(res[1:], d["grad"], 1e-10, what="grad")
+
+
+# ---------------------------------------------------------------- map_rect executor
+MAPRECT_LIB = os.path.join(ROOT, "tests", "cpp", "_bin", "libmaprect_dist.so")
+_AG = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.c_longlong, ctypes.POINTER(ctypes.c_double),
+                       ctypes.c_void_p)
+
+
+def _maprect_call(lib, world, rank, cb, xr, xi, th, mode):
+    J = xr.shape[0]
+    fx = ctypes.c_double()
+    grad = np.zeros(2 + J)
+    vals = np.zeros(3 * J + 3)
+    nv = ctypes.c_int()
+    err = ctypes.create_string_buffer(512)
+    xrf = np.ascontiguousarray(xr, dtype=np.float64)
+    xif = np.ascontiguousarray(xi, dtype=np.int32)
+    thf = np.ascontiguousarray(th, dtype=np.float64)
+    rc = lib.maprect_hier(world, rank, cb, None, J, xrf.ctypes.data_as(ctypes.c_void_p), xr.shape[1],
+                          xif.ctypes.data_as(ctypes.c_void_p), thf.ctypes.data_as(ctypes.c_void_p), mode,
+                          ctypes.byref(fx), grad.ctypes.data_as(ctypes.c_void_p),
+                          vals.ctypes.data_as(ctypes.c_void_p), ctypes.byref(nv), err, 512)
+    return rc, fx.value, grad, vals[:nv.value], err.value.decode()
+
+
+def _maprect_lib():
+    lib = ctypes.CDLL(MAPRECT_LIB)
+    lib.maprect_hier.restype = ctypes.c_int
+    lib.maprect_hier.argtypes = [ctypes.c_int, ctypes.c_int, _AG, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+    return lib
+
+
+def _maprect_rank(rank, world, port, cases, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def allgather(send, count, recv, _user):
+        t = torch.from_numpy(np.ctypeslib.as_array(send, shape=(count,)).copy())
+        parts = [torch.empty(count, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, t)
+        np.ctypeslib.as_array(recv, shape=(count * world,))[:] = torch.cat(parts).numpy()
+        calls.append(count)
+
+    cb = _AG(allgather)
+    lib = _maprect_lib()
+    res = {}
+    for J, fail in cases:
+        xr, xi, th = gen.maprect_inputs(J)
+        if fail >= 0:
+            xi[fail, 1] = 1
+        for mode in range(4):
+            rc, fx, grad, vals, err = _maprect_call(lib, world, rank, cb, xr, xi, th, mode)
+            res[f"{J}_{fail}_{mode}"] = dict(rc=rc, fx=fx, grad=grad, vals=vals, err=err)
+    res["collectives"] = len(calls)
+    np.save(out + f".{rank}.npy", np.array(res, dtype=object), allow_pickle=True)
+    dist.destroy_process_group()
+
+
+MAPRECT_CASES = [(7, -1), (1, -1), (16, -1), (7, 5), (16, 0)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_map_rect_executor_gloo(tmp_path, world):
+    """map_rect over W gloo ranks (each evaluates its mpi_map_chunks share and
+    two all-gathers exchange the per-job columns) == the same executor in one
+    process, bit for bit, and == the real reference's map_rect (fixtures
+    map_rect_hier_J*, jobs with 1..3 outputs each) within 1e-12 / 1e-10; every
+    operand combination (var/var, var/data, data/var, data/data); a job that
+    throws on one rank makes every rank throw the reference's
+    "Error during MPI evaluation."."""
+    out = str(tmp_path / "mr")
+    mp.start_processes(_maprect_rank, args=(world, _free_port(), MAPRECT_CASES, out), nprocs=world, join=True,
+                       start_method="spawn")
+    ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(world)]
+    lib = _maprect_lib()
+    cb = _AG(lambda *a: None)
+    for J, fail in MAPRECT_CASES:
+        xr, xi, th = gen.maprect_inputs(J)
+        if fail >= 0:
+            xi[fail, 1] = 1
+        for mode in range(4):
+            key = f"{J}_{fail}_{mode}"
+            rc1, fx1, g1, v1, err1 = _maprect_call(lib, 1, 0, cb, xr, xi, th, mode)
+            for r in range(world):
+                got = ranks[r][key]
+                if fail >= 0:
+                    assert rc1 == 1 and err1 == "hier_job: job failed", (key, rc1, err1)
+                    assert got["rc"] == 1 and got["err"] == "Error during MPI evaluation.", (key, r, got)
+                    continue
+                assert rc1 == 0 and got["rc"] == 0, (key, r, got["err"], err1)
+                assert got["fx"] == fx1 and np.array_equal(got["grad"], g1) and np.array_equal(got["vals"], v1), (key, r)
+            if fail < 0:
+                d = golden(f"map_rect_hier_J{J}")
+                near_rel(fx1, d["fx"], 1e-12, what=f"{key} fx")
+                near_rel(v1, d["values"], 1e-12, what=f"{key} values")
+                want = np.array(d["grad"])
+                if mode == 1:
+                    want[2:] = 0.0
+                if mode == 2:
+                    want[:2] = 0.0
+                if mode == 3:
+                    want[:] = 0.0
+                near_rel(g1, want, 1e-10, what=f"{key} grad")
+    # two all-gathers per call on every rank; a failed evaluation stops after the status exchange
+    n_ok = sum(1 for _, fail in MAPRECT_CASES if fail < 0)
+    want = 4 * (2 * n_ok + (len(MAPRECT_CASES) - n_ok))
+    assert all(rk["collectives"] == want for rk in ranks), [rk["collectives"] for rk in ranks]
