@@ -766,7 +766,7 @@ __device__ inline void lds_trtri64_mfma(const double* D, double* X, double* T) {
 
 // Drop-in for lds_potrf_inv64_v2 built from the blocked pieces: factor (if
 // asked) then invert, then one coalesced write of L (lower) and X = L^{-1}.
-__device__ inline void lds_potrf_inv64_blk(double* D, double* X, int b, double* Lout, int ldl,
+__device__ __forceinline__ void lds_potrf_inv64_blk(double* D, double* X, int b, double* Lout, int ldl,
                                            double* Xout, int ldx, int* status, bool factor) {
   __shared__ double T[3 * 256];
   if (factor) lds_potrf64_lookahead(D, status);

@@ -1,32 +1,42 @@
-// Reference point only (not used by the product): rocBLAS DGEMM throughput on
-// the Cholesky update shapes, to size the headroom of the hand-written GEMM.
+// Reference point only (not used by the product): rocBLAS DGEMM / DSYRK
+// throughput on the GP N = 4096 shapes (tools/ubench_shapes.h), to size the
+// headroom of the hand-written GEMM.  Lower-trapezoid shapes run as full
+// DGEMMs (timed; TF/s counted on the trapezoid's flops like the product's).
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <cstdio>
+#include <vector>
+#include "ubench_shapes.h"
 int main() {
   rocblas_handle h;
   rocblas_create_handle(&h);
   const int n = 4096;
   double *A, *B, *C;
   hipMalloc(&A, 8ull * n * n); hipMalloc(&B, 8ull * n * n); hipMalloc(&C, 8ull * n * n);
-  hipMemset(A, 0, 8ull * n * n); hipMemset(B, 0, 8ull * n * n); hipMemset(C, 0, 8ull * n * n);
-  struct S { const char* nm; rocblas_operation ta, tb; int m, nn, k; };
-  S sh[] = {{"NN 4096^3", rocblas_operation_none, rocblas_operation_none, 4096, 4096, 4096},
-            {"NN (1792,2048,256)", rocblas_operation_none, rocblas_operation_none, 1792, 2048, 256},
-            {"NT (2048,2048,256)", rocblas_operation_none, rocblas_operation_transpose, 2048, 2048, 256},
-            {"TN (256,2304,1792)", rocblas_operation_transpose, rocblas_operation_none, 256, 2304, 1792},
-            {"NN (2048,2048,64)", rocblas_operation_none, rocblas_operation_none, 2048, 2048, 64}};
-  const double al = -1.0, be = 1.0;
+  std::vector<double> hv((size_t)n * n);
+  for (size_t i = 0; i < hv.size(); ++i) hv[i] = ((i * 2654435761u) % 2000) * 1e-3 - 1.0;
+  hipMemcpy(A, hv.data(), 8ull * n * n, hipMemcpyHostToDevice);
+  hipMemcpy(B, hv.data(), 8ull * n * n, hipMemcpyHostToDevice);
+  hipMemcpy(C, hv.data(), 8ull * n * n, hipMemcpyHostToDevice);
+  const double al = -1e-3, be = 1.0;
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  for (auto& s : sh) {
-    for (int w = 0; w < 3; ++w)
-      rocblas_dgemm(h, s.ta, s.tb, s.m, s.nn, s.k, &al, A, n, B, n, &be, C, n);
+  auto op = [](int t) { return t ? rocblas_operation_transpose : rocblas_operation_none; };
+  for (int si = 0; si < ub_nshapes; ++si) {
+    const ub_shape& s = ub_shapes[si];
+    const bool syrk = s.uplo && s.m == s.n;
+    auto run = [&] {
+      if (syrk)
+        rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, s.m, s.k, &al, A, n, &be, C, n);
+      else
+        rocblas_dgemm(h, op(s.ta), op(s.tb), s.m, s.n, s.k, &al, A, n, B, n, &be, C, n);
+    };
+    for (int w = 0; w < 3; ++w) run();
     const int reps = s.k == 4096 ? 5 : 50;
     hipEventRecord(e0);
-    for (int r = 0; r < reps; ++r) rocblas_dgemm(h, s.ta, s.tb, s.m, s.nn, s.k, &al, A, n, B, n, &be, C, n);
+    for (int r = 0; r < reps; ++r) run();
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     const double us = ms * 1000 / reps;
-    printf("%-22s %9.2f us %7.2f TF/s\n", s.nm, us, 2.0 * s.m * s.nn * s.k / us * 1e-6);
+    printf("%-34s %8.2f us  %6.2f TF/s  %s\n", s.name, us, ub_flops(s) / us * 1e-6, syrk ? "dsyrk" : "dgemm");
   }
 }

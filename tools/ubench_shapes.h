@@ -1,0 +1,39 @@
+// Dev microbenchmarks: the GEMM shapes of one GP N = 4096 gradient evaluation
+// (two-level Cholesky forward with 512-column panels, Murray reverse with
+// 512-column blocks), shared by tools/ubench_gemm.cpp (the hand-written GEMM)
+// and tools/ubench_rocblas.cpp (rocBLAS, a reference point only).
+#pragma once
+struct ub_shape {
+  const char* name;
+  int ta, tb, uplo, m, n, k;
+};
+static const ub_shape ub_shapes[] = {
+    // forward: (a) next panel's columns (lower trapezoid), (b) the rest (SYRK)
+    {"fwd (a) NT lower (3584,512,512)", 0, 1, 1, 3584, 512, 512},
+    {"fwd (a) NT lower (2048,512,512)", 0, 1, 1, 2048, 512, 512},
+    {"fwd (b) SYRK (3072,3072,512)", 0, 1, 1, 3072, 3072, 512},
+    {"fwd (b) SYRK (2048,2048,512)", 0, 1, 1, 2048, 2048, 512},
+    {"fwd (b) SYRK (1024,1024,512)", 0, 1, 1, 1024, 1024, 512},
+    // reverse, block P (J = 512 P, K = J + 512, m = 4096 - K)
+    {"rev C*W NN (3072,512,512)", 0, 0, 0, 3072, 512, 512},
+    {"rev C*W NN (1536,512,512)", 0, 0, 0, 1536, 512, 512},
+    {"rev B_adj NN (2048,1536,512)", 0, 0, 0, 2048, 1536, 512},
+    {"rev B_adj NN (1024,2560,512)", 0, 0, 0, 1024, 2560, 512},
+    {"rev B_adj NN (3072,512,512)", 0, 0, 0, 3072, 512, 512},
+    {"rev [R|D] TN (512,2048,2048)", 1, 0, 0, 512, 2048, 2048},
+    {"rev [R|D] TN (512,1024,3072)", 1, 0, 0, 512, 1024, 3072},
+    {"rev [R|D] TN (512,3584,512)", 1, 0, 0, 512, 3584, 512},
+    {"rev sym TN (512,512,512)", 1, 0, 0, 512, 512, 512},
+    {"rev sym NN (512,512,512)", 0, 0, 0, 512, 512, 512},
+    {"rev P*R NN (512,2048,512)", 0, 0, 0, 512, 2048, 512},
+    {"rev P*R NN (512,3584,512)", 0, 0, 0, 512, 3584, 512},
+    {"big NN (4096,4096,4096)", 0, 0, 0, 4096, 4096, 4096},
+};
+static const int ub_nshapes = sizeof(ub_shapes) / sizeof(ub_shapes[0]);
+static inline double ub_flops(const ub_shape& s) {
+  if (s.uplo) {  // lower trapezoid of an m x n product (n <= m): n (n + 1) / 2 + (m - n) n entries
+    const double e = (double)s.n * (s.n + 1) / 2 + (double)(s.m - s.n) * s.n;
+    return 2.0 * e * s.k;
+  }
+  return 2.0 * s.m * s.n * s.k;
+}
