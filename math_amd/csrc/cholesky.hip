@@ -276,22 +276,30 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       PANEL_EV((j << 16) | (t << 8) | 7);
       if (t < nb) panel_publish(&row[j * S + t], epoch);
       if (next) continue;
-      // A_tc -= L_tj L_cj^T for the panel's later column blocks c <= t
+      // A_tc -= L_tj L_cj^T for the panel's later column blocks c <= t.  The
+      // rows L_cj (c < t) are published by their owners at about the same
+      // time, so ONE wait covers all of them; the operands of update c + 1
+      // are then loaded while update c's product runs.
       const int clast = min(t, nb - 1);
+      const int cwait = min(clast, t - 1);  // L_tt's row is this tile's own
+      if (j + 1 <= cwait) panel_wait_all(row + j * S, j + 1, cwait, 1, epoch, status);
+      panel_regs Ryn, Rzn;
+      auto issue = [&](int c) {
+        const int cc = J + SMG_NB * c;
+        const bool own = c == t;
+        panel_gload(Rzn, L + rt0 + (size_t)cc * ldl, ldl, rt, min(SMG_NB, K - cc), own);
+        if (!own) panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
+      };
+      if (j + 1 <= clast) issue(j + 1);
       for (int c = j + 1; c <= clast; ++c) {
         const int cc = J + SMG_NB * c;
         const int bc = min(SMG_NB, K - cc);
         const bool own = c == t;  // L_cj is L_tj itself; A_tt: lower triangle
-        panel_regs Ry, Rz;
-        panel_gload(Rz, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
-        if (!own) {
-          panel_wait(&row[j * S + c], epoch, status);
-          panel_gload(Ry, L + cc + (size_t)cj * ldl, ldl, bc, bj, false);
-        }
         __syncthreads();  // previous product's Y / Z consumed
-        if (!own) panel_lstore(Y, Ry);
-        panel_lstore(Z, Rz);
+        if (!own) panel_lstore(Y, Ryn);
+        panel_lstore(Z, Rzn);
         __syncthreads();
+        if (c + 1 <= clast) issue(c + 1);  // in flight during this product
         lds_mma64_8w<false, true>(Z, D, own ? D : Y, -1.0, 1.0);
         panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
         PANEL_EV((j << 16) | (t << 8) | (16 + c));

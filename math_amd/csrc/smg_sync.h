@@ -37,3 +37,28 @@ __device__ inline void panel_wait(const int* flag, int epoch, int* status) {
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
+
+// panel_wait over flags[first], flags[first + stride], ..., flags[last]
+// (at most 64 flags): wave 0 polls them in parallel, one lane per flag, then
+// one barrier and ONE acquire fence for the whole set (so that the payload
+// loads issued after it can be prefetched without a fence between them)
+__device__ inline void panel_wait_all(const int* flags, int first, int last, int stride, int epoch,
+                                      int* status) {
+  if (threadIdx.x < 64) {
+    const int c = first + (int)threadIdx.x;
+    const bool mine = c <= last;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool seen = !mine;
+    while (true) {
+      if (!seen) seen = __hip_atomic_load(&flags[c * stride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (__all(seen)) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        if (threadIdx.x == 0) atomicOr(status, (int)SMG_ERR_SYNC);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
