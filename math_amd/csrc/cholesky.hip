@@ -145,7 +145,7 @@ __device__ inline void panel_gload(panel_regs& R, const double* A, int ld, int r
   for (int q = 0; q < 8; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
     const int c = e >> 6, r = e & 63;
-    R.v[q] = A[min(r, rows - 1) + (size_t)min(c, cols - 1) * ld];
+    R.v[q] = ld_dev(&A[min(r, rows - 1) + (size_t)min(c, cols - 1) * ld]);  // handed-off data: sc1
     R.ok |= (r < rows && c < cols && (!lower || r >= c)) ? (1u << q) : 0u;
   }
 }

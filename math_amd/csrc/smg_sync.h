@@ -1,11 +1,16 @@
 // Cross-workgroup hand-off primitives of the persistent kernels (the
 // Cholesky panel kernel, the persistent triangular solves).
 //
-// Producers store payload with device-scope (sc1) stores, so no XCD's L2
-// holds dirty payload and the release fence before a flag has nothing to
-// write back; the flag is a release store of the launch's epoch (no reset
-// launch between uses).  Consumers spin on a relaxed device-scope load (no
-// L2 invalidation per poll) and take ONE acquire fence once the flag is seen.
+// The fence-free form of MI355X_MICROARCH.md's hand-off table (row 1): the
+// producer stores every payload byte with device-scope (sc1) stores
+// (st_dev), EVERY storing wave waits for its own stores (s_waitcnt
+// vmcnt(0)), a workgroup barrier, then ONE lane stores the flag sc1; the
+// consumer polls the flag with sc1 loads, a workgroup barrier, and then reads
+// every payload byte with sc1 loads (ld_dev).  No release fence (an L2
+// write-back, ~1.7 us) and no acquire fence (an L1 invalidate, ~1.7 us) on
+// either side of a hand-off.  Requirements kept by the callers: payload in
+// hipMalloc memory, one workgroup per CU, every load of handed-off bytes an
+// ld_dev.  Flags carry the launch's epoch (no reset launch between uses).
 // Every wait gives up after ~4 s and latches SMG_ERR_SYNC, so a protocol
 // fault can never hang the device.
 #pragma once
@@ -15,11 +20,15 @@ __device__ __forceinline__ void st_dev(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ double ld_dev(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // all threads of the workgroup call it (barrier inside)
 __device__ inline void panel_publish(int* flag, int epoch) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 payload stores have landed
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // all threads of the workgroup call it (barrier inside)
@@ -34,14 +43,12 @@ __device__ inline void panel_wait(const int* flag, int epoch, int* status) {
       }
     }
   }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();  // the other waves read the payload after the polling wave saw the flag
 }
 
 // panel_wait over flags[first], flags[first + stride], ..., flags[last]
 // (at most 64 flags): wave 0 polls them in parallel, one lane per flag, then
-// one barrier and ONE acquire fence for the whole set (so that the payload
-// loads issued after it can be prefetched without a fence between them)
+// one barrier for the whole set
 __device__ inline void panel_wait_all(const int* flags, int first, int last, int stride, int epoch,
                                       int* status) {
   if (threadIdx.x < 64) {
@@ -59,6 +66,5 @@ __device__ inline void panel_wait_all(const int* flags, int first, int last, int
       }
     }
   }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();  // the other waves read the payload after the polling wave saw the flag
 }

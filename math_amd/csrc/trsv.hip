@@ -260,20 +260,7 @@ struct trsv_step {
 // everything else overlaps.  All n / 64 workgroups must be co-resident
 // (n / 64 <= 256 CUs; SMG_ERR_SYNC otherwise).
 __device__ inline void wait_strips(const int* f, int s0, int cnt, int epoch, int* status) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (int k = 0; k < cnt; ++k)
-      while (__hip_atomic_load(&f[s0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
-          atomicOr(status, (int)SMG_ERR_SYNC);
-          k = cnt;
-          break;
-        }
-      }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  panel_wait_all(f, s0, s0 + cnt - 1, 1, epoch, status);
 }
 
 template <bool TRANS>
@@ -288,6 +275,8 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
   // the y block it multiplies, so only LDS traffic and FMAs follow a flag.
   __shared__ double vp[256];
   __shared__ double part[256];
+  // (one workgroup per CU, the fence-free hand-off's residency rule in
+  // smg_sync.h: the 256 VGPRs of wv / lv leave one wave per SIMD)
   const int s = blockIdx.x, p = s >> 2, sub = s & 3, nb = n >> 8, ns = n >> 6;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   int* yf = flags;
@@ -305,7 +294,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
 #pragma unroll
       for (int k = 0; k < 64; ++k) lv[k] = Lc[(size_t)k * ldl];
       wait_strips(yf, 4 * q, 4, epoch, status);
-      vp[t] = y[256 * q + t];
+      vp[t] = ld_dev(&y[256 * q + t]);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 64; k += 2) {
@@ -321,7 +310,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
     panel_publish(&rf[s], epoch);
     // y rows 256 p + 64 sub + lane = W_p[64 sub + lane, :] r_p
     wait_strips(rf, 4 * p, 4, epoch, status);
-    vp[t] = r[256 * p + t];
+    vp[t] = ld_dev(&r[256 * p + t]);
     __syncthreads();
     acc0 = 0.0;
     acc1 = 0.0;
@@ -356,7 +345,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
         for (int cc = 0; cc < 16; ++cc)
           lv[16 * k + cc] = L[(256 * q + lane + 64 * k) + (size_t)(j0 + cc) * ldl];
       wait_strips(yf, 4 * q, 4, epoch, status);
-      vp[t] = y[256 * q + t];
+      vp[t] = ld_dev(&y[256 * q + t]);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -376,7 +365,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
     panel_publish(&rf[s], epoch);
     // y entries 256 p + 64 sub + 16 w + cc = (W_p^T r_p)[..] = W_p[:, col] . r_p
     wait_strips(rf, 4 * p, 4, epoch, status);
-    vp[t] = r[256 * p + t];
+    vp[t] = ld_dev(&r[256 * p + t]);
     __syncthreads();
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) acc[cc] = 0.0;

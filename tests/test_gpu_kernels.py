@@ -607,3 +607,43 @@ def test_gp_marginal_golden(ctx, N):
     assert ctx.status() == 0
     near_rel(fx, d["fx"], 1e-12, what="fx")
     near_rel(g, d["grad"], RTOL, what="grad")
+
+
+def test_handoff_stress_repeat_under_load(ctx):
+    """The persistent kernels' fence-free hand-offs (smg_sync.h: sc1 payload,
+    flag after every wave's vmcnt(0), sc1 loads after the poll) under uneven
+    load: the GP gradient at N = 4096 and 2048 (panel kernel + persistent
+    TRSVs) repeated while a second context keeps a large GEMM running on its
+    own stream; every repetition must reproduce the first bit for bit (a
+    stale read would not) and the first must match the reference."""
+    from math_amd import hip
+    other = hip.Context(0, 1 << 29)
+    try:
+        m = 4096
+        A = other.put(np.random.default_rng(1).uniform(-1, 1, m * m // 4))
+        C = other.zeros(m * m // 4)
+        for N in (4096, 2048):
+            d = golden(f"gp_N{N}") if N == 4096 else None
+            x = gen.unif(gen.SEED + 7, N, -10.0, 10.0)
+            y = np.sin(x)
+            theta = (1.0, 1.5, 0.3)
+            if d is not None:
+                x, y, theta = d["x"], d["y"], d["theta"]
+            runs = []
+            for rep in range(6):
+                if rep % 2 == 1:  # the other stream busy while this one runs
+                    other.call("smg_gemm", 0, 1, 0, m // 2, m // 2, m // 2, 1e-3, A, m // 2, A, m // 2, 1.0, C,
+                               m // 2)
+                m0 = ctx.mark()
+                runs.append(gp_gradient_abi(ctx, x, y, theta))
+                assert ctx.status() == 0
+                ctx.rewind(m0)
+            fx0, g0 = runs[0]
+            for fx, g in runs[1:]:
+                assert fx == fx0 and np.array_equal(g, g0), (N, fx, fx0, g, g0)
+            if d is not None:
+                near_rel(fx0, d["fx"], 1e-12, what="fx")
+                near_rel(g0, d["grad"], RTOL, what="grad")
+        other.sync()
+    finally:
+        other.close()
