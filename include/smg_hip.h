@@ -154,6 +154,12 @@ int smg_cholesky_block_size(int n);
 int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n);
 int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L,
                      int ldl, double* aux);
+/* check_symmetric(A) (tolerance 1e-8, prim/mat/err/check_symmetric.hpp:37-52)
+ * fused with smg_cholesky_fwd's copy of A into L -- one pass over A; the
+ * status latches SMG_ERR_NOT_SYMMETRIC and / or SMG_ERR_NOT_PD.  Replaces
+ * smg_check_symmetric followed by smg_cholesky_fwd. */
+int smg_cholesky_fwd_checked(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                             double* Dinv);
 int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux,
                      double* Ladj, int ldla, int n, double* Aadj, int ldaa);
 

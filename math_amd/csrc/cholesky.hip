@@ -59,6 +59,42 @@ __global__ __launch_bounds__(256) void k_check_symmetric(const double* __restric
   if (__any(bad) && lane == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
 }
 
+// k_check_symmetric fused with the copy of A's lower triangle into L (zeros
+// above): one pass over A instead of two.  Tile pair (bi, bj), bj <= bi:
+// L's lower tile (bi, bj) from A's, L's upper tile (bj, bi) zero.
+__global__ __launch_bounds__(256) void k_check_symmetric_copy(const double* __restrict__ A, int lda,
+                                                              int n, int* status,
+                                                              double* __restrict__ L, int ldl) {
+  __shared__ double T[64][65];
+  int bi, bj;
+  {
+    const int t = blockIdx.x;
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    bi = r;
+    bj = t - r * (r + 1) / 2;
+  }
+  const int i0 = 64 * bi, j0 = 64 * bj;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int c = w; c < 64; c += 4) {
+    const int gr = j0 + lane, gc = i0 + c;
+    T[c][lane] = (gr < n && gc < n) ? A[gr + (size_t)gc * lda] : 0.0;
+  }
+  __syncthreads();
+  bool bad = false;
+  for (int c = w; c < 64; c += 4) {
+    const int gr = i0 + lane, gc = j0 + c;
+    if (gr < n && gc < n) {
+      const double a = A[gr + (size_t)gc * lda];
+      if (gr > gc) bad |= !(fabs(a - T[lane][c]) <= 1e-8);
+      L[gr + (size_t)gc * ldl] = gr >= gc ? a : 0.0;
+    }
+    if (bi != bj && j0 + lane < n && i0 + c < n) L[(j0 + lane) + (size_t)(i0 + c) * ldl] = 0.0;
+  }
+  if (__any(bad) && lane == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
+}
+
 __global__ void k_copy_lower(const double* __restrict__ A, int lda, int n,
                              double* __restrict__ L, int ldl) {
   for (smg_mn it(n, n); it.ok(); it.next()) {
@@ -609,6 +645,9 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
   return SMG_OK;
 }
 
+int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
+             bool check_sym);
+
 }  // namespace
 
 extern "C" {
@@ -632,6 +671,20 @@ int smg_check_symmetric(smg_ctx* ctx, const double* A, int lda, int n) {
 
 int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                      double* Dinv) {
+  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, false);
+}
+
+int smg_cholesky_fwd_checked(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                             double* Dinv) {
+  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true);
+}
+
+}  // extern "C"
+
+namespace {
+
+int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
+             bool check_sym) {
   if (!ctx || n < 0 || (n > 0 && (!A || !L || lda < n || ldl < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_FWD);
@@ -641,9 +694,18 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
     if (!aux) return SMG_ERR_OOM;
   }
   Dinv = aux;  // the SMG_NB level comes first
-  if (A != L || lda != ldl)
-    hipLaunchKernelGGL(k_copy_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
-                       A, lda, n, L, ldl);
+  const int tb = smg_ceil_div(n, 64);
+  if (A != L || lda != ldl) {
+    if (check_sym)
+      hipLaunchKernelGGL(k_check_symmetric_copy, dim3(tb * (tb + 1) / 2), dim3(256), 0, ctx->stream, A,
+                         lda, n, ctx->status_d, L, ldl);
+    else
+      hipLaunchKernelGGL(k_copy_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
+                         A, lda, n, L, ldl);
+  } else if (check_sym) {
+    hipLaunchKernelGGL(k_check_symmetric, dim3(tb * (tb + 1) / 2), dim3(256), 0, ctx->stream, A, lda,
+                       n, ctx->status_d);
+  }
   // Two-level right-looking: panels of SMG_NBF columns factored with SMG_NB
   // steps whose updates stay inside the panel (all rows below), then ONE
   // rank-SMG_NBF update of the trailing matrix per panel (compute-bound, vs a
@@ -717,6 +779,10 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, i
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv, double* La,
                      int ldla, int n, double* Aadj, int ldaa) {

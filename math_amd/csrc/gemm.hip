@@ -461,6 +461,12 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   // the diagonal, and the split-K those few tiles need costs a reduction)
   if (MODE == 0 && big_tiles >= 256 && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  // long-K transposed-A products with a small output (the Murray reverse's
+  // [R_adj | D_adj] -= C_adj^T [B | C]: 512 x K x m, m >= 1536): 128 x 64
+  // tiles split over K (tools/ubench_gemm: (512,2048,2048) 87 vs 100 us,
+  // (512,1024,3072) 68 vs 81 us with 32 x 32)
+  if (MODE == 0 && TA && !TB && k >= 1536 && mid_tiles < 512)
+    return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
   // 64 x 64 only when its grid fills two workgroups per CU without split-K:
   // below that, 32 x 32 tiles (4x the workgroups) beat a split 64 x 64 grid
   // (tools/ubench_gemm: (3584,256,256) 18.6 vs 28 us)

@@ -54,6 +54,7 @@ _SIGS = {
     "smg_cholesky_block_size": (_I, [_I]),
     "smg_check_symmetric": (_I, [_P, _P, _I, _I]),
     "smg_cholesky_fwd": (_I, [_P, _P, _I, _I, _P, _I, _P]),
+    "smg_cholesky_fwd_checked": (_I, [_P, _P, _I, _I, _P, _I, _P]),
     "smg_cholesky_rev": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_fwd": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_rev": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P]),

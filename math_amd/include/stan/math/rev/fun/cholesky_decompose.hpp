@@ -96,10 +96,10 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   const int n = A.rows();
   smg_ctx* c = amd::ctx();
   if (n == 0) return dev_var_matrix(new dev_matrix_vari(0, 0, dev_structure::lower));
-  amd::check(smg_check_symmetric(c, A.val_ptr(), n, n), fn);
   auto* L = new dev_matrix_vari(n, n, dev_structure::lower);
   L->aux_ = amd::alloc_doubles(size_t(smg_cholesky_aux_doubles(n)));
-  amd::check(smg_cholesky_fwd(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
+  // check_symmetric fused with the factorisation's copy of A (one pass)
+  amd::check(smg_cholesky_fwd_checked(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
   int st = 0;
   amd::check(smg_status(c, &st), fn);
   if (st & SMG_ERR_NOT_SYMMETRIC) amd::throw_status(SMG_ERR_NOT_SYMMETRIC, fn, "A");

@@ -647,3 +647,30 @@ def test_handoff_stress_repeat_under_load(ctx):
         other.sync()
     finally:
         other.close()
+
+
+@pytest.mark.parametrize("N", [70, 300, 1000])
+def test_cholesky_fwd_checked(ctx, N):
+    """check_symmetric fused with the factorisation's copy: the same L and aux
+    as smg_cholesky_fwd on a symmetric input; NOT_SYMMETRIC latched (and the
+    upper triangle of L still zero) on an asymmetric one."""
+    rng = np.random.default_rng(N + 5)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + np.eye(N)
+    A = 0.5 * (A + A.T)
+    na = ctx.lib.smg_cholesky_aux_doubles(N)
+    dA = ctx.put(F(A))
+    L1, D1 = ctx.put(np.full(N * N, 7.0)), ctx.zeros(na)
+    L2, D2 = ctx.put(np.full(N * N, 7.0)), ctx.zeros(na)
+    ctx.call("smg_cholesky_fwd", dA, N, N, L1, N, D1)
+    ctx.call("smg_cholesky_fwd_checked", dA, N, N, L2, N, D2)
+    assert ctx.status() == 0
+    assert np.array_equal(ctx.get(L1, N * N), ctx.get(L2, N * N))
+    assert np.array_equal(ctx.get(D1, na), ctx.get(D2, na))
+    A[N - 1, N // 2] += 1e-6
+    dA = ctx.put(F(A))
+    L3 = ctx.put(np.full(N * N, 7.0))
+    ctx.call("smg_cholesky_fwd_checked", dA, N, N, L3, N, ctx.zeros(na))
+    assert ctx.status() & 4
+    L = ctx.get(L3, N * N).reshape(N, N, order="F")
+    assert np.all(np.triu(L, 1) == 0.0)
