@@ -263,6 +263,24 @@ __device__ inline void wait_strips(const int* f, int s0, int cnt, int epoch, int
   panel_wait_all(f, s0, s0 + cnt - 1, 1, epoch, status);
 }
 
+// Column sums of the backward solve's per-lane partials: acc[cc] on lane l of
+// wave w is the partial of column 16 w + cc over rows l, l + 64, ...; the 64
+// column sums land in part[0 .. 63].  One LDS transpose and a 4-lane
+// reduction instead of 16 full-wave reductions per wave.
+__device__ __forceinline__ void cols_reduce(const double (&acc)[16], double (*red)[65], double* part) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int cc = 0; cc < 16; ++cc) red[16 * w + cc][lane] = acc[cc];
+  __syncthreads();
+  const int c = t >> 2, q = t & 3;
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v += red[c][16 * q + k];
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  if (q == 0) part[c] = v;
+}
+
 template <bool TRANS>
 __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__ L, int ldl,
                                                       const double* __restrict__ W, int ldw,
@@ -275,6 +293,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
   // the y block it multiplies, so only LDS traffic and FMAs follow a flag.
   __shared__ double vp[256];
   __shared__ double part[256];
+  __shared__ double red[TRANS ? 64 : 1][65];
   // (one workgroup per CU, the fence-free hand-off's residency rule in
   // smg_sync.h: the 256 VGPRs of wv / lv leave one wave per SIMD)
   const int s = blockIdx.x, p = s >> 2, sub = s & 3, nb = n >> 8, ns = n >> 6;
@@ -355,11 +374,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
       }
       __syncthreads();
     }
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      const double v = wave_sum(acc[cc]);
-      if (lane == cc) part[16 * w + cc] = v;
-    }
+    cols_reduce(acc, red, part);
     __syncthreads();
     if (t < 64) st_dev(&r[64 * s + t], x[64 * s + t] - part[t]);
     panel_publish(&rf[s], epoch);
@@ -375,11 +390,7 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) acc[cc] += wv[16 * k + cc] * v;
     }
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      const double v = wave_sum(acc[cc]);
-      if (lane == cc) part[16 * w + cc] = v;
-    }
+    cols_reduce(acc, red, part);
     __syncthreads();
     if (t < 64) st_dev(&y[256 * p + 64 * sub + t], part[t]);
     panel_publish(&yf[s], epoch);
