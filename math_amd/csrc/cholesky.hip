@@ -268,15 +268,9 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       PANEL_EV((j << 16) | (t << 8) | 12);
       lds_mma64_8w<false, true>(Y, Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T (private)
       PANEL_EV((j << 16) | (t << 8) | 13);
-      lds_mma64_8w<false, true>(Zn, Y, Y, -1.0, 1.0);  // A_tt -= L_tj L_tj^T
-      // the factorisation's input: lower triangle, zero strict upper (the
-      // symmetric update filled it), identity padding beyond bt
-      for (int e = threadIdx.x; e < SMG_NB * SMG_NB; e += blockDim.x) {
-        const int r = e >> 6, c = e & 63;
-        if (c > r) Zn[r * SMG_NBP + c] = 0.0;
-        else if (r == c && r >= bt) Zn[r * SMG_NBP + c] = 1.0;
-      }
-      __syncthreads();
+      // A_tt -= L_tj L_tj^T, written as the factorisation's input: lower
+      // triangle, zero strict upper, identity padding beyond bt
+      lds_syrk64_8w_next(Zn, Y, bt);
       double* tmp = Dc;
       Dc = Zn;
       Zn = tmp;

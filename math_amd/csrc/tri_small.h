@@ -99,6 +99,39 @@ __device__ inline void lds_mma64_8w(double* C, const double* A, const double* B,
   __syncthreads();
 }
 
+// The panel chain's next diagonal block: C = C - A A^T (A, C: 64 x 64 in
+// LDS), written straight in the factorisation's input form -- lower triangle,
+// zero strict upper, identity padding beyond row / column b -- so no separate
+// pass over C follows
+__device__ inline void lds_syrk64_8w_next(double* C, const double* A, int b) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = l & 15, fk = l >> 4;
+  const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
+  d4 acc[2];
+  acc[0] = d4{0.0, 0.0, 0.0, 0.0};
+  acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < SMG_NB; k0 += 4) {
+    const int kk = k0 + fk;
+    const double a = A[i * SMG_NBP + kk];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = 16 * (t0 + t) + fr;
+      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, A[j * SMG_NBP + kk], acc[t], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * (w & 3) + fk + 4 * r, col = 16 * (t0 + t) + fr;
+      double* c = &C[row * SMG_NBP + col];
+      *c = col > row ? 0.0 : (row == col && row >= b ? 1.0 : *c - acc[t][r]);
+    }
+  __syncthreads();
+}
+
 // One wave: Cholesky of the 16x16 leaf p of D (lower), then its inverse into X.
 // Latches SMG_ERR_NOT_PD (check_pos_definite, prim/mat/err/check_pos_definite.hpp:77-81).
 __device__ inline void wave_leaf_potrf_inv(double* D, double* X, int p, int* status) {
