@@ -114,6 +114,7 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
   // the Cholesky forward's aux holds the 64- and 256-row diagonal-block
   // inverses (smg_cholesky_aux_doubles); without it, build the 64-row level
   const double* W256 = nullptr;
+  const double* W512 = nullptr;
   if (!Dinv) {
     double* W = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_NB);
     if (!W) return SMG_ERR_OOM;
@@ -122,11 +123,12 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
     Dinv = W;
   } else {
     W256 = Dinv + (size_t)n * SMG_AUX_W256;
+    W512 = Dinv + (size_t)n * SMG_AUX_W512;
   }
   hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(256), 0, ctx->stream, y, mu, n, res);
-  rc = smg_trsv_lower_impl(ctx, 0, L, ldl, Dinv, W256, n, res, w, r, n);  // w = L^{-1}(y - mu)
+  rc = smg_trsv_lower_impl(ctx, 0, L, ldl, Dinv, W256, W512, n, res, w, r, n);  // w = L^{-1}(y - mu)
   if (rc) return rc;
-  rc = smg_trsv_lower_impl(ctx, 1, L, ldl, Dinv, W256, n, w, sd, r, n);  // sd = L^{-T} w
+  rc = smg_trsv_lower_impl(ctx, 1, L, ldl, Dinv, W256, W512, n, w, sd, r, n);  // sd = L^{-T} w
   if (rc) return rc;
   hipLaunchKernelGGL(k_mvn_lp, dim3(1), dim3(1024), 0, ctx->stream, w, L, ldl, n, out_lp);
   SMG_LAUNCH_CHECK();

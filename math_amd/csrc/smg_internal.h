@@ -118,7 +118,8 @@ int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* 
                   double alpha, int accumulate);
 int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,
-                        const double* W256, int ldw, const double* x, double* y, double* r, int n);
+                        const double* W256, const double* W512, int ldw, const double* x, double* y,
+                        double* r, int n);
 
 // internal GEMM entry used by other units (no argument re-validation)
 int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,

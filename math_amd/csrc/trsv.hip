@@ -264,56 +264,62 @@ __device__ inline void wait_strips(const int* f, int s0, int cnt, int epoch, int
 }
 
 // Column sums of the backward solve's per-lane partials: acc[cc] on lane l of
-// wave w is the partial of column 16 w + cc over rows l, l + 64, ...; the 64
-// column sums land in part[0 .. 63].  One LDS transpose and a 4-lane
-// reduction instead of 16 full-wave reductions per wave.
-__device__ __forceinline__ void cols_reduce(const double (&acc)[16], double (*red)[65], double* part) {
+// wave w is the partial of column 16 (w & 3) + cc over rows 256 (w >> 2) + l,
+// + 64, ...; the 64 column sums land in part[0 .. 63].  One LDS transpose and
+// a (4 H)-lane reduction instead of 16 full-wave reductions per wave.
+template <int H>
+__device__ __forceinline__ void cols_reduce(const double (&acc)[16], double (*red)[64][65], double* part) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
-  for (int cc = 0; cc < 16; ++cc) red[16 * w + cc][lane] = acc[cc];
+  for (int cc = 0; cc < 16; ++cc) red[w >> 2][16 * (w & 3) + cc][lane] = acc[cc];
   __syncthreads();
-  const int c = t >> 2, q = t & 3;
+  const int c = t / (4 * H), q = t % (4 * H);
   double v = 0.0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) v += red[c][16 * q + k];
+  for (int k = 0; k < 16; ++k) v += red[q >> 2][c][16 * (q & 3) + k];
   v += __shfl_xor(v, 1);
   v += __shfl_xor(v, 2);
+  if (H == 2) v += __shfl_xor(v, 4);
   if (q == 0) part[c] = v;
 }
 
-template <bool TRANS>
-__global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__ L, int ldl,
-                                                      const double* __restrict__ W, int ldw,
-                                                      const double* __restrict__ x,
-                                                      double* __restrict__ y,
-                                                      double* __restrict__ r, int n, int* flags,
-                                                      int epoch, int* status) {
+// BS: the diagonal-block size of the inverses used (256 or 512); BS threads
+// per workgroup, G = BS / 64 strips per block.
+template <bool TRANS, int BS>
+__global__ __launch_bounds__(BS) void k_trsv_persist(const double* __restrict__ L, int ldl,
+                                                     const double* __restrict__ W, int ldw,
+                                                     const double* __restrict__ x,
+                                                     double* __restrict__ y,
+                                                     double* __restrict__ r, int n, int* flags,
+                                                     int epoch, int* status) {
   // Operand reads never wait on a flag: this strip's W_p slice is loaded into
   // registers at entry, and each block of L is loaded before the wait for
   // the y block it multiplies, so only LDS traffic and FMAs follow a flag.
-  __shared__ double vp[256];
-  __shared__ double part[256];
-  __shared__ double red[TRANS ? 64 : 1][65];
+  constexpr int G = BS / 64, H = BS / 256;
+  __shared__ double vp[BS];
+  __shared__ double part[BS];
+  __shared__ double red[TRANS ? H : 1][64][65];
   // (one workgroup per CU, the fence-free hand-off's residency rule in
-  // smg_sync.h: the 256 VGPRs of wv / lv leave one wave per SIMD)
-  const int s = blockIdx.x, p = s >> 2, sub = s & 3, nb = n >> 8, ns = n >> 6;
+  // smg_sync.h: the 256 VGPRs of wv / lv leave room for BS / 256 waves per
+  // SIMD, i.e. this one workgroup)
+  const int s = blockIdx.x, p = s / G, sub = s % G, nb = n / BS, ns = n >> 6;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   int* yf = flags;
   int* rf = flags + ns;
   double wv[64], lv[64];
   if (!TRANS) {
-    // thread (row 64 s + lane, quarter w of each 256-column block)
+    // thread (row 64 s + lane, 64-column slice w of each BS-column block)
     const int i = 64 * s + lane;
-    const double* Wr = W + (256 * p + 64 * sub + lane) + (size_t)(64 * w) * ldw;
+    const double* Wr = W + (BS * p + 64 * sub + lane) + (size_t)(64 * w) * ldw;
 #pragma unroll
     for (int k = 0; k < 64; ++k) wv[k] = Wr[(size_t)k * ldw];
     double acc0 = 0.0, acc1 = 0.0;
     for (int q = 0; q < p; ++q) {
-      const double* Lc = L + i + (size_t)(256 * q + 64 * w) * ldl;
+      const double* Lc = L + i + (size_t)(BS * q + 64 * w) * ldl;
 #pragma unroll
       for (int k = 0; k < 64; ++k) lv[k] = Lc[(size_t)k * ldl];
-      wait_strips(yf, 4 * q, 4, epoch, status);
-      vp[t] = ld_dev(&y[256 * q + t]);
+      wait_strips(yf, G * q, G, epoch, status);
+      vp[t] = ld_dev(&y[BS * q + t]);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 64; k += 2) {
@@ -324,12 +330,16 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
     }
     part[t] = acc0 + acc1;
     __syncthreads();
-    if (w == 0)
-      st_dev(&r[i], x[i] - ((part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane])));
+    if (w == 0) {
+      double sum = 0.0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) sum += part[64 * g + lane];
+      st_dev(&r[i], x[i] - sum);
+    }
     panel_publish(&rf[s], epoch);
-    // y rows 256 p + 64 sub + lane = W_p[64 sub + lane, :] r_p
-    wait_strips(rf, 4 * p, 4, epoch, status);
-    vp[t] = ld_dev(&r[256 * p + t]);
+    // y rows BS p + 64 sub + lane = W_p[64 sub + lane, :] r_p
+    wait_strips(rf, G * p, G, epoch, status);
+    vp[t] = ld_dev(&r[BS * p + t]);
     __syncthreads();
     acc0 = 0.0;
     acc1 = 0.0;
@@ -340,59 +350,64 @@ __global__ __launch_bounds__(256) void k_trsv_persist(const double* __restrict__
     }
     part[t] = acc0 + acc1;
     __syncthreads();
-    if (w == 0)
-      st_dev(&y[i], (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]));
+    if (w == 0) {
+      double sum = 0.0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) sum += part[64 * g + lane];
+      st_dev(&y[i], sum);
+    }
     panel_publish(&yf[s], epoch);
   } else {
-    // wave w: 16 columns j = 64 s + 16 w + cc of L (rows of L^T); lanes run
-    // down the contiguous column segments (rows lane + 64 k of a block);
-    // one wave reduction per column at the end
-    const int c0 = 64 * sub + 16 * w;
+    // wave w: 16 columns j = 64 s + 16 (w & 3) + cc of L (rows of L^T) over
+    // the row half h = w >> 2 of a BS-row block; lanes run down the
+    // contiguous column segments (rows 256 h + lane + 64 k of a block)
+    const int h = w >> 2;
+    const int c0 = 64 * sub + 16 * (w & 3);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc)
-        wv[16 * k + cc] = W[(256 * p + lane + 64 * k) + (size_t)(c0 + cc) * ldw];
+        wv[16 * k + cc] = W[(BS * p + 256 * h + lane + 64 * k) + (size_t)(c0 + cc) * ldw];
     double acc[16];
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) acc[cc] = 0.0;
-    const int j0 = 64 * s + 16 * w;
+    const int j0 = 64 * s + 16 * (w & 3);
     for (int q = nb - 1; q > p; --q) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
 #pragma unroll
         for (int cc = 0; cc < 16; ++cc)
-          lv[16 * k + cc] = L[(256 * q + lane + 64 * k) + (size_t)(j0 + cc) * ldl];
-      wait_strips(yf, 4 * q, 4, epoch, status);
-      vp[t] = ld_dev(&y[256 * q + t]);
+          lv[16 * k + cc] = L[(BS * q + 256 * h + lane + 64 * k) + (size_t)(j0 + cc) * ldl];
+      wait_strips(yf, G * q, G, epoch, status);
+      vp[t] = ld_dev(&y[BS * q + t]);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const double v = vp[lane + 64 * k];
+        const double v = vp[256 * h + lane + 64 * k];
 #pragma unroll
         for (int cc = 0; cc < 16; ++cc) acc[cc] += lv[16 * k + cc] * v;
       }
       __syncthreads();
     }
-    cols_reduce(acc, red, part);
+    cols_reduce<H>(acc, red, part);
     __syncthreads();
     if (t < 64) st_dev(&r[64 * s + t], x[64 * s + t] - part[t]);
     panel_publish(&rf[s], epoch);
-    // y entries 256 p + 64 sub + 16 w + cc = (W_p^T r_p)[..] = W_p[:, col] . r_p
-    wait_strips(rf, 4 * p, 4, epoch, status);
-    vp[t] = ld_dev(&r[256 * p + t]);
+    // y entries BS p + 64 sub + 16 (w & 3) + cc = W_p[:, col] . r_p
+    wait_strips(rf, G * p, G, epoch, status);
+    vp[t] = ld_dev(&r[BS * p + t]);
     __syncthreads();
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) acc[cc] = 0.0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const double v = vp[lane + 64 * k];
+      const double v = vp[256 * h + lane + 64 * k];
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) acc[cc] += wv[16 * k + cc] * v;
     }
-    cols_reduce(acc, red, part);
+    cols_reduce<H>(acc, red, part);
     __syncthreads();
-    if (t < 64) st_dev(&y[256 * p + 64 * sub + t], part[t]);
+    if (t < 64) st_dev(&y[BS * p + 64 * sub + t], part[t]);
     panel_publish(&yf[s], epoch);
   }
 }
@@ -403,20 +418,33 @@ constexpr int TRSV_FLAG_OFFSET = 256;
 }  // namespace
 
 // y = L^{-1} x (trans = 0) or L^{-T} x (trans = 1); L lower.  W64: the 64-row
-// diagonal-block inverses (n x 64, ld ldw); W256: the 256-row ones (n x 256,
-// ld ldw) or NULL.  r: n-double workspace.
+// diagonal-block inverses (n x 64, ld ldw); W256 / W512: the 256- / 512-row
+// ones (ld ldw) or NULL.  r: n-double workspace.  The persistent solve takes
+// n / BS block steps, so the 512-row level halves its hand-offs.
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,
-                        const double* W256, int ldw, const double* x, double* y, double* r, int n) {
+                        const double* W256, const double* W512, int ldw, const double* x, double* y,
+                        double* r, int n) {
   if (n <= 0) return SMG_OK;
-  if (W256 && n % 256 == 0 && n >= 512 && n / 64 <= 256 &&
-      TRSV_FLAG_OFFSET + 2 * (n / 64) <= 4096) {
+  const bool fits = n / 64 <= 256 && TRSV_FLAG_OFFSET + 2 * (n / 64) <= 4096;
+  // forward only: the backward's 512-row form needs 32 more VGPRs per lane
+  // than two waves per SIMD leave and spills (100 vs 83 us at n = 4096);
+  // the forward's spills less and gains (65 vs 75 us)
+  if (fits && !trans && W512 && n % 512 == 0 && n >= 1024) {
+    const int epoch = ++ctx->flag_epoch;
+    int* f = ctx->flags_d + TRSV_FLAG_OFFSET;
+    hipLaunchKernelGGL((k_trsv_persist<false, 512>), dim3(n / 64), dim3(512), 0, ctx->stream, L, ldl,
+                       W512, ldw, x, y, r, n, f, epoch, ctx->status_d);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
+  if (fits && W256 && n % 256 == 0 && n >= 512) {
     const int epoch = ++ctx->flag_epoch;
     int* f = ctx->flags_d + TRSV_FLAG_OFFSET;
     if (trans)
-      hipLaunchKernelGGL(k_trsv_persist<true>, dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl, W256,
-                         ldw, x, y, r, n, f, epoch, ctx->status_d);
+      hipLaunchKernelGGL((k_trsv_persist<true, 256>), dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl,
+                         W256, ldw, x, y, r, n, f, epoch, ctx->status_d);
     else
-      hipLaunchKernelGGL(k_trsv_persist<false>, dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl,
+      hipLaunchKernelGGL((k_trsv_persist<false, 256>), dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl,
                          W256, ldw, x, y, r, n, f, epoch, ctx->status_d);
     SMG_LAUNCH_CHECK();
     return SMG_OK;
