@@ -622,7 +622,7 @@ def test_handoff_stress_repeat_under_load(ctx):
         m = 4096
         A = other.put(np.random.default_rng(1).uniform(-1, 1, m * m // 4))
         C = other.zeros(m * m // 4)
-        for N in (4096, 2048):
+        for N in (4096, 2048, 1024):
             d = golden(f"gp_N{N}") if N == 4096 else None
             x = gen.unif(gen.SEED + 7, N, -10.0, 10.0)
             y = np.sin(x)
@@ -630,7 +630,7 @@ def test_handoff_stress_repeat_under_load(ctx):
             if d is not None:
                 x, y, theta = d["x"], d["y"], d["theta"]
             runs = []
-            for rep in range(6):
+            for rep in range(16):
                 if rep % 2 == 1:  # the other stream busy while this one runs
                     other.call("smg_gemm", 0, 1, 0, m // 2, m // 2, m // 2, 1e-3, A, m // 2, A, m // 2, 1.0, C,
                                m // 2)
