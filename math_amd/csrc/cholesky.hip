@@ -551,6 +551,9 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
   const bool side = smg_side_begin(ctx) == SMG_OK;
   int nev = 0;
   hipEvent_t F = nullptr;
+  // the C_adj D^{-1} workspace at its largest (m grows as P falls), so that
+  // no block reallocates it (a reallocation synchronises the streams)
+  if (n > SMG_NBR && !smg_ws(ctx, SMG_WS_CW, (size_t)(n - SMG_NBR) * SMG_NBR)) return SMG_ERR_OOM;
   for (int P = nbo - 1; P >= 0; --P) {
     if (F) {
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
@@ -563,10 +566,20 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
     double* Da = La + J + (size_t)J * ldla;
     const double* Ld = L + J + (size_t)J * ldl;
     const double* Wp = W + J;  // this block's inverse, ld n
+    // C_adj D^{-1} of a full block goes to a workspace (Cw, ld m) that the two
+    // updates read; its copy back into La (read again only by the final
+    // accumulation into A's adjoint) runs on the side stream behind B_adj
+    const double* Cr = Ca;
+    int ldcr = ldla;
+    double* Cw = nullptr;
     if (m > 0) {
       if (full) {  // C_adj = C_adj D^{-1}
-        rc = smg_gemm_impl(ctx, 0, 0, 0, m, bs, bs, 1.0, Ca, ldla, Wp, n, 0.0, Ca, ldla);
+        Cw = smg_ws(ctx, SMG_WS_CW, (size_t)m * bs);
+        if (!Cw) return SMG_ERR_OOM;
+        rc = smg_gemm_impl(ctx, 0, 0, 0, m, bs, bs, 1.0, Ca, ldla, Wp, n, 0.0, Cw, m);
         if (rc) return rc;
+        Cr = Cw;
+        ldcr = m;
       } else {  // ragged: blocked right solve with the SMG_NB inverses
         const int nbi = (bs + SMG_NB - 1) / SMG_NB;
         for (int q = nbi - 1; q >= 0; --q) {
@@ -590,20 +603,26 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
           SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
           {
             smg_on_side on(ctx);
-            rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Ca, ldla, L + J, ldl, 1.0, La + K, ldla);
+            rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Cr, ldcr, L + J, ldl, 1.0, La + K, ldla);
+            if (!rc && Cw) rc = smg_copy_impl(ctx, m, bs, Cw, m, Ca, ldla, 1.0, 0);
           }
           if (rc) return rc;
+          Cw = nullptr;  // copied back on the side stream
           F = smg_event(ctx, nev++);
           if (!F) return SMG_ERR_HIP;
           SMG_HIP_TRY(hipEventRecord(F, ctx->side));
         } else {
-          rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Ca, ldla, L + J, ldl, 1.0, La + K, ldla);
+          rc = smg_gemm_impl(ctx, 0, 0, 0, m, J, bs, -1.0, Cr, ldcr, L + J, ldl, 1.0, La + K, ldla);
           if (rc) return rc;
         }
       }
       // [R_adj | D_adj] -= C_adj^T [B | C]
-      rc = smg_gemm_impl(ctx, 1, 0, 0, bs, K, m, -1.0, Ca, ldla, L + K, ldl, 1.0, La + J, ldla);
+      rc = smg_gemm_impl(ctx, 1, 0, 0, bs, K, m, -1.0, Cr, ldcr, L + K, ldl, 1.0, La + J, ldla);
       if (rc) return rc;
+      if (Cw) {  // no side-stream copy was queued
+        rc = smg_copy_impl(ctx, m, bs, Cw, m, Ca, ldla, 1.0, 0);
+        if (rc) return rc;
+      }
     }
     double* Pm;
     if (full) {

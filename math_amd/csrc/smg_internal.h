@@ -48,8 +48,8 @@ struct smg_ctx {
   void* host_scratch;
   size_t host_scratch_size;
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[7];
-  size_t ws_doubles[7];
+  double* ws[8];  // SMG_WS_COUNT
+  size_t ws_doubles[8];
   // profiling
   int prof_on;
   std::vector<smg_prof_slot> prof_pending;
@@ -93,7 +93,8 @@ struct smg_prof_scope {
 // named persistent workspaces (grow on demand; a growth synchronises the
 // stream, so steady-state evaluations never reallocate)
 enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_ALIAS = 4,
-       SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_COUNT = 7 };
+       SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_COUNT = 8 };
+static_assert(SMG_WS_COUNT == sizeof(((smg_ctx*)nullptr)->ws) / sizeof(double*), "workspace slots");
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 
 // side-stream helpers (ctx.hip): events come from a per-context pool
