@@ -631,8 +631,10 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
       double* S = G + bb;
       double* T = S + bb;
       const int gb = grid_for((long long)bb);
-      rc = smg_gemm_symtril_impl(ctx, bs, bs, Ld, ldl, Da, ldla, S, bs);  // sym(D^T tril(Dadj))
+      hipLaunchKernelGGL(k_tril_copy, dim3(gb), dim3(256), 0, ctx->stream, Da, ldla, bs, G);
+      rc = smg_gemm_impl(ctx, 1, 0, 0, bs, bs, bs, 1.0, Ld, ldl, G, bs, 0.0, S, bs);  // D^T tril(Dadj)
       if (rc) return rc;
+      hipLaunchKernelGGL(k_mirror_lower, dim3(gb), dim3(256), 0, ctx->stream, S, bs);
       rc = smg_gemm_impl(ctx, 1, 0, 0, bs, bs, bs, 1.0, Wp, n, S, bs, 0.0, T, bs);  // D^{-T} S
       if (rc) return rc;
       rc = smg_gemm_impl(ctx, 0, 0, 0, bs, bs, bs, 1.0, T, bs, Wp, n, 0.0, S, bs);  // ... D^{-1}

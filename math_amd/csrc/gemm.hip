@@ -68,7 +68,7 @@ __device__ double g_gemm_zero[2] = {0.0, 0.0};  // global (not constant) address
 // to its LDS store.  (A select on the loaded value lets the scheduler hoist
 // the select -- and with it a wait for that load -- ahead of the previous
 // stage's MFMAs, which serialises the prefetch.)
-template <int BM, int BK, bool KCONTIG, bool TRI = false>
+template <int BM, int BK, bool KCONTIG>
 __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
                                           int rows, int k, int i0, int k0,
                                           double (&r)[BM * BK / 256]) {
@@ -86,8 +86,7 @@ __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
     }
     const int gi = i0 + i, gk = k0 + kk;
     const double* p = KCONTIG ? X + ((size_t)gi * ld + gk) : X + (gi + (size_t)gk * ld);
-    // TRI: the operand is lower triangular in (k, i) -- entries with k < i read as zero
-    r[q] = *((gi < rows && gk < k && (!TRI || gk >= gi)) ? p : g_gemm_zero);
+    r[q] = *((gi < rows && gk < k) ? p : g_gemm_zero);
   }
 }
 
@@ -118,10 +117,7 @@ __device__ __forceinline__ void tri_decode(int t, int& bi, int& bj) {
   bj = t - r * (r + 1) / 2;
 }
 
-// MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n),
-// 3 = sym(op(A) tril(B)): B read as its lower triangle, the lower triangle of
-// the product computed and written to both triangles of C (beta = 0, no
-// split-K; the Murray reverse's symbolic step, D^T tril(Dadj) symmetrised)
+// MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n)
 template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
 __global__ __launch_bounds__(256) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
@@ -175,7 +171,7 @@ __global__ __launch_bounds__(256) void k_gemm(
   // (tri_decode); trapezoidal C (m != n, the panel updates of the two-level
   // Cholesky) -> the full grid, tiles wholly outside the triangle exit
   const bool tri_sq = MODE != 0 && m == n && BM == BN;
-  if ((MODE == 1 || MODE == 3) && tri_sq) {
+  if (MODE == 1 && tri_sq) {
     tri_decode(tile, bi, bj);
   } else if (MODE == 2 && tri_sq) {
     tri_decode(tile, bj, bi);
@@ -207,7 +203,7 @@ __global__ __launch_bounds__(256) void k_gemm(
   const int nst = (kend - kbeg + BK - 1) / BK;  // K stages of this split
   auto gload = [&](int set, int st) {
     load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + st * BK, ra[set]);
-    load_tile<BN, BK, BKC, MODE == 3>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set]);
+    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set]);
   };
   auto lstore = [&](int set, int buf) {
     store_tile<BM, BK, AK>(pool + buf * STAGE, ra[set]);
@@ -304,13 +300,10 @@ __global__ __launch_bounds__(256) void k_gemm(
       const int il = e % BM, jl = e / BM;
       const int i = i0 + il, j = j0 + c0 + jl;
       if (i >= m || j >= n) continue;
-      if ((MODE == 1 || MODE == 3) && i < j) continue;
+      if (MODE == 1 && i < j) continue;
       if (MODE == 2 && i > j) continue;
       const double v = pool[jl * (BM + 1) + il];
-      if (MODE == 3) {
-        C[i + (size_t)j * ldc] = alpha * v;
-        if (i > j) C[j + (size_t)i * ldc] = alpha * v;
-      } else if (slab) {
+      if (slab) {
         slab[(size_t)split * m * n + (size_t)j * m + i] = v;
       } else if (!use_c) {
         C[i + (size_t)j * ldc] = alpha * v;
@@ -361,7 +354,6 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
     if (splits > 64) splits = 64;
     if (splits < 1) splits = 1;
   }
-  if (MODE == 3) splits = 1;  // the mirrored epilogue writes final values
   int kchunk = smg_ceil_div(smg_ceil_div(k, splits), BK) * BK;
   splits = smg_ceil_div(k, kchunk);
   double* slab = nullptr;
@@ -488,16 +480,6 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
 }
 
 }  // namespace
-
-// C = sym(A^T tril(B)) for n x n C, A k x n, B k x n (B's strict upper
-// triangle ignored): the lower triangle of A^T tril(B), mirrored into the
-// upper one.  One launch instead of a masked copy, a GEMM and a mirror pass.
-int smg_gemm_symtril_impl(smg_ctx* ctx, int n, int k, const double* A, int lda, const double* B,
-                          int ldb, double* C, int ldc) {
-  if (n <= 0) return SMG_OK;
-  if (k <= 0) return smg_scale_impl(ctx, n, n, 0.0, C, ldc, 0);
-  return launch<32, 32, 32, true, false, 3>(ctx, n, n, k, 1.0, A, lda, B, ldb, 0.0, C, ldc);
-}
 
 // batch x (C_i = alpha op(A_i) op(B_i) + beta C_i), operand i at base + i * stride
 // (doubles); full C only, no split-K, operands must not alias

@@ -123,8 +123,6 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
                         double* r, int n);
 
 // internal GEMM entry used by other units (no argument re-validation)
-int smg_gemm_symtril_impl(smg_ctx* ctx, int n, int k, const double* A, int lda, const double* B,
-                          int ldb, double* C, int ldc);
 int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
                   int k, double alpha, const double* A, int lda, const double* B,
                   int ldb, double beta, double* C, int ldc);
