@@ -59,12 +59,39 @@ inline dev_fvar_matrix add_diag(const dev_fvar_matrix& A, double d) {
   return dev_fvar_matrix{add_diag(A.val_, d), A.d_};
 }
 
+namespace internal {
+// C = L Phi for lower-triangular L and Phi: C is lower, so the product fills
+// only the lower tiles (half the GEMM); zero strict upper.  The reverse is the
+// general product's (multiply.hpp).
+class multiply_lower_dev_vari : public vari {
+ public:
+  dev_matrix_vari* A_;
+  dev_matrix_vari* B_;
+  dev_matrix_vari* C_;
+  multiply_lower_dev_vari(dev_matrix_vari* A, dev_matrix_vari* B)
+      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, B->cols_)) {
+    smg_ctx* c = amd::ctx();
+    const int n = A->rows_;
+    amd::check(smg_memset(c, C_->val_, 0, size_t(n) * n * sizeof(double)), "multiply");
+    amd::check(smg_gemm(c, 0, 0, 1, n, n, n, 1.0, A_->val_, n, B_->val_, n, 0.0, C_->val_, n), "multiply");
+  }
+  void chain() override {
+    const int n = A_->rows_;
+    amd::check(smg_multiply_rev(amd::ctx(), A_->val_, n, B_->val_, n, C_->adj_, n, n, n, n, A_->adj_, n,
+                                B_->adj_, n),
+               "multiply");
+  }
+};
+}  // namespace internal
+
 inline dev_fvar_matrix cholesky_decompose(const dev_fvar_matrix& A) {
   dev_fvar_matrix L;
   L.val_ = cholesky_decompose(A.val_);                    // checks + L (structurally lower)
   dev_var_matrix X = mdivide_left_tri<1>(L.val_, A.d_);   // L^{-1} A'
   dev_var_matrix Y = mdivide_left_tri<1>(L.val_, transpose(X));  // L^{-1} A' L^{-T}
-  L.d_ = multiply(L.val_, phi_lower(Y));
+  // L' = L Phi(Y): lower times lower
+  dev_var_matrix P = phi_lower(Y);
+  L.d_ = dev_var_matrix((new internal::multiply_lower_dev_vari(L.val_.vi_, P.vi_))->C_);
   return L;
 }
 
