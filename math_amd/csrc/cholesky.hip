@@ -663,6 +663,12 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
 
 }  // namespace
 
+// the 128- / 256- / 512-row diagonal-block inverses of a lower L from the
+// 64-row ones (aux: n x SMG_AUX_COLS, ld n, 64-row level filled)
+int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux, int n) {
+  return chol_block_inverses(ctx, L, ldl, aux, n);
+}
+
 extern "C" {
 
 int smg_cholesky_block_size(int n) { return SMG_NB; }

@@ -118,6 +118,7 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
 int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);
+int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux, int n);
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,
                         const double* W256, const double* W512, int ldw, const double* x, double* y,
                         double* r, int n);

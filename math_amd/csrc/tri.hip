@@ -90,23 +90,35 @@ int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double*
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
                   int ldw, double* B, int ldb, int m, int n) {
   if (m <= 0 || n <= 0) return SMG_OK;
-  const int nblk = (m + SMG_NB - 1) / SMG_NB;
+  int BSZ = SMG_NB;  // diagonal-block size of the solve
   if (!W) {
-    double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)m * SMG_NB);
+    // a large lower solve without given inverses: 512-row blocks (inverses
+    // doubled up from the 64-row ones, as the Cholesky aux), so the updates
+    // are rank-512 GEMMs instead of rank-64 ones and the step count is m / 512
+    const bool big = lower && m >= 4 * SMG_NBR && m % SMG_NBR == 0 && n >= SMG_NBR;
+    const size_t wd = big ? (size_t)m * SMG_AUX_COLS : (size_t)m * SMG_NB;
+    double* w = smg_ws(ctx, SMG_WS_TMP2, wd);
     if (!w) return SMG_ERR_OOM;
-    hipLaunchKernelGGL(k_trtri_blocks, dim3(nblk), dim3(SMG_DIAG_THREADS), 0, ctx->stream, A, lda, m,
-                       lower ? 0 : 1, w);
+    hipLaunchKernelGGL(k_trtri_blocks, dim3((m + SMG_NB - 1) / SMG_NB), dim3(SMG_DIAG_THREADS), 0,
+                       ctx->stream, A, lda, m, lower ? 0 : 1, w);
     W = w;
     ldw = m;
+    if (big) {
+      const int rc = smg_block_inverses_impl(ctx, A, lda, w, m);
+      if (rc) return rc;
+      W = w + (size_t)m * SMG_AUX_W512;
+      BSZ = SMG_NBR;
+    }
   }
+  const int nblk = (m + BSZ - 1) / BSZ;
   const bool forward = (lower && !trans) || (!lower && trans);
   const bool wt = (trans != 0) != (lower == 0);  // X_p = W_p^T B_p
   int rc;
   for (int q = 0; q < nblk; ++q) {
     const int p = forward ? q : nblk - 1 - q;
-    const int j = p * SMG_NB, b = min(SMG_NB, m - j), k = j + b;
+    const int j = p * BSZ, b = min(BSZ, m - j), k = j + b;
     double* Bp = B + j;
-    // X_p = W_p (or W_p^T) B_p, in place (the row extent b fits one tile)
+    // X_p = W_p (or W_p^T) B_p, in place (the GEMM's aliasing path)
     rc = smg_gemm_impl(ctx, wt ? 1 : 0, 0, 0, b, n, b, 1.0, W + j, ldw, Bp, ldb, 0.0, Bp, ldb);
     if (rc) return rc;
     if (forward && k < m) {

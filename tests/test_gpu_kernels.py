@@ -674,3 +674,29 @@ def test_cholesky_fwd_checked(ctx, N):
     assert ctx.status() & 4
     L = ctx.get(L3, N * N).reshape(N, N, order="F")
     assert np.all(np.triu(L, 1) == 0.0)
+
+
+@pytest.mark.parametrize("m,n", [(2048, 512), (2048, 700)])
+def test_mdivide_left_tri_512_blocks(ctx, m, n):
+    """The large lower solve on 512-row blocks (inverses doubled up from the
+    64-row level, tri.hip smg_trsm_impl) against scipy's triangular solves:
+    C = L^{-1} B, and the reverse's adjB = L^{-T} W, adjA = -tril(adjB C^T)
+    (mdivide_left_tri.hpp:104-123)."""
+    import scipy.linalg as sl
+    rng = np.random.default_rng(m + n)
+    S = rng.uniform(-1, 1, (m, m))
+    S = S @ S.T / m + np.eye(m)
+    L = np.linalg.cholesky(S)
+    B = rng.uniform(-1, 1, (m, n))
+    W = rng.uniform(-1, 1, (m, n))
+    dA, dB, dC = ctx.put(F(L)), ctx.put(F(B)), ctx.zeros(m * n)
+    ctx.call("smg_mdivide_left_tri_fwd", 1, dA, m, dB, m, m, n, dC, m)
+    C = ctx.get(dC, m * n).reshape(n, m).T
+    Cref = sl.solve_triangular(L, B, lower=True)
+    near_rel(C, Cref, 1e-10, atol=1e-11 * np.abs(Cref).max(), what="C")
+    dW, dAa, dBa, ws = ctx.put(F(W)), ctx.zeros(m * m), ctx.zeros(m * n), ctx.zeros(m * n)
+    ctx.call("smg_mdivide_left_tri_rev", 1, dA, m, dC, m, dW, m, m, n, dAa, m, dBa, m, ws)
+    gB = sl.solve_triangular(L, W, lower=True, trans="T")
+    gA = -np.tril(gB @ Cref.T)
+    near_rel(ctx.get(dBa, m * n).reshape(n, m).T, gB, 1e-10, atol=1e-11 * np.abs(gB).max(), what="gB")
+    near_rel(ctx.get(dAa, m * m).reshape(m, m).T, gA, 1e-10, atol=1e-11 * np.abs(gA).max(), what="gA")
