@@ -91,6 +91,22 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
                   int ldw, double* B, int ldb, int m, int n) {
   if (m <= 0 || n <= 0) return SMG_OK;
   int BSZ = SMG_NB;  // diagonal-block size of the solve
+  if (!W && n == 1 && lower && ldb >= m && m >= 512 && m % 256 == 0 && m / 64 <= 256) {
+    // one right-hand side: the persistent solve (trsv.hip) on the 256- / 512-
+    // row inverses, one launch instead of 2 m / 64 small GEMMs
+    double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)m * SMG_AUX_COLS);
+    double* xr = smg_ws(ctx, SMG_WS_CW, 2 * (size_t)m);
+    if (!w || !xr) return SMG_ERR_OOM;
+    hipLaunchKernelGGL(k_trtri_blocks, dim3(m / SMG_NB), dim3(SMG_DIAG_THREADS), 0, ctx->stream, A, lda,
+                       m, 0, w);
+    int rc = smg_block_inverses_impl(ctx, A, lda, w, m);
+    if (rc) return rc;
+    rc = smg_copy_impl(ctx, m, 1, B, ldb, xr, m, 1.0, 0);
+    if (rc) return rc;
+    return smg_trsv_lower_impl(ctx, trans, A, lda, w, w + (size_t)m * SMG_AUX_W256,
+                               m % SMG_NBR == 0 ? w + (size_t)m * SMG_AUX_W512 : nullptr, m, xr, B,
+                               xr + m, m);
+  }
   if (!W) {
     // a large lower solve without given inverses: 512-row blocks (inverses
     // doubled up from the 64-row ones, as the Cholesky aux), so the updates
