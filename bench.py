@@ -20,8 +20,16 @@ generated in HBM before the timed region, ONE RCCL all-reduce of the M+2
 --workload mulchol (config 2): gradient of sum(cholesky_decompose(add_diag(
 multiply(A, A^T), N))) wrt all N^2 entries of A, N=2048, A resident in HBM.
 
-Each line also carries the roofline of the dominant kernel family (algorithmic
-work / HIP-event time over a profiled copy of the timed region) and, on rank 0
+--workload normal (config 1): gradient of normal_lpdf(theta | 0, 1), N=1024,
+theta a host std::vector<var> (latency-bound: one host round trip per eval).
+
+--gpus N without an external launcher spawns N child processes (one per GPU,
+torchrun's environment) before any GPU call; under torchrun WORLD_SIZE must
+equal --gpus.
+
+Each line carries the roofline (algorithmic flops or bytes
+of one eval / the measured step time, or / the dominant kernel's HIP-event
+launch time for the GLM; the GEMM family's executed flops beside it) and, on rank 0
 at N=1, the reference CPU path (oracle/_ref/ref_harness: the real Stan Math
 3.0.0 compiled from /root/reference) timed on one host core on a bounded sample.
 """
@@ -82,6 +90,28 @@ def unif(seed, n, a, b):
     return a + (b - a) * ((z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0))
 
 
+def eval_roofline(wl, fams, steps, ms_per_step, traffic_src):
+    """algorithmic flops of ONE gradient eval (the unit a step
+    processes) / the measured step time / the fp64 MFMA peak.  The GEMM kernel
+    family (HIP events on the context stream) is reported beside it with the
+    flops its launches execute (block-inverse doubling and the symbolic
+    adjoint's extra products included), named as such."""
+    fl = wl.eval_flops()
+    ach = fl / (ms_per_step * 1e-3) / 1e12
+    gms, gn, gfl = fams["gemm"]
+    traffic, src = traffic_src
+    return {"bound": "mfma", "kernel": "whole gradient eval (algorithmic flops / step time)",
+            "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP64_TFLOPS,
+            "traffic": traffic, "traffic_unit": "HBM bytes per k_gemm launch (PMC)" if traffic else None,
+            "traffic_source": src, "algorithmic_flops_per_eval": fl, "eval_flops": wl.eval_flops_expr,
+            "gemm_family": {"launches_per_step": gn / steps, "avg_launch_ms": gms / max(gn, 1),
+                            "executed_flops_per_launch": gfl / max(gn, 1),
+                            "executed_tflops": gfl / (gms * 1e-3) / 1e12 if gms > 0 else None,
+                            "ms_per_step": gms / steps,
+                            "note": "executed flops (incl. block-inverse doubling, symbolic-adjoint "
+                                    "products); HIP events on the context stream"}}
+
+
 class Workload:
     """init() puts the data in HBM; step() is one gradient eval; guard() checks parity."""
     unit = "gradient evals/s"
@@ -126,18 +156,13 @@ class GP(Workload):
 
     data = "synthetic (reference harness config-3 inputs: x~U(-10,10), y=sin(x)+0.3eps; theta=(1,1.5,0.3))"
 
-    def roofline(self, fams, steps, t_prof):
-        ms, n, fl = fams["gemm"]
-        ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
-        ev = self.N ** 3 / (t_prof / steps) / 1e12
-        traffic, src = pmc_traffic("gp")
-        return {"bound": "mfma", "kernel": "k_gemm (fp64 MFMA, all launches of the family)",
-                "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_FP64_TFLOPS if ach else None, "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
-                "launches_per_step": n / steps, "flops_per_launch": fl / max(n, 1),
-                "avg_launch_ms": ms / max(n, 1), "eval_achieved": ev, "eval_frac": ev / PEAK_FP64_TFLOPS,
-                "eval_flops": "N^3 (chol fwd N^3/3 + Murray adjoint 2N^3/3), SURVEY.md §8(d)"}
+    eval_flops_expr = "N^3 (chol fwd N^3/3 + Murray adjoint 2N^3/3), SURVEY.md §8(d)"
+
+    def eval_flops(self):
+        return float(self.N) ** 3
+
+    def roofline(self, fams, steps, t_prof, ms_per_step):
+        return eval_roofline(self, fams, steps, ms_per_step, pmc_traffic("gp"))
 
     def cpu_baseline(self):
         r = ref_bench("gp", self.N, 1)
@@ -198,7 +223,7 @@ class GLM(Workload):
 
     data = "synthetic (reference harness config-4 streams: x~U(-sqrt3,sqrt3), y~Bern(0.5), generated in HBM)"
 
-    def roofline(self, fams, steps, t_prof):
+    def roofline(self, fams, steps, t_prof, ms_per_step):
         ms, n, _ = fams["glm"]
         byts = self.rows * self.M * 8 + self.rows * 4  # one read of x and y
         avg = ms / max(n, 1)
@@ -255,16 +280,13 @@ class MulChol(Workload):
 
     data = "synthetic (reference harness config-2 input: A = U(-1,1) sqrt(3/N), generated in HBM)"
 
-    def roofline(self, fams, steps, t_prof):
-        ms, n, fl = fams["gemm"]
-        ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
-        ev = 7 * self.N ** 3 / (t_prof / steps) / 1e12
-        return {"bound": "mfma", "kernel": "k_gemm (fp64 MFMA, all launches of the family)",
-                "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_FP64_TFLOPS if ach else None, "traffic": None,
-                "launches_per_step": n / steps, "avg_launch_ms": ms / max(n, 1),
-                "eval_achieved": ev, "eval_frac": ev / PEAK_FP64_TFLOPS,
-                "eval_flops": "7N^3 (fwd GEMM 2N^3 + rev 2 GEMM 4N^3 + chol N^3), SURVEY.md §8(d)"}
+    eval_flops_expr = "7N^3 (fwd GEMM 2N^3 + rev 2 GEMM 4N^3 + chol N^3), SURVEY.md §8(d)"
+
+    def eval_flops(self):
+        return 7.0 * float(self.N) ** 3
+
+    def roofline(self, fams, steps, t_prof, ms_per_step):
+        return eval_roofline(self, fams, steps, ms_per_step, (None, None))
 
     def cpu_baseline(self):
         r = ref_bench("mulchol", self.N, 1)
@@ -299,18 +321,23 @@ class HVP(GP):
               and np.array_equal(h0, self.hv) and np.all(np.isfinite(h0)))
         return ok, f"fx={self.fx[0]!r} Hv={h0} / {self.hv}"
 
+    parity = ("value vs the reference golden at 1e-9; Hv at N=4096 self-consistent only (two products bitwise "
+              "equal): the reference's fvar<var> tape is infeasible at N=4096; Hv pinned vs the reference at "
+              "N<=256 in tests/test_cpp_functors.py")
+
     def config(self):
         c = super().config()
         c["workload"] = "gp_marginal_hessian_times_vector"
         c["v"] = [1.0, -0.5, 0.25]
         return c
 
-    def roofline(self, fams, steps, t_prof):
-        r = super().roofline(fams, steps, t_prof)
-        ev = 4 * self.N ** 3 / (t_prof / steps) / 1e12
-        r.update(eval_achieved=ev, eval_frac=ev / PEAK_FP64_TFLOPS,
-                 eval_flops="4N^3 (primal N^3 + tangent fwd N^3 + its reverse 2N^3), SURVEY.md §8(d)")
-        return r
+    eval_flops_expr = "4N^3 (primal N^3 + tangent fwd N^3 + its reverse 2N^3), SURVEY.md §8(d)"
+
+    def eval_flops(self):
+        return 4.0 * float(self.N) ** 3
+
+    def roofline(self, fams, steps, t_prof, ms_per_step):
+        return eval_roofline(self, fams, steps, ms_per_step, (None, None))
 
     def cpu_baseline(self):
         # the reference's fvar<var> tape is O(N^3) scalar nodes: infeasible at N=4096 (~1.7 h);
@@ -323,7 +350,89 @@ class HVP(GP):
                           f"per product ({r['evals_per_sec']:.3f}/s), Stan Math 3.0.0 compiled from /root/reference"}
 
 
-WORKLOADS = {"gp": GP, "glm": GLM, "mulchol": MulChol, "hvp": HVP}
+class Normal(Workload):
+    """config 1: gradient of normal_lpdf(theta | 0, 1), N=1024, theta a host
+    std::vector<var> (the reference's normal_functor, prim/scal/prob/normal_lpdf.hpp:36-119)."""
+    N = 1024
+    metric = "gradient evals/sec (fp64), normal_lpdf N=1024"
+    scaling = "weak"
+
+    def init(self):
+        bl = self.bl
+        bl.smg_bench_device_init.argtypes = [ctypes.c_int]
+        bl.smg_bench_normal_step.argtypes = [ctypes.c_int, D, D, D]
+        with open(os.path.join(ROOT, "tests", "golden", f"normal_N{self.N}.json")) as f:
+            self.gold = json.load(f)
+        self.theta = np.array(self.gold["theta"], dtype=np.float64)
+        self.g = np.zeros(self.N)
+        return bl.smg_bench_device_init(self.local)
+
+    def step(self):
+        return self.bl.smg_bench_normal_step(self.N, ptr(self.theta), ptr(self.fx), ptr(self.g))
+
+    def guard(self):
+        want = np.array(self.gold["grad"])
+        ok = (np.all(np.abs(self.g - want) <= 1e-10 * np.maximum(np.abs(want), 1e-10))
+              and abs(self.fx[0] - self.gold["fx"]) <= 1e-12 * abs(self.gold["fx"]))
+        return ok, f"fx={self.fx[0]!r} vs {self.gold['fx']}"
+
+    def units_per_step(self):
+        return self.world
+
+    def config(self):
+        return {"workload": "normal_lpdf_gradient", "N": self.N, "parallelism": f"replicas{self.world}",
+                "path": "stan::math::gradient over std::vector<var> via header-only layer"}
+
+    data = "synthetic (reference harness config-1 input: theta ~ N(0,1), tests/golden/normal_N1024.json)"
+
+    def roofline(self, fams, steps, t_prof, ms_per_step):
+        byts = self.N * 8 * 2  # theta up, partials down (SURVEY.md §8(d): 16 B per element)
+        ach = byts / (ms_per_step * 1e-3) / 1e9
+        return {"bound": "hbm", "kernel": "whole gradient eval (latency-bound: one host round trip)",
+                "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                "traffic": None, "bytes_per_eval": byts}
+
+    def cpu_baseline(self):
+        reps = 500000
+        r = ref_bench("normal", self.N, reps)
+        if r is None:
+            return None
+        return {"value": r["evals_per_sec"], "unit": "gradient evals/s", "cores": 1, "kind": "reference",
+                "sample": f"{reps} gradient evals at N={self.N} (Stan Math 3.0.0, "
+                          f"{r['seconds_per_eval'] * 1e6:.2f} us each)"}
+
+
+WORKLOADS = {"gp": GP, "glm": GLM, "mulchol": MulChol, "hvp": HVP, "normal": Normal}
+
+
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def spawn_ranks(n):
+    """--gpus N without a launcher: start N fresh child processes, one per GPU,
+    with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*),
+    before this process touches the GPU; rank 0's stdout is the bench line."""
+    import torch  # device_count() does not initialise the GPU on this image
+    have = torch.cuda.device_count()
+    if have < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible")
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        raise SystemExit(f"bench.py: rank(s) failed: {bad}")
+    return 0
 
 
 def main():
@@ -336,9 +445,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     dist = None
     if world > 1:
         import torch.distributed as dist  # CPU-side barrier / max / id exchange (gloo)
@@ -408,9 +521,10 @@ def main():
         "dtype": "f64",
         "data": wl.data,
         "config": wl.config(),
-        "roofline": wl.roofline(fams, args.steps, tp),
-        "families_ms_per_step": {f: v[0] / args.steps for f, v in fams.items()},
+        "roofline": wl.roofline(fams, args.steps, tp, ms_per_step),
     }
+    if getattr(wl, "parity", None):
+        line["parity"] = wl.parity
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = wl.cpu_baseline()
@@ -422,7 +536,8 @@ def main():
         lib.smg_comm_destroy(ctx)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

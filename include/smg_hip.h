@@ -76,6 +76,16 @@ int smg_memset(smg_ctx* ctx, void* dst, int value, size_t bytes);
 int smg_sync(smg_ctx* ctx);
 /* synchronise, return the latched status bits (0 = ok) and clear them */
 int smg_status(smg_ctx* ctx, int* status_host);
+/* 1 when a launch that can latch the status word asynchronously (a persistent
+ * solve or panel: SMG_ERR_SYNC on a timed-out hand-off) was enqueued since the
+ * status was last read; the reverse sweep reads it then (stan::math::grad) */
+int smg_status_armed(smg_ctx* ctx, int* armed);
+/* enqueue (no sync) the copy of the status word into pinned host_dst (the
+ * word stays latched: smg_status reads and clears it); the caller reads
+ * host_dst after its next smg_sync */
+int smg_status_enqueue(smg_ctx* ctx, int* host_dst);
+/* test hook: OR `bits` into the device status word (arms it) */
+int smg_status_inject(smg_ctx* ctx, int bits);
 
 /* ------------------------------------------------------- instrumentation ---
  * HIP-event timing of the kernel families on the context stream (used by

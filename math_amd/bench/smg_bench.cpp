@@ -154,6 +154,29 @@ int smg_bench_hvp_step(const double* theta, const double* v, double* fx, double*
   }
 }
 
+/* config 1: gradient of normal_lpdf(theta | 0, 1) wrt the n entries of theta
+ * (host std::vector<var> operand, as the reference's normal_functor) */
+int smg_bench_normal_step(int n, const double* theta, double* fx, double* grad) {
+  try {
+    std::vector<double> th(theta, theta + n), g;
+    stan::math::gradient(
+        [](const std::vector<var>& t) { return stan::math::normal_lpdf(t, 0.0, 1.0); }, th, *fx, g);
+    for (int i = 0; i < n; ++i) grad[i] = g[i];
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+int smg_bench_device_init(int device) {
+  try {
+    stan::math::amd::set_device(device);
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
 long long smg_bench_glm_local_rows() { return g_shard.rows; }
 
 /* the row partition every sharded reducer uses (stan::math::row_partition) */

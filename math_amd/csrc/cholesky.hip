@@ -754,6 +754,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int T = smg_ceil_div(n - J, SMG_NB);
       const int grid = T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID;  // chain + owners of tiles 1..T-1
       const int epoch = ++ctx->flag_epoch;
+      ctx->status_armed = 1;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);
     }

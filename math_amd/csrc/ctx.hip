@@ -126,6 +126,7 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->cur_block = 0;
   ctx->offset = 0;
   ctx->host_status = 0;
+  ctx->status_armed = 0;
   for (int i = 0; i < SMG_WS_COUNT; ++i) {
     ctx->ws[i] = nullptr;
     ctx->ws_doubles[i] = 0;
@@ -315,7 +316,35 @@ int smg_status(smg_ctx* ctx, int* status) {
   if (ctx->prof_on) prof_drain(ctx);
   int s = ctx->status_h[0] | ctx->host_status;
   ctx->host_status = 0;
+  ctx->status_armed = 0;
   if (status) *status = s;
+  return SMG_OK;
+}
+
+int smg_status_armed(smg_ctx* ctx, int* armed) {
+  if (!ctx || !armed) return SMG_ERR_ARG;
+  *armed = ctx->status_armed;
+  return SMG_OK;
+}
+
+int smg_status_enqueue(smg_ctx* ctx, int* host_dst) {
+  if (!ctx || !host_dst) return SMG_ERR_ARG;
+  SMG_HIP_TRY(hipMemcpyAsync(host_dst, ctx->status_d, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->status_armed = 0;
+  return SMG_OK;
+}
+
+namespace {
+__global__ void k_status_or(int* st, int bits) {
+  if (threadIdx.x == 0) st[0] |= bits;
+}
+}  // namespace
+
+int smg_status_inject(smg_ctx* ctx, int bits) {
+  if (!ctx) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_status_or, dim3(1), dim3(64), 0, ctx->stream, ctx->status_d, bits);
+  SMG_LAUNCH_CHECK();
+  ctx->status_armed = 1;
   return SMG_OK;
 }
 

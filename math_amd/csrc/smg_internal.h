@@ -40,6 +40,10 @@ struct smg_ctx {
   int* status_d;
   int* status_h;
   int host_status;  // host-detected errors (OOM, HIP)
+  // set when a launch that can latch the status word (the persistent solves
+  // and panels: SMG_ERR_SYNC on a timed-out hand-off) is enqueued; cleared
+  // when the status is read (smg_status / smg_status_enqueue)
+  int status_armed;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;

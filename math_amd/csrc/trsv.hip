@@ -432,6 +432,7 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
   if (fits && !trans && W512 && n % 512 == 0 && n >= 1024) {
     const int epoch = ++ctx->flag_epoch;
     int* f = ctx->flags_d + TRSV_FLAG_OFFSET;
+    ctx->status_armed = 1;
     hipLaunchKernelGGL((k_trsv_persist<false, 512>), dim3(n / 64), dim3(512), 0, ctx->stream, L, ldl,
                        W512, ldw, x, y, r, n, f, epoch, ctx->status_d);
     SMG_LAUNCH_CHECK();
@@ -440,6 +441,7 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
   if (fits && W256 && n % 256 == 0 && n >= 512) {
     const int epoch = ++ctx->flag_epoch;
     int* f = ctx->flags_d + TRSV_FLAG_OFFSET;
+    ctx->status_armed = 1;
     if (trans)
       hipLaunchKernelGGL((k_trsv_persist<true, 256>), dim3(n / 64), dim3(256), 0, ctx->stream, L, ldl,
                          W256, ldw, x, y, r, n, f, epoch, ctx->status_d);

@@ -41,6 +41,9 @@ _SIGS = {
     "smg_memset": (_I, [_P, _P, _I, _S]),
     "smg_sync": (_I, [_P]),
     "smg_status": (_I, [_P, ctypes.POINTER(_I)]),
+    "smg_status_armed": (_I, [_P, ctypes.POINTER(_I)]),
+    "smg_status_enqueue": (_I, [_P, _P]),
+    "smg_status_inject": (_I, [_P, _I]),
     "smg_profile_enable": (_I, [_P, _I]),
     "smg_profile_read": (_I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
     "smg_profile_flops": (_I, [_P, _I, ctypes.POINTER(_D)]),

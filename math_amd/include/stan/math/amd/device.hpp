@@ -106,6 +106,16 @@ inline void check(int rc, const char* function, const char* what = "") {
   if (__builtin_expect(rc != SMG_OK, 0)) throw_status(rc, function, what);
 }
 
+/** After a status word read with smg_status_enqueue: a timed-out hand-off
+ * (SMG_ERR_SYNC) throws here, after clearing the latch; other latched bits
+ * (domain errors) stay for the functor that checks them (smg_status). */
+inline void throw_if_sync(int st, const char* function, const char* what) {
+  if (__builtin_expect(!(st & SMG_ERR_SYNC), 1)) return;
+  int cleared = 0;
+  smg_status(state().ctx, &cleared);
+  throw_status(SMG_ERR_SYNC, function, what);
+}
+
 /** Synchronise and translate latched device-side domain errors. */
 inline void check_status(const char* function, const char* what = "") {
   int st = 0;
@@ -145,14 +155,21 @@ inline void to_device_int(int* dst, const int* src, size_t n) {
   check(smg_sync(c), "to_device");
 }
 
-/** Blocking device -> host copy. */
+/** Blocking device -> host copy.  When a launch that can latch the status
+ * word asynchronously is in flight (a persistent solve / panel, whose timed-out
+ * hand-off latches SMG_ERR_SYNC), the status is read in the same sync and a
+ * latched error throws here instead of returning a wrong value. */
 inline void to_host(double* dst, const double* src, size_t n) {
   if (!n) return;
   smg_ctx* c = ctx();
-  void* stage = smg_host_scratch(c, n * sizeof(double));
+  int armed = 0;
+  check(smg_status_armed(c, &armed), "to_host");
+  double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
   if (!stage) throw std::bad_alloc();
   check(smg_memcpy_d2h(c, stage, src, n * sizeof(double)), "to_host");
+  if (armed) check(smg_status_enqueue(c, reinterpret_cast<int*>(stage + n)), "to_host");
   check(smg_sync(c), "to_host");
+  if (armed) throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
   __builtin_memcpy(dst, stage, n * sizeof(double));
 }
 

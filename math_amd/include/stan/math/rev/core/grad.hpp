@@ -34,18 +34,28 @@ inline void add_pending_adjoint(vari* target, const double* src) {
   ChainableStack::instance_->pending_.push_back({target, src});
 }
 
-/** Land every queued device->host adjoint contribution (one sync). */
-inline void flush_pending() {
+/** Land every queued device->host adjoint contribution (one sync).  With
+ * `status` (the end of the reverse sweep), the device status word is read in
+ * the same sync when a launch that can latch it asynchronously was enqueued
+ * (a persistent solve / panel whose hand-off timed out: SMG_ERR_SYNC), so
+ * such a failure throws from the grad() that ran it. */
+inline void flush_pending(bool status = false) {
   auto& pend = ChainableStack::instance_->pending_;
-  if (pend.empty()) return;
+  int armed = 0;
+  if (status && amd::has_ctx()) amd::check(smg_status_armed(amd::ctx(), &armed), "grad");
+  if (pend.empty() && !armed) return;
   smg_ctx* c = amd::ctx();
-  double* stage = static_cast<double*>(smg_host_scratch(c, pend.size() * sizeof(double)));
+  const size_t n = pend.size();
+  double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
   if (!stage) throw std::bad_alloc();
-  for (size_t i = 0; i < pend.size(); ++i)
+  for (size_t i = 0; i < n; ++i)
     amd::check(smg_memcpy_d2h(c, stage + i, pend[i].src, sizeof(double)), "flush_pending");
+  int* st = reinterpret_cast<int*>(stage + n);
+  if (armed) amd::check(smg_status_enqueue(c, st), "grad");
   amd::check(smg_sync(c), "flush_pending");
-  for (size_t i = 0; i < pend.size(); ++i) pend[i].target->adj_ += stage[i];
+  for (size_t i = 0; i < n; ++i) pend[i].target->adj_ += stage[i];
   pend.clear();
+  if (armed) amd::throw_if_sync(*st, "grad", "the reverse sweep");
 }
 
 static inline bool empty_nested() {
@@ -72,7 +82,7 @@ static void grad(vari* vi) {
     if (__builtin_expect(!st->pending_.empty(), 0)) flush_pending();
     (*it)->chain();
   }
-  flush_pending();
+  flush_pending(true);
 }
 
 static inline void start_nested() {

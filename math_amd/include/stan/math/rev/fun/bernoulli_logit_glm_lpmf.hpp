@@ -14,8 +14,8 @@
 // Row sharding (the reduce_sum / map_rect path): each rank
 // holds a contiguous row block of (y, x) on its own GPU (glm_shard); every
 // rank computes its local [logp, alpha', beta'] and ONE RCCL all-reduce sums
-// the M + 2 doubles across ranks (smg_comm_allreduce_sum); every rank then
-// builds the same node.  Replaces map_rect's MPI/TBB gather
+// the M + 2 doubles and the y-bounds flag across ranks (amd::allreduce_sum);
+// every rank then builds the same node (or throws the same error).  Replaces map_rect's MPI/TBB gather
 // (prim/mat/functor/map_rect.hpp:120-177, map_rect_combine.hpp:36-92).
 
 #include <stan/math/amd/comm.hpp>
@@ -75,6 +75,34 @@ class glm_dev_vari : public vari {
                  "bernoulli_logit_glm_lpmf");
   }
 };
+
+// check_bounded(fn, "Vector of dependent variables", y, 0, 1)'s message
+// (prim/scal/err/check_bounded.hpp:40-50) for the first y outside [lo, hi],
+// with the global index (row0 = the shard's first row); error path only.  A
+// rank whose own rows are all in bounds (the flag came from another rank's
+// shard) names no element.
+inline void glm_throw_y_bounds(const char* fn, const int* y, long long n, int lo, int hi, long long row0) {
+  smg_ctx* c = amd::ctx();
+  const long long chunk = 1 << 20;
+  for (long long i0 = 0; i0 < n; i0 += chunk) {
+    const long long k = n - i0 < chunk ? n - i0 : chunk;
+    int* stage = static_cast<int*>(smg_host_scratch(c, size_t(k) * sizeof(int)));
+    if (!stage) throw std::bad_alloc();
+    amd::check(smg_memcpy_d2h(c, stage, y + i0, size_t(k) * sizeof(int)), fn);
+    amd::check(smg_sync(c), fn);
+    for (long long i = 0; i < k; ++i)
+      if (stage[i] < lo || stage[i] > hi) {
+        std::ostringstream m;
+        m << fn << ": Vector of dependent variables[" << row0 + i0 + i + 1 << "] is " << stage[i]
+          << ", but must be in the interval [" << lo << ", " << hi << "]";
+        throw std::domain_error(m.str());
+      }
+  }
+  std::ostringstream m;
+  m << fn << ": Vector of dependent variables is out of bounds (on another rank's rows), but must be in "
+          "the interval [" << lo << ", " << hi << "]";
+  throw std::domain_error(m.str());
+}
 
 struct glm_params {
   double alpha = 0;
@@ -137,12 +165,11 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
     double* ws = amd::alloc_doubles(size_t(smg_glm_ws_doubles(s.rows, M)));
     amd::check(smg_bernoulli_logit_glm(c, s.y, s.x, s.rows, M, s.ldx, ab, ws, out), fn);
   }
-  if (s.distributed) amd::check(smg_comm_allreduce_sum(c, out, M + 2), fn);
+  // [logp, alpha', beta'(M) | flag] are contiguous: the y-support flag is
+  // summed with them, so a bad y on any rank makes every rank throw
+  if (s.distributed) amd::allreduce_sum(out, M + 3, fn);
   amd::to_host(h.data(), buf, h.size());
-  if (h[2 * M + 3] != 0.0)
-    throw std::domain_error(std::string(fn) +
-                            ": Vector of dependent variables is out of bounds, but must be in the "
-                            "interval [0, 1]");
+  if (h[2 * M + 3] != 0.0) glm_throw_y_bounds(fn, s.y, s.rows, 0, 1, s.row0);
   if (s.total_rows == 0 || !(p.any_var() || !propto)) return glm_result{};
   const double lp = h[M + 1];
   if (!std::isfinite(lp)) {

@@ -63,8 +63,12 @@ inline void glm_check_finite_dev(const char* fn, const char* name, const double*
   }
 }
 
-// check_bounded's message for the first y outside [lo, hi]
-inline void glm_throw_out_of_support(const char* fn, const int* y, long long n, int lo, int hi) {
+// check_bounded's message for the first y outside [lo, hi]; row0: the shard's
+// first global row (indices are global).  A rank whose own rows are all in
+// support (the flag came from another rank's shard) throws a message naming
+// no element.
+inline void glm_throw_out_of_support(const char* fn, const int* y, long long n, int lo, int hi,
+                                     long long row0 = 0) {
   smg_ctx* c = amd::ctx();
   const long long chunk = 1 << 20;
   std::vector<int> h(size_t(n > chunk ? chunk : (n > 0 ? n : 0)));
@@ -78,11 +82,15 @@ inline void glm_throw_out_of_support(const char* fn, const int* y, long long n, 
     for (long long i = 0; i < k; ++i)
       if (h[size_t(i)] < lo || h[size_t(i)] > hi) {
         std::ostringstream m;
-        m << fn << ": categorical outcome out of support[" << i0 + i + 1 << "] is " << h[size_t(i)]
+        m << fn << ": categorical outcome out of support[" << row0 + i0 + i + 1 << "] is " << h[size_t(i)]
           << ", but must be in the interval [" << lo << ", " << hi << "]";
         throw std::domain_error(m.str());
       }
   }
+  std::ostringstream m;
+  m << fn << ": categorical outcome out of support (on another rank's rows), but must be in the interval ["
+    << lo << ", " << hi << "]";
+  throw std::domain_error(m.str());
 }
 
 /** One node over device alpha (C) and beta (M x C); out = [lp, alpha', beta']
@@ -134,11 +142,13 @@ inline glm_result categorical_glm_eval(const glm_shard& s, const dev_operand& al
     } else {
       amd::zero(out, size_t(W));
     }
-    if (s.distributed) amd::check(smg_comm_allreduce_sum(c, out, W), fn);
   }
+  // out (W) and the y flag are contiguous: summed together, so every rank
+  // throws together (only the flag when the pass did not run)
+  if (s.distributed) amd::allreduce_sum(run ? out : flag, run ? W + 1 : 1, fn);
   double h[2] = {0.0, 0.0};  // [lp, flag]
   amd::to_host(&h[1], flag, 1);
-  if (h[1] != 0.0) glm_throw_out_of_support(fn, s.y, s.rows, 1, C);
+  if (h[1] != 0.0) glm_throw_out_of_support(fn, s.y, s.rows, 1, C, s.row0);
   if (!run) return glm_result{};
   amd::to_host(&h[0], out, 1);
   const double lp = h[0];

@@ -57,7 +57,7 @@ class glm_sigma_dev_vari : public vari {
 };
 
 // first non-finite y (host copy: error path only) -> check_finite's message
-inline void glm_throw_nonfinite_y(const char* fn, const double* y, long long n) {
+inline void glm_throw_nonfinite_y(const char* fn, const double* y, long long n, long long row0 = 0) {
   std::vector<double> h(size_t(n > 0 ? n : 0));
   for (long long i0 = 0; i0 < n; i0 += 1 << 20) {
     const long long c = std::min<long long>(1 << 20, n - i0);
@@ -66,7 +66,7 @@ inline void glm_throw_nonfinite_y(const char* fn, const double* y, long long n) 
   for (long long i = 0; i < n; ++i)
     if (!std::isfinite(h[size_t(i)])) {
       std::ostringstream m;
-      m << fn << ": Vector of dependent variables[" << i + 1 << "] is " << h[size_t(i)]
+      m << fn << ": Vector of dependent variables[" << row0 + i + 1 << "] is " << h[size_t(i)]
         << ", but must be finite!";
       throw std::domain_error(m.str());
     }
@@ -119,11 +119,11 @@ inline glm_result normal_glm_eval(const glm_shard& s, const glm_params& p, doubl
   } else {
     amd::zero(out, size_t(M + 2));
   }
-  if (s.distributed) amd::check(smg_comm_allreduce_sum(c, out, M + 2), fn);
+  if (s.distributed) amd::allreduce_sum(out, M + 2, fn);
   amd::to_host(h.data(), buf, h.size());
   const double sq = h[M + 2];
   if (!std::isfinite(sq)) {  // (:130-136)
-    glm_throw_nonfinite_y(fn, s.yd, s.rows);
+    glm_throw_nonfinite_y(fn, s.yd, s.rows, s.row0);
     for (int j = 0; j < M; ++j)
       if (!std::isfinite(p.beta[j])) {
         std::ostringstream m;

@@ -31,8 +31,10 @@ namespace stan {
 namespace math {
 namespace internal {
 
-// index and value of the first negative y (host copy: error path only)
-inline void glm_throw_negative_y(const char* fn, const int* y, long long n) {
+// index (global: row0 = the shard's first row) and value of the first
+// negative y (host copy: error path only); a rank whose own rows are all
+// non-negative (the flag came from another rank) names no element
+inline void glm_throw_negative_y(const char* fn, const int* y, long long n, long long row0 = 0) {
   smg_ctx* c = amd::ctx();
   const long long chunk = 1 << 20;
   std::vector<int> h(size_t(n > chunk ? chunk : (n > 0 ? n : 0)));
@@ -46,11 +48,13 @@ inline void glm_throw_negative_y(const char* fn, const int* y, long long n) {
     for (long long i = 0; i < k; ++i)
       if (h[size_t(i)] < 0) {
         std::ostringstream m;
-        m << fn << ": Vector of dependent variables[" << i0 + i + 1 << "] is " << h[size_t(i)]
+        m << fn << ": Vector of dependent variables[" << row0 + i0 + i + 1 << "] is " << h[size_t(i)]
           << ", but must be >= 0!";
         throw std::domain_error(m.str());
       }
   }
+  throw std::domain_error(std::string(fn) +
+                          ": Vector of dependent variables is negative (on another rank's rows), but must be >= 0!");
 }
 
 template <bool propto>
@@ -82,10 +86,12 @@ inline glm_result poisson_glm_eval(const glm_shard& s, const glm_params& p) {
       double* ws = amd::alloc_doubles(size_t(smg_glm_ws_doubles(s.rows, M)));
       amd::check(smg_poisson_log_glm(c, s.y, s.x, s.rows, M, s.ldx, ab, ws, out), fn);
     }
-    if (s.distributed) amd::check(smg_comm_allreduce_sum(c, out, M + 3), fn);
   }
+  // [s, alpha', beta'(M), lgamma sum | flag] are contiguous (zeros when not
+  // run): the y flag is summed with them, so every rank throws together
+  if (s.distributed) amd::allreduce_sum(out, M + 4, fn);
   amd::to_host(h.data(), buf, h.size());
-  if (h[2 * M + 4] != 0.0) glm_throw_negative_y(fn, s.y, s.rows);
+  if (h[2 * M + 4] != 0.0) glm_throw_negative_y(fn, s.y, s.rows, s.row0);
   if (!run) return glm_result{};
   const double sd = h[M + 2];
   if (!std::isfinite(sd)) {  // (:87-91)

@@ -30,6 +30,8 @@
 //                                 beta, 5 row shards), Eigen path (Matrix<var>), mixed and
 //                                 all-double operands; x filled on the device (gen.glm_cat_inputs)
 //   glm_cat_errors                the reference's exceptions / early returns on small inputs
+//   status                        a latched SMG_ERR_SYNC throws from the gradient() / readback that
+//                                 ran it, and is cleared
 #include <stan/math.hpp>
 
 #include <cmath>
@@ -913,6 +915,38 @@ static void cmd_glm_cat_errors() {
               ChainableStack::instance_->dev_adj_stack_.size());
 }
 
+// a node whose reverse step latches SMG_ERR_SYNC, as a persistent solve whose
+// hand-off timed out would
+struct inject_sync_vari : public vari {
+  inject_sync_vari() : vari(0.0) {}
+  void chain() override { amd::check(smg_status_inject(amd::ctx(), SMG_ERR_SYNC), "inject"); }
+};
+
+static void cmd_status() {
+  std::vector<double> x = {0.5, -1.0, 2.0}, g;
+  double fx = 0;
+  expect_throw("sync_in_reverse", [&] {
+    gradient(
+        [](const std::vector<var>& t) {
+          var a(new inject_sync_vari());  // first on the tape: its chain() runs last
+          var b = normal_lpdf(t, 0.0, 1.0);
+          return a + b;
+        },
+        x, fx, g);
+  });
+  expect_throw("sync_in_forward_readback", [&] {
+    auto A = to_dev_var_matrix(x.data(), 3, 1);
+    amd::check(smg_status_inject(amd::ctx(), SMG_ERR_SYNC), "inject");
+    A.val();
+  });
+  // the latch is cleared by the throw: the next gradient is clean
+  gradient([](const std::vector<var>& t) { return normal_lpdf(t, 0.0, 1.0); }, x, fx, g);
+  print1("fx", fx);
+  print("grad", g);
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
 int main() {
   std::string cmd;
   std::cin >> cmd;
@@ -939,6 +973,7 @@ int main() {
     else if (cmd == "hvp") cmd_hvp();
     else if (cmd == "hessian") cmd_hessian();
     else if (cmd == "map_rect_glm") cmd_map_rect_glm();
+    else if (cmd == "status") cmd_status();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;

@@ -702,3 +702,36 @@ def test_mdivide_left_tri_512_blocks(ctx, m, n):
     gA = -np.tril(gB @ Cref.T)
     near_rel(ctx.get(dBa, m * n).reshape(n, m).T, gB, 1e-10, atol=1e-11 * np.abs(gB).max(), what="gB")
     near_rel(ctx.get(dAa, m * m).reshape(m, m).T, gA, 1e-10, atol=1e-11 * np.abs(gA).max(), what="gA")
+
+
+@pytest.mark.parametrize("m,n", [(1024, 1), (2048, 1), (4096, 1), (2048, 512)])
+def test_mdivide_left_tri_ill_conditioned(ctx, m, n):
+    """Rows scaled by a permuted grading 1e-6 .. 1 (cond(L) ~ 1e6, not a
+    well-conditioned Cholesky factor): the large lower solves that multiply
+    by explicit diagonal-block inverses must stay as backward stable as
+    substitution (the reference's Eigen triangularView::solve).  Normwise
+    backward error ||L C - B|| / (||L|| ||C|| + ||B||) within 20x scipy's
+    substitution (+1e-16), both for C = L^{-1} B and for the reverse's L^{-T} W."""
+    import scipy.linalg as sl
+    rng = np.random.default_rng(7 * m + n)
+    d = np.logspace(-6, 0, m)[rng.permutation(m)]
+    S = rng.uniform(-1, 1, (m, m))
+    L = d[:, None] * np.linalg.cholesky(S @ S.T / m + np.eye(m))
+    B = rng.uniform(-1, 1, (m, n))
+    W = rng.uniform(-1, 1, (m, n))
+
+    def berr(A, X, R):
+        return np.linalg.norm(A @ X - R) / (np.linalg.norm(A) * np.linalg.norm(X) + np.linalg.norm(R))
+
+    dA, dB, dC = ctx.put(F(L)), ctx.put(F(B)), ctx.zeros(m * n)
+    ctx.call("smg_mdivide_left_tri_fwd", 1, dA, m, dB, m, m, n, dC, m)
+    C = ctx.get(dC, m * n).reshape(n, m).T
+    Cref = sl.solve_triangular(L, B, lower=True)
+    assert np.all(np.isfinite(C))
+    assert berr(L, C, B) <= 20 * berr(L, Cref, B) + 1e-16, (berr(L, C, B), berr(L, Cref, B))
+    dW, dAa, dBa, ws = ctx.put(F(W)), ctx.zeros(m * m), ctx.zeros(m * n), ctx.zeros(m * n)
+    ctx.call("smg_mdivide_left_tri_rev", 1, dA, m, dC, m, dW, m, m, n, dAa, m, dBa, m, ws)
+    gB = ctx.get(dBa, m * n).reshape(n, m).T
+    gref = sl.solve_triangular(L, W, lower=True, trans="T")
+    assert np.all(np.isfinite(gB))
+    assert berr(L.T, gB, W) <= 20 * berr(L.T, gref, W) + 1e-16, (berr(L.T, gB, W), berr(L.T, gref, W))

@@ -214,3 +214,97 @@ def test_map_rect_executor_gloo(tmp_path, world):
     n_ok = sum(1 for _, fail in MAPRECT_CASES if fail < 0)
     want = 4 * (2 * n_ok + (len(MAPRECT_CASES) - n_ok))
     assert all(rk["collectives"] == want for rk in ranks), [rk["collectives"] for rk in ranks]
+
+
+# ---------------------------------------------------------------- product GLM reducers, W = 2
+GLMDIST_LIB = os.path.join(ROOT, "tests", "cpp", "_bin", "libglm_dist.so")
+_AR = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.c_longlong, ctypes.c_void_p)
+
+# (kind, fixture, bad global row or -1): kind 0 bernoulli (bad y = 2), 1 poisson (bad y = -1)
+GLM_DIST_CASES = [(0, "glm_R100000_M256", -1), (1, "poisson_log_glm_R20000_M64", -1),
+                  (0, "glm_R100000_M256", 77777), (1, "poisson_log_glm_R20000_M64", 123)]
+
+
+def _glm_case_block(kind, name, b0, b1):
+    d = golden(name)
+    R, M = int(d["R"]), int(d["M"])
+    if kind == 0:
+        x, y = _block(R, M, b0, b1)
+        th = gen.glm_inputs(1, M)[2]
+    else:
+        xf, yf, th = gen.glm2_inputs(R, M, "poisson")
+        x, y = xf[b0:b1], yf[b0:b1]
+    return R, M, np.asfortranarray(x), np.ascontiguousarray(y, dtype=np.int32), f64(th)
+
+
+def _glm_dist_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def allgather(send, count, recv, _user):  # unused by the reducers
+        raise RuntimeError("allgather called")
+
+    def allreduce(buf, count, _user):
+        a = np.ctypeslib.as_array(buf, shape=(count,))
+        t = torch.from_numpy(a.copy())
+        dist.all_reduce(t)
+        a[:] = t.numpy()
+        calls.append(count)
+
+    ag, ar = _AG(allgather), _AR(allreduce)
+    lib = ctypes.CDLL(GLMDIST_LIB)
+    lib.glm_dist_eval.restype = ctypes.c_int
+    res = {}
+    for kind, name, bad in GLM_DIST_CASES:
+        R = int(golden(name)["R"])
+        b0, b1 = _partition(R, world, rank)
+        R, M, x, y, th = _glm_case_block(kind, name, b0, b1)
+        if b0 <= bad < b1:
+            y[bad - b0] = 2 if kind == 0 else -1
+        fx = ctypes.c_double()
+        g = np.zeros(M + 1)
+        err = ctypes.create_string_buffer(512)
+        rc = lib.glm_dist_eval(world, rank, ag, ar, None, kind, ctypes.c_longlong(R), ctypes.c_longlong(b0),
+                               ctypes.c_longlong(b1 - b0), M, x.ctypes.data_as(ctypes.c_void_p),
+                               y.ctypes.data_as(ctypes.c_void_p), th.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.byref(fx), g.ctypes.data_as(ctypes.c_void_p), err, 512)
+        res[f"{kind}_{bad}"] = dict(rc=rc, fx=fx.value, g=g, err=err.value.decode(), own=b0 <= bad < b1)
+    res["allreduce_counts"] = calls
+    np.save(out + f".{rank}.npy", np.array(res, dtype=object), allow_pickle=True)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_glm_reducers_two_ranks_product_path(tmp_path):
+    """The product's row-sharded reducers (reduce_sum_bernoulli_logit_glm,
+    poisson_log_glm_lpmf on a glm_shard) in W = 2 processes sharing the GPU,
+    joined by a gloo all-reduce hook (amd::set_host_collective): each rank's
+    row block on the device, ONE all-reduce of [logp, alpha', beta' | y flag]
+    per call.  Both ranks return the reference's single-call result
+    (glm_R100000_M256 / poisson_log_glm_R20000_M64, real Stan Math) within
+    1e-12 / 1e-10, bitwise equal to each other; an out-of-support y on one
+    rank makes BOTH ranks throw domain_error (the owner with the reference's
+    message and the global index)."""
+    out = str(tmp_path / "gd")
+    mp.start_processes(_glm_dist_rank, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(2)]
+    for kind, name, bad in GLM_DIST_CASES:
+        key = f"{kind}_{bad}"
+        r0, r1 = ranks[0][key], ranks[1][key]
+        if bad < 0:
+            assert r0["rc"] == 0 and r1["rc"] == 0, (key, r0["err"], r1["err"])
+            assert r0["fx"] == r1["fx"] and np.array_equal(r0["g"], r1["g"]), key
+            d = golden(name)
+            near_rel(r0["fx"], d["fx"], 1e-12, what=f"{key} fx")
+            near_rel(r0["g"], d["grad"], 1e-10, what=f"{key} grad")
+        else:
+            assert r0["rc"] == 1 and r1["rc"] == 1, (key, r0, r1)
+            owner = r0 if r0["own"] else r1
+            fn = "bernoulli_logit_glm_lpmf" if kind == 0 else "poisson_log_glm_lpmf"
+            want = (f"{fn}: Vector of dependent variables[{bad + 1}] is 2, but must be in the interval [0, 1]"
+                    if kind == 0 else f"{fn}: Vector of dependent variables[{bad + 1}] is -1, but must be >= 0!")
+            assert owner["err"] == want, owner["err"]
+    # one all-reduce per call on every rank (M + 3 bernoulli, M + 4 poisson)
+    for rk in ranks:
+        assert rk["allreduce_counts"] == [259, 68, 259, 68], rk["allreduce_counts"]
