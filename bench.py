@@ -365,10 +365,14 @@ class Normal(Workload):
             self.gold = json.load(f)
         self.theta = np.array(self.gold["theta"], dtype=np.float64)
         self.g = np.zeros(self.N)
+        # pointers and the bound entry made once: per-call ctypes conversions
+        # would add several us to a ~20 us step
+        self._call = bl.smg_bench_normal_step
+        self._args = (self.N, ptr(self.theta), ptr(self.fx), ptr(self.g))
         return bl.smg_bench_device_init(self.local)
 
     def step(self):
-        return self.bl.smg_bench_normal_step(self.N, ptr(self.theta), ptr(self.fx), ptr(self.g))
+        return self._call(*self._args)
 
     def guard(self):
         want = np.array(self.gold["grad"])

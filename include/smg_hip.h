@@ -68,6 +68,10 @@ size_t smg_arena_used(const smg_ctx* ctx);
 size_t smg_arena_reserved(const smg_ctx* ctx);
 /* pinned host staging buffer (lifetime of the context) */
 void* smg_host_scratch(smg_ctx* ctx, size_t bytes);
+/* pinned host memory mapped into the device (zero-copy operands and outputs
+ * of the *_fused entries; coarse-grained: the kernels publish it with one
+ * system-scope release); grown on demand, reused by the next call */
+void* smg_pinned_io(smg_ctx* ctx, size_t bytes);
 
 int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src_host, size_t bytes);
 int smg_memcpy_d2h(smg_ctx* ctx, void* dst_host, const void* src, size_t bytes);
@@ -290,6 +294,17 @@ int smg_normal_lpdf(smg_ctx* ctx, const double* y, int sy, const double* mu,
                     int smu, const double* sigma, int ssig, long long n,
                     int include, double* out, double* gy, double* gmu,
                     double* gsigma);
+/* The same reduction fused with the three domain checks in ONE launch that
+ * completes before returning (latency-bound calls, e.g. config 1's 1024 host
+ * vars).  A vector operand is a pointer (device memory, or pinned host memory
+ * from smg_pinned_io: zero-copy, no separate copies); a NULL pointer selects
+ * the scalar value y0 / mu0 / sigma0 (a kernel argument: no memory read).
+ * res = [lp, bad_y, bad_mu, bad_sigma, gy, gmu, gsigma (the reduced partials
+ * of scalar operands)]; vector partials are WRITTEN (not accumulated).
+ * Replaces the body of prim/scal/prob/normal_lpdf.hpp:36-119. */
+int smg_normal_lpdf_fused(smg_ctx* ctx, const double* y, const double* mu, const double* sigma, double y0,
+                          double mu0, double sigma0, long long n, int include, double* res, double* gy,
+                          double* gmu, double* gsigma);
 
 /* bernoulli_logit_glm_lpmf<false>(y | x, alpha, beta), scalar alpha
  * (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-138) in ONE fused pass over

@@ -127,6 +127,11 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->offset = 0;
   ctx->host_status = 0;
   ctx->status_armed = 0;
+  ctx->pin_io = nullptr;
+  ctx->pin_io_size = 0;
+  ctx->done_h = nullptr;
+  ctx->done_seq = 0;
+  ctx->red_counter_d = nullptr;
   for (int i = 0; i < SMG_WS_COUNT; ++i) {
     ctx->ws[i] = nullptr;
     ctx->ws_doubles[i] = 0;
@@ -166,6 +171,13 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
     delete ctx;
     return SMG_ERR_HIP;
   }
+  if (hipHostMalloc(&ctx->done_h, 256, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipMalloc(&ctx->red_counter_d, 256) != hipSuccess) {
+    delete ctx;
+    return SMG_ERR_HIP;
+  }
+  *(volatile long long*)ctx->done_h = 0;
+  hipMemset(ctx->red_counter_d, 0, 256);
   hipDeviceSynchronize();
   *out = ctx;
   return SMG_OK;
@@ -189,6 +201,9 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   hipFree(ctx->status_d);
   hipHostFree(ctx->status_h);
   hipHostFree(ctx->host_scratch);
+  if (ctx->pin_io) hipHostFree(ctx->pin_io);
+  hipHostFree(ctx->done_h);
+  hipFree(ctx->red_counter_d);
   hipStreamDestroy(ctx->stream);
   delete ctx;
   return SMG_OK;
@@ -276,6 +291,37 @@ void* smg_host_scratch(smg_ctx* ctx, size_t bytes) {
     ctx->host_scratch_size = n;
   }
   return ctx->host_scratch;
+}
+
+void* smg_pinned_io(smg_ctx* ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  if (bytes > ctx->pin_io_size) {
+    hipStreamSynchronize(ctx->stream);
+    if (ctx->pin_io) hipHostFree(ctx->pin_io);
+    size_t n = ctx->pin_io_size ? ctx->pin_io_size : (size_t)1 << 16;
+    while (n < bytes) n *= 2;
+    // coarse-grained: kernel stores leave the L2 as whole lines at the
+    // system-scope release, instead of one PCIe write per store
+    if (hipHostMalloc(&ctx->pin_io, n, hipHostMallocNonCoherent | hipHostMallocMapped) != hipSuccess) {
+      hipGetLastError();
+      ctx->pin_io = nullptr;
+      ctx->pin_io_size = 0;
+      return nullptr;
+    }
+    ctx->pin_io_size = n;
+  }
+  return ctx->pin_io;
+}
+
+int smg_wait_done(smg_ctx* ctx, long long seq) {
+  // the kernel publishes seq after a system-scope release; spin briefly (the
+  // common case completes in microseconds), then fall back to the stream
+  // sync so a failed launch still returns
+  volatile long long* d = ctx->done_h;
+  for (long long spin = 0; spin < (1ll << 22); ++spin)
+    if (*d >= seq) return SMG_OK;
+  SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return *d >= seq ? SMG_OK : SMG_ERR_HIP;
 }
 
 int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {

@@ -258,6 +258,98 @@ __global__ void k_normal_final(const double* part, int np, double* out, double* 
   }
 }
 
+// fused normal_lpdf: domain checks, value and partials in ONE launch; every
+// operand / output pointer may be device memory or pinned host memory
+// (zero-copy: the latency-bound small calls on host vars read and write the
+// host directly).  Per-block [lp, bad_y, bad_mu, bad_s, sum gy, sum gmu,
+// sum gs]; with several blocks the last to arrive (self-resetting ticket)
+// sums them in block order (deterministic).  Publication: plain stores (the
+// pinned staging is coarse-grained, so partials leave the L2 as whole lines
+// at the release, not one PCIe write per 8-B store: write-through stores
+// measured 1.5 us slower at N = 1024), ONE system-scope release per block
+// (an L2 write-back), drained, then ONE system-scope store of seq to the host
+// completion word.
+__global__ void __launch_bounds__(1024) k_normal_fused(
+    const double* __restrict__ y, const double* __restrict__ mu, const double* __restrict__ sg, double y0,
+    double mu0, double s0, long long n, int inc, double* gy, double* gmu, double* gs,
+    int red_y, int red_mu, int red_s, double* part, unsigned int* counter, double* res,
+    long long* done, long long seq) {
+  __shared__ double lds[7][16];
+  __shared__ int last;
+  const double neg_log_sqrt_two_pi = -0.91893853320467274178;  // -log(sqrt(2 pi))
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const double yv = y ? y[i] : y0, mv = mu ? mu[i] : mu0, s = sg ? sg[i] : s0;
+    if (yv != yv) v[1] = 1.0;                               // check_not_nan(y)
+    if (!(fabs(mv) <= 1.7976931348623157e308)) v[2] = 1.0;  // check_finite(mu)
+    if (!(s > 0.0)) v[3] = 1.0;                             // check_positive(sigma)
+    const double inv_s = 1.0 / s;
+    const double z = (yv - mv) * inv_s;
+    const double z2 = z * z;
+    if (inc & 1) v[0] += neg_log_sqrt_two_pi;
+    if (inc & 2) v[0] -= log(s);
+    if (inc & 4) v[0] += -0.5 * z2;
+    const double sc = inv_s * z;
+    const double gsv = -inv_s + inv_s * z2;
+    if (gy) {
+      if (red_y) v[4] -= sc; else gy[i] = -sc;
+    }
+    if (gmu) {
+      if (red_mu) v[5] += sc; else gmu[i] = sc;
+    }
+    if (gs) {
+      if (red_s) v[6] += gsv; else gs[i] = gsv;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // flags by ballot; shuffle reductions (ds_bpermute round trips, the bulk
+  // of a small call's kernel time) only for the sums that are used
+  const bool any_y = __any(v[1] != 0.0), any_mu = __any(v[2] != 0.0), any_s = __any(v[3] != 0.0);
+  const double t0 = wave_sum(v[0]);
+  const double t4 = (gy && red_y) ? wave_sum(v[4]) : 0.0;
+  const double t5 = (gmu && red_mu) ? wave_sum(v[5]) : 0.0;
+  const double t6 = (gs && red_s) ? wave_sum(v[6]) : 0.0;
+  if (lane == 0) {
+    lds[0][w] = t0;
+    lds[1][w] = any_y ? 1.0 : 0.0;
+    lds[2][w] = any_mu ? 1.0 : 0.0;
+    lds[3][w] = any_s ? 1.0 : 0.0;
+    lds[4][w] = t4;
+    lds[5][w] = t5;
+    lds[6][w] = t6;
+  }
+  __syncthreads();
+  double tot = 0.0;  // thread c < 7: column c summed over the block's waves in order
+  if (threadIdx.x < 7)
+    for (int k = 0; k < nw; ++k) tot += lds[threadIdx.x][k];
+  if (gridDim.x > 1) {
+    if (threadIdx.x < 7)
+      __hip_atomic_store(part + 7 * blockIdx.x + threadIdx.x, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this block's partial vectors
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x < 7) {
+      tot = 0.0;
+      for (unsigned int b = 0; b < gridDim.x; ++b)
+        tot += __hip_atomic_load(part + 7 * b + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x < 7) res[threadIdx.x] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the L2 lines of every output
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ------------------------------------------------------------- helpers
 __global__ void k_axpy(long long n, double a, const double* __restrict__ x, int incx,
                        double* __restrict__ y, int incy) {
@@ -375,6 +467,22 @@ int smg_normal_lpdf(smg_ctx* ctx, const double* y, int sy, const double* mu, int
                      gsigma, ry, rmu, rs);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
+}
+
+int smg_normal_lpdf_fused(smg_ctx* ctx, const double* y, const double* mu, const double* sigma, double y0,
+                          double mu0, double sigma0, long long n, int include, double* res, double* gy,
+                          double* gmu, double* gsigma) {
+  if (!ctx || n < 0 || !res) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_ELEMWISE);
+  const int nb = n <= 4096 ? 1 : (int)(n / 4096 < 512 ? (n + 4095) / 4096 : 512);
+  double* part = nb > 1 ? smg_ws(ctx, SMG_WS_RED, 7 * (size_t)nb) : nullptr;
+  if (nb > 1 && !part) return SMG_ERR_OOM;
+  const long long seq = ++ctx->done_seq;
+  const int ry = y == nullptr, rmu = mu == nullptr, rs = sigma == nullptr;
+  hipLaunchKernelGGL(k_normal_fused, dim3(nb), dim3(1024), 0, ctx->stream, y, mu, sigma, y0, mu0, sigma0, n,
+                     include, gy, gmu, gsigma, ry, rmu, rs, part, ctx->red_counter_d, res, ctx->done_h, seq);
+  SMG_LAUNCH_CHECK();
+  return smg_wait_done(ctx, seq);
 }
 
 int smg_axpy(smg_ctx* ctx, long long n, double a, const double* x, int incx, double* y, int incy) {

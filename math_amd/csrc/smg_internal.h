@@ -51,6 +51,14 @@ struct smg_ctx {
   // pinned host scratch
   void* host_scratch;
   size_t host_scratch_size;
+  // zero-copy io: pinned, host-coherent memory the kernels of the latency-
+  // bound entries (smg_normal_lpdf_fused) read and write directly, plus the
+  // completion word they publish (host spins on it instead of a stream sync)
+  void* pin_io;
+  size_t pin_io_size;
+  long long* done_h;     // host-coherent completion word
+  long long done_seq;
+  unsigned int* red_counter_d;  // last-block-done counter of the fused reductions (device, self-resetting)
   // persistent device workspaces (grow on demand; NOT arena-managed)
   double* ws[8];  // SMG_WS_COUNT
   size_t ws_doubles[8];
@@ -100,6 +108,9 @@ enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_
        SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_COUNT = 8 };
 static_assert(SMG_WS_COUNT == sizeof(((smg_ctx*)nullptr)->ws) / sizeof(double*), "workspace slots");
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
+// spin on the host-coherent completion word until it reaches seq (then the
+// stream sync as a bounded fallback)
+extern "C" int smg_wait_done(smg_ctx* ctx, long long seq);
 
 // side-stream helpers (ctx.hip): events come from a per-context pool
 int smg_side_begin(smg_ctx* ctx);          // ensure `side` exists

@@ -44,6 +44,7 @@ _SIGS = {
     "smg_status_armed": (_I, [_P, ctypes.POINTER(_I)]),
     "smg_status_enqueue": (_I, [_P, _P]),
     "smg_status_inject": (_I, [_P, _I]),
+    "smg_pinned_io": (_P, [_P, _S]),
     "smg_profile_enable": (_I, [_P, _I]),
     "smg_profile_read": (_I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
     "smg_profile_flops": (_I, [_P, _I, ctypes.POINTER(_D)]),
@@ -73,6 +74,7 @@ _SIGS = {
     "smg_digamma_rev": (_I, [_P, _P, _L, _P, _P]),
     "smg_trigamma_fwd": (_I, [_P, _P, _L, _P]),
     "smg_normal_lpdf": (_I, [_P, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _P, _P]),
+    "smg_normal_lpdf_fused": (_I, [_P, _P, _P, _P, _D, _D, _D, _L, _I, _P, _P, _P, _P]),
     "smg_glm_ws_doubles": (_L, [_L, _I]),
     "smg_bernoulli_logit_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_normal_id_glm": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),

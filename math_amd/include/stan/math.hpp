@@ -11,6 +11,7 @@
 #include <stan/math/eigen/num_traits.hpp>
 #include <stan/math/rev/core.hpp>
 #include <stan/math/amd/matrix.hpp>
+#include <stan/math/rev/meta/operands_and_partials.hpp>
 #include <stan/math/rev/fun/gp_exp_quad_cov.hpp>
 #include <stan/math/rev/fun/cholesky_decompose.hpp>
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>

@@ -2,22 +2,31 @@
 #define STAN_MATH_REV_FUN_NORMAL_LPDF_HPP
 
 // normal_lpdf<propto>(y | mu, sigma) (prim/scal/prob/normal_lpdf.hpp:36-119)
-// as one device reduction: value sum_i [-1/2 z_i^2 - log sigma_i - log sqrt(2 pi)]
-// and the partials dy = -z/sigma, dmu = z/sigma, dsigma = -1/sigma + z^2/sigma
-// (:92-104) written by the same kernel (smg_normal_lpdf).
+// as ONE fused device launch (smg_normal_lpdf_fused): the three domain checks,
+// the value sum_i [-1/2 z_i^2 - log sigma_i - log sqrt(2 pi)] and the
+// partials dy = -z/sigma, dmu = z/sigma, dsigma = -1/sigma + z^2/sigma
+// (:92-104).  The node is built with operands_and_partials, as in the
+// reference (:61-62, :117).
 //
-// Operands: double, var, std::vector<double>, std::vector<var>, dev_data<double>
-// and dev_var_matrix (a vector of vars kept on the device).  Semantics kept:
-//   size_zero -> 0 (:45-47); checks in the reference order (:51-55)
-//   check_not_nan(y), check_finite(mu), check_positive(sigma) -- evaluated on
-//   the device, one flag per argument, read back with the value -- then
-//   check_consistent_sizes; include_summand<propto, ...> drops constant terms
-//   (:56-58, :86-91).  One node per call; its chain() scatters adj * partial
-//   into device adjoints (axpy) or host varis.
+// Operands: double, var, std::vector<double|var>, Eigen vectors of double|var
+// (host values), dev_data<double> and dev_var_matrix (device values).  Host
+// operands are staged in pinned, host-coherent memory the kernel reads and
+// writes directly (zero-copy): a call over host vars is one launch and one
+// completion wait, no separate copies, and its partials land in host memory
+// (the node's chain() is then pure host work).  Device operands stay on the
+// device and get device partials (a device edge: one axpy in chain()).
+//
+// Semantics kept: size_zero -> 0 (:45-47); check_not_nan(y),
+// check_finite(mu), check_positive(sigma) -- reported in that order -- then
+// check_consistent_sizes (:51-55); include_summand<propto, ...> drops the
+// constant terms (:56-58, :86-91); all-double propto -> 0.
 
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/core.hpp>
+#include <stan/math/rev/meta/operands_and_partials.hpp>
 
+#include <cmath>
+#include <cstring>
 #include <sstream>
 #include <stdexcept>
 #include <type_traits>
@@ -28,101 +37,96 @@ namespace math {
 
 namespace internal {
 
-/** An argument of a device lpdf reducer. */
-struct lpdf_operand {
-  const double* val = nullptr;  // device values (null: host scalar, uploaded by the caller)
-  double host = 0.0;            // host scalar value
+/** One operand as the fused kernel sees it. */
+struct fused_operand {
   size_t n = 1;
   bool vec = false;
-  vari* svi = nullptr;              // scalar var
-  dev_matrix_vari* dvi = nullptr;   // device vector of vars
-  bool is_var() const { return svi || dvi; }
+  bool host = true;             // values staged in pinned memory
+  const double* dev = nullptr;  // device values (host == false)
+  double scalar = 0.0;          // value of a scalar operand
 };
 
-inline lpdf_operand lpdf_arg(double x) {
-  lpdf_operand o;
-  o.host = x;
+inline fused_operand fused_of(double x) {
+  fused_operand o;
+  o.scalar = x;
   return o;
 }
-inline lpdf_operand lpdf_arg(const var& x) {
-  lpdf_operand o;
-  o.host = x.val();
-  o.svi = x.vi_;
-  return o;
-}
-inline lpdf_operand lpdf_arg(const dev_data<double>& x) {
-  lpdf_operand o;
-  o.val = x.data();
-  o.n = x.size();
+inline fused_operand fused_of(const var& x) { return fused_of(x.val()); }
+template <typename T>
+inline fused_operand fused_vec(size_t n) {
+  fused_operand o;
+  o.n = n;
   o.vec = true;
   return o;
 }
-inline lpdf_operand lpdf_arg(const dev_var_matrix& x) {
-  lpdf_operand o;
-  o.val = x.val_ptr();
+inline fused_operand fused_of(const std::vector<double>& x) { return fused_vec<double>(x.size()); }
+inline fused_operand fused_of(const std::vector<var>& x) { return fused_vec<var>(x.size()); }
+inline fused_operand fused_of(const dev_data<double>& x) {
+  fused_operand o;
   o.n = x.size();
   o.vec = true;
-  o.dvi = x.vi_;
+  o.host = false;
+  o.dev = x.data();
   return o;
 }
-inline lpdf_operand lpdf_arg(const std::vector<double>& x) {
-  if (x.empty()) {
-    lpdf_operand o;
-    o.n = 0;
-    o.vec = true;
-    return o;
-  }
-  return lpdf_arg(to_dev_data(x));
+inline fused_operand fused_of(const dev_var_matrix& x) {
+  fused_operand o;
+  o.n = x.size();
+  o.vec = true;
+  o.host = false;
+  o.dev = x.val_ptr();
+  return o;
 }
-inline lpdf_operand lpdf_arg(const std::vector<var>& x) {
-  if (x.empty()) {
-    lpdf_operand o;
-    o.n = 0;
-    o.vec = true;
-    return o;
-  }
-  return lpdf_arg(to_dev(x));
-}
-
 #ifdef STAN_MATH_AMD_HAS_EIGEN
-template <int R, int C>
-inline lpdf_operand lpdf_arg(const Eigen::Matrix<var, R, C>& x) {
-  std::vector<var> v(x.data(), x.data() + x.size());
-  return lpdf_arg(v);
+template <typename T, int R, int C>
+inline fused_operand fused_of(const Eigen::Matrix<T, R, C>& x) {
+  return fused_vec<T>(size_t(x.size()));
 }
-template <int R, int C>
-inline lpdf_operand lpdf_arg(const Eigen::Matrix<double, R, C>& x) {
-  std::vector<double> v(x.data(), x.data() + x.size());
-  return lpdf_arg(v);
-}
-template <typename T>
-struct is_eigen_double : std::false_type {};
-template <int R, int C>
-struct is_eigen_double<Eigen::Matrix<double, R, C>> : std::true_type {};
-#else
-template <typename T>
-struct is_eigen_double : std::false_type {};
 #endif
 
+/** Host values of a host vector operand into dst. */
+inline void fused_stage(const std::vector<double>& x, double* dst) {
+  if (!x.empty()) std::memcpy(dst, x.data(), x.size() * sizeof(double));
+}
+inline void fused_stage(const std::vector<var>& x, double* dst) {
+  for (size_t i = 0; i < x.size(); ++i) dst[i] = x[i].vi_->val_;
+}
+#ifdef STAN_MATH_AMD_HAS_EIGEN
+template <int R, int C>
+inline void fused_stage(const Eigen::Matrix<double, R, C>& x, double* dst) {
+  for (Eigen::Index i = 0; i < x.size(); ++i) dst[i] = x(i);
+}
+template <int R, int C>
+inline void fused_stage(const Eigen::Matrix<var, R, C>& x, double* dst) {
+  for (Eigen::Index i = 0; i < x.size(); ++i) dst[i] = x(i).vi_->val_;
+}
+#endif
 template <typename T>
-struct is_var_arg : std::integral_constant<bool, !std::is_same<T, double>::value &&
-                                                     !std::is_same<T, std::vector<double>>::value &&
-                                                     !std::is_same<T, dev_data<double>>::value &&
-                                                     !is_eigen_double<T>::value> {};
+inline void fused_stage(const T&, double*) {}  // scalars and device operands
 
-inline void lpdf_check_sizes(const char* fn, const char* const names[], const lpdf_operand* ops,
-                             int k) {
+/** Host partials of a host vector edge from the staging area. */
+template <typename Edge>
+inline void fused_take(Edge& e, const double* src, size_t n) {
+  for (size_t i = 0; i < n; ++i) e.partials_[int(i)] = src[i];
+}
+
+template <typename T>
+struct is_device_operand
+    : std::integral_constant<bool, std::is_same<T, dev_var_matrix>::value ||
+                                       std::is_same<T, dev_data<double>>::value> {};
+
+inline void normal_check_sizes(const char* fn, const fused_operand* ops) {
+  static const char* const names[3] = {"Random variable", "Location parameter", "Scale parameter"};
   size_t expect = 0;
   int first = -1;
-  for (int i = 0; i < k; ++i)
+  for (int i = 0; i < 3; ++i)
     if (ops[i].vec) {
       if (first < 0) {
         first = i;
         expect = ops[i].n;
       } else if (ops[i].n != expect) {
         std::ostringstream m;
-        m << fn << ": " << names[i] << " has dimension = " << ops[i].n
-          << ", expecting dimension = " << expect
+        m << fn << ": " << names[i] << " has dimension = " << ops[i].n << ", expecting dimension = " << expect
           << "; a function was called with arguments of different scalar, array, vector, or "
              "matrix types, and they were not consistently sized;  all arguments must be "
              "scalars or multidimensional values of the same shape.";
@@ -131,100 +135,121 @@ inline void lpdf_check_sizes(const char* fn, const char* const names[], const lp
     }
 }
 
-class lpdf_dev_vari : public vari {
- public:
-  static constexpr int K = 3;
-  lpdf_operand ops_[K];
-  double* g_[K];  // device partials (vector operands) -- null when constant
-  double gs_[K];  // host partials of scalar var operands
-  lpdf_dev_vari(double v, const lpdf_operand* ops, double* const* g, const double* gs)
-      : vari(v) {
-    for (int i = 0; i < K; ++i) {
-      ops_[i] = ops[i];
-      g_[i] = g[i];
-      gs_[i] = gs[i];
-    }
-  }
-  void chain() override {
-    for (int i = 0; i < K; ++i) {
-      if (ops_[i].dvi)
-        amd::check(smg_axpy(amd::ctx(), (long long)ops_[i].n, adj_, g_[i], 1, ops_[i].dvi->adj_, 1),
-                   "lpdf");
-      else if (ops_[i].svi)
-        ops_[i].svi->adj_ += adj_ * gs_[i];
-    }
-  }
-};
-
 }  // namespace internal
 
 template <bool propto, typename T_y, typename T_loc, typename T_scale>
-inline typename std::conditional<internal::is_var_arg<T_y>::value ||
-                                     internal::is_var_arg<T_loc>::value ||
-                                     internal::is_var_arg<T_scale>::value,
-                                 var, double>::type
-normal_lpdf(const T_y& y, const T_loc& mu, const T_scale& sigma) {
-  using internal::lpdf_operand;
+inline typename internal::ops_return<T_y, T_loc, T_scale>::type normal_lpdf(const T_y& y, const T_loc& mu,
+                                                                            const T_scale& sigma) {
+  using internal::fused_operand;
   static const char* fn = "normal_lpdf";
-  constexpr bool vy = internal::is_var_arg<T_y>::value, vmu = internal::is_var_arg<T_loc>::value,
-                 vs = internal::is_var_arg<T_scale>::value;
-  lpdf_operand ops[3] = {internal::lpdf_arg(y), internal::lpdf_arg(mu), internal::lpdf_arg(sigma)};
-  if ((ops[0].vec && ops[0].n == 0) || (ops[1].vec && ops[1].n == 0) ||
-      (ops[2].vec && ops[2].n == 0))
-    return 0.0;
+  constexpr bool vy = internal::op_is_var<T_y>::value, vmu = internal::op_is_var<T_loc>::value,
+                 vs = internal::op_is_var<T_scale>::value;
+  using ret_t = typename internal::ops_return<T_y, T_loc, T_scale>::type;
+  fused_operand ops[3] = {internal::fused_of(y), internal::fused_of(mu), internal::fused_of(sigma)};
+  for (auto& o : ops)
+    if (o.vec && o.n == 0) return ret_t(0.0);
   // include_summand<propto, ...>
   const bool inc_const = !propto;
   const bool inc_logsig = !propto || vs;
   const bool inc_quad = !propto || vy || vmu || vs;
   size_t N = 1;
-  for (auto& o : ops)
-    if (o.vec && o.n > N) N = o.n;
-
-  smg_ctx* c = amd::ctx();
-  // res = [lp, flag_y, flag_mu, flag_sigma, g_y, g_mu, g_sigma (scalar partials), host scalars y, mu, sigma]
-  double* res = amd::alloc_doubles(10);
-  std::vector<double> init(10, 0.0);
-  for (int i = 0; i < 3; ++i)
-    if (!ops[i].vec) init[7 + i] = ops[i].host;
-  amd::to_device(res, init.data(), 10);
-  for (int i = 0; i < 3; ++i)
-    if (!ops[i].vec) ops[i].val = res + 7 + i;
-  amd::check(smg_check_domain(c, ops[0].val, (long long)ops[0].n, 0, res + 1), fn);
-  amd::check(smg_check_domain(c, ops[1].val, (long long)ops[1].n, 1, res + 2), fn);
-  amd::check(smg_check_domain(c, ops[2].val, (long long)ops[2].n, 2, res + 3), fn);
-  double* g[3] = {nullptr, nullptr, nullptr};
-  for (int i = 0; i < 3; ++i) {
-    if (!ops[i].is_var()) continue;
-    if (ops[i].vec) {
-      g[i] = amd::alloc_doubles(ops[i].n);
-      amd::zero(g[i], ops[i].n);
-    } else {
-      g[i] = res + 4 + i;
-    }
-  }
-  // sizes are checked after the domain checks (reference order) but before
-  // the reduction reads N elements of every vector operand
   bool sizes_ok = true;
   for (auto& o : ops)
+    if (o.vec) N = o.n > N ? o.n : N;
+  for (auto& o : ops)
     if (o.vec && o.n != N) sizes_ok = false;
-  double h[10];
+
+  smg_ctx* c = amd::ctx();
+  // pinned staging: [res(8) | host values of y, mu, sigma | host partials of y, mu, sigma]
+  size_t off = 8, val_off[3], g_off[3];
+  for (int i = 0; i < 3; ++i) {
+    val_off[i] = off;
+    if (ops[i].host && ops[i].vec) off += ops[i].n;
+  }
+  const bool want_g[3] = {vy, vmu, vs};
+  for (int i = 0; i < 3; ++i) {
+    g_off[i] = off;
+    if (want_g[i] && ops[i].vec && ops[i].host) off += ops[i].n;
+  }
+  double* st = static_cast<double*>(smg_pinned_io(c, off * sizeof(double)));
+  if (!st) throw std::bad_alloc();
+  for (int i = 0; i < 8; ++i) st[i] = 0.0;
+  internal::fused_stage(y, st + val_off[0]);
+  internal::fused_stage(mu, st + val_off[1]);
+  internal::fused_stage(sigma, st + val_off[2]);
+  const double* vals[3];  // vector operands; NULL: the scalar value (a kernel argument)
+  for (int i = 0; i < 3; ++i) vals[i] = !ops[i].vec ? nullptr : (ops[i].host ? st + val_off[i] : ops[i].dev);
+  operands_and_partials<T_y, T_loc, T_scale> ops_partials(y, mu, sigma);
+  // partial outputs: host vectors -> staging, device vars -> the device edge,
+  // scalars -> reduced into res[4 + i]
+  double* g[3] = {nullptr, nullptr, nullptr};
+  if constexpr (vy) {
+    if (ops[0].vec) {
+      if constexpr (internal::is_device_operand<T_y>::value) g[0] = ops_partials.edge1_.partials_;
+      else g[0] = st + g_off[0];
+    } else {
+      g[0] = st + 4;
+    }
+  }
+  if constexpr (vmu) {
+    if (ops[1].vec) {
+      if constexpr (internal::is_device_operand<T_loc>::value) g[1] = ops_partials.edge2_.partials_;
+      else g[1] = st + g_off[1];
+    } else {
+      g[1] = st + 5;
+    }
+  }
+  if constexpr (vs) {
+    if (ops[2].vec) {
+      if constexpr (internal::is_device_operand<T_scale>::value) g[2] = ops_partials.edge3_.partials_;
+      else g[2] = st + g_off[2];
+    } else {
+      g[2] = st + 6;
+    }
+  }
   const int include = (inc_const ? 1 : 0) | (inc_logsig ? 2 : 0) | (inc_quad ? 4 : 0);
-  const bool any_var = vy || vmu || vs;
-  if (sizes_ok && (any_var || !propto))
-    amd::check(smg_normal_lpdf(c, ops[0].val, ops[0].vec ? 1 : 0, ops[1].val, ops[1].vec ? 1 : 0,
-                               ops[2].val, ops[2].vec ? 1 : 0, (long long)N, include, res, g[0],
-                               g[1], g[2]),
+  if (sizes_ok) {
+    amd::check(smg_normal_lpdf_fused(c, vals[0], vals[1], vals[2], ops[0].scalar, ops[1].scalar, ops[2].scalar,
+                                     (long long)N, include, st, g[0], g[1], g[2]),
                fn);
-  amd::to_host(h, res, 10);
-  static const char* const names[3] = {"Random variable", "Location parameter", "Scale parameter"};
-  if (h[1] != 0.0) throw std::domain_error(std::string(fn) + ": Random variable is nan, but must not be nan!");
-  if (h[2] != 0.0) throw std::domain_error(std::string(fn) + ": Location parameter is not finite, but must be finite!");
-  if (h[3] != 0.0) throw std::domain_error(std::string(fn) + ": Scale parameter is not positive, but must be > 0!");
-  internal::lpdf_check_sizes(fn, names, ops, 3);
-  if constexpr (vy || vmu || vs) {
-    return var(new internal::lpdf_dev_vari(h[0], ops, g, h + 4));
   } else {
-    return propto ? 0.0 : h[0];
+    // error path: the domain checks over each operand's own length, in order
+    for (int i = 0; i < 3; ++i) {
+      if (vals[i]) {
+        amd::check(smg_check_domain(c, vals[i], (long long)ops[i].n, i, st + 1 + i), fn);
+      } else {
+        const double x = ops[i].scalar;
+        st[1 + i] = (i == 0 ? x != x : i == 1 ? !(std::fabs(x) <= 1.7976931348623157e308) : !(x > 0.0)) ? 1.0 : 0.0;
+      }
+    }
+    amd::check(smg_sync(c), fn);
+  }
+  if (st[1] != 0.0) throw std::domain_error(std::string(fn) + ": Random variable is nan, but must not be nan!");
+  if (st[2] != 0.0)
+    throw std::domain_error(std::string(fn) + ": Location parameter is not finite, but must be finite!");
+  if (st[3] != 0.0)
+    throw std::domain_error(std::string(fn) + ": Scale parameter is not positive, but must be > 0!");
+  internal::normal_check_sizes(fn, ops);
+  const double logp = st[0];
+  if constexpr (vy || vmu || vs) {
+    if constexpr (vy) {
+      if (!ops[0].vec) ops_partials.edge1_.partials_[0] = st[4];
+      else if constexpr (!internal::is_device_operand<T_y>::value)
+        internal::fused_take(ops_partials.edge1_, st + g_off[0], ops[0].n);
+    }
+    if constexpr (vmu) {
+      if (!ops[1].vec) ops_partials.edge2_.partials_[0] = st[5];
+      else if constexpr (!internal::is_device_operand<T_loc>::value)
+        internal::fused_take(ops_partials.edge2_, st + g_off[1], ops[1].n);
+    }
+    if constexpr (vs) {
+      if (!ops[2].vec) ops_partials.edge3_.partials_[0] = st[6];
+      else if constexpr (!internal::is_device_operand<T_scale>::value)
+        internal::fused_take(ops_partials.edge3_, st + g_off[2], ops[2].n);
+    }
+    return ops_partials.build(logp);
+  } else {
+    return propto ? 0.0 : logp;
   }
 }
 

@@ -30,6 +30,8 @@
 //                                 beta, 5 row shards), Eigen path (Matrix<var>), mixed and
 //                                 all-double operands; x filled on the device (gen.glm_cat_inputs)
 //   glm_cat_errors                the reference's exceptions / early returns on small inputs
+//   ops_partials y mu sigma (9)   a user lpdf on operands_and_partials (vector / Eigen / device /
+//                                 data / broadcast edges)
 //   status                        a latched SMG_ERR_SYNC throws from the gradient() / readback that
 //                                 ran it, and is cleared
 #include <stan/math.hpp>
@@ -325,6 +327,70 @@ static void cmd_normal_vec() {
   var fp = normal_lpdf<true>(yv, mv, sv);
   print1("fx_propto", fp.val());
   recover_memory_nested();
+}
+
+// A user-written lpdf on the reference's operands_and_partials API
+// (rev/scal/meta/operands_and_partials.hpp:72-127): host arithmetic, one
+// node over three edges of different kinds.
+template <typename T_y, typename T_mu, typename T_s>
+static var user_normal_lpdf(const T_y& y, const T_mu& mu, const T_s& sigma, const std::vector<double>& yv,
+                            const std::vector<double>& mv, const std::vector<double>& sv) {
+  operands_and_partials<T_y, T_mu, T_s> ops_partials(y, mu, sigma);
+  double logp = 0.0;
+  for (size_t i = 0; i < yv.size(); ++i) {
+    const double inv_s = 1.0 / sv[i], z = (yv[i] - mv[i]) * inv_s;
+    logp += -0.5 * z * z - std::log(sv[i]) - 0.5 * std::log(2.0 * M_PI);
+    ops_partials.edge1_.partials_[int(i)] -= inv_s * z;
+    ops_partials.edge2_.partials_[int(i)] += inv_s * z;
+    ops_partials.edge3_.partials_[int(i)] += -inv_s + inv_s * z * z;
+  }
+  return ops_partials.build(logp);
+}
+
+static void cmd_ops_partials() {
+  auto y = read_vec(9), mu = read_vec(9), s = read_vec(9);
+  start_nested();
+  {  // std::vector<var>, Eigen::Matrix<var>, std::vector<var> edges
+    std::vector<var> yv = vars(y), sv = vars(s);
+    Eigen::Matrix<var, Eigen::Dynamic, 1> mv(9);
+    for (int i = 0; i < 9; ++i) mv(i) = mu[size_t(i)];
+    var f = user_normal_lpdf(yv, mv, sv, y, mu, s);
+    f.grad();
+    print1("fx", f.val());
+    print("grad_y", adjs(yv));
+    std::vector<double> gm(9);
+    for (int i = 0; i < 9; ++i) gm[size_t(i)] = mv(i).adj();
+    print("grad_mu", gm);
+    print("grad_sigma", adjs(sv));
+  }
+  set_zero_all_adjoints_nested();
+  {  // a data edge (y), a device edge (mu: dev_var_matrix, partials set from the host), a scalar-broadcast var
+    auto md = to_dev_var_matrix(mu.data(), 9, 1);
+    var s0 = s[0];
+    std::vector<double> s9(9, s[0]);
+    operands_and_partials<std::vector<double>, dev_var_matrix, var> op(y, md, s0);
+    double logp = 0.0;
+    std::vector<double> gmu(9);
+    for (int i = 0; i < 9; ++i) {
+      const double z = (y[size_t(i)] - mu[size_t(i)]) / s[0];
+      logp += -0.5 * z * z - std::log(s[0]) - 0.5 * std::log(2.0 * M_PI);
+      op.edge1_.partials_[i] -= z / s[0];  // swallowed: data
+      gmu[size_t(i)] = z / s[0];
+      op.edge3_.partials_[i] += -1.0 / s[0] + z * z / s[0];  // broadcast: all alias one partial
+    }
+    op.edge2_.set_partials(gmu.data());
+    var f = op.build(logp);
+    f.grad();
+    print1("fx_mixed", f.val());
+    print("grad_mu_dev", md.adj());
+    print1("grad_sigma_scalar", s0.adj());
+    // all-double operands: build() returns the value
+    operands_and_partials<std::vector<double>, double> od(y, 1.0);
+    print1("double_build", od.build(3.5));
+  }
+  recover_memory_nested();
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
 }
 
 static void cmd_normal_known() {
@@ -974,6 +1040,7 @@ int main() {
     else if (cmd == "hessian") cmd_hessian();
     else if (cmd == "map_rect_glm") cmd_map_rect_glm();
     else if (cmd == "status") cmd_status();
+    else if (cmd == "ops_partials") cmd_ops_partials();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;

@@ -83,8 +83,33 @@ int main() {
   }
   hipStreamSynchronize(s);
   double td = (now() - t0) / reps;
+  double *cx, *cg;
+  hipHostMalloc(&cx, n * 8, hipHostMallocCoherent | hipHostMallocMapped);
+  hipHostMalloc(&cg, (n + 1) * 8, hipHostMallocCoherent | hipHostMallocMapped);
+  for (int i = 0; i < n; ++i) cx[i] = 0.001 * i;
+  t0 = now();
+  for (int r = 0; r < reps; ++r) {
+    hipLaunchKernelGGL(k_neg, dim3(1), dim3(1024), 0, s, cx, cg, n, hflag, reps + r + 1);
+    while (*(volatile int*)hflag != reps + r + 1) {
+    }
+  }
+  hipStreamSynchronize(s);
+  double te = (now() - t0) / reps;
+  // f) coarse-grained data, but the host rewrites the input every call and checks the output
+  int bad = 0;
+  t0 = now();
+  for (int r = 0; r < reps; ++r) {
+    for (int i = 0; i < n; ++i) hx[i] = 0.001 * i + r;
+    hipLaunchKernelGGL(k_neg, dim3(1), dim3(1024), 0, s, hx, hg, n, hflag, 2 * reps + r + 1);
+    while (*(volatile int*)hflag != 2 * reps + r + 1) {
+    }
+    bad += hg[7] != -(0.007 + r);
+  }
+  hipStreamSynchronize(s);
+  double tf = (now() - t0) / reps;
   std::printf("{\"empty_launch_sync_us\": %.2f, \"h2d_kernel_d2h_sync_us\": %.2f, \"zero_copy_sync_us\": %.2f, "
-              "\"zero_copy_spin_us\": %.2f, \"check\": %.6f}\n",
-              ta * 1e6, tb * 1e6, tc * 1e6, td * 1e6, hg[n]);
+              "\"zero_copy_spin_us\": %.2f, \"zero_copy_spin_coherent_us\": %.2f, "
+              "\"zero_copy_spin_rewrite_us\": %.2f, \"stale_reads\": %d, \"check\": %.6f}\n",
+              ta * 1e6, tb * 1e6, tc * 1e6, td * 1e6, te * 1e6, tf * 1e6, bad, hg[n]);
   return 0;
 }
