@@ -120,6 +120,19 @@ int smg_fill_bernoulli(smg_ctx* ctx, int* out, long long n, unsigned long long s
 int smg_gemm(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n, int k,
              double alpha, const double* A, int lda, const double* B, int ldb,
              double beta, double* C, int ldc);
+/* smg_gemm with triangular operands: tri = OR of SMG_TRI_A_LOWER (op(A)(i,k)
+ * = 0 for k > i), SMG_TRI_A_UPPER (= 0 for k < i), SMG_TRI_B_LOWER (op(B)(k,j)
+ * = 0 for k < j), SMG_TRI_B_UPPER (= 0 for k > j).  Every output tile's K
+ * loop covers only the k where both operands can be nonzero (a lower x lower
+ * product with lower output: 1/6 of the dense multiply-adds); the zeros must
+ * be stored.  Used by the tangent L' = L Phi and its reverse, and by the
+ * triangular solves' diagonal-block products. */
+#define SMG_TRI_A_LOWER 1
+#define SMG_TRI_A_UPPER 2
+#define SMG_TRI_B_LOWER 4
+#define SMG_TRI_B_UPPER 8
+int smg_gemm_tri(smg_ctx* ctx, int transA, int transB, int uplo, int tri, int m, int n, int k, double alpha,
+                 const double* A, int lda, const double* B, int ldb, double beta, double* C, int ldc);
 
 /* ---------------------------------------------------------- functors ---- */
 
@@ -242,6 +255,15 @@ int smg_quad_form_sym_rev(smg_ctx* ctx, const double* A, int lda,
 
 /* multiply(A, B) (rev/mat/fun/multiply.hpp:65-135): fwd C = A B;
  * rev Aadj += Cadj B^T, Badj += A^T Cadj (NULL skips an operand). */
+/* C = L P for lower-triangular L, P (the Cholesky tangent L' = L Phi(Y) of
+ * the fvar<var> functors): lower output, every tile's K range cut to the
+ * triangles (N^3/3 flops instead of 2 N^3); the reverse accumulates the
+ * lower triangles of L_adj += tril(C_adj) P^T and P_adj += L^T tril(C_adj)
+ * (ws: n x n doubles). */
+int smg_multiply_lower_fwd(smg_ctx* ctx, const double* L, int ldl, const double* P, int ldp, int n, double* C,
+                           int ldc);
+int smg_multiply_lower_rev(smg_ctx* ctx, const double* L, int ldl, const double* P, int ldp, const double* Cadj,
+                           int ldca, int n, double* Ladj, int ldla, double* Padj, int ldpa, double* ws);
 int smg_multiply_fwd(smg_ctx* ctx, const double* A, int lda, const double* B,
                      int ldb, int m, int k, int n, double* C, int ldc);
 int smg_multiply_rev(smg_ctx* ctx, const double* A, int lda, const double* B,

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
     int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab, long long sA,
-    long long sB, long long sC, int px, int ntp) {
+    long long sB, long long sC, int px, int ntp, int tri) {
   // strided batch over blockIdx.y (sA = sB = sC = 0 for a single product)
   A += blockIdx.y * sA;
   B += blockIdx.y * sB;
@@ -182,8 +182,22 @@ __global__ __launch_bounds__(256) void k_gemm(
   if (MODE == 1 && !tri_sq && bj * BN > bi * BM + BM - 1) return;
   if (MODE == 2 && !tri_sq && bi * BM > bj * BN + BN - 1) return;
   const int i0 = bi * BM, j0 = bj * BN;
-  const int kbeg = split * kchunk;
-  const int kend = min(k, kbeg + kchunk);
+  int kbeg = split * kchunk;
+  int kend = min(k, kbeg + kchunk);
+  if (tri) {
+    // triangular operands: only k where both op(A)(i, k) and op(B)(k, j) can
+    // be nonzero for some (i, j) of this tile (BK-aligned: the extra
+    // elements are stored zeros)
+    int lo = 0, hi = k;
+    if (tri & 1) hi = min(hi, i0 + BM);  // op(A) lower: zero for k > i
+    if (tri & 2) lo = max(lo, i0);       // op(A) upper: zero for k < i
+    if (tri & 4) lo = max(lo, j0);       // op(B) lower: zero for k < j
+    if (tri & 8) hi = min(hi, j0 + BN);  // op(B) upper: zero for k > j
+    lo = lo / BK * BK;
+    kbeg = max(kbeg, lo);
+    kend = min(kend, hi);
+    if (kend < kbeg) kend = kbeg;
+  }
 
   constexpr int TM = BM / 32, TN = BN / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -335,7 +349,7 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
 template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
 int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
            int lda, const double* B, int ldb, double beta, double* C, int ldc, int batch = 1,
-           long long sA = 0, long long sB = 0, long long sC = 0) {
+           long long sA = 0, long long sB = 0, long long sC = 0, int tri = 0) {
   const int tm = smg_ceil_div(m, BM), tn = smg_ceil_div(n, BN);
   const int ntiles = (MODE != 0 && m == n && BM == BN) ? tm * (tm + 1) / 2 : tm * tn;
   // split K when the tile grid cannot fill the 256 CUs and K is long
@@ -347,7 +361,8 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   // 512^3 with 32 x 32 tiles, 256 tiles: 12.3 us unsplit vs 15.9 us split
   // in two plus the reduction)
   const bool covers = ntiles >= 256 && k <= 1024;
-  if (!nosplit && batch == 1 && ntiles < target && !covers && k >= 2 * KMIN) {
+  // (triangular operands: every tile has its own K range, no split)
+  if (!nosplit && !tri && batch == 1 && ntiles < target && !covers && k >= 2 * KMIN) {
     splits = smg_ceil_div(target, ntiles);
     const int maxs = k / KMIN;
     if (splits > maxs) splits = maxs;
@@ -383,7 +398,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   }
   hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntp * splits, batch), dim3(256), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
-                     ntiles, kchunk, slab, sA, sB, sC, px, ntp);
+                     ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri);
   if (splits > 1) {
     const long long tot = (long long)m * n;
     hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
@@ -416,7 +431,7 @@ constexpr int BK64 = 16;
 
 template <bool TA, bool TB, int MODE>
 int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
-                  int lda, const double* B, int ldb, double beta, double* C, int ldc) {
+                  int lda, const double* B, int ldb, double beta, double* C, int ldc, int tri) {
   // In-place products (C aliases an operand: the blocked TRSMs C = C Dinv,
   // L21 = A21 Dinv^T, X_p = W_p B_p) are race-free only when every workgroup
   // owns whole rows (C aliases A) or whole columns (C aliases B) of C.
@@ -424,13 +439,13 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   const bool alias_b = overlaps(B, ldb, TB ? n : k, TB ? k : n, C, ldc, m, n);
   if (alias_a || alias_b) {
     if (MODE == 0 && alias_a && !alias_b && n <= 64)
-      return launch<32, 64, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+      return launch<32, 64, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (MODE == 0 && alias_b && !alias_a && m <= 64)
-      return launch<64, 32, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+      return launch<64, 32, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     // general aliasing: out of place through a workspace, then C = T (+ beta C)
     double* T = smg_ws(ctx, SMG_WS_ALIAS, (size_t)m * n);
     if (!T) return SMG_ERR_OOM;
-    int rc = dispatch_tile<TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, 0.0, T, m);
+    int rc = dispatch_tile<TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, 0.0, T, m, tri);
     if (rc) return rc;
     if (beta == 0.0) return smg_copy_impl(ctx, m, n, T, m, C, ldc, 1.0, 0);
     if (beta != 1.0) {
@@ -453,30 +468,30 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
       return e ? atoi(e) : 0;
     }();
     if (forced == 128)
-      return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+      return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (forced == 12864)
-      return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+      return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (forced == 64)
-      return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+      return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (forced == 32)
-      return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+      return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   }
   // (triangle modes keep 64 x 64 tiles: half the 128-tile grid would sit on
   // the diagonal, and the split-K those few tiles need costs a reduction)
   if (MODE == 0 && big_tiles >= 256 && k > 128)
-    return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   // long-K transposed-A products with a small output (the Murray reverse's
   // [R_adj | D_adj] -= C_adj^T [B | C]: 512 x K x m, m >= 1536): 128 x 64
   // tiles split over K (tools/ubench_gemm: (512,2048,2048) 87 vs 100 us,
   // (512,1024,3072) 68 vs 81 us with 32 x 32)
   if (MODE == 0 && TA && !TB && k >= 1536 && mid_tiles < 512)
-    return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   // 64 x 64 only when its grid fills two workgroups per CU without split-K:
   // below that, 32 x 32 tiles (4x the workgroups) beat a split 64 x 64 grid
   // (tools/ubench_gemm: (3584,256,256) 18.6 vs 28 us)
   if (mid_tiles >= 512)
-    return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+  return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
 }
 
 }  // namespace
@@ -505,7 +520,7 @@ int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, dou
 
 int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
                   double alpha, const double* A, int lda, const double* B, int ldb,
-                  double beta, double* C, int ldc) {
+                  double beta, double* C, int ldc, int tri) {
   if (m <= 0 || n <= 0) return SMG_OK;
   if (k <= 0 || alpha == 0.0) {
     if (beta == 1.0) return SMG_OK;
@@ -516,21 +531,33 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
     ctx->prof_flops[SMG_FAM_GEMM] +=
         uplo ? 2.0 * k * ((double)m * n - (double)n * (n - 1) / 2) : 2.0 * m * n * k;
   if (uplo == 1) {
-    if (!ta && tb) return dispatch_tile<false, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-    if (ta && !tb) return dispatch_tile<true, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-    if (!ta && !tb) return dispatch_tile<false, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-    return dispatch_tile<true, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (!ta && tb) return dispatch_tile<false, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    if (ta && !tb) return dispatch_tile<true, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    if (!ta && !tb) return dispatch_tile<false, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    return dispatch_tile<true, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   }
   if (uplo == 2) {
-    if (!ta && tb) return dispatch_tile<false, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-    if (ta && !tb) return dispatch_tile<true, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-    if (!ta && !tb) return dispatch_tile<false, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-    return dispatch_tile<true, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    if (!ta && tb) return dispatch_tile<false, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    if (ta && !tb) return dispatch_tile<true, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    if (!ta && !tb) return dispatch_tile<false, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    return dispatch_tile<true, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   }
-  if (!ta && !tb) return dispatch_tile<false, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  if (!ta && tb) return dispatch_tile<false, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  if (ta && !tb) return dispatch_tile<true, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
-  return dispatch_tile<true, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+  if (!ta && !tb) return dispatch_tile<false, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  if (!ta && tb) return dispatch_tile<false, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  if (ta && !tb) return dispatch_tile<true, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  return dispatch_tile<true, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+}
+
+extern "C" int smg_gemm_tri(smg_ctx* ctx, int ta, int tb, int uplo, int tri, int m, int n, int k,
+                            double alpha, const double* A, int lda, const double* B, int ldb, double beta,
+                            double* C, int ldc) {
+  if (!ctx || m < 0 || n < 0 || k < 0 || tri < 0 || tri > 15) return SMG_ERR_ARG;
+  if ((m > 0 && n > 0) && (!C || ldc < m)) return SMG_ERR_ARG;
+  if (k > 0 && m > 0 && n > 0 && alpha != 0.0) {
+    if (!A || !B) return SMG_ERR_ARG;
+    if (lda < (ta ? k : m) || ldb < (tb ? n : k)) return SMG_ERR_ARG;
+  }
+  return smg_gemm_impl(ctx, ta, tb, uplo, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
 }
 
 extern "C" int smg_gemm(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,

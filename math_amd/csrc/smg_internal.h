@@ -138,10 +138,13 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
                         const double* W256, const double* W512, int ldw, const double* x, double* y,
                         double* r, int n);
 
-// internal GEMM entry used by other units (no argument re-validation)
+// internal GEMM entry used by other units (no argument re-validation).
+// tri: triangular operands (SMG_TRI_* bits of smg_hip.h, in op() orientation);
+// every tile's K loop is cut to the range where both operands can be nonzero
+// (the caller guarantees stored zeros outside each triangle)
 int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
                   int k, double alpha, const double* A, int lda, const double* B,
-                  int ldb, double beta, double* C, int ldc);
+                  int ldb, double beta, double* C, int ldc, int tri = 0);
 
 int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha,
                           const double* A, int lda, long long sA, const double* B, int ldb,

@@ -134,8 +134,10 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
     const int p = forward ? q : nblk - 1 - q;
     const int j = p * BSZ, b = min(BSZ, m - j), k = j + b;
     double* Bp = B + j;
-    // X_p = W_p (or W_p^T) B_p, in place (the GEMM's aliasing path)
-    rc = smg_gemm_impl(ctx, wt ? 1 : 0, 0, 0, b, n, b, 1.0, W + j, ldw, Bp, ldb, 0.0, Bp, ldb);
+    // X_p = W_p (or W_p^T) B_p, in place (the GEMM's aliasing path); W_p is
+    // lower triangular with stored zeros: each tile's K loop skips them
+    rc = smg_gemm_impl(ctx, wt ? 1 : 0, 0, 0, b, n, b, 1.0, W + j, ldw, Bp, ldb, 0.0, Bp, ldb,
+                       wt ? SMG_TRI_A_UPPER : SMG_TRI_A_LOWER);
     if (rc) return rc;
     if (forward && k < m) {
       if (lower)  // B[k:] -= L[k:, j:k] X_p
@@ -197,6 +199,41 @@ int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda, 
   }
   if (Badj) return smg_copy_impl(ctx, m, n, ws, m, Badj, ldba, 1.0, 1);
   return SMG_OK;
+}
+
+int smg_multiply_lower_fwd(smg_ctx* ctx, const double* L, int ldl, const double* P, int ldp, int n, double* C,
+                           int ldc) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!L || !P || !C || ldl < n || ldp < n || ldc < n) return SMG_ERR_ARG;
+  // C = L P is lower: the lower tiles only, each over k in [j, i]
+  int rc = smg_scale_impl(ctx, n, n, 0.0, C, ldc, 3);
+  if (rc) return rc;
+  return smg_gemm_impl(ctx, 0, 0, 1, n, n, n, 1.0, L, ldl, P, ldp, 0.0, C, ldc,
+                       SMG_TRI_A_LOWER | SMG_TRI_B_LOWER);
+}
+
+int smg_multiply_lower_rev(smg_ctx* ctx, const double* L, int ldl, const double* P, int ldp, const double* Cadj,
+                           int ldca, int n, double* Ladj, int ldla, double* Padj, int ldpa, double* ws) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!L || !P || !Cadj || !ws || ldl < n || ldp < n || ldca < n) return SMG_ERR_ARG;
+  // only C's lower triangle depends on (L, P); only the lower triangles of
+  // Ladj and Padj are read downstream (both operands are lower-structured):
+  //   T = tril(Cadj);  tril(Ladj) += tril(T P^T);  tril(Padj) += tril(L^T T)
+  int rc = smg_copy_impl(ctx, n, n, Cadj, ldca, ws, n, 1.0, 0);
+  if (rc) return rc;
+  rc = smg_scale_impl(ctx, n, n, 0.0, ws, n, 3);
+  if (rc) return rc;
+  if (Ladj) {  // (T P^T)(i, j) = sum_{k <= j} T(i, k) P(j, k)
+    rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, ws, n, P, ldp, 1.0, Ladj, ldla,
+                       SMG_TRI_A_LOWER | SMG_TRI_B_UPPER);
+    if (rc) return rc;
+  }
+  if (Padj)  // (L^T T)(i, j) = sum_{k >= i} L(k, i) T(k, j)
+    rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, ws, n, 1.0, Padj, ldpa,
+                       SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+  return rc;
 }
 
 int smg_multiply_fwd(smg_ctx* ctx, const double* A, int lda, const double* B, int ldb, int m, int k,

@@ -51,6 +51,7 @@ _SIGS = {
     "smg_fill_unif": (_I, [_P, _P, _L, ctypes.c_ulonglong, _D, _D, _D]),
     "smg_fill_bernoulli": (_I, [_P, _P, _L, ctypes.c_ulonglong, _D]),
     "smg_gemm": (_I, [_P, _I, _I, _I, _I, _I, _I, _D, _P, _I, _P, _I, _D, _P, _I]),
+    "smg_gemm_tri": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _D, _P, _I, _P, _I, _D, _P, _I]),
     "smg_gp_exp_quad_cov_fwd": (_I, [_P, _P, _I, _D, _D, _P, _I]),
     "smg_gp_exp_quad_cov_rev": (_I, [_P, _P, _I, _D, _D, _P, _I, _P]),
     "smg_add_diag_fwd": (_I, [_P, _P, _I, _I, _D, _P, _P, _I]),
@@ -62,6 +63,8 @@ _SIGS = {
     "smg_cholesky_rev": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_fwd": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_rev": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
+    "smg_multiply_lower_fwd": (_I, [_P, _P, _I, _P, _I, _I, _P, _I]),
+    "smg_multiply_lower_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
     "smg_multiply_fwd": (_I, [_P, _P, _I, _P, _I, _I, _I, _I, _P, _I]),
     "smg_multiply_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I]),
     "smg_mvn_cholesky_fwd": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),

@@ -60,25 +60,25 @@ inline dev_fvar_matrix add_diag(const dev_fvar_matrix& A, double d) {
 }
 
 namespace internal {
-// C = L Phi for lower-triangular L and Phi: C is lower, so the product fills
-// only the lower tiles (half the GEMM); zero strict upper.  The reverse is the
-// general product's (multiply.hpp).
+// C = L Phi for lower-triangular L and Phi (smg_multiply_lower_fwd: lower
+// tiles, K ranges cut to the triangles, N^3/3 flops); the reverse reads only
+// the lower triangle of C's adjoint and writes only the lower triangles of
+// L's and Phi's (both lower-structured: their upper adjoints are never read).
 class multiply_lower_dev_vari : public vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* B_;
   dev_matrix_vari* C_;
   multiply_lower_dev_vari(dev_matrix_vari* A, dev_matrix_vari* B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, B->cols_)) {
-    smg_ctx* c = amd::ctx();
+      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, B->cols_, dev_structure::lower)) {
     const int n = A->rows_;
-    amd::check(smg_memset(c, C_->val_, 0, size_t(n) * n * sizeof(double)), "multiply");
-    amd::check(smg_gemm(c, 0, 0, 1, n, n, n, 1.0, A_->val_, n, B_->val_, n, 0.0, C_->val_, n), "multiply");
+    amd::check(smg_multiply_lower_fwd(amd::ctx(), A_->val_, n, B_->val_, n, n, C_->val_, n), "multiply");
   }
   void chain() override {
     const int n = A_->rows_;
-    amd::check(smg_multiply_rev(amd::ctx(), A_->val_, n, B_->val_, n, C_->adj_, n, n, n, n, A_->adj_, n,
-                                B_->adj_, n),
+    double* ws = amd::alloc_doubles(size_t(n) * n);
+    amd::check(smg_multiply_lower_rev(amd::ctx(), A_->val_, n, B_->val_, n, C_->adj_, n, n, A_->adj_, n,
+                                      B_->adj_, n, ws),
                "multiply");
   }
 };

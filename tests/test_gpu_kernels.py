@@ -735,3 +735,58 @@ def test_mdivide_left_tri_ill_conditioned(ctx, m, n):
     gref = sl.solve_triangular(L, W, lower=True, trans="T")
     assert np.all(np.isfinite(gB))
     assert berr(L.T, gB, W) <= 20 * berr(L.T, gref, W) + 1e-16, (berr(L.T, gB, W), berr(L.T, gref, W))
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("tri", [1, 2, 4, 8, 5, 6, 9, 10])
+@pytest.mark.parametrize("uplo", [0, 1])
+@pytest.mark.parametrize("m,n,k", [(70, 70, 45), (300, 300, 257), (1100, 1100, 700)])
+def test_gemm_triangular_operands(ctx, ta, tb, tri, uplo, m, n, k):
+    """smg_gemm_tri: K loops cut to the operands' triangles (stored zeros
+    outside) give the dense product, for every operand orientation and output
+    mode; the other output triangle is untouched."""
+    rng = np.random.default_rng(m + 3 * k + 7 * tri + 11 * ta + 13 * tb + uplo)
+    opA = rng.standard_normal((m, k))
+    opB = rng.standard_normal((k, n))
+    if tri & 1: opA = np.tril(opA)
+    if tri & 2: opA = np.triu(opA)
+    if tri & 4: opB = np.tril(opB)
+    if tri & 8: opB = np.triu(opB)
+    C = rng.standard_normal((m, n))
+    ref = 0.75 * opA @ opB + 0.5 * C
+    A = opA.T if ta else opA
+    B = opB.T if tb else opB
+    dA, dB, dC = ctx.put(F(A)), ctx.put(F(B)), ctx.put(F(C))
+    ctx.call("smg_gemm_tri", ta, tb, uplo, tri, m, n, k, 0.75, dA, A.shape[0], dB, B.shape[0], 0.5, dC, m)
+    out = ctx.get(dC, m * n).reshape(n, m).T
+    scale = np.abs(opA).max() * np.abs(opB).max() * k + np.abs(C).max()
+    mask = np.tril(np.ones((m, n), bool)) if uplo == 1 else np.ones((m, n), bool)
+    assert np.abs(out[mask] - ref[mask]).max() <= 1e-13 * scale
+    assert np.array_equal(out[~mask], C[~mask])
+
+
+@pytest.mark.parametrize("n", [130, 1000, 2048])
+def test_multiply_lower(ctx, n):
+    """The tangent's L P product (both lower): C = L P with zero upper; the
+    reverse accumulates tril(tril(Cadj) P^T) into Ladj and tril(L^T tril(Cadj))
+    into Padj (upper triangles untouched)."""
+    rng = np.random.default_rng(n)
+    L = np.tril(rng.standard_normal((n, n)))
+    P = np.tril(rng.standard_normal((n, n)))
+    W = rng.standard_normal((n, n))
+    La0, Pa0 = rng.standard_normal((n, n)), rng.standard_normal((n, n))
+    dL, dP, dC = ctx.put(F(L)), ctx.put(F(P)), ctx.put(F(rng.standard_normal((n, n))))
+    ctx.call("smg_multiply_lower_fwd", dL, n, dP, n, n, dC, n)
+    C = ctx.get(dC, n * n).reshape(n, n).T
+    ref = L @ P
+    sc = np.sqrt(n) * 4
+    assert np.abs(C - ref).max() <= 1e-13 * sc * n and np.all(np.triu(C, 1) == 0.0)
+    dW, dLa, dPa, ws = ctx.put(F(W)), ctx.put(F(La0)), ctx.put(F(Pa0)), ctx.zeros(n * n)
+    ctx.call("smg_multiply_lower_rev", dL, n, dP, n, dW, n, n, dLa, n, dPa, n, ws)
+    La = ctx.get(dLa, n * n).reshape(n, n).T
+    Pa = ctx.get(dPa, n * n).reshape(n, n).T
+    Wl = np.tril(W)
+    lo = np.tril(np.ones((n, n), bool))
+    assert np.abs(La[lo] - (La0 + Wl @ P.T)[lo]).max() <= 1e-13 * sc * n
+    assert np.abs(Pa[lo] - (Pa0 + L.T @ Wl)[lo]).max() <= 1e-13 * sc * n
+    assert np.array_equal(La[~lo], La0[~lo]) and np.array_equal(Pa[~lo], Pa0[~lo])
