@@ -17,11 +17,6 @@
 #include "smg_internal.h"
 #include "tri_small.h"
 
-int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
-                  int ldw, double* B, int ldb, int m, int n);
-int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
-                  double alpha, int accumulate);
-
 namespace {
 
 __global__ void k_residual(const double* __restrict__ y, const double* __restrict__ mu, int n,

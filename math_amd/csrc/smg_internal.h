@@ -60,8 +60,8 @@ struct smg_ctx {
   long long done_seq;
   unsigned int* red_counter_d;  // last-block-done counter of the fused reductions (device, self-resetting)
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[8];  // SMG_WS_COUNT
-  size_t ws_doubles[8];
+  double* ws[9];  // SMG_WS_COUNT
+  size_t ws_doubles[9];
   // profiling
   int prof_on;
   std::vector<smg_prof_slot> prof_pending;
@@ -105,7 +105,7 @@ struct smg_prof_scope {
 // named persistent workspaces (grow on demand; a growth synchronises the
 // stream, so steady-state evaluations never reallocate)
 enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_ALIAS = 4,
-       SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_COUNT = 8 };
+       SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_RHS = 8, SMG_WS_COUNT = 9 };
 static_assert(SMG_WS_COUNT == sizeof(((smg_ctx*)nullptr)->ws) / sizeof(double*), "workspace slots");
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 // spin on the host-coherent completion word until it reaches seq (then the
@@ -128,8 +128,11 @@ struct smg_on_side {
 int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int lower);
 
 // blocked triangular helpers (tri.hip, trsv.hip)
+// B <- op(tri(A))^{-1} B in place; or, with X, X <- op(tri(A))^{-1} B out of
+// place (B is then the right-hand side's workspace, overwritten): each
+// block's X_p = W_p R_p is written straight to X, no in-place copy-back
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
-                  int ldw, double* B, int ldb, int m, int n);
+                  int ldw, double* B, int ldb, int m, int n, double* X = nullptr, int ldx = 0);
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
 int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);

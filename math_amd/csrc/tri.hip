@@ -88,9 +88,19 @@ int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double*
 
 // W: inverse diagonal blocks (m x SMG_NB, ld m) or NULL (computed here)
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
-                  int ldw, double* B, int ldb, int m, int n) {
+                  int ldw, double* B, int ldb, int m, int n, double* X, int ldx) {
   if (m <= 0 || n <= 0) return SMG_OK;
+  if (X == B) X = nullptr;
   int BSZ = SMG_NB;  // diagonal-block size of the solve
+  if (X && !(!W && n == 1 && lower && ldb >= m && m >= 512 && m % 256 == 0 && m / 64 <= 256)) {
+    // out of place below; (the one-right-hand-side path copies into place first)
+  } else if (X) {
+    int rc = smg_copy_impl(ctx, m, n, B, ldb, X, ldx, 1.0, 0);
+    if (rc) return rc;
+    B = X;
+    ldb = ldx;
+    X = nullptr;
+  }
   if (!W && n == 1 && lower && ldb >= m && m >= 512 && m % 256 == 0 && m / 64 <= 256) {
     // one right-hand side: the persistent solve (trsv.hip) on the 256- / 512-
     // row inverses, one launch instead of 2 m / 64 small GEMMs
@@ -133,27 +143,29 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
   for (int q = 0; q < nblk; ++q) {
     const int p = forward ? q : nblk - 1 - q;
     const int j = p * BSZ, b = min(BSZ, m - j), k = j + b;
-    double* Bp = B + j;
-    // X_p = W_p (or W_p^T) B_p, in place (the GEMM's aliasing path); W_p is
-    // lower triangular with stored zeros: each tile's K loop skips them
-    rc = smg_gemm_impl(ctx, wt ? 1 : 0, 0, 0, b, n, b, 1.0, W + j, ldw, Bp, ldb, 0.0, Bp, ldb,
+    // X_p = W_p (or W_p^T) B_p: in place through the GEMM's aliasing path, or
+    // straight into X; W_p is lower triangular with stored zeros: each
+    // tile's K loop skips them.  Bp / ldp: where X_p lives afterwards.
+    double* Bp = X ? X + j : B + j;
+    const int ldp = X ? ldx : ldb;
+    rc = smg_gemm_impl(ctx, wt ? 1 : 0, 0, 0, b, n, b, 1.0, W + j, ldw, B + j, ldb, 0.0, Bp, ldp,
                        wt ? SMG_TRI_A_UPPER : SMG_TRI_A_LOWER);
     if (rc) return rc;
     if (forward && k < m) {
       if (lower)  // B[k:] -= L[k:, j:k] X_p
-        rc = smg_gemm_impl(ctx, 0, 0, 0, m - k, n, b, -1.0, A + k + (size_t)j * lda, lda, Bp, ldb,
+        rc = smg_gemm_impl(ctx, 0, 0, 0, m - k, n, b, -1.0, A + k + (size_t)j * lda, lda, Bp, ldp,
                            1.0, B + k, ldb);
       else  // B[k:] -= (U[j:k, k:])^T X_p
-        rc = smg_gemm_impl(ctx, 1, 0, 0, m - k, n, b, -1.0, A + j + (size_t)k * lda, lda, Bp, ldb,
+        rc = smg_gemm_impl(ctx, 1, 0, 0, m - k, n, b, -1.0, A + j + (size_t)k * lda, lda, Bp, ldp,
                            1.0, B + k, ldb);
       if (rc) return rc;
     }
     if (!forward && j > 0) {
       if (!lower)  // B[0:j] -= U[0:j, j:k] X_p
-        rc = smg_gemm_impl(ctx, 0, 0, 0, j, n, b, -1.0, A + (size_t)j * lda, lda, Bp, ldb, 1.0, B,
+        rc = smg_gemm_impl(ctx, 0, 0, 0, j, n, b, -1.0, A + (size_t)j * lda, lda, Bp, ldp, 1.0, B,
                            ldb);
       else  // B[0:j] -= (L[j:k, 0:j])^T X_p
-        rc = smg_gemm_impl(ctx, 1, 0, 0, j, n, b, -1.0, A + j, lda, Bp, ldb, 1.0, B, ldb);
+        rc = smg_gemm_impl(ctx, 1, 0, 0, j, n, b, -1.0, A + j, lda, Bp, ldp, 1.0, B, ldb);
       if (rc) return rc;
     }
   }
@@ -176,6 +188,13 @@ int smg_mdivide_left_tri_fwd(smg_ctx* ctx, int lower, const double* A, int lda, 
   if (m == 0 || n == 0) return SMG_OK;
   if (!A || !B || !C || lda < m || ldb < m || ldc < m) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_TRSV);
+  if (m >= 512 && n >= 64) {  // the right-hand side in a workspace, blocks written straight to C
+    double* R = smg_ws(ctx, SMG_WS_RHS, (size_t)m * n);
+    if (!R) return SMG_ERR_OOM;
+    int rc = smg_copy_impl(ctx, m, n, B, ldb, R, m, 1.0, 0);
+    if (rc) return rc;
+    return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, R, m, m, n, C, ldc);
+  }
   int rc = smg_copy_impl(ctx, m, n, B, ldb, C, ldc, 1.0, 0);
   if (rc) return rc;
   return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, C, ldc, m, n);
@@ -189,9 +208,18 @@ int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda, 
   if (!A || !C || !Cadj || !ws) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_TRSV);
   // adjB = tri(A)^{-T} Cadj   (mdivide_left_tri.hpp:104-107)
-  int rc = smg_copy_impl(ctx, m, n, Cadj, ldca, ws, m, 1.0, 0);
-  if (rc) return rc;
-  rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, ws, m, m, n);
+  int rc;
+  if (m >= 512 && n >= 64) {  // out of place: Cadj's copy in a workspace, the solve into ws
+    double* R = smg_ws(ctx, SMG_WS_RHS, (size_t)m * n);
+    if (!R) return SMG_ERR_OOM;
+    rc = smg_copy_impl(ctx, m, n, Cadj, ldca, R, m, 1.0, 0);
+    if (rc) return rc;
+    rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, R, m, m, n, ws, m);
+  } else {
+    rc = smg_copy_impl(ctx, m, n, Cadj, ldca, ws, m, 1.0, 0);
+    if (rc) return rc;
+    rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, ws, m, m, n);
+  }
   if (rc) return rc;
   if (Aadj) {  // adjA = -adjB C^T on the triangle only (:108, :111-123)
     rc = smg_gemm_impl(ctx, 0, 1, lower ? 1 : 2, m, m, n, -1.0, ws, m, C, ldc, 1.0, Aadj, ldaa);

@@ -676,7 +676,7 @@ def test_cholesky_fwd_checked(ctx, N):
     assert np.all(np.triu(L, 1) == 0.0)
 
 
-@pytest.mark.parametrize("m,n", [(2048, 512), (2048, 700), (1024, 1), (1536, 1), (4096, 1)])
+@pytest.mark.parametrize("m,n", [(2048, 512), (2048, 700), (1024, 1), (1536, 1), (4096, 1), (1024, 96), (600, 64)])
 def test_mdivide_left_tri_512_blocks(ctx, m, n):
     """The large lower solve on 512-row blocks (inverses doubled up from the
     64-row level, tri.hip smg_trsm_impl) -- or, with one right-hand side, the
