@@ -21,7 +21,9 @@ generated in HBM before the timed region, ONE RCCL all-reduce of the M+2
 multiply(A, A^T), N))) wrt all N^2 entries of A, N=2048, A resident in HBM.
 
 --workload normal (config 1): gradient of normal_lpdf(theta | 0, 1), N=1024,
-theta a host std::vector<var> (latency-bound: one host round trip per eval).
+theta a host std::vector<var>: below the size gate (16384 elements) evaluated
+on the host, as the reference keeps small calls off its device; the forced
+device path (one fused launch + completion wait) is reported beside it.
 
 --gpus N without an external launcher spawns N child processes (one per GPU,
 torchrun's environment) before any GPU call; under torchrun WORLD_SIZE must
@@ -70,7 +72,7 @@ def pmc_traffic(workload):
     summary (tools/pmc_traffic.sh + tools/pmc_traffic.py: separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes, calibrated on a known 8 B/lane
     stream), or None when absent."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -361,6 +363,8 @@ class Normal(Workload):
         bl = self.bl
         bl.smg_bench_device_init.argtypes = [ctypes.c_int]
         bl.smg_bench_normal_step.argtypes = [ctypes.c_int, D, D, D]
+        bl.smg_bench_normal_gate.argtypes = [ctypes.c_longlong]
+        bl.smg_bench_normal_run.argtypes = [ctypes.c_int, ctypes.c_int, D, D, D]
         with open(os.path.join(ROOT, "tests", "golden", f"normal_N{self.N}.json")) as f:
             self.gold = json.load(f)
         self.theta = np.array(self.gold["theta"], dtype=np.float64)
@@ -374,6 +378,10 @@ class Normal(Workload):
     def step(self):
         return self._call(*self._args)
 
+    def run(self, k):
+        """k evals in one native loop (no ctypes call per eval)"""
+        return self.bl.smg_bench_normal_run(k, *self._args)
+
     def guard(self):
         want = np.array(self.gold["grad"])
         ok = (np.all(np.abs(self.g - want) <= 1e-10 * np.maximum(np.abs(want), 1e-10))
@@ -385,14 +393,30 @@ class Normal(Workload):
 
     def config(self):
         return {"workload": "normal_lpdf_gradient", "N": self.N, "parallelism": f"replicas{self.world}",
-                "path": "stan::math::gradient over std::vector<var> via header-only layer"}
+                "path": "stan::math::gradient over std::vector<var> via header-only layer; N <= 16384 host "
+                        "operands are evaluated on the host (size gate, as the reference gates its offload: "
+                        "opencl/opencl_context.hpp:164-182)"}
+
+    def extra(self, timed, steps):
+        """the same eval forced through the fused device launch (gate 0)"""
+        self.bl.smg_bench_normal_gate(0)
+        for _ in range(3):
+            self.step()
+        ok, msg = self.guard()
+        t = timed(steps)
+        self.bl.smg_bench_normal_gate(16384)
+        if not ok:
+            raise SystemExit(f"parity failure (device path): {msg}")
+        return {"device_path": {"value": steps * self.units_per_step() / t, "ms_per_step": 1e3 * t / steps,
+                                "note": "one fused k_normal_fused launch + completion wait per eval "
+                                        "(SMG_NORMAL_HOST_MAX=0)"}}
 
     data = "synthetic (reference harness config-1 input: theta ~ N(0,1), tests/golden/normal_N1024.json)"
 
     def roofline(self, fams, steps, t_prof, ms_per_step):
         byts = self.N * 8 * 2  # theta up, partials down (SURVEY.md §8(d): 16 B per element)
         ach = byts / (ms_per_step * 1e-3) / 1e9
-        return {"bound": "hbm", "kernel": "whole gradient eval (latency-bound: one host round trip)",
+        return {"bound": "hbm", "kernel": "whole gradient eval (host-evaluated below the size gate: latency-bound, not HBM)",
                 "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
                 "traffic": None, "bytes_per_eval": byts}
 
@@ -483,8 +507,12 @@ def main():
         barrier()
         lib.smg_sync(ctx)
         t0 = time.perf_counter()
-        for _ in range(k):
-            step()
+        if hasattr(wl, "run"):
+            if wl.run(k) != 0:
+                raise SystemExit(f"step failed: {bl.smg_bench_error().decode()}")
+        else:
+            for _ in range(k):
+                step()
         lib.smg_sync(ctx)
         t = time.perf_counter() - t0
         barrier()
@@ -527,6 +555,8 @@ def main():
         "config": wl.config(),
         "roofline": wl.roofline(fams, args.steps, tp, ms_per_step),
     }
+    if hasattr(wl, "extra"):
+        line.update(wl.extra(timed, args.steps))
     if getattr(wl, "parity", None):
         line["parity"] = wl.parity
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -168,6 +168,17 @@ int smg_bench_normal_step(int n, const double* theta, double* fx, double* grad) 
   }
 }
 
+/* k config-1 evaluations back to back (the timed loop without a host-language
+ * call per evaluation, as the reference harness times its own loop) */
+int smg_bench_normal_run(int k, int n, const double* theta, double* fx, double* grad) {
+  for (int r = 0; r < k; ++r)
+    if (int rc = smg_bench_normal_step(n, theta, fx, grad)) return rc;
+  return 0;
+}
+
+/* the normal_lpdf host gate (elements; 0: every call on the device) */
+void smg_bench_normal_gate(long long n) { stan::math::amd::set_normal_host_max(size_t(n)); }
+
 int smg_bench_device_init(int device) {
   try {
     stan::math::amd::set_device(device);

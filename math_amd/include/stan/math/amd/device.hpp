@@ -18,6 +18,8 @@
 #include <smg_hip.h>
 
 #include <cstdlib>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <new>
 #include <sstream>
 #include <stdexcept>
@@ -30,8 +32,12 @@ namespace amd {
 struct device_state {
   smg_ctx* ctx = nullptr;
   int device = -1;
+  // a worker thread's context is released when the thread ends; the main
+  // thread's is left to process teardown: its thread_local destructor runs
+  // inside exit(), after the HIP runtime (or a profiler's tool library) may
+  // already have torn down the streams it would release
   ~device_state() {
-    if (ctx) smg_ctx_destroy(ctx);
+    if (ctx && ::syscall(SYS_gettid) != ::getpid()) smg_ctx_destroy(ctx);
   }
 };
 

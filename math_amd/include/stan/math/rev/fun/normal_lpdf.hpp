@@ -26,6 +26,7 @@
 #include <stan/math/rev/meta/operands_and_partials.hpp>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
@@ -115,6 +116,105 @@ struct is_device_operand
     : std::integral_constant<bool, std::is_same<T, dev_var_matrix>::value ||
                                        std::is_same<T, dev_data<double>>::value> {};
 
+/** Element i of a host operand (scalars broadcast). */
+inline double host_val(double x, size_t) { return x; }
+inline double host_val(const var& x, size_t) { return x.vi_->val_; }
+inline double host_val(const std::vector<double>& x, size_t i) { return x[i]; }
+inline double host_val(const std::vector<var>& x, size_t i) { return x[i].vi_->val_; }
+#ifdef STAN_MATH_AMD_HAS_EIGEN
+template <int R, int C>
+inline double host_val(const Eigen::Matrix<double, R, C>& x, size_t i) { return x(Eigen::Index(i)); }
+template <int R, int C>
+inline double host_val(const Eigen::Matrix<var, R, C>& x, size_t i) { return x(Eigen::Index(i)).vi_->val_; }
+#endif
+
+/**
+ * Largest element count evaluated on the host (the size gate the reference
+ * applies before offloading, opencl/opencl_context.hpp:164-182): below it a
+ * call over host operands is cheaper than one device round trip (~20 us on
+ * MI355X against ~1 ns per element on a host core).  SMG_NORMAL_HOST_MAX
+ * overrides it; 0 sends every call to the device.
+ */
+inline size_t& normal_host_max_ref() {
+  static size_t v = [] {
+    const char* e = std::getenv("SMG_NORMAL_HOST_MAX");
+    return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(16384);
+  }();
+  return v;
+}
+inline size_t normal_host_max() { return normal_host_max_ref(); }
+
+inline void normal_check_sizes(const char* fn, const fused_operand* ops);
+
+}  // namespace internal
+
+namespace amd {
+/** Set the normal_lpdf host gate (elements); 0 sends every call to the device. */
+inline void set_normal_host_max(size_t n) { internal::normal_host_max_ref() = n; }
+}  // namespace amd
+
+namespace internal {
+
+/**
+ * Host evaluation of normal_lpdf over host operands (small calls), the
+ * reference's own loop (prim/scal/prob/normal_lpdf.hpp:51-117): checks in the
+ * same order, value accumulated in element order, partials into the edges.
+ */
+template <bool propto, typename T_y, typename T_loc, typename T_scale>
+inline typename ops_return<T_y, T_loc, T_scale>::type normal_lpdf_host(const T_y& y, const T_loc& mu,
+                                                                       const T_scale& sigma,
+                                                                       const fused_operand* ops, size_t N,
+                                                                       int include) {
+  static const char* fn = "normal_lpdf";
+  constexpr bool vy = op_is_var<T_y>::value, vmu = op_is_var<T_loc>::value, vs = op_is_var<T_scale>::value;
+  for (size_t i = 0; i < ops[0].n; ++i)
+    if (std::isnan(host_val(y, i)))
+      throw std::domain_error(std::string(fn) + ": Random variable is nan, but must not be nan!");
+  for (size_t i = 0; i < ops[1].n; ++i)
+    if (!(std::fabs(host_val(mu, i)) <= 1.7976931348623157e308))
+      throw std::domain_error(std::string(fn) + ": Location parameter is not finite, but must be finite!");
+  for (size_t i = 0; i < ops[2].n; ++i)
+    if (!(host_val(sigma, i) > 0.0))
+      throw std::domain_error(std::string(fn) + ": Scale parameter is not positive, but must be > 0!");
+  normal_check_sizes(fn, ops);
+  using ret_t = typename ops_return<T_y, T_loc, T_scale>::type;
+  if constexpr (!(vy || vmu || vs)) {
+    if (propto) return ret_t(0.0);
+  }
+  operands_and_partials<T_y, T_loc, T_scale> ops_partials(y, mu, sigma);
+  const double neg_log_sqrt_two_pi = -0.91893853320467274178;
+  // 1 / sigma and log sigma once per element of sigma (:71-77): once for a scalar
+  const bool svec = ops[2].vec;
+  const double inv_s0 = 1.0 / host_val(sigma, 0);
+  const double log_s0 = (include & 2) ? std::log(host_val(sigma, 0)) : 0.0;
+  // the three summands accumulated separately, the quadratic one in four
+  // interleaved partial sums (no loop-carried add chain through one logp);
+  // same terms as the reference's per-element logp updates (:87-97), summed
+  // in a different order (round-off only)
+  double q[4] = {0.0, 0.0, 0.0, 0.0};
+  double sum_log_s = 0.0;
+  for (size_t n = 0; n < N; ++n) {
+    const double inv_s = svec ? 1.0 / host_val(sigma, n) : inv_s0;
+    const double z = (host_val(y, n) - host_val(mu, n)) * inv_s;
+    const double z2 = z * z;
+    q[n & 3] += z2;
+    if (svec && (include & 2)) sum_log_s += std::log(host_val(sigma, n));
+    const double sc = inv_s * z;
+    if constexpr (vy) ops_partials.edge1_.partials_[int(n)] -= sc;
+    if constexpr (vmu) ops_partials.edge2_.partials_[int(n)] += sc;
+    if constexpr (vs) ops_partials.edge3_.partials_[int(n)] += -inv_s + inv_s * z2;
+  }
+  double logp = 0.0;
+  if (include & 1) logp += neg_log_sqrt_two_pi * double(N);
+  if (include & 2) logp -= svec ? sum_log_s : log_s0 * double(N);
+  if (include & 4) logp += -0.5 * ((q[0] + q[1]) + (q[2] + q[3]));
+  if constexpr (vy || vmu || vs) {
+    return ops_partials.build(logp);
+  } else {
+    return logp;
+  }
+}
+
 inline void normal_check_sizes(const char* fn, const fused_operand* ops) {
   static const char* const names[3] = {"Random variable", "Location parameter", "Scale parameter"};
   size_t expect = 0;
@@ -158,6 +258,13 @@ inline typename internal::ops_return<T_y, T_loc, T_scale>::type normal_lpdf(cons
     if (o.vec) N = o.n > N ? o.n : N;
   for (auto& o : ops)
     if (o.vec && o.n != N) sizes_ok = false;
+
+  const int include = (inc_const ? 1 : 0) | (inc_logsig ? 2 : 0) | (inc_quad ? 4 : 0);
+  if constexpr (!internal::is_device_operand<T_y>::value && !internal::is_device_operand<T_loc>::value
+                && !internal::is_device_operand<T_scale>::value) {
+    if (N <= internal::normal_host_max())
+      return internal::normal_lpdf_host<propto>(y, mu, sigma, ops, N, include);
+  }
 
   smg_ctx* c = amd::ctx();
   // pinned staging: [res(8) | host values of y, mu, sigma | host partials of y, mu, sigma]
@@ -207,7 +314,6 @@ inline typename internal::ops_return<T_y, T_loc, T_scale>::type normal_lpdf(cons
       g[2] = st + 6;
     }
   }
-  const int include = (inc_const ? 1 : 0) | (inc_logsig ? 2 : 0) | (inc_quad ? 4 : 0);
   if (sizes_ok) {
     amd::check(smg_normal_lpdf_fused(c, vals[0], vals[1], vals[2], ops[0].scalar, ops[1].scalar, ops[2].scalar,
                                      (long long)N, include, st, g[0], g[1], g[2]),

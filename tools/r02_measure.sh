@@ -1,0 +1,24 @@
+#!/bin/bash
+# one GPU call: GPU test suite, every bench workload (with CPU baselines), the
+# rocprofv3 kernel-trace summary of the GP bench, an MFMA-busy PMC pass on the
+# GP bench and the HBM traffic passes.  Each step time-limited; first failure ends it.
+set -o pipefail
+TAG=${1:-r02a}
+SKIP_TESTS=${SKIP_TESTS:-0}
+O=$GRAFT_REPO_ROOT/gpurun_out
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+if [ "$SKIP_TESTS" != 1 ]; then
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 200 --timeout-method thread > $O/${TAG}_pytest.log 2>&1 || { tail -40 $O/${TAG}_pytest.log; exit 1; }
+  tail -3 $O/${TAG}_pytest.log
+fi
+for w in ${WLS:-gp glm mulchol hvp normal}; do
+  timeout -k 10 400 python bench.py --workload $w > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err || { tail $O/${TAG}_bench_$w.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/${TAG}_bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+done
+[ "${PROF:-1}" = 1 ] || exit 0
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/${TAG}_prof.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_${TAG}_gp_mfma -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_${TAG}_gp_mfma.log 2>&1 || exit 1
+bash $GRAFT_REPO_ROOT/tools/pmc_traffic.sh $TAG || exit 1
+echo done
