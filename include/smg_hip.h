@@ -226,6 +226,19 @@ int smg_log_determinant_spd_rev(smg_ctx* ctx, const double* L,
                                 const double* aux, int n, double adj,
                                 double* Aadj, int ldaa, double* ws);
 
+/* log_determinant(A) of a general square A (rev/mat/fun/log_determinant.hpp:14-37;
+ * the reference factors with a full-pivoting Householder QR, this with a
+ * blocked LU with partial pivoting: the same |det| and A^{-T})
+ *   fwd: LU (n x n, ld n) = P A's unit-lower L and U, piv (n ints) = the row
+ *        swaps (LAPACK ipiv, 0-based), out[0] = sum_i log|u_ii| (-inf for a
+ *        singular A).  ws: >= 64*64 doubles.
+ *   rev: Aadj += adj * A^{-T}.  ws: >= 3*n*n doubles, iws: >= n ints. */
+int smg_log_determinant_fwd(smg_ctx* ctx, const double* A, int lda, int n,
+                            double* LU, int* piv, double* ws, double* out);
+int smg_log_determinant_rev(smg_ctx* ctx, const double* LU, const int* piv,
+                            int n, double adj, double* Aadj, int ldaa,
+                            double* ws, int* iws);
+
 /* multiply_lower_tri_self_transpose(L), L: K x J
  * (rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44)
  *   fwd: C (K x K) = T T^T, T = lower trapezoid of L.  ws: >= K*J.

@@ -25,6 +25,7 @@
 #include <stan/math/rev/fun/poisson_log_glm_lpmf.hpp>
 #include <stan/math/rev/fun/categorical_logit_glm_lpmf.hpp>
 #include <stan/math/rev/fun/spd_functors.hpp>
+#include <stan/math/rev/fun/log_determinant.hpp>
 #include <stan/math/rev/functor/gradient.hpp>
 #include <stan/math/eigen/interop.hpp>
 #include <stan/math/mix/fvar_functors.hpp>

@@ -228,6 +228,21 @@ inline var log_determinant_spd(const Eigen::Matrix<var, R, C>& m) {
   internal::check_square("log_determinant_spd", "m", int(m.rows()), int(m.cols()));
   return log_determinant_spd(to_dev(m));
 }
+/** rev/mat/fun/log_determinant.hpp:14 signature. */
+template <int R, int C>
+inline var log_determinant(const Eigen::Matrix<var, R, C>& m) {
+  internal::check_square("log_determinant", "m", int(m.rows()), int(m.cols()));
+  if (m.size() == 0) return var(0.0);
+  return log_determinant(to_dev(m));
+}
+/** prim/mat/fun/log_determinant.hpp:20 signature (double matrix -> double). */
+template <int R, int C>
+inline double log_determinant(const Eigen::Matrix<double, R, C>& m) {
+  internal::check_square("log_determinant", "m", int(m.rows()), int(m.cols()));
+  if (m.size() == 0) return 0.0;
+  const Eigen::Matrix<double, -1, -1> md = m;
+  return log_determinant(to_dev_data(md.data(), size_t(md.size()), int(md.rows()), int(md.cols())));
+}
 /** rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14 signature. */
 inline matrix_v multiply_lower_tri_self_transpose(const matrix_v& L) {
   if (L.rows() == 0) return matrix_v(0, 0);

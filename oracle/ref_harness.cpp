@@ -34,6 +34,7 @@
  *   categorical_logit_glm_lpmf stan/math/prim/mat/prob/categorical_logit_glm_lpmf.hpp:38-183
  *   mdivide_left_spd         stan/math/rev/mat/fun/mdivide_left_spd.hpp:232-260
  *   log_determinant_spd      stan/math/rev/mat/fun/log_determinant_spd.hpp:16-57
+ *   log_determinant          stan/math/rev/mat/fun/log_determinant.hpp:14-37
  *   multiply_lower_tri_self_transpose  stan/math/rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44
  *   quad_form_sym            stan/math/rev/mat/fun/quad_form_sym.hpp:15-27
  *   map_rect                 stan/math/prim/mat/functor/map_rect.hpp:120-177
@@ -1118,6 +1119,44 @@ static void fix_spd() {
   }
 }
 
+// ---- log_determinant (rev/mat/fun/log_determinant.hpp:14-37)
+// of general square matrices: A = U[-1, 1) (n x n, col-major, tests/gen.py
+// logdet_input) + shift sqrt(n) I, row 0 negated when flip (det < 0);
+// gradient wrt every entry.  Plus the prim value of a singular matrix.
+struct logdet_functor {
+  int n;
+  var operator()(const Matrix<var, Dynamic, 1>& th) const { return stan::math::log_determinant(take(th, 0, n, n)); }
+};
+static void fix_logdet() {
+  struct Case {
+    int n, shift, flip;
+  };
+  for (Case c : {Case{1, 1, 1}, Case{5, 1, 1}, Case{40, 0, 0}, Case{40, 1, 1}, Case{130, 1, 0}}) {
+    MatrixXd A = unif_mat(c.n, c.n, SEED + 130 + c.n);
+    for (int i = 0; i < c.n; ++i) A(i, i) += c.shift * std::sqrt((double)c.n);
+    if (c.flip) A.row(0) *= -1.0;
+    VectorXd th = Eigen::Map<VectorXd>(A.data(), A.size()), g;
+    double fx;
+    stan::math::gradient(logdet_functor{c.n}, th, fx, g);
+    Json j;
+    j.put_str("what", "gradient of log_determinant(A) (log|det A|) wrt every entry of A; input: tests/gen.py "
+                      "logdet_input");
+    j.put_int("n", c.n);
+    j.put_int("shift", c.shift);
+    j.put_int("flip", c.flip);
+    j.put("fx", fx);
+    j.put("fx_prim", stan::math::log_determinant(A));
+    j.put_vec("grad", g);
+    write_fixture("log_determinant_n" + std::to_string(c.n) + "_s" + std::to_string(c.shift), j);
+  }
+  MatrixXd S(3, 3);
+  S << 1, 2, 3, 2, 4, 6, 1, 0, 1;  // rank 2
+  Json j;
+  j.put_str("what", "prim log_determinant of the rank-2 matrix [[1,2,3],[2,4,6],[1,0,1]] (row-major)");
+  j.put("fx", stan::math::log_determinant(S));
+  write_fixture("log_determinant_singular3", j);
+}
+
 static void fix_hessian() {  // mix/mat/functor/hessian.hpp on the GP marginal
   for (int N : {8, 32, 100}) {
     std::vector<double> x;
@@ -1244,6 +1283,7 @@ int main(int argc, char** argv) {
       fix_glm_cat_errors();
     }
     if (want("spd")) fix_spd();
+    if (want("logdet")) fix_logdet();
     if (want("maprect")) fix_maprect();
     if (want("hessian")) fix_hessian();
     if (want("hvp")) fix_hvp();

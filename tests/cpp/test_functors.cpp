@@ -487,6 +487,52 @@ static void cmd_spd() {
   print("grad", g);
 }
 
+// log_determinant (rev/mat/fun/log_determinant.hpp:14-37): gradient through
+// the Eigen signature (host vars bridged to one device node), the device
+// signature (dev_var_matrix leaf), the prim double value, and check_square
+static void cmd_logdet() {
+  int n;
+  std::cin >> n;
+  auto a = read_vec(size_t(n) * n);
+  double fx;
+  std::vector<double> g;
+  gradient(
+      [&](const std::vector<var>& t) -> var {
+        matrix_v m(n, n);
+        for (int i = 0; i < n * n; ++i) m(i) = t[size_t(i)];
+        return log_determinant(m);
+      },
+      a, fx, g);
+  print1("fx", fx);
+  print("grad", g);
+  smg_ctx* c = amd::ctx();
+  double* ad = amd::alloc_doubles(size_t(n) * n);
+  amd::to_device(ad, a.data(), size_t(n) * n);
+  double* gd = amd::alloc_doubles(size_t(n) * n);
+  double fxd;
+  gradient([&](const dev_var_matrix& m) { return log_determinant(m); }, dev_data<double>(ad, size_t(n) * n, n, n),
+           fxd, gd);
+  std::vector<double> gh(size_t(n) * n);
+  amd::to_host(gh.data(), gd, gh.size());
+  print1("fx_dev", fxd);
+  print("grad_dev", gh);
+  const Eigen::MatrixXd md = Eigen::Map<const Eigen::MatrixXd>(a.data(), n, n);
+  print1("fx_prim", log_determinant(md));
+  try {
+    matrix_v r(2, 3);
+    for (int i = 0; i < 6; ++i) r(i) = var(double(i + 1));
+    log_determinant(r);
+    std::printf("square none\n");
+  } catch (const std::invalid_argument& e) {
+    std::printf("square %s\n", e.what());
+  }
+  matrix_v e0(0, 0);
+  print1("empty", log_determinant(e0).val());
+  recover_memory();  // the check_square / empty-input vars above live on the outer tape
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->nested_var_stack_sizes_.size());
+}
+
 static void cmd_glm2() {
   int kind, M;
   long long R;
@@ -1034,6 +1080,7 @@ int main() {
     else if (cmd == "glm_cat") cmd_glm_cat();
     else if (cmd == "glm_cat_errors") cmd_glm_cat_errors();
     else if (cmd == "spd") cmd_spd();
+    else if (cmd == "logdet") cmd_logdet();
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
     else if (cmd == "hvp") cmd_hvp();

@@ -106,3 +106,13 @@ def spd_inputs(kind: int, n: int, k: int):
         return (spd_exact(n, s0),)
     L = unif_mat(n, k, s0 + 1)
     return L, unif_mat(n, n, s0 + 2)
+
+
+def logdet_input(n: int, shift: int, flip: int) -> np.ndarray:
+    """ref_harness.cpp fix_logdet input: U[-1, 1) (n x n) + shift sqrt(n) I,
+    row 0 negated when flip."""
+    A = unif_mat(n, n, SEED + 130 + n)
+    A[np.diag_indices(n)] += shift * np.sqrt(float(n))
+    if flip:
+        A[0, :] *= -1.0
+    return A
