@@ -88,6 +88,8 @@ _SIGS = {
     "smg_mdivide_left_spd_rev": (_I, [_P, _P, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P]),
     "smg_log_determinant_spd_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P]),
     "smg_log_determinant_spd_rev": (_I, [_P, _P, _P, _I, _D, _P, _I, _P]),
+    "smg_log_determinant_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "smg_log_determinant_rev": (_I, [_P, _P, _P, _I, _D, _P, _I, _P, _P]),
     "smg_multiply_lower_tri_self_transpose_fwd": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "smg_multiply_lower_tri_self_transpose_rev": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
     "smg_quad_form_sym_fwd": (_I, [_P, _P, _I, _P, _I, _I, _I, _P, _I, _P]),
