@@ -239,6 +239,32 @@ int smg_log_determinant_rev(smg_ctx* ctx, const double* LU, const int* piv,
                             int n, double adj, double* Aadj, int ldaa,
                             double* ws, int* iws);
 
+/* Tangent pieces of the fvar<var> (fwd-over-rev) functors (SURVEY.md 8(f)
+ * row 4; mix/fvar_functors.hpp):
+ *   smg_add_tril: Y(i >= j) += alpha X(i >= j) (m x n).
+ *   smg_lse_tangent_fwd: out[0] = log_sum_exp(x), out[1] = sum_i
+ *     exp(x_i - out[0]) xd_i (fwd/mat/fun/log_sum_exp.hpp).  rev: xadj +=
+ *     adj p (xd - t), xdadj += adj p, p = exp(x - lse) (either may be NULL).
+ *   smg_glm_tangent_fwd: out[0] = sum_i d_i (etad_i + alphad), d_i = the
+ *     reference's theta_derivative of bernoulli_logit_glm_lpmf at theta_i =
+ *     eta_i + alpha (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:117-123).
+ *     rev: eta_adj += adj d'(theta) (etad + alphad), etad_adj += adj d;
+ *     out[0], out[1] = their sums (alpha's and alphad's adjoints). */
+int smg_add_tril(smg_ctx* ctx, int m, int n, double alpha, const double* X,
+                 int ldx, double* Y, int ldy);
+int smg_lse_tangent_fwd(smg_ctx* ctx, const double* x, const double* xd,
+                        long long n, double* out);
+int smg_lse_tangent_rev(smg_ctx* ctx, const double* x, const double* xd,
+                        long long n, double lse, double t, double adj,
+                        double* xadj, double* xdadj);
+int smg_glm_tangent_fwd(smg_ctx* ctx, const double* eta, double alpha,
+                        const double* etad, double alphad, const int* y,
+                        long long n, double* out);
+int smg_glm_tangent_rev(smg_ctx* ctx, const double* eta, double alpha,
+                        const double* etad, double alphad, const int* y,
+                        long long n, double adj, double* eta_adj,
+                        double* etad_adj, double* out);
+
 /* multiply_lower_tri_self_transpose(L), L: K x J
  * (rev/mat/fun/multiply_lower_tri_self_transpose.hpp:14-44)
  *   fwd: C (K x K) = T T^T, T = lower trapezoid of L.  ws: >= K*J.

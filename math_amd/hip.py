@@ -89,6 +89,11 @@ _SIGS = {
     "smg_log_determinant_spd_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P]),
     "smg_log_determinant_spd_rev": (_I, [_P, _P, _P, _I, _D, _P, _I, _P]),
     "smg_log_determinant_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "smg_add_tril": (_I, [_P, _I, _I, _D, _P, _I, _P, _I]),
+    "smg_lse_tangent_fwd": (_I, [_P, _P, _P, _L, _P]),
+    "smg_lse_tangent_rev": (_I, [_P, _P, _P, _L, _D, _D, _D, _P, _P]),
+    "smg_glm_tangent_fwd": (_I, [_P, _P, _D, _P, _D, _P, _L, _P]),
+    "smg_glm_tangent_rev": (_I, [_P, _P, _D, _P, _D, _P, _L, _D, _P, _P, _P]),
     "smg_log_determinant_rev": (_I, [_P, _P, _P, _I, _D, _P, _I, _P, _P]),
     "smg_multiply_lower_tri_self_transpose_fwd": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "smg_multiply_lower_tri_self_transpose_rev": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _I, _P]),

@@ -16,6 +16,17 @@
 //   lp' = w^T L^{-1} L' w - sum_i L'_ii / L_ii,  w = L^{-1}(y - mu)
 // (the derivative of -|w|^2/2 - sum log L_ii, prim/mat/prob/
 // multi_normal_cholesky_lpdf.hpp:117-131).
+// Beyond the GP set, with the reference's tangent
+// rules:
+//   (A B)'            = A' B + A B'                (fwd/mat/fun/multiply.hpp)
+//   (A^{-1} B)'       = A^{-1} (B' - tril(A') C)   (fwd/mat/fun/mdivide_left_tri_low.hpp:40-44)
+//   log_sum_exp(x)'   = softmax(x) . x'            (fwd/mat/fun/log_sum_exp.hpp)
+//   bernoulli_logit_glm_lpmf' = sum_i d_i (x_i beta' + alpha')
+//                     (fwd operands_and_partials over the prim GLM's
+//                      theta_derivative d, prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:117-141)
+// plus transpose, sum, add_diag and the Eigen Matrix<fvar<var>> bridge, so
+// hessian() (mix/mat/functor/hessian.hpp:39-72) runs on models built from
+// multiply / cholesky_decompose / mdivide_left_tri / log_sum_exp / the GLM.
 
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/fwd/core/fvar.hpp>
@@ -26,6 +37,8 @@
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
 #include <stan/math/rev/fun/multiply.hpp>
 #include <stan/math/rev/fun/tangent_ops.hpp>
+#include <stan/math/rev/fun/log_sum_exp.hpp>
+#include <stan/math/rev/fun/bernoulli_logit_glm_lpmf.hpp>
 
 #include <vector>
 
@@ -83,6 +96,216 @@ class multiply_lower_dev_vari : public vari {
   }
 };
 }  // namespace internal
+
+namespace internal {
+// C = A + B (same shape)
+class add_dev_vari : public vari {
+ public:
+  dev_matrix_vari* A_;
+  dev_matrix_vari* B_;
+  dev_matrix_vari* C_;
+  add_dev_vari(dev_matrix_vari* A, dev_matrix_vari* B)
+      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, A->cols_)) {
+    smg_ctx* c = amd::ctx();
+    amd::check(smg_copy_matrix(c, A->rows_, A->cols_, A->val_, A->rows_, C_->val_, C_->rows_, 0, 0), "add");
+    amd::check(smg_axpy(c, (long long)C_->size(), 1.0, B->val_, 1, C_->val_, 1), "add");
+  }
+  void chain() override {
+    smg_ctx* c = amd::ctx();
+    amd::check(smg_axpy(c, (long long)C_->size(), 1.0, C_->adj_, 1, A_->adj_, 1), "add");
+    amd::check(smg_axpy(c, (long long)C_->size(), 1.0, C_->adj_, 1, B_->adj_, 1), "add");
+  }
+};
+
+// C = tril(A): the lower triangle (diagonal included), zeros above
+class tril_dev_vari : public vari {
+ public:
+  dev_matrix_vari* A_;
+  dev_matrix_vari* C_;
+  explicit tril_dev_vari(dev_matrix_vari* A)
+      : vari(0.0), A_(A), C_(new dev_matrix_vari(A->rows_, A->cols_, dev_structure::lower)) {
+    smg_ctx* c = amd::ctx();
+    amd::zero(C_->val_, C_->size());
+    amd::check(smg_add_tril(c, A->rows_, A->cols_, 1.0, A->val_, A->rows_, C_->val_, C_->rows_), "tril");
+  }
+  void chain() override {
+    amd::check(smg_add_tril(amd::ctx(), A_->rows_, A_->cols_, 1.0, C_->adj_, C_->rows_, A_->adj_, A_->rows_),
+               "tril");
+  }
+};
+
+// t = softmax(x) . x' (a var of x and x')
+class lse_tangent_dev_vari : public vari {
+ public:
+  dev_matrix_vari* x_;
+  dev_matrix_vari* xd_;
+  double lse_;
+  lse_tangent_dev_vari(double t, double lse, dev_matrix_vari* x, dev_matrix_vari* xd)
+      : vari(t), x_(x), xd_(xd), lse_(lse) {}
+  void chain() override {
+    amd::check(smg_lse_tangent_rev(amd::ctx(), x_->val_, xd_->val_, (long long)x_->size(), lse_, val_, adj_,
+                                   x_->adj_, xd_->adj_),
+               "log_sum_exp");
+  }
+};
+
+// t = sum_i d(eta_i + alpha) (eta'_i + alpha') of the bernoulli logit GLM
+class glm_tangent_dev_vari : public vari {
+ public:
+  dev_matrix_vari* eta_;
+  dev_matrix_vari* etad_;
+  vari* alpha_;   // null: data
+  vari* alphad_;  // null: data
+  double a_, ad_;
+  const int* y_;
+  double* out2_;
+  glm_tangent_dev_vari(double t, dev_matrix_vari* eta, dev_matrix_vari* etad, vari* alpha, vari* alphad, double a,
+                       double ad, const int* y)
+      : vari(t), eta_(eta), etad_(etad), alpha_(alpha), alphad_(alphad), a_(a), ad_(ad), y_(y),
+        out2_(amd::alloc_doubles(2)) {}
+  void chain() override {
+    amd::check(smg_glm_tangent_rev(amd::ctx(), eta_->val_, a_, etad_->val_, ad_, y_, (long long)eta_->size(), adj_,
+                                   eta_->adj_, etad_->adj_, out2_),
+               "bernoulli_logit_glm_lpmf");
+    if (alpha_) add_pending_adjoint(alpha_, out2_);
+    if (alphad_) add_pending_adjoint(alphad_, out2_ + 1);
+  }
+};
+}  // namespace internal
+
+/** A + B of two device matrices of vars (same shape). */
+inline dev_var_matrix add(const dev_var_matrix& A, const dev_var_matrix& B) {
+  if (A.rows() != B.rows() || A.cols() != B.cols()) throw std::invalid_argument("add: size mismatch");
+  return dev_var_matrix((new internal::add_dev_vari(A.vi_, B.vi_))->C_);
+}
+/** tril(A) of a device matrix of vars. */
+inline dev_var_matrix tril(const dev_var_matrix& A) {
+  return dev_var_matrix((new internal::tril_dev_vari(A.vi_))->C_);
+}
+
+/** Eigen Matrix<fvar<var>> (host) -> dual device matrix (both parts bridged). */
+#ifdef STAN_MATH_AMD_HAS_EIGEN
+template <int R, int C>
+inline dev_fvar_matrix to_dev(const Eigen::Matrix<fvar<var>, R, C>& m, int rows = -1, int cols = -1) {
+  const size_t n = size_t(m.size());
+  std::vector<var> v(n), d(n);
+  for (size_t i = 0; i < n; ++i) {
+    v[i] = m(Eigen::Index(i)).val_;
+    d[i] = m(Eigen::Index(i)).d_;
+  }
+  if (rows < 0) {  // the matrix's own shape; rows x cols reshapes (column-major)
+    rows = int(m.rows());
+    cols = int(m.cols());
+  }
+  return dev_fvar_matrix{to_dev(v, rows, cols), to_dev(d, rows, cols)};
+}
+#endif
+inline dev_fvar_matrix to_dev(const std::vector<fvar<var>>& x, int rows = -1, int cols = 1) {
+  std::vector<var> v(x.size()), d(x.size());
+  for (size_t i = 0; i < x.size(); ++i) {
+    v[i] = x[i].val_;
+    d[i] = x[i].d_;
+  }
+  return dev_fvar_matrix{to_dev(v, rows, cols), to_dev(d, rows, cols)};
+}
+
+inline dev_fvar_matrix transpose(const dev_fvar_matrix& A) {
+  return dev_fvar_matrix{transpose(A.val_), transpose(A.d_)};
+}
+inline fvar<var> sum(const dev_fvar_matrix& A) {
+  fvar<var> s;
+  s.val_ = sum(A.val_);
+  s.d_ = sum(A.d_);
+  return s;
+}
+
+/** (A B)' = A' B + A B' (fwd/mat/fun/multiply.hpp). */
+inline dev_fvar_matrix multiply(const dev_fvar_matrix& A, const dev_fvar_matrix& B) {
+  dev_fvar_matrix C;
+  C.val_ = multiply(A.val_, B.val_);
+  C.d_ = add(multiply(A.d_, B.val_), multiply(A.val_, B.d_));
+  return C;
+}
+inline dev_fvar_matrix multiply(const dev_fvar_matrix& A, const dev_data<double>& B) {
+  return dev_fvar_matrix{multiply(A.val_, B), multiply(A.d_, B)};
+}
+inline dev_fvar_matrix multiply(const dev_data<double>& A, const dev_fvar_matrix& B) {
+  return dev_fvar_matrix{multiply(A, B.val_), multiply(A, B.d_)};
+}
+
+/** C = A^{-1} B for lower-triangular A: C' = A^{-1} (B' - tril(A') C)
+ * (fwd/mat/fun/mdivide_left_tri_low.hpp:40-44). */
+template <int TriView>
+inline dev_fvar_matrix mdivide_left_tri(const dev_fvar_matrix& A, const dev_fvar_matrix& B) {
+  static_assert(TriView == 1, "mdivide_left_tri<fvar<var>>: lower-triangular view (Eigen::Lower)");
+  dev_fvar_matrix C;
+  C.val_ = mdivide_left_tri<TriView>(A.val_, B.val_);
+  C.d_ = mdivide_left_tri<TriView>(A.val_, add(B.d_, multiply(-1.0, multiply(tril(A.d_), C.val_))));
+  return C;
+}
+template <int TriView>
+inline dev_fvar_matrix mdivide_left_tri(const dev_data<double>& A, const dev_fvar_matrix& B) {
+  static_assert(TriView == 1, "mdivide_left_tri<fvar<var>>: lower-triangular view (Eigen::Lower)");
+  return dev_fvar_matrix{mdivide_left_tri<TriView>(A, B.val_), mdivide_left_tri<TriView>(A, B.d_)};
+}
+template <int TriView>
+inline dev_fvar_matrix mdivide_left_tri(const dev_fvar_matrix& A, const dev_data<double>& B) {
+  static_assert(TriView == 1, "mdivide_left_tri<fvar<var>>: lower-triangular view (Eigen::Lower)");
+  dev_fvar_matrix C;
+  C.val_ = mdivide_left_tri<TriView>(A.val_, B);
+  C.d_ = mdivide_left_tri<TriView>(A.val_, multiply(-1.0, multiply(tril(A.d_), C.val_)));
+  return C;
+}
+
+/** log_sum_exp' = softmax(x) . x' (fwd/mat/fun/log_sum_exp.hpp). */
+inline fvar<var> log_sum_exp(const dev_fvar_matrix& x) {
+  fvar<var> r;
+  r.val_ = log_sum_exp(x.val_);
+  if (x.val_.size() == 0) {
+    r.d_ = var(0.0);
+    return r;
+  }
+  smg_ctx* c = amd::ctx();
+  double* out = amd::alloc_doubles(2);
+  amd::check(smg_lse_tangent_fwd(c, x.val_.val_ptr(), x.d_.val_ptr(), (long long)x.val_.size(), out),
+             "log_sum_exp");
+  double h[2];
+  amd::to_host(h, out, 2);
+  r.d_ = var(new internal::lse_tangent_dev_vari(h[1], h[0], x.val_.vi_, x.d_.vi_));
+  return r;
+}
+inline fvar<var> log_sum_exp(const std::vector<fvar<var>>& x) { return log_sum_exp(to_dev(x)); }
+
+/** bernoulli_logit_glm_lpmf(y | x, alpha, beta) at fvar<var> alpha / beta,
+ * x and y data on the device: the value by the var GLM, the tangent
+ * sum_i d_i (x_i beta' + alpha') by the reference's theta_derivative. */
+template <bool propto = false>
+inline fvar<var> bernoulli_logit_glm_lpmf(const dev_data<int>& y, const dev_data<double>& x, const fvar<var>& alpha,
+                                          const dev_fvar_matrix& beta) {
+  fvar<var> lp;
+  lp.val_ = bernoulli_logit_glm_lpmf<propto>(y, x, alpha.val_, beta.val_);
+  const long long R = x.rows();
+  if (R == 0) {
+    lp.d_ = var(0.0);
+    return lp;
+  }
+  dev_var_matrix eta = multiply(x, beta.val_);
+  dev_var_matrix etad = multiply(x, beta.d_);
+  smg_ctx* c = amd::ctx();
+  double* out = amd::alloc_doubles(1);
+  amd::check(smg_glm_tangent_fwd(c, eta.val_ptr(), alpha.val_.val(), etad.val_ptr(), alpha.d_.val(), y.data(), R, out),
+             "bernoulli_logit_glm_lpmf");
+  double t = 0.0;
+  amd::to_host(&t, out, 1);
+  lp.d_ = var(new internal::glm_tangent_dev_vari(t, eta.vi_, etad.vi_, alpha.val_.vi_, alpha.d_.vi_,
+                                                 alpha.val_.val(), alpha.d_.val(), y.data()));
+  return lp;
+}
+template <bool propto = false>
+inline fvar<var> bernoulli_logit_glm_lpmf(const dev_data<int>& y, const dev_data<double>& x, const fvar<var>& alpha,
+                                          const std::vector<fvar<var>>& beta) {
+  return bernoulli_logit_glm_lpmf<propto>(y, x, alpha, to_dev(beta));
+}
 
 inline dev_fvar_matrix cholesky_decompose(const dev_fvar_matrix& A) {
   dev_fvar_matrix L;

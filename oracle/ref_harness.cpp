@@ -1157,6 +1157,99 @@ static void fix_logdet() {
   write_fixture("log_determinant_singular3", j);
 }
 
+// ---- hessian() (mix/mat/functor/hessian.hpp:39-72) of
+// models built from multiply, mdivide_left_tri_low, log_sum_exp and the
+// bernoulli logit GLM (fvar<var> instantiations of the reference).
+struct lse_h_functor {
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    return stan::math::log_sum_exp(th);
+  }
+};
+struct tri_h_functor {  // sum(mdivide_left_tri_low(L, B) w), L n x n (lower used), B n x k
+  int n, k;
+  VectorXd w;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, Dynamic> L(n, n), B(n, k);
+    for (int i = 0; i < n * n; ++i) L(i) = th(i);
+    for (int i = 0; i < n * k; ++i) B(i) = th(n * n + i);
+    Matrix<T, Dynamic, Dynamic> C = stan::math::mdivide_left_tri_low(L, B);
+    return stan::math::sum(stan::math::multiply(C, w));
+  }
+};
+static void put_hessian(Json& j, const MatrixXd& H, bool full) {
+  j.put("H_sum", H.sum());
+  j.put("H_l2", H.norm());
+  if (full) {
+    j.put_mat("H", H);
+    return;
+  }
+  smg_rng r = smg_rng_make(SEED + 224);
+  std::vector<double> idx, val;
+  for (int s = 0; s < 2048; ++s) {
+    size_t kk = smg_rng_next(&r) % (size_t)H.size();
+    idx.push_back((double)kk);
+    val.push_back(H((Eigen::Index)kk));
+  }
+  j.put_vec("H_sample_index", idx);
+  j.put_vec("H_sample", val);
+}
+static void fix_hessian2() {
+  for (int N : {8, 40}) {  // config 2: sum(cholesky_decompose(add_diag(A A^T, N)))
+    VectorXd a = mulchol_input(N), g;
+    double fx;
+    MatrixXd H;
+    stan::math::hessian(mulchol_functor{N}, a, fx, g, H);
+    Json j;
+    j.put_str("what", "hessian of sum(cholesky_decompose(add_diag(multiply(A,A^T),N))) wrt A (col-major), "
+                      "A = tests/gen.py mulchol_input");
+    j.put_int("N", N);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    put_hessian(j, H, N <= 8);
+    write_fixture("hessian_mulchol_N" + std::to_string(N), j);
+  }
+  // (the bernoulli logit GLM does not instantiate at fvar<var> in the
+  // reference: prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:106 calls
+  // std::isfinite on a var; its Hessian is pinned in tests/ by the closed form)
+  {  // log_sum_exp of 7 values with a wide spread
+    VectorXd th(7), g;
+    th << -3.0, 0.5, 2.0, -0.25, 10.0, 9.5, -40.0;
+    double fx;
+    MatrixXd H;
+    stan::math::hessian(lse_h_functor{}, th, fx, g, H);
+    Json j;
+    j.put_str("what", "hessian of log_sum_exp(x)");
+    j.put_vec("x", th);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    put_hessian(j, H, true);
+    write_fixture("hessian_lse7", j);
+  }
+  {  // mdivide_left_tri_low: L 6 x 6 (lower: U[-1,1) + 4 on the diagonal; upper entries unused), B 6 x 2
+    const int n = 6, k = 2;
+    MatrixXd L = unif_mat(n, n, SEED + 140);
+    for (int i = 0; i < n; ++i) L(i, i) += 4.0;
+    MatrixXd B = unif_mat(n, k, SEED + 141);
+    VectorXd w = Eigen::Map<VectorXd>(unif_mat(k, 1, SEED + 142).data(), k);
+    VectorXd th(n * n + n * k), g;
+    th << Eigen::Map<VectorXd>(L.data(), L.size()), Eigen::Map<VectorXd>(B.data(), B.size());
+    double fx;
+    MatrixXd H;
+    stan::math::hessian(tri_h_functor{n, k, w}, th, fx, g, H);
+    Json j;
+    j.put_str("what", "hessian of sum(mdivide_left_tri_low(L, B) w) wrt (L (all n^2 entries, lower used), B); "
+                      "inputs tests/gen.py tri_h_inputs");
+    j.put_vec("theta", th);
+    j.put_vec("w", w);
+    j.put("fx", fx);
+    j.put_vec("grad", g);
+    put_hessian(j, H, true);
+    write_fixture("hessian_tri_n6_k2", j);
+  }
+}
+
 static void fix_hessian() {  // mix/mat/functor/hessian.hpp on the GP marginal
   for (int N : {8, 32, 100}) {
     std::vector<double> x;
@@ -1286,6 +1379,7 @@ int main(int argc, char** argv) {
     if (want("logdet")) fix_logdet();
     if (want("maprect")) fix_maprect();
     if (want("hessian")) fix_hessian();
+    if (want("hessian2")) fix_hessian2();
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();
     if (want("gp")) fix_gp();

@@ -768,6 +768,80 @@ static void cmd_hessian() {
               ChainableStack::instance_->dev_adj_stack_.size());
 }
 
+// hessian() (mix/mat/functor/hessian.hpp:39-72) of models built from the
+// fvar<var> device functors beyond the GP set:
+//   hessian2 mulchol N a(N^2)        sum(cholesky_decompose(add_diag(A A^T, N)))
+//   hessian2 lse n x(n)              log_sum_exp(x)
+//   hessian2 tri n k theta w(k)      sum(mdivide_left_tri<Lower>(L, B) w)
+//   hessian2 glm R M beta(M)         bernoulli_logit_glm_lpmf(y | x, alpha, beta), config-4 streams
+// prints fx, grad, H (column-major) and the tape sizes after the call
+static void cmd_hessian2() {
+  std::string kind;
+  std::cin >> kind;
+  Eigen::VectorXd x0, g;
+  Eigen::MatrixXd H;
+  double fx = 0;
+  using VF = Eigen::Matrix<fvar<var>, Eigen::Dynamic, 1>;
+  if (kind == "mulchol") {
+    int N;
+    std::cin >> N;
+    auto a = read_vec(size_t(N) * N);
+    x0 = Eigen::Map<Eigen::VectorXd>(a.data(), N * N);
+    hessian(
+        [N](const VF& th) {
+          dev_fvar_matrix Am = to_dev(th, N, N);
+          return sum(cholesky_decompose(add_diag(multiply(Am, transpose(Am)), double(N))));
+        },
+        x0, fx, g, H);
+  } else if (kind == "lse") {
+    int n;
+    std::cin >> n;
+    auto x = read_vec(size_t(n));
+    x0 = Eigen::Map<Eigen::VectorXd>(x.data(), n);
+    hessian([](const VF& th) { return log_sum_exp(to_dev(th)); }, x0, fx, g, H);
+  } else if (kind == "tri") {
+    int n, k;
+    std::cin >> n >> k;
+    auto th = read_vec(size_t(n) * n + size_t(n) * k);
+    auto w = read_vec(size_t(k));
+    x0 = Eigen::Map<Eigen::VectorXd>(th.data(), Eigen::Index(th.size()));
+    hessian(
+        [n, k, &w](const VF& t) {
+          dev_fvar_matrix L = to_dev(t.head(n * n).eval(), n, n);
+          dev_fvar_matrix B = to_dev(t.tail(n * k).eval(), n, k);
+          dev_fvar_matrix C = mdivide_left_tri<Eigen::Lower>(L, B);
+          return sum(multiply(C, to_dev_data(w.data(), w.size(), k, 1)));
+        },
+        x0, fx, g, H);
+  } else if (kind == "glm") {
+    long long R;
+    int M;
+    std::cin >> R >> M;
+    auto beta = read_vec(M);
+    smg_ctx* c = amd::ctx();
+    int* y = amd::alloc_ints(size_t(R));
+    double* x = amd::alloc_doubles(size_t(R) * M);
+    amd::check(smg_fill_unif(c, x, R * M, 20260101ull + 41, -1.0, 1.0, std::sqrt(3.0)), "fill");
+    amd::check(smg_fill_bernoulli(c, y, R, 20260101ull + 42, 0.5), "fill");
+    dev_data<int> yd(y, size_t(R), int(R), 1);
+    dev_data<double> xd(x, size_t(R) * M, int(R), M);
+    x0.resize(M + 1);
+    x0(0) = 0.1;
+    for (int j = 0; j < M; ++j) x0(1 + j) = beta[size_t(j)];
+    hessian(
+        [&](const VF& t) {
+          std::vector<fvar<var>> b(t.data() + 1, t.data() + t.size());
+          return bernoulli_logit_glm_lpmf(yd, xd, t(0), b);
+        },
+        x0, fx, g, H);
+  }
+  print1("fx", fx);
+  print("grad", std::vector<double>(g.data(), g.data() + g.size()));
+  print("H", std::vector<double>(H.data(), H.data() + H.size()));
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->dev_adj_stack_.size());
+}
+
 template <typename F>
 static void expect_throw(const char* name, F&& f) {
   start_nested();
@@ -1085,6 +1159,7 @@ int main() {
     else if (cmd == "errors") cmd_errors();
     else if (cmd == "hvp") cmd_hvp();
     else if (cmd == "hessian") cmd_hessian();
+    else if (cmd == "hessian2") cmd_hessian2();
     else if (cmd == "map_rect_glm") cmd_map_rect_glm();
     else if (cmd == "status") cmd_status();
     else if (cmd == "ops_partials") cmd_ops_partials();
