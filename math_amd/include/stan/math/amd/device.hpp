@@ -17,6 +17,7 @@
 
 #include <smg_hip.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -90,6 +91,28 @@ inline void throw_status(int st, const char* function, const char* what = "") {
   }
   m << "HIP runtime failure (status " << st << ")";
   throw std::runtime_error(m.str());
+}
+
+/**
+ * The reference's check_symmetric message (prim/mat/err/check_symmetric.hpp:
+ * 36-55): the first pair (m < n, m outer) with !(|A(m,n) - A(n,m)| <= 1e-8),
+ * "<fn>: <name> is not symmetric. <name>[m,n] = a, but <name>[n,m] = b"
+ * (1-based).  A: host, column-major n x n.
+ */
+inline void throw_not_symmetric_host(const char* fn, const char* name, const double* A, int n) {
+  for (int m = 0; m < n; ++m)
+    for (int q = m + 1; q < n; ++q) {
+      const double a = A[m + size_t(q) * n], b = A[q + size_t(m) * n];
+      if (!(std::fabs(a - b) <= 1e-8)) {
+        std::ostringstream o;
+        o << fn << ": " << name << " is not symmetric. " << name << "[" << m + 1 << "," << q + 1 << "] = " << a
+          << ", but " << name << "[" << q + 1 << "," << m + 1 << "] = " << b;
+        throw std::domain_error(o.str());
+      }
+    }
+  std::ostringstream o;  // (the device flagged it; no pair found on the host copy)
+  o << fn << ": " << name << " is not symmetric";
+  throw std::domain_error(o.str());
 }
 
 /** This thread's device context (created on first use). */

@@ -77,6 +77,14 @@ inline void check_square(const char* fn, const char* name, int rows, int cols) {
   }
 }
 
+/** check_symmetric's message for a device matrix the device check flagged
+ * (error path: one host copy of A). */
+inline void throw_not_symmetric_dev(const char* fn, const char* name, const double* A, int n) {
+  std::vector<double> h(size_t(n) * n);
+  amd::to_host(h.data(), A, h.size());
+  amd::throw_not_symmetric_host(fn, name, h.data(), n);
+}
+
 }  // namespace internal
 
 inline dev_var_matrix add_diag(const dev_var_matrix& A, const var& d) {
@@ -102,7 +110,7 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   amd::check(smg_cholesky_fwd_checked(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
   int st = 0;
   amd::check(smg_status(c, &st), fn);
-  if (st & SMG_ERR_NOT_SYMMETRIC) amd::throw_status(SMG_ERR_NOT_SYMMETRIC, fn, "A");
+  if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
   if (st) amd::throw_status(st, fn, "m");
   new internal::cholesky_dev_vari(A.vi_, L);
   return dev_var_matrix(L);

@@ -76,7 +76,8 @@ inline dev_data<double> gp_x_to_device(const std::vector<double>& x) {
   for (size_t i = 0; i < x.size(); ++i)
     if (std::isnan(x[i])) {
       std::ostringstream m;
-      m << "gp_exp_quad_cov: x[" << i + 1 << "] is nan, but must not be nan!";
+      // check_not_nan("gp_exp_quad_cov", "x", x[i]) on the element (:220): no index in the message
+      m << "gp_exp_quad_cov: x is nan, but must not be nan!";
       throw std::domain_error(m.str());
     }
   return to_dev_data(x);

@@ -59,37 +59,56 @@ inline void mvn_check_sizes(int ny, int nmu, const dev_var_matrix& L) {
   if (ny != L.cols()) mismatch("Size of random variable", ny, "columns of covariance parameter", L.cols());
 }
 
+inline void mvn_check_data(const std::vector<double>& y, const std::vector<double>* mu) {
+  // (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:100-103: check_finite of
+  // the location vector, then check_not_nan of the random variable; the
+  // whole vectors are checked, so the message carries the 1-based index)
+  const char* fn = "multi_normal_cholesky_lpdf";
+  if (mu)
+    for (size_t i = 0; i < mu->size(); ++i)
+      if (!std::isfinite((*mu)[i])) {
+        std::ostringstream m;
+        m << fn << ": Location parameter[" << i + 1 << "] is " << (*mu)[i] << ", but must be finite!";
+        throw std::domain_error(m.str());
+      }
+  for (size_t i = 0; i < y.size(); ++i)
+    if (std::isnan(y[i])) {
+      std::ostringstream m;
+      m << fn << ": Random variable[" << i + 1 << "] is nan, but must not be nan!";
+      throw std::domain_error(m.str());
+    }
+}
+
 template <bool propto>
 inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const dev_var_matrix& L,
                             dev_matrix_vari* y_vi = nullptr, dev_matrix_vari* mu_vi = nullptr) {
   const char* fn = "multi_normal_cholesky_lpdf";
   if (n == 0) return var(0.0);
   smg_ctx* c = amd::ctx();
-  double* ws = amd::alloc_doubles(2 * size_t(n) + 1);
-  double* lp_d = ws + 2 * size_t(n);
+  double* ws = amd::alloc_doubles(2 * size_t(n) + 3);
+  double* lp_d = ws + 2 * size_t(n);  // [lp, mu not finite, y nan]: read back together
+  // check_finite(mu), check_not_nan(y) (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:100-103)
+  // on the device values, their flags landing with the value (one sync)
+  amd::check(smg_memset(c, lp_d + 1, 0, 2 * sizeof(double)), fn);
+  if (mu_d) amd::check(smg_check_domain(c, mu_d, n, 1, lp_d + 1), fn);
+  amd::check(smg_check_domain(c, y_d, n, 0, lp_d + 2), fn);
   amd::check(smg_mvn_cholesky_fwd(c, y_d, mu_d, L.val_ptr(), n, L.vi_->aux_, n, ws, lp_d), fn);
-  double lp = 0;
-  amd::to_host(&lp, lp_d, 1);
+  double out[3] = {0, 0, 0};
+  amd::to_host(out, lp_d, 3);
+  if (out[1] != 0.0 || out[2] != 0.0) {  // error path: the values on the host, the reference's message
+    std::vector<double> yh(static_cast<size_t>(n)), mh;
+    amd::to_host(yh.data(), y_d, yh.size());
+    if (mu_d) {
+      mh.resize(size_t(n));
+      amd::to_host(mh.data(), mu_d, mh.size());
+    }
+    mvn_check_data(yh, mu_d ? &mh : nullptr);
+  }
+  double lp = out[0];
   if (propto) lp -= -std::log(std::sqrt(2.0 * 3.14159265358979323846)) * n;
   return var(new mvn_cholesky_dev_vari(lp, L.vi_, ws, y_vi, mu_vi));
 }
 
-inline void mvn_check_data(const std::vector<double>& y, const std::vector<double>* mu) {
-  const char* fn = "multi_normal_cholesky_lpdf";
-  for (size_t i = 0; i < y.size(); ++i)
-    if (std::isnan(y[i])) {
-      std::ostringstream m;
-      m << fn << ": Random variable is nan, but must not be nan!";
-      throw std::domain_error(m.str());
-    }
-  if (mu)
-    for (double v : *mu)
-      if (!std::isfinite(v)) {
-        std::ostringstream m;
-        m << fn << ": Location parameter is " << v << ", but must be finite!";
-        throw std::domain_error(m.str());
-      }
-}
 
 }  // namespace internal
 

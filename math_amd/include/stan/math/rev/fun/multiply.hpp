@@ -32,7 +32,7 @@ inline void check_multiplicable(const char* fn, int a_rows, int a_cols, int b_ro
   (void)b_cols;
   if (a_cols != b_rows) {
     std::ostringstream m;
-    m << fn << ": Columns of m1 (" << a_cols << ") and Rows of m2 (" << b_rows
+    m << fn << ": Columns of A (" << a_cols << ") and Rows of B (" << b_rows
       << ") must match in size";
     throw std::invalid_argument(m.str());
   }

@@ -116,6 +116,29 @@ struct is_device_operand
     : std::integral_constant<bool, std::is_same<T, dev_var_matrix>::value ||
                                        std::is_same<T, dev_data<double>>::value> {};
 
+/**
+ * The reference's domain error for the first offending element of one
+ * operand (check_not_nan / check_finite / check_positive,
+ * prim/scal/err/check_*.hpp: "name[i] is v, but must ...", 1-based index for
+ * a vector, no index for a scalar; v printed with the stream defaults).
+ * kind: 0 not nan, 1 finite, 2 positive.  Returns without throwing when no
+ * element fails.
+ */
+inline void normal_throw_first(const char* fn, int kind, const double* v, size_t n, bool vec) {
+  static const char* const names[3] = {"Random variable", "Location parameter", "Scale parameter"};
+  static const char* const musts[3] = {"not be nan!", "be finite!", "be > 0!"};
+  for (size_t i = 0; i < n; ++i) {
+    const double x = v[i];
+    const bool bad = kind == 0 ? std::isnan(x) : (kind == 1 ? !(std::fabs(x) <= 1.7976931348623157e308) : !(x > 0.0));
+    if (!bad) continue;
+    std::ostringstream m;
+    m << fn << ": " << names[kind];
+    if (vec) m << "[" << i + 1 << "]";
+    m << " is " << x << ", but must " << musts[kind];
+    throw std::domain_error(m.str());
+  }
+}
+
 /** Element i of a host operand (scalars broadcast). */
 inline double host_val(double x, size_t) { return x; }
 inline double host_val(const var& x, size_t) { return x.vi_->val_; }
@@ -167,15 +190,17 @@ inline typename ops_return<T_y, T_loc, T_scale>::type normal_lpdf_host(const T_y
                                                                        int include) {
   static const char* fn = "normal_lpdf";
   constexpr bool vy = op_is_var<T_y>::value, vmu = op_is_var<T_loc>::value, vs = op_is_var<T_scale>::value;
-  for (size_t i = 0; i < ops[0].n; ++i)
-    if (std::isnan(host_val(y, i)))
-      throw std::domain_error(std::string(fn) + ": Random variable is nan, but must not be nan!");
-  for (size_t i = 0; i < ops[1].n; ++i)
-    if (!(std::fabs(host_val(mu, i)) <= 1.7976931348623157e308))
-      throw std::domain_error(std::string(fn) + ": Location parameter is not finite, but must be finite!");
-  for (size_t i = 0; i < ops[2].n; ++i)
-    if (!(host_val(sigma, i) > 0.0))
-      throw std::domain_error(std::string(fn) + ": Scale parameter is not positive, but must be > 0!");
+  {
+    std::vector<double> v;
+    auto check = [&](int kind, const auto& x, const fused_operand& o) {
+      v.resize(o.n);
+      for (size_t i = 0; i < o.n; ++i) v[i] = host_val(x, i);
+      normal_throw_first(fn, kind, v.data(), o.n, o.vec);
+    };
+    check(0, y, ops[0]);
+    check(1, mu, ops[1]);
+    check(2, sigma, ops[2]);
+  }
   normal_check_sizes(fn, ops);
   using ret_t = typename ops_return<T_y, T_loc, T_scale>::type;
   if constexpr (!(vy || vmu || vs)) {
@@ -216,22 +241,21 @@ inline typename ops_return<T_y, T_loc, T_scale>::type normal_lpdf_host(const T_y
 }
 
 inline void normal_check_sizes(const char* fn, const fused_operand* ops) {
+  // check_consistent_sizes (prim/scal/err/check_consistent_sizes.hpp): the
+  // expected size is the largest vector's; the first vector operand of
+  // another size is reported
   static const char* const names[3] = {"Random variable", "Location parameter", "Scale parameter"};
   size_t expect = 0;
-  int first = -1;
   for (int i = 0; i < 3; ++i)
-    if (ops[i].vec) {
-      if (first < 0) {
-        first = i;
-        expect = ops[i].n;
-      } else if (ops[i].n != expect) {
-        std::ostringstream m;
-        m << fn << ": " << names[i] << " has dimension = " << ops[i].n << ", expecting dimension = " << expect
-          << "; a function was called with arguments of different scalar, array, vector, or "
-             "matrix types, and they were not consistently sized;  all arguments must be "
-             "scalars or multidimensional values of the same shape.";
-        throw std::invalid_argument(m.str());
-      }
+    if (ops[i].vec && ops[i].n > expect) expect = ops[i].n;
+  for (int i = 0; i < 3; ++i)
+    if (ops[i].vec && ops[i].n != expect) {
+      std::ostringstream m;
+      m << fn << ": " << names[i] << " has dimension = " << ops[i].n << ", expecting dimension = " << expect
+        << "; a function was called with arguments of different scalar, array, vector, or "
+           "matrix types, and they were not consistently sized;  all arguments must be "
+           "scalars or multidimensional values of the same shape.";
+      throw std::invalid_argument(m.str());
     }
 }
 
@@ -330,11 +354,15 @@ inline typename internal::ops_return<T_y, T_loc, T_scale>::type normal_lpdf(cons
     }
     amd::check(smg_sync(c), fn);
   }
-  if (st[1] != 0.0) throw std::domain_error(std::string(fn) + ": Random variable is nan, but must not be nan!");
-  if (st[2] != 0.0)
-    throw std::domain_error(std::string(fn) + ": Location parameter is not finite, but must be finite!");
-  if (st[3] != 0.0)
-    throw std::domain_error(std::string(fn) + ": Scale parameter is not positive, but must be > 0!");
+  for (int i = 0; i < 3; ++i) {
+    if (st[1 + i] == 0.0) continue;
+    // error path: the operand's values on the host, the first offending one reported
+    std::vector<double> hv(ops[i].vec ? ops[i].n : 1);
+    if (!ops[i].vec) hv[0] = ops[i].scalar;
+    else if (ops[i].host) std::memcpy(hv.data(), st + val_off[i], ops[i].n * sizeof(double));
+    else amd::to_host(hv.data(), ops[i].dev, ops[i].n);
+    internal::normal_throw_first(fn, i, hv.data(), hv.size(), ops[i].vec);
+  }
   internal::normal_check_sizes(fn, ops);
   const double logp = st[0];
   if constexpr (vy || vmu || vs) {

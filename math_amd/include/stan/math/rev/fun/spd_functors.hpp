@@ -52,6 +52,7 @@ inline void check_symmetric_dev(const char* fn, const char* name, const double* 
   amd::check(smg_check_symmetric(c, A, n, n), fn);
   int st = 0;
   amd::check(smg_status(c, &st), fn);
+  if (st & SMG_ERR_NOT_SYMMETRIC) throw_not_symmetric_dev(fn, name, A, n);
   if (st) amd::throw_status(st, fn, name);
 }
 

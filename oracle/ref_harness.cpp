@@ -1250,6 +1250,97 @@ static void fix_hessian2() {
   }
 }
 
+// The error messages of the hot-path functors (the cases of
+// tests/cpp/test_functors.cpp cmd_errors, with the reference's own argument
+// types): "<kind> <what()>" per case.
+static void fix_errors() {
+  using stan::math::var;
+  using VV = Matrix<var, Dynamic, 1>;
+  using MV = Matrix<var, Dynamic, Dynamic>;
+  Json j;
+  auto run = [&](const char* name, auto&& f) {
+    std::string out;
+    try {
+      f();
+      out = "nothrow";
+    } catch (const std::domain_error& e) {
+      out = std::string("domain_error ") + e.what();
+    } catch (const std::invalid_argument& e) {
+      out = std::string("invalid_argument ") + e.what();
+    } catch (const std::exception& e) {
+      out = std::string("other ") + e.what();
+    }
+    stan::math::recover_memory();
+    j.put_str(name, out.c_str());
+  };
+  auto M = [](std::initializer_list<double> v, int r, int c) {
+    MV m(r, c);
+    int i = 0;
+    for (double t : v) m(i++) = t;
+    return m;
+  };
+  const double nan = std::nan("");
+  run("normal_nan_y", [&] { return stan::math::normal_lpdf(std::vector<var>{1.0, nan}, 0.0, 1.0); });
+  run("normal_inf_mu", [&] { return stan::math::normal_lpdf(var(1.0), INFINITY, 1.0); });
+  run("normal_neg_sigma", [&] { return stan::math::normal_lpdf(var(1.0), 0.0, -1.0); });
+  run("normal_sizes", [&] {
+    return stan::math::normal_lpdf(std::vector<var>{1.0, 2.0}, std::vector<double>{0, 0, 0}, 1.0);
+  });
+  run("multiply_sizes", [&] {
+    MV A = M({1, 1, 1, 1, 1, 1}, 2, 3);
+    return stan::math::multiply(A, A);
+  });
+  run("mdivide_square", [&] {
+    MV A = M({1, 1, 1, 1, 1, 1}, 2, 3);
+    return stan::math::mdivide_left_tri<Eigen::Lower>(A, A);
+  });
+  run("chol_not_symmetric", [&] { return stan::math::cholesky_decompose(M({2, 1, 0, 2}, 2, 2)); });
+  run("chol_not_pd", [&] { return stan::math::cholesky_decompose(M({1, 2, 2, 1}, 2, 2)); });
+  run("chol_not_square", [&] { return stan::math::cholesky_decompose(M({1, 2, 2, 1, 3, 3}, 2, 3)); });
+  run("chol_nan", [&] { return stan::math::cholesky_decompose(M({1, nan, nan, 1}, 2, 2)); });
+  const MatrixXd x = Eigen::Map<const MatrixXd>(std::vector<double>{1, 2}.data(), 2, 1);
+  run("glm_y_bounds", [&] {
+    VV b(1);
+    b << 1.0;
+    return stan::math::bernoulli_logit_glm_lpmf(std::vector<int>{0, 2}, x, var(0.0), b);
+  });
+  run("glm_beta_size", [&] {
+    VV b(2);
+    b << 1.0, 2.0;
+    return stan::math::bernoulli_logit_glm_lpmf(std::vector<int>{0, 1}, x, var(0.0), b);
+  });
+  run("glm_nonfinite_beta", [&] {
+    VV b(1);
+    b << INFINITY;
+    return stan::math::bernoulli_logit_glm_lpmf(std::vector<int>{0, 1}, x, var(0.0), b);
+  });
+  run("mvn_not_square", [&] {
+    VV y(2), mu(2);
+    y << 1, 2;
+    mu << 0, 0;
+    return stan::math::multi_normal_cholesky_lpdf(y, mu, M({1, 0, 0, 1, 0, 0}, 2, 3));
+  });
+  run("mvn_size_mu", [&] {
+    VV y(2), mu(3);
+    y << 1, 2;
+    mu << 0, 0, 0;
+    return stan::math::multi_normal_cholesky_lpdf(y, mu, M({1, 0, 0, 1}, 2, 2));
+  });
+  run("mvn_nan_y", [&] {
+    VV y(2), mu(2);
+    y << 1, nan;
+    mu << 0, 0;
+    return stan::math::multi_normal_cholesky_lpdf(y, mu, M({1, 0, 0, 1}, 2, 2));
+  });
+  run("gp_nonpositive_l", [&] {
+    return stan::math::gp_exp_quad_cov(std::vector<double>{1, 2}, var(1.0), var(-1.0));
+  });
+  run("gp_nan_x", [&] {
+    return stan::math::gp_exp_quad_cov(std::vector<double>{1, nan}, var(1.0), var(1.0));
+  });
+  write_fixture("errors_hot_path", j);
+}
+
 static void fix_hessian() {  // mix/mat/functor/hessian.hpp on the GP marginal
   for (int N : {8, 32, 100}) {
     std::vector<double> x;
@@ -1380,6 +1471,7 @@ int main(int argc, char** argv) {
     if (want("maprect")) fix_maprect();
     if (want("hessian")) fix_hessian();
     if (want("hessian2")) fix_hessian2();
+    if (want("errors")) fix_errors();
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();
     if (want("gp")) fix_gp();

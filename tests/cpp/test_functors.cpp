@@ -858,6 +858,70 @@ static void expect_throw(const char* name, F&& f) {
   recover_memory_nested();
 }
 
+// the reference's own error cases for the hot-path functors
+// (tests/golden/errors_hot_path.json, oracle/ref_harness.cpp fix_errors),
+// through the drop-in Eigen / std::vector signatures
+static void cmd_errors_hot() {
+  const double nan = std::nan("");
+  auto M = [](std::initializer_list<double> v, int r, int c) {
+    matrix_v m(r, c);
+    int i = 0;
+    for (double t : v) m(i++) = t;
+    return m;
+  };
+  expect_throw("normal_nan_y", [&] { normal_lpdf(std::vector<var>{1.0, nan}, 0.0, 1.0); });
+  expect_throw("normal_inf_mu", [&] { normal_lpdf(var(1.0), INFINITY, 1.0); });
+  expect_throw("normal_neg_sigma", [&] { normal_lpdf(var(1.0), 0.0, -1.0); });
+  expect_throw("normal_sizes",
+               [&] { normal_lpdf(std::vector<var>{1.0, 2.0}, std::vector<double>{0, 0, 0}, 1.0); });
+  expect_throw("multiply_sizes", [&] {
+    matrix_v A = M({1, 1, 1, 1, 1, 1}, 2, 3);
+    multiply(A, A);
+  });
+  expect_throw("mdivide_square", [&] {
+    matrix_v A = M({1, 1, 1, 1, 1, 1}, 2, 3);
+    mdivide_left_tri<Eigen::Lower>(A, A);
+  });
+  expect_throw("chol_not_symmetric", [&] { cholesky_decompose(M({2, 1, 0, 2}, 2, 2)); });
+  expect_throw("chol_not_pd", [&] { cholesky_decompose(M({1, 2, 2, 1}, 2, 2)); });
+  expect_throw("chol_not_square", [&] { cholesky_decompose(M({1, 2, 2, 1, 3, 3}, 2, 3)); });
+  expect_throw("chol_nan", [&] { cholesky_decompose(M({1, nan, nan, 1}, 2, 2)); });
+  expect_throw("glm_y_bounds", [&] {
+    bernoulli_logit_glm_lpmf(std::vector<int>{0, 2}, std::vector<double>{1, 2}, 1, var(0.0), std::vector<var>{1.0});
+  });
+  expect_throw("glm_beta_size", [&] {
+    bernoulli_logit_glm_lpmf(std::vector<int>{0, 1}, std::vector<double>{1, 2}, 1, var(0.0),
+                             std::vector<var>{1.0, 2.0});
+  });
+  expect_throw("glm_nonfinite_beta", [&] {
+    bernoulli_logit_glm_lpmf(std::vector<int>{0, 1}, std::vector<double>{1, 2}, 1, var(0.0),
+                             std::vector<var>{INFINITY});
+  });
+  expect_throw("mvn_not_square", [&] {
+    vector_v y(2), mu(2);
+    y << 1, 2;
+    mu << 0, 0;
+    multi_normal_cholesky_lpdf(y, mu, M({1, 0, 0, 1, 0, 0}, 2, 3));
+  });
+  expect_throw("mvn_size_mu", [&] {
+    vector_v y(2), mu(3);
+    y << 1, 2;
+    mu << 0, 0, 0;
+    multi_normal_cholesky_lpdf(y, mu, M({1, 0, 0, 1}, 2, 2));
+  });
+  expect_throw("mvn_nan_y", [&] {
+    vector_v y(2), mu(2);
+    y << 1, nan;
+    mu << 0, 0;
+    multi_normal_cholesky_lpdf(y, mu, M({1, 0, 0, 1}, 2, 2));
+  });
+  expect_throw("gp_nonpositive_l", [&] { gp_exp_quad_cov(std::vector<double>{1, 2}, var(1.0), var(-1.0)); });
+  expect_throw("gp_nan_x", [&] { gp_exp_quad_cov(std::vector<double>{1, nan}, var(1.0), var(1.0)); });
+  recover_memory();
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->nested_var_stack_sizes_.size());
+}
+
 static void cmd_errors() {
   const double nan = std::nan("");
   expect_throw("normal_nan_y", [&] { normal_lpdf(std::vector<var>{1.0, nan}, 0.0, 1.0); });
@@ -1157,6 +1221,7 @@ int main() {
     else if (cmd == "logdet") cmd_logdet();
     else if (cmd == "mvn") cmd_mvn();
     else if (cmd == "errors") cmd_errors();
+    else if (cmd == "errors_hot") cmd_errors_hot();
     else if (cmd == "hvp") cmd_hvp();
     else if (cmd == "hessian") cmd_hessian();
     else if (cmd == "hessian2") cmd_hessian2();
