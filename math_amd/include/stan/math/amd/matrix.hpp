@@ -138,6 +138,7 @@ class dev_to_host_vari : public vari {
   double* stage_;  // device scratch for the gathered adjoints
   dev_to_host_vari(dev_matrix_vari* src, vari** elems)
       : vari(0.0), src_(src), elems_(elems), stage_(amd::alloc_doubles(src->size())) {}
+  bool reads_other_adjoints() const override { return true; }
   void chain() override {
     const size_t n = src_->size();
     std::vector<double> h(n);

@@ -79,7 +79,14 @@ static void grad(vari* vi) {
   it_t begin = st->var_stack_.rbegin();
   it_t end = empty_nested() ? st->var_stack_.rend() : begin + nested_size();
   for (it_t it = begin; it < end; ++it) {
-    if (__builtin_expect(!st->pending_.empty(), 0)) flush_pending();
+    // a device->host contribution must land before its target's chain() reads
+    // its adj_; nodes that are not a target run without a synchronisation
+    // (device nodes keep streaming)
+    if (__builtin_expect(!st->pending_.empty(), 0)) {
+      bool need = (*it)->reads_other_adjoints();
+      for (size_t i = 0; !need && i < st->pending_.size(); ++i) need = st->pending_[i].target == *it;
+      if (need) flush_pending();
+    }
     (*it)->chain();
   }
   flush_pending(true);

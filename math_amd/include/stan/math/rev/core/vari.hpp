@@ -37,6 +37,11 @@ class vari {
 
   virtual void chain() {}
 
+  /** True for a node whose chain() reads the adjoints of OTHER varis (not
+   * only its own adj_): the reverse sweep lands pending device->host
+   * contributions before such a node runs (grad.hpp). */
+  virtual bool reads_other_adjoints() const { return false; }
+
   void init_dependent() { adj_ = 1.0; }
 
   void set_zero_adjoint() { adj_ = 0.0; }
