@@ -140,6 +140,56 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
   const bool forward = (lower && !trans) || (!lower && trans);
   const bool wt = (trans != 0) != (lower == 0);  // X_p = W_p^T B_p
   int rc;
+  static const bool recursive = [] {  // dev A/B switch (SMG_TRSM_REC=0: the block loop)
+    const char* e = getenv("SMG_TRSM_REC");
+    return !e || atoi(e) != 0;
+  }();
+  if (recursive && lower && BSZ == SMG_NBR && m % SMG_NBR == 0) {
+    // Recursive halving: solve the first half, ONE update of the second half
+    // by the whole first half (a rank-m/2 GEMM), solve the second half (for
+    // the transposed solve the halves swap roles).  The same flops as the
+    // block loop, in fewer, larger GEMMs (m/2, m/4, ... ranks instead of
+    // m/512 rank-512 updates); leaves are the 512-row blocks' W_p B_p.
+    struct rec_t {
+      smg_ctx* ctx;
+      const double* A;
+      int lda;
+      const double* W;
+      int ldw;
+      double* B;
+      int ldb;
+      double* X;
+      int ldx;
+      int n, trans;
+      int solve(int lo, int hi) {
+        if (hi - lo == SMG_NBR) {
+          double* Bp = X ? X + lo : B + lo;
+          const int ldp = X ? ldx : ldb;
+          return smg_gemm_impl(ctx, trans ? 1 : 0, 0, 0, SMG_NBR, n, SMG_NBR, 1.0, W + lo, ldw, B + lo, ldb, 0.0,
+                               Bp, ldp, trans ? SMG_TRI_A_UPPER : SMG_TRI_A_LOWER);
+        }
+        const int mid = lo + ((hi - lo) / SMG_NBR / 2) * SMG_NBR;
+        const double* Xs = X ? X : B;
+        const int lds = X ? ldx : ldb;
+        int rc;
+        if (!trans) {  // X[lo:mid], then B[mid:hi] -= L[mid:hi, lo:mid] X[lo:mid], then X[mid:hi]
+          if ((rc = solve(lo, mid))) return rc;
+          rc = smg_gemm_impl(ctx, 0, 0, 0, hi - mid, n, mid - lo, -1.0, A + mid + (size_t)lo * lda, lda, Xs + lo,
+                             lds, 1.0, B + mid, ldb);
+          if (rc) return rc;
+          return solve(mid, hi);
+        }
+        // L^T X = B: X[mid:hi], then B[lo:mid] -= L[mid:hi, lo:mid]^T X[mid:hi], then X[lo:mid]
+        if ((rc = solve(mid, hi))) return rc;
+        rc = smg_gemm_impl(ctx, 1, 0, 0, mid - lo, n, hi - mid, -1.0, A + mid + (size_t)lo * lda, lda, Xs + mid,
+                           lds, 1.0, B + lo, ldb);
+        if (rc) return rc;
+        return solve(lo, mid);
+      }
+    };
+    rec_t r{ctx, A, lda, W, ldw, B, ldb, X, ldx, n, trans};
+    return r.solve(0, m);
+  }
   for (int q = 0; q < nblk; ++q) {
     const int p = forward ? q : nblk - 1 - q;
     const int j = p * BSZ, b = min(BSZ, m - j), k = j + b;
