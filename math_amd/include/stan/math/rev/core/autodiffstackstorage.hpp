@@ -72,7 +72,10 @@ struct AutodiffStackSingleton {
   AutodiffStackSingleton(const AutodiffStackSingleton_t&) = delete;
   AutodiffStackSingleton& operator=(const AutodiffStackSingleton_t&) = delete;
 
-  static inline thread_local AutodiffStackStorage* instance_ = nullptr;
+  // initial-exec TLS: the tape pointer is read on every var construction and
+  // every chain() of the sweep; in a shared library the default
+  // (general-dynamic) model would make each read a __tls_get_addr call
+  static inline thread_local AutodiffStackStorage* instance_ __attribute__((tls_model("initial-exec"))) = nullptr;
 
  private:
   static bool init() {

@@ -191,9 +191,16 @@ inline typename ops_return<T_y, T_loc, T_scale>::type normal_lpdf_host(const T_y
   static const char* fn = "normal_lpdf";
   constexpr bool vy = op_is_var<T_y>::value, vmu = op_is_var<T_loc>::value, vs = op_is_var<T_scale>::value;
   {
-    std::vector<double> v;
+    // one scan per operand (no copy); the message is built from a copy of the
+    // values only when an element fails
     auto check = [&](int kind, const auto& x, const fused_operand& o) {
-      v.resize(o.n);
+      bool bad = false;
+      for (size_t i = 0; i < o.n; ++i) {
+        const double v = host_val(x, i);
+        bad |= kind == 0 ? std::isnan(v) : (kind == 1 ? !(std::fabs(v) <= 1.7976931348623157e308) : !(v > 0.0));
+      }
+      if (!bad) return;
+      std::vector<double> v(o.n);
       for (size_t i = 0; i < o.n; ++i) v[i] = host_val(x, i);
       normal_throw_first(fn, kind, v.data(), o.n, o.vec);
     };

@@ -124,16 +124,30 @@ using vec_partials_t = Eigen::VectorXd;
 using vec_partials_t = std::vector<double>;
 #endif
 
+#ifdef STAN_MATH_AMD_HAS_EIGEN
+// the partials of a std::vector<var> edge live in the tape's arena (no heap
+// allocation per call); an Eigen vector view, indexed and assigned like the
+// reference's Eigen::VectorXd
+using vec_partials_view_t = Eigen::Map<Eigen::VectorXd>;
+inline vec_partials_view_t arena_partials(size_t n) {
+  double* p = ChainableStack::instance_->memalloc_.alloc_array<double>(n ? n : 1);
+  vec_partials_view_t v(p, Eigen::Index(n));
+  v.setZero();
+  return v;
+}
+#else
+using vec_partials_view_t = vec_partials_t;
+inline vec_partials_view_t arena_partials(size_t n) { return vec_partials_t(n, 0.0); }
+#endif
+
 /** std::vector<var> (rev/mat/meta/operands_and_partials.hpp:15-43). */
 template <>
 class ops_partials_edge<double, std::vector<var>> {
  public:
-  vec_partials_t partials_;
-  broadcast_array<vec_partials_t> partials_vec_;
+  vec_partials_view_t partials_;
+  broadcast_array<vec_partials_view_t> partials_vec_;
   explicit ops_partials_edge(const std::vector<var>& op)
-      : partials_(vec_partials_t(op.size())), partials_vec_(partials_), operands_(op) {
-    for (size_t i = 0; i < op.size(); ++i) partials_[i] = 0.0;
-  }
+      : partials_(arena_partials(op.size())), partials_vec_(partials_), operands_(op) {}
   int size() const { return int(operands_.size()); }
   void dump_operands(vari** v) const {
     for (size_t i = 0; i < operands_.size(); ++i) v[i] = operands_[i].vi_;

@@ -13,7 +13,8 @@ if [ "$SKIP_TESTS" != 1 ]; then
   tail -3 $O/${TAG}_pytest.log
 fi
 for w in ${WLS:-gp glm mulchol hvp normal}; do
-  timeout -k 10 400 python bench.py --workload $w > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err || { tail $O/${TAG}_bench_$w.err; exit 1; }
+  ST=20; [ $w = normal ] && ST=20000
+  timeout -k 10 400 python bench.py --workload $w --steps $ST > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err || { tail $O/${TAG}_bench_$w.err; exit 1; }
   python -c "import json;d=json.load(open('$O/${TAG}_bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 done
 [ "${PROF:-1}" = 1 ] || exit 0
