@@ -231,7 +231,7 @@ class GLM(Workload):
         avg = ms / max(n, 1)
         ach = byts / (avg * 1e-3) / 1e9 if avg > 0 else None
         traffic, src = pmc_traffic("glm")
-        return {"bound": "hbm", "kernel": "k_glm_fused (one pass over x)", "achieved": ach,
+        return {"bound": "hbm", "kernel": "k_glm_reg (one pass over x)", "achieved": ach,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS if ach else None,
                 "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
                 "bytes_per_launch": byts, "avg_launch_ms": avg,

@@ -25,12 +25,25 @@
 //               : sign exp(-ytheta) / (exp(-ytheta) + 1)         (:115-121)
 //   d/dbeta = x^T theta',  d/dalpha = sum theta'                  (:123, :133)
 // The reference makes two GEMV passes over x (HBM-bound).  Here persistent
-// workgroups stream 32-row tiles of x (column-major) through LDS once: the
-// tile yields eta for its rows, then theta', then its contribution to x^T
-// theta' while it is still on chip.  Each workgroup keeps per-column
-// accumulators in registers and writes one [logp, alpha', beta'(M)] partial;
-// a fixed-order second pass sums the partials (deterministic).
+// workgroups stream 32-row tiles of x (column-major) once: the tile yields
+// eta for its rows, then theta', then its contribution to x^T theta' while it
+// is still on chip.  Each workgroup keeps per-column accumulators in
+// registers and writes one [logp, alpha', beta'(M)] partial; a fixed-order
+// second pass sums the partials (deterministic).  The default kernel is
+// k_glm_reg (the tile stays in registers); k_glm_fused (the tile staged
+// through LDS) is kept behind SMG_GLM_REG=0 for A/B runs.
+//
+// Measured at 1e7 x 256 on MI355X (bench.py --workload glm, same box):
+//   k_glm_fused 32 rows x 256 threads, 512 WGs   5.08 TB/s
+//   k_glm_reg   32 rows x 512 threads            5.67-5.74 TB/s (256 or 512 WGs)
+//   k_glm_reg   16 rows x 256 threads            4.75 TB/s (128-byte column segments)
+//   k_glm_reg   16 rows x 512 threads            4.04 TB/s
+//   k_glm_reg   32 x 512 with two tiles in flight (3 register buffers): no gain
+// The first k_glm_reg build ran at 1.7 TB/s: a branch or a select next to a
+// load, a loop-carried register copy and a y load issued after x each made
+// the compiler wait for the loads within the tile that issued them.
 #include <cmath>
+#include <cstdlib>
 
 #include "smg_internal.h"
 
@@ -156,6 +169,145 @@ __global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
   if (t < M) p[2 + t] = gacc;
 }
 
+// Register-resident variant: the tile never goes through LDS.  512 threads:
+// thread t holds row r = t & 31 of the tile and the 16 columns c = g + 16q
+// (g = t >> 5, q = 0..15): eta_r is 16 FMAs per thread plus one 16-way sum through a small
+// LDS array (double-buffered: one barrier per tile), every thread forms
+// theta'_r for its own row, and x^T theta' accumulates in 16 registers per
+// thread (summed over the 32 rows of a column group once, at the end, by
+// lane shuffles).  A load instruction still covers two 256-byte column
+// segments per wave.
+template <int KIND, int RB, int NT>
+__global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, const double* __restrict__ x,
+                                                long long R, int M, long long ldx, const double* __restrict__ ab,
+                                                double* __restrict__ part) {
+  constexpr int G = NT / RB, Q = MMAX / G;
+  const int* __restrict__ y = static_cast<const int*>(yv);
+  const double* __restrict__ yd = static_cast<const double*>(yv);
+  __shared__ double beta[MMAX];
+  __shared__ double red[2][G][RB];
+  __shared__ double lds[16];
+  const int t = threadIdx.x, r = t % RB, g = t / RB;
+  for (int c = t; c < MMAX; c += NT) beta[c] = c < M ? ab[1 + c] : 0.0;
+  const double alpha = ab[0];
+  const double inv_sigma = KIND == 1 ? 1.0 / ab[1 + M] : 0.0;
+  const long long ntiles = (R + RB - 1) / RB;
+  double gacc[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) gacc[q] = 0.0;
+  double lp_acc = 0.0, ga_acc = 0.0, c_acc = 0.0;
+  double xc[Q], xn[Q];
+  double yc = 0.0, yn = 0.0;  // the row's y (as double), loaded one tile ahead with x
+  // Loads are straight-line code: addresses are clamped into x and the
+  // values masked where they are consumed (a branch or a select next to a
+  // load makes the compiler wait for it there), and y is issued before x so
+  // that waiting for it leaves the x loads in flight (vmcnt counts in order).
+  auto load = [&](double (&v)[Q], double& yv_, long long tile) {
+    const long long gr = tile * RB + r;
+    const size_t rc = (size_t)(gr < R ? gr : R - 1);
+    yv_ = KIND == 1 ? yd[rc] : (double)y[rc];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int c = g + G * q;
+      const int cc = c < M ? c : M - 1;
+      v[q] = x[rc + (size_t)cc * ldx];
+    }
+  };
+  // one tile's work on the registers cur / cy (the other buffer's loads
+  // stay in flight meanwhile); ping-pong buffers instead of a copy, which
+  // would wait for the loads
+  auto work = [&](double (&cur)[Q], double cy, long long tile, int buf) {
+    const long long gr = tile * RB + r;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cur[q] = (gr < R && g + G * q < M) ? cur[q] : 0.0;
+    double e = 0.0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) e += cur[q] * beta[g + G * q];
+    red[buf][g][r] = e;
+    __syncthreads();
+    double th = 0.0;
+    if (gr < R) {
+      double eta = 0.0;
+#pragma unroll
+      for (int k = 0; k < G; ++k) eta += red[buf][k][r];
+      double lp;
+      if (KIND == 0) {
+        const double sgn = 2.0 * cy - 1.0;
+        const double yt = sgn * (eta + alpha);
+        const double ex = exp(-yt);
+        lp = yt > 20.0 ? -ex : (yt < -20.0 ? yt : -log1p(ex));
+        th = yt > 20.0 ? -ex : (yt < -20.0 ? sgn : sgn * ex / (ex + 1));
+      } else if (KIND == 1) {
+        const double ys = (cy - eta - alpha) * inv_sigma;
+        lp = ys * ys;
+        th = ys * inv_sigma;
+      } else {
+        const double yi = cy;
+        const double theta = eta + alpha;
+        const double ex = exp(theta);
+        lp = yi * theta - ex;
+        th = yi - ex;
+      }
+      if (g == 0) {  // one thread per row accumulates the row's terms
+        lp_acc += lp;
+        ga_acc += th;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) gacc[q] += th * cur[q];
+  };
+  __syncthreads();  // beta
+  long long tile = blockIdx.x;
+  const long long gs = gridDim.x;
+  auto clampt = [&](long long tt) { return tt < ntiles ? tt : tile; };
+  {
+    if (tile < ntiles) load(xc, yc, tile);
+    for (;;) {
+      if (tile >= ntiles) break;
+      load(xn, yn, clampt(tile + gs));
+      work(xc, yc, tile, 0);
+      tile += gs;
+      if (tile >= ntiles) break;
+      load(xc, yc, clampt(tile + gs));
+      work(xn, yn, tile, 1);
+      tile += gs;
+    }
+  }
+  if (KIND == 2)  // sum of lgamma(y + 1) over this workgroup's rows, off the streaming loop
+    for (long long k = t / RB;; k += NT / RB) {
+      const long long tl2 = blockIdx.x + k * gridDim.x;
+      if (tl2 >= ntiles) break;
+      const long long gr = tl2 * RB + r;
+      if (gr < R) c_acc += lgamma((double)y[gr] + 1.0);
+    }
+  // column sums over the RB rows of each column group: RB adjacent lanes
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    for (int off = RB / 2; off > 0; off >>= 1) gacc[q] += __shfl_xor(gacc[q], off, RB);
+  const int W = M + 2 + (KIND == 2);
+  double* p = part + (size_t)blockIdx.x * W;
+  __syncthreads();
+  const double lp = block_sum(lp_acc, lds);
+  __syncthreads();
+  const double ga = block_sum(ga_acc, lds);
+  double cs = 0.0;
+  if (KIND == 2) {
+    __syncthreads();
+    cs = block_sum(c_acc, lds);
+  }
+  if (t == 0) {
+    p[0] = lp;
+    p[1] = ga;
+    if (KIND == 2) p[M + 2] = cs;
+  }
+  if (r == 0)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int c = g + G * q;
+      if (c < M) p[2 + c] = gacc[q];
+    }
+}
+
 // rows per tile (measured on MI355X: 16 rows 4.3 TB/s, 32 rows 5.1, 64 rows 4.0).
 // Also measured and rejected: 16-byte loads (two rows per lane) 4.8 TB/s vs
 // 5.0 for 8-byte loads; contiguous per-workgroup tile ranges 3.9 TB/s (the
@@ -170,6 +322,37 @@ int glm_blocks(long long R) {
   if (nb > ntiles) nb = ntiles;
   if (nb < 1) nb = 1;
   return (int)nb;
+}
+
+// dev A/B switches: SMG_GLM_REG selects the streaming kernel (0: LDS-staged
+// k_glm_fused; 1: k_glm_reg 32 rows x 512 threads; 2: 16 x 256; 3: 16 x 512),
+// SMG_GLM_NB caps the number of workgroups (<= glm_blocks(R), the workspace size)
+inline int glm_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+template <int KIND>
+int glm_launch(hipStream_t st, const void* y, const double* x, long long R, int M, long long ldx,
+               const double* ab, double* ws) {
+  static const int variant = glm_env("SMG_GLM_REG", 1);
+  static const int nb_cap = glm_env("SMG_GLM_NB", 0);
+  int nb = glm_blocks(R);
+  if (nb_cap > 0 && nb_cap < nb) nb = nb_cap;
+  switch (variant) {
+    case 0:
+      hipLaunchKernelGGL((k_glm_fused<GLM_RB, KIND>), dim3(nb), dim3(256), 0, st, y, x, R, M, ldx, ab, ws);
+      break;
+    case 2:
+      hipLaunchKernelGGL((k_glm_reg<KIND, 16, 256>), dim3(nb), dim3(256), 0, st, y, x, R, M, ldx, ab, ws);
+      break;
+    case 3:
+      hipLaunchKernelGGL((k_glm_reg<KIND, 16, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
+      break;
+    default:
+      hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
+  }
+  return nb;
 }
 
 // ------------------------------------------------ categorical_logit_glm_lpmf
@@ -357,9 +540,7 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x, long lo
   if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_GLM);
   if (M <= MMAX) {
-    const int nb = glm_blocks(R);
-    hipLaunchKernelGGL((k_glm_fused<GLM_RB, 0>), dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx,
-                       ab, ws);
+    const int nb = glm_launch<0>(ctx->stream, y, x, R, M, ldx, ab, ws);
     smg_reduce_partials(ctx, ws, nb, M + 2, out, 0);
     SMG_LAUNCH_CHECK();
     return SMG_OK;
@@ -425,9 +606,7 @@ int smg_normal_id_glm(smg_ctx* ctx, const double* y, const double* x, long long 
   if (!ctx || R < 0 || M < 0 || M > MMAX || !abs || !ws || !out) return SMG_ERR_ARG;
   if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_GLM);
-  const int nb = glm_blocks(R);
-  hipLaunchKernelGGL((k_glm_fused<GLM_RB, 1>), dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx,
-                     abs, ws);
+  const int nb = glm_launch<1>(ctx->stream, y, x, R, M, ldx, abs, ws);
   smg_reduce_partials(ctx, ws, nb, M + 2, out, 0);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
@@ -438,9 +617,7 @@ int smg_poisson_log_glm(smg_ctx* ctx, const int* y, const double* x, long long R
   if (!ctx || R < 0 || M < 0 || M > MMAX || !ab || !ws || !out) return SMG_ERR_ARG;
   if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_GLM);
-  const int nb = glm_blocks(R);
-  hipLaunchKernelGGL((k_glm_fused<GLM_RB, 2>), dim3(nb), dim3(256), 0, ctx->stream, y, x, R, M, ldx,
-                     ab, ws);
+  const int nb = glm_launch<2>(ctx->stream, y, x, R, M, ldx, ab, ws);
   smg_reduce_partials(ctx, ws, nb, M + 3, out, 0);
   SMG_LAUNCH_CHECK();
   return SMG_OK;

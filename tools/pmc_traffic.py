@@ -36,7 +36,7 @@ rf = calib_bytes / (mean(f["k_read8"]) * 1024.0)   # true bytes per reported byt
 rw = calib_bytes / (mean(w["k_write8"]) * 1024.0)
 res = {"calibration": {"kernel": "tools/calib_fetch.hip (8 B/lane, 1 GiB)", "fetch_scale": rf,
                        "write_scale": rw}}
-for wl, kern in (("glm", "k_glm_fused"), ("gp", "k_gemm")):
+for wl, kern in (("glm", "k_glm_reg"), ("gp", "k_gemm")):
     fk, wk = per_kernel(f"{wl}_fetch"), per_kernel(f"{wl}_write")
     fv = [v for k, vs in fk.items() if k.startswith(kern) for v in vs]
     wv = [v for k, vs in wk.items() if k.startswith(kern) for v in vs]
