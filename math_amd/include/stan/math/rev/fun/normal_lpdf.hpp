@@ -190,28 +190,47 @@ inline typename ops_return<T_y, T_loc, T_scale>::type normal_lpdf_host(const T_y
                                                                        int include) {
   static const char* fn = "normal_lpdf";
   constexpr bool vy = op_is_var<T_y>::value, vmu = op_is_var<T_loc>::value, vs = op_is_var<T_scale>::value;
-  {
-    // one scan per operand (no copy); the message is built from a copy of the
-    // values only when an element fails
-    auto check = [&](int kind, const auto& x, const fused_operand& o) {
-      bool bad = false;
-      for (size_t i = 0; i < o.n; ++i) {
-        const double v = host_val(x, i);
-        bad |= kind == 0 ? std::isnan(v) : (kind == 1 ? !(std::fabs(v) <= 1.7976931348623157e308) : !(v > 0.0));
-      }
-      if (!bad) return;
-      std::vector<double> v(o.n);
-      for (size_t i = 0; i < o.n; ++i) v[i] = host_val(x, i);
-      normal_throw_first(fn, kind, v.data(), o.n, o.vec);
-    };
+  // the reference's checks in its order (not NaN y, finite mu, positive
+  // sigma, then consistent sizes); the message is built from a copy of the
+  // values only when an element fails
+  auto check = [&](int kind, const auto& x, const fused_operand& o) {
+    bool bad = false;
+    for (size_t i = 0; i < o.n; ++i) {
+      const double v = host_val(x, i);
+      bad |= kind == 0 ? std::isnan(v) : (kind == 1 ? !(std::fabs(v) <= 1.7976931348623157e308) : !(v > 0.0));
+    }
+    if (!bad) return;
+    std::vector<double> v(o.n);
+    for (size_t i = 0; i < o.n; ++i) v[i] = host_val(x, i);
+    normal_throw_first(fn, kind, v.data(), o.n, o.vec);
+  };
+  auto check_all = [&] {
     check(0, y, ops[0]);
     check(1, mu, ops[1]);
     check(2, sigma, ops[2]);
+  };
+  bool sizes_ok = true;
+  for (int i = 0; i < 3; ++i)
+    if (ops[i].vec && ops[i].n != N) sizes_ok = false;
+  if (!sizes_ok) {  // no element loop over ragged operands: the checks, then the sizes error
+    check_all();
+    normal_check_sizes(fn, ops);
   }
-  normal_check_sizes(fn, ops);
+  // scalar operands are checked now; the vector operands' checks ride along
+  // in the element loop below (one pass over the values instead of two), and
+  // a failure re-runs the ordered checks before anything reaches the tape
+  for (int i = 0; i < 3; ++i)
+    if (!ops[i].vec) {
+      if (i == 0) check(0, y, ops[0]);
+      if (i == 1) check(1, mu, ops[1]);
+      if (i == 2) check(2, sigma, ops[2]);
+    }
   using ret_t = typename ops_return<T_y, T_loc, T_scale>::type;
   if constexpr (!(vy || vmu || vs)) {
-    if (propto) return ret_t(0.0);
+    if (propto) {
+      check_all();
+      return ret_t(0.0);
+    }
   }
   operands_and_partials<T_y, T_loc, T_scale> ops_partials(y, mu, sigma);
   const double neg_log_sqrt_two_pi = -0.91893853320467274178;
@@ -225,17 +244,24 @@ inline typename ops_return<T_y, T_loc, T_scale>::type normal_lpdf_host(const T_y
   // in a different order (round-off only)
   double q[4] = {0.0, 0.0, 0.0, 0.0};
   double sum_log_s = 0.0;
+  bool bad = false;
+  const bool yvec = ops[0].vec, mvec = ops[1].vec;
   for (size_t n = 0; n < N; ++n) {
-    const double inv_s = svec ? 1.0 / host_val(sigma, n) : inv_s0;
-    const double z = (host_val(y, n) - host_val(mu, n)) * inv_s;
+    const double yv = host_val(y, n), mv = host_val(mu, n), sv = host_val(sigma, n);
+    if (yvec) bad |= std::isnan(yv);
+    if (mvec) bad |= !(std::fabs(mv) <= 1.7976931348623157e308);
+    if (svec) bad |= !(sv > 0.0);
+    const double inv_s = svec ? 1.0 / sv : inv_s0;
+    const double z = (yv - mv) * inv_s;
     const double z2 = z * z;
     q[n & 3] += z2;
-    if (svec && (include & 2)) sum_log_s += std::log(host_val(sigma, n));
+    if (svec && (include & 2)) sum_log_s += std::log(sv);
     const double sc = inv_s * z;
     if constexpr (vy) ops_partials.edge1_.partials_[int(n)] -= sc;
     if constexpr (vmu) ops_partials.edge2_.partials_[int(n)] += sc;
     if constexpr (vs) ops_partials.edge3_.partials_[int(n)] += -inv_s + inv_s * z2;
   }
+  if (bad) check_all();  // throws the reference's first failure
   double logp = 0.0;
   if (include & 1) logp += neg_log_sqrt_two_pi * double(N);
   if (include & 2) logp -= svec ? sum_log_s : log_s0 * double(N);

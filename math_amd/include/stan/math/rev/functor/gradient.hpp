@@ -33,8 +33,11 @@ void gradient(const F& f, const Vec& x, double& fx, Vec& grad_fx) {
   using VarVec = typename internal::var_vector_of<Vec>::type;
   start_nested();
   try {
+    // the independent variables are leaves (their chain() is a no-op): they
+    // go on the no-chain stack, so the reverse sweep makes no call for them;
+    // set_zero_all_adjoints and the nested recovery cover both stacks
     VarVec x_var(x.size());
-    for (size_t i = 0; i < size_t(x.size()); ++i) x_var[i] = x[i];
+    for (size_t i = 0; i < size_t(x.size()); ++i) x_var[i] = var(new vari(x[i], false));
     var fx_var = f(x_var);
     fx = fx_var.val();
     grad(fx_var.vi_);
