@@ -20,6 +20,13 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef SMG_GEMM_NR64
+#define SMG_GEMM_NR64 2
+#endif
+#ifndef SMG_GEMM_NR32
+#define SMG_GEMM_NR32 2
+#endif
+
 namespace {
 
 // LDS images of the operand tiles, unpadded and XOR-swizzled so that both
@@ -68,14 +75,14 @@ __device__ double g_gemm_zero[2] = {0.0, 0.0};  // global (not constant) address
 // to its LDS store.  (A select on the loaded value lets the scheduler hoist
 // the select -- and with it a wait for that load -- ahead of the previous
 // stage's MFMAs, which serialises the prefetch.)
-template <int BM, int BK, bool KCONTIG>
+template <int BM, int BK, bool KCONTIG, int NT = 256>
 __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
                                           int rows, int k, int i0, int k0,
-                                          double (&r)[BM * BK / 256]) {
-  constexpr int PER = BM * BK / 256;
+                                          double (&r)[BM * BK / NT]) {
+  constexpr int PER = BM * BK / NT;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int e = threadIdx.x + 256 * q;
+    const int e = threadIdx.x + NT * q;
     int i, kk;
     if (KCONTIG) {
       i = e / BK;
@@ -90,12 +97,12 @@ __device__ __forceinline__ void load_tile(const double* __restrict__ X, int ld,
   }
 }
 
-template <int BM, int BK, bool KCONTIG>
-__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / 256]) {
-  constexpr int PER = BM * BK / 256;
+template <int BM, int BK, bool KCONTIG, int NT = 256>
+__device__ __forceinline__ void store_tile(double* lds, const double (&r)[BM * BK / NT]) {
+  constexpr int PER = BM * BK / NT;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int e = threadIdx.x + 256 * q;
+    const int e = threadIdx.x + NT * q;
     int i, kk;
     if (KCONTIG) {
       i = e / BK;
@@ -118,8 +125,12 @@ __device__ __forceinline__ void tri_decode(int t, int& bi, int& bj) {
 }
 
 // MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n)
-template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
-__global__ __launch_bounds__(256) void k_gemm(
+// KS: waves per output sub-tile (KS = 2: 8 waves, the two 4-wave groups take
+// alternate halves of every K stage and their accumulators are summed in the
+// epilogue -- twice the waves per CU for grids that cover the CUs only once
+// or twice)
+template <int BM, int BN, int BK, bool TA, bool TB, int MODE, int KS = 1>
+__global__ __launch_bounds__(256 * KS) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
     int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab, long long sA,
@@ -138,7 +149,7 @@ __global__ __launch_bounds__(256) void k_gemm(
   // the C tile (column chunks of ECH columns, stride BM + 1) so that C is read
   // and written in whole column segments (coalesced 8*BM-byte runs)
   // operand tiles are double-buffered in LDS (one barrier per K stage)
-  constexpr int NR = BM == 128 ? 1 : 2;
+  constexpr int NR = BM == 128 ? 1 : (BM == 64 ? SMG_GEMM_NR64 : SMG_GEMM_NR32);
   constexpr int STAGE = LA::size + LB::size;
   constexpr int OPS = 2 * STAGE;
   constexpr int ECH = (BM * BN + BN <= OPS) ? BN : 32;
@@ -200,8 +211,9 @@ __global__ __launch_bounds__(256) void k_gemm(
   }
 
   constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int NT = 256 * KS;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = (wave & 3) >> 1, wc = wave & 1, kg = wave >> 2;
   d4 acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
@@ -212,16 +224,16 @@ __global__ __launch_bounds__(256) void k_gemm(
   // that the load of stage s + NR is in flight while stages s .. s + NR - 1
   // are consumed (NR = 2 for the small tiles, whose grids leave only two or
   // three waves per SIMD to hide the load latency behind)
-  constexpr int PA = BM * BK / 256, PB = BN * BK / 256;
+  constexpr int PA = BM * BK / NT, PB = BN * BK / NT;
   double ra[NR][PA], rb[NR][PB];
   const int nst = (kend - kbeg + BK - 1) / BK;  // K stages of this split
   auto gload = [&](int set, int st) {
-    load_tile<BM, BK, AK>(A, lda, m, kend, i0, kbeg + st * BK, ra[set]);
-    load_tile<BN, BK, BKC>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set]);
+    load_tile<BM, BK, AK, NT>(A, lda, m, kend, i0, kbeg + st * BK, ra[set]);
+    load_tile<BN, BK, BKC, NT>(B, ldb, n, kend, j0, kbeg + st * BK, rb[set]);
   };
   auto lstore = [&](int set, int buf) {
-    store_tile<BM, BK, AK>(pool + buf * STAGE, ra[set]);
-    store_tile<BN, BK, BKC>(pool + buf * STAGE + LA::size, rb[set]);
+    store_tile<BM, BK, AK, NT>(pool + buf * STAGE, ra[set]);
+    store_tile<BN, BK, BKC, NT>(pool + buf * STAGE + LA::size, rb[set]);
   };
   // every stage load is unconditional (addresses are clamped in range and
   // stages past the end are masked to zero): a conditional load would make
@@ -232,22 +244,24 @@ __global__ __launch_bounds__(256) void k_gemm(
   // epilogue operand in flight during the K loop (small tiles only: the
   // 128 x 128 tile would double its register count); coalesced mapping
   // e = tid + 256 q -> (i = e % BM, j = e / BM), the same as the store
-  constexpr int EPT = BM * BN / 256;
+  constexpr int EPT = BM * BN / NT;
   constexpr bool PREFETCH_C = EPT <= 16;
   const bool use_c = !slab && beta != 0.0;
   double cpre[PREFETCH_C ? EPT : 1];
   if (PREFETCH_C) {
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
-      const int e = threadIdx.x + 256 * q;
+      const int e = threadIdx.x + NT * q;
       const int i = i0 + e % BM, j = j0 + e / BM;
       cpre[q] = (use_c && i < m && j < n) ? C[i + (size_t)j * ldc] : 0.0;
     }
   }
   const int fr = lane & 15, fk = lane >> 4;
+  static_assert(BK / 4 % KS == 0, "K stage split");
   auto mma_stage = [&](const double* Ab, const double* Bb) {
 #pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
+    for (int kq = 0; kq < BK / 4 / KS; ++kq) {
+      const int ks = kg * (BK / 4 / KS) + kq;
       double af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
@@ -297,20 +311,28 @@ __global__ __launch_bounds__(256) void k_gemm(
   __syncthreads();  // operand tiles no longer needed
 #pragma unroll
   for (int c0 = 0; c0 < BN; c0 += ECH) {
+    // k-group 0 stores its accumulators, the other groups add theirs in turn
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+    for (int g = 0; g < KS; ++g) {
+      if (kg == g) {
 #pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int jl = wc * (BN / 2) + b * 16 + (lane & 15) - c0;
-        if (jl < 0 || jl >= ECH) continue;
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          pool[jl * (BM + 1) + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r] = acc[a][b][r];
+          for (int b = 0; b < TN; ++b) {
+            const int jl = wc * (BN / 2) + b * 16 + (lane & 15) - c0;
+            if (jl < 0 || jl >= ECH) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              double* d = &pool[jl * (BM + 1) + wr * (BM / 2) + a * 16 + (lane >> 4) + 4 * r];
+              *d = g == 0 ? acc[a][b][r] : *d + acc[a][b][r];
+            }
+          }
       }
-    __syncthreads();
+      __syncthreads();
+    }
 #pragma unroll
-    for (int q = 0; q < BM * ECH / 256; ++q) {
-      const int e = threadIdx.x + 256 * q;
+    for (int q = 0; q < BM * ECH / NT; ++q) {
+      const int e = threadIdx.x + NT * q;
       const int il = e % BM, jl = e / BM;
       const int i = i0 + il, j = j0 + c0 + jl;
       if (i >= m || j >= n) continue;
@@ -323,7 +345,7 @@ __global__ __launch_bounds__(256) void k_gemm(
         C[i + (size_t)j * ldc] = alpha * v;
       } else {
         double cv;
-        if (PREFETCH_C) cv = cpre[(c0 / ECH) * (BM * ECH / 256) + q];
+        if (PREFETCH_C) cv = cpre[(c0 / ECH) * (BM * ECH / NT) + q];
         else cv = C[i + (size_t)j * ldc];
         C[i + (size_t)j * ldc] = alpha * v + beta * cv;
       }
@@ -346,7 +368,7 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
   *c = (beta == 0.0) ? alpha * s : alpha * s + beta * *c;
 }
 
-template <int BM, int BN, int BK, bool TA, bool TB, int MODE>
+template <int BM, int BN, int BK, bool TA, bool TB, int MODE, int KS = 1>
 int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
            int lda, const double* B, int ldb, double beta, double* C, int ldc, int batch = 1,
            long long sA = 0, long long sB = 0, long long sC = 0, int tri = 0) {
@@ -396,7 +418,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
       }
     }
   }
-  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE>), dim3(ntp * splits, batch), dim3(256), 0,
+  hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE, KS>), dim3(ntp * splits, batch), dim3(256 * KS), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
                      ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri);
   if (splits > 1) {
@@ -475,6 +497,10 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
       return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (forced == 32)
       return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+    if (forced == 6402)
+      return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+    if (forced == 3202)
+      return launch<32, 32, 32, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   }
   // (triangle modes keep 64 x 64 tiles: half the 128-tile grid would sit on
   // the diagonal, and the split-K those few tiles need costs a reduction; at
@@ -488,11 +514,29 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   // (512,1024,3072) 68 vs 81 us with 32 x 32)
   if (MODE == 0 && TA && !TB && k >= 1536 && mid_tiles < 512)
     return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-  // 64 x 64 only when its grid fills two workgroups per CU without split-K:
-  // below that, 32 x 32 tiles (4x the workgroups) beat a split 64 x 64 grid
-  // (tools/ubench_gemm: (3584,256,256) 18.6 vs 28 us)
-  if (mid_tiles >= 512)
+  // 64 x 64 tiles from 256 tiles on (one per CU), with 8 waves (KS = 2: the
+  // two wave groups split every K stage) up to ~6 tiles per CU; 32 x 32
+  // below that (4x the workgroups), and for the tall NN products with
+  // n <= 512 (C_adj D^{-1}, B_adj -= C_adj R at small J), where the
+  // 4-wave 32 x 32 grid measured fastest.  tools/ubench_gemm at N = 4096
+  // (us, 32x32 / 64x64 / 64x64 KS=2):
+  //   (3584,512,512) NT lower 57.6 / 54.6 / 51.4   (512,3584,512) NN 49.6 / 51.8 / 47.3
+  //   (2048,1536,512) NN 80.5 (64x64) / 70.6       (3072,512,512) NN 45.1 / 52.5 / 48.4
+  //   (512,512,512) 11.5 (32x32) / 10.2 (32x32 KS=2)
+  // (and a 64 x 64 grid below 256 tiles, split over K or not, loses to 32 x 32:
+  // (3584,256,256) 18.6 vs 28 us)
+  if (mid_tiles >= 512) {
+    if (mid_tiles <= 1536)
+      return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+  }
+  const bool tall_nn = MODE == 0 && !TA && !TB && n <= 512;
+  if (mid_tiles >= 256 && !tall_nn)
+    return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+  const long long t32 = smg_ceil_div(m, 32);
+  const long long small_tiles = (MODE != 0 && m == n) ? t32 * (t32 + 1) / 2 : t32 * smg_ceil_div(n, 32);
+  if (small_tiles <= 256)
+    return launch<32, 32, 32, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
 }
 
