@@ -213,7 +213,9 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int NT = 256 * KS;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wr = (wave & 3) >> 1, wc = wave & 1, kg = wave >> 2;
+  // (kg a compile-time 0 for KS == 1: the fragment reads' LDS offsets fold
+  // into immediates; a run-time kg cost the 128 x 128 tile 15 %)
+  const int wr = (wave & 3) >> 1, wc = wave & 1, kg = KS == 1 ? 0 : wave >> 2;
   d4 acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
