@@ -187,6 +187,17 @@ int smg_cholesky_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L,
  * smg_check_symmetric followed by smg_cholesky_fwd. */
 int smg_cholesky_fwd_checked(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                              double* Dinv);
+/* smg_cholesky_fwd_checked with a status mark after the last launch that can
+ * latch the status (before the block inverses): smg_status_mark_wait then
+ * returns the symmetric / not-PD bits (and resets them) without waiting for
+ * the rest of the entry, so the host enqueues the next node's work while the
+ * device finishes it.  Same throw points as the reference
+ * (rev/mat/fun/cholesky_decompose.hpp:380-406: the check fails the call). */
+int smg_cholesky_fwd_checked_mark(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                  double* Dinv);
+/* Wait for the latest status mark and read (and reset) the status it copied;
+ * with no mark pending this is smg_status. */
+int smg_status_mark_wait(smg_ctx* ctx, int* status);
 int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux,
                      double* Ladj, int ldla, int n, double* Aadj, int ldaa);
 
@@ -250,6 +261,10 @@ int smg_log_determinant_rev(smg_ctx* ctx, const double* LU, const int* piv,
  *     eta_i + alpha (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:117-123).
  *     rev: eta_adj += adj d'(theta) (etad + alphad), etad_adj += adj d;
  *     out[0], out[1] = their sums (alpha's and alphad's adjoints). */
+/* Y(i >= j) = X(i >= j) (m x n); Y's strict upper triangle is left alone.
+ * The work copy of L's adjoint that smg_cholesky_rev overwrites (it reads the
+ * lower triangle only): half of a full copy's traffic. */
+int smg_copy_tril(smg_ctx* ctx, int m, int n, const double* X, int ldx, double* Y, int ldy);
 int smg_add_tril(smg_ctx* ctx, int m, int n, double alpha, const double* X,
                  int ldx, double* Y, int ldy);
 int smg_lse_tangent_fwd(smg_ctx* ctx, const double* x, const double* xd,

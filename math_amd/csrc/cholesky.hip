@@ -663,7 +663,7 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
 }
 
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym);
+             bool check_sym, bool mark = false);
 
 }  // namespace
 
@@ -702,12 +702,17 @@ int smg_cholesky_fwd_checked(smg_ctx* ctx, const double* A, int lda, int n, doub
   return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true);
 }
 
+int smg_cholesky_fwd_checked_mark(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                  double* Dinv) {
+  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true);
+}
+
 }  // extern "C"
 
 namespace {
 
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym) {
+             bool check_sym, bool mark) {
   if (!ctx || n < 0 || (n > 0 && (!A || !L || lda < n || ldl < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_FWD);
@@ -795,6 +800,13 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if (!F) return SMG_ERR_HIP;
       SMG_HIP_TRY(hipEventRecord(F, ctx->side));
     }
+  }
+  // every launch that can latch the status (the symmetric check, the panels'
+  // not-PD and hand-off bits) is enqueued: the status mark goes here, so a
+  // host waiting on it does not also wait for the block inverses below
+  if (mark) {
+    const int rc = smg_status_mark_impl(ctx);
+    if (rc) return rc;
   }
   if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
   // the 128- and 256-block inverses (reverse pass, triangular solves)

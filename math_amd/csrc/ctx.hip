@@ -138,6 +138,8 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   }
   ctx->prof_on = 0;
   ctx->comm = nullptr;
+  ctx->status_ev = nullptr;
+  ctx->status_mark = 0;
   ctx->side = nullptr;
   ctx->main_stream = nullptr;
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
@@ -192,6 +194,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   for (auto& b : ctx->blocks) hipFree(b.base);
   for (auto e : ctx->prof_pool) hipEventDestroy(e);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  if (ctx->status_ev) hipEventDestroy(ctx->status_ev);
   if (ctx->side) {
     hipStreamSynchronize(ctx->side);
     hipStreamDestroy(ctx->side);
@@ -363,6 +366,37 @@ int smg_status(smg_ctx* ctx, int* status) {
   int s = ctx->status_h[0] | ctx->host_status;
   ctx->host_status = 0;
   ctx->status_armed = 0;
+  if (status) *status = s;
+  return SMG_OK;
+}
+
+}  // extern "C"
+
+int smg_status_mark_impl(smg_ctx* ctx) {
+  if (!ctx->status_ev && hipEventCreateWithFlags(&ctx->status_ev, hipEventDisableTiming) != hipSuccess) {
+    ctx->status_ev = nullptr;
+    return SMG_ERR_HIP;
+  }
+  SMG_HIP_TRY(hipMemcpyAsync(ctx->status_h + 1, ctx->status_d, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  SMG_HIP_TRY(hipMemsetAsync(ctx->status_d, 0, sizeof(int), ctx->stream));
+  SMG_HIP_TRY(hipEventRecord(ctx->status_ev, ctx->stream));
+  ctx->status_mark = 1;
+  return SMG_OK;
+}
+
+extern "C" {
+
+int smg_status_mark_wait(smg_ctx* ctx, int* status) {
+  if (!ctx) return SMG_ERR_ARG;
+  if (!ctx->status_mark || ctx->prof_on) {  // no mark (or profiling): the whole-stream status read
+    ctx->status_mark = 0;
+    return smg_status(ctx, status);
+  }
+  SMG_HIP_TRY(hipEventSynchronize(ctx->status_ev));
+  int s = ctx->status_h[1] | ctx->host_status;
+  ctx->host_status = 0;
+  ctx->status_mark = 0;
+  ctx->status_armed = 0;  // the launches that could latch it ran before the mark
   if (status) *status = s;
   return SMG_OK;
 }

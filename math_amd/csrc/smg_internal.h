@@ -44,6 +44,11 @@ struct smg_ctx {
   // and panels: SMG_ERR_SYNC on a timed-out hand-off) is enqueued; cleared
   // when the status is read (smg_status / smg_status_enqueue)
   int status_armed;
+  // status mark (smg_cholesky_fwd_checked_mark / smg_status_mark_wait): the
+  // status word copied into status_h[1] and reset at a point inside an entry,
+  // with an event the host waits on instead of the whole stream
+  hipEvent_t status_ev;
+  int status_mark;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;
@@ -135,6 +140,7 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
                   int ldw, double* B, int ldb, int m, int n, double* X = nullptr, int ldx = 0);
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
+int smg_status_mark_impl(smg_ctx* ctx);
 int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);
 int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux, int n);
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,

@@ -1,6 +1,8 @@
 // Tangent (fvar<var>) pieces for the fwd-over-rev functors of
 // include/stan/math/mix/fvar_functors.hpp:
 //
+//   copy_tril           Y(lower) = X(lower) (the Murray reverse's work copy of
+//                       a Cholesky factor's adjoint: its strict upper is never read)
 //   add_tril            Y(lower) += alpha X(lower): tril() of a tangent
 //                       (fwd/mat/fun/mdivide_left_tri_low.hpp:28-33 reads only
 //                       A's lower triangle)
@@ -61,6 +63,11 @@ __global__ void k_add_tril(int m, int n, double alpha, const double* __restrict_
                            int ldy) {
   for (smg_mn it(m, n); it.ok(); it.next())
     if (it.i >= it.j) Y[it.i + (size_t)it.j * ldy] += alpha * X[it.i + (size_t)it.j * ldx];
+}
+
+__global__ void k_copy_tril(int m, int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy) {
+  for (smg_mn it(m, n); it.ok(); it.next())
+    if (it.i >= it.j) Y[it.i + (size_t)it.j * ldy] = X[it.i + (size_t)it.j * ldx];
 }
 
 // out = [lse(x), sum_i exp(x_i - lse) x'_i]
@@ -176,6 +183,16 @@ int smg_add_tril(smg_ctx* ctx, int m, int n, double alpha, const double* X, int 
   if (m == 0 || n == 0) return SMG_OK;
   if (!X || !Y || ldx < m || ldy < m) return SMG_ERR_ARG;
   hipLaunchKernelGGL(k_add_tril, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n, alpha, X, ldx, Y,
+                     ldy);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_copy_tril(smg_ctx* ctx, int m, int n, const double* X, int ldx, double* Y, int ldy) {
+  if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
+  if (m == 0 || n == 0) return SMG_OK;
+  if (!X || !Y || ldx < m || ldy < m) return SMG_ERR_ARG;
+  hipLaunchKernelGGL(k_copy_tril, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n, X, ldx, Y,
                      ldy);
   SMG_LAUNCH_CHECK();
   return SMG_OK;

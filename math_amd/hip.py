@@ -60,6 +60,8 @@ _SIGS = {
     "smg_check_symmetric": (_I, [_P, _P, _I, _I]),
     "smg_cholesky_fwd": (_I, [_P, _P, _I, _I, _P, _I, _P]),
     "smg_cholesky_fwd_checked": (_I, [_P, _P, _I, _I, _P, _I, _P]),
+    "smg_cholesky_fwd_checked_mark": (_I, [_P, _P, _I, _I, _P, _I, _P]),
+    "smg_status_mark_wait": (_I, [_P, _P]),
     "smg_cholesky_rev": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_fwd": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_rev": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
@@ -90,6 +92,7 @@ _SIGS = {
     "smg_log_determinant_spd_rev": (_I, [_P, _P, _P, _I, _D, _P, _I, _P]),
     "smg_log_determinant_fwd": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "smg_add_tril": (_I, [_P, _I, _I, _D, _P, _I, _P, _I]),
+    "smg_copy_tril": (_I, [_P, _I, _I, _P, _I, _P, _I]),
     "smg_lse_tangent_fwd": (_I, [_P, _P, _P, _L, _P]),
     "smg_lse_tangent_rev": (_I, [_P, _P, _P, _L, _D, _D, _D, _P, _P]),
     "smg_glm_tangent_fwd": (_I, [_P, _P, _D, _P, _D, _P, _L, _P]),

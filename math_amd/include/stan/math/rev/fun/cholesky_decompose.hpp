@@ -61,8 +61,9 @@ class cholesky_dev_vari : public vari {
   void chain() override {
     smg_ctx* c = amd::ctx();
     const size_t nn = size_t(n_) * n_;
-    double* work = amd::alloc_doubles(nn);  // Murray's algorithm overwrites its input
-    amd::check(smg_memcpy_d2d(c, work, L_->adj_, nn * sizeof(double)), "cholesky_decompose");
+    // Murray's algorithm overwrites its input and reads only its lower triangle
+    double* work = amd::alloc_doubles(nn);
+    amd::check(smg_copy_tril(c, n_, n_, L_->adj_, n_, work, n_), "cholesky_decompose");
     amd::check(smg_cholesky_rev(c, L_->val_, n_, L_->aux_, work, n_, n_, A_->adj_, n_),
                "cholesky_decompose");
   }
@@ -106,10 +107,12 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   if (n == 0) return dev_var_matrix(new dev_matrix_vari(0, 0, dev_structure::lower));
   auto* L = new dev_matrix_vari(n, n, dev_structure::lower);
   L->aux_ = amd::alloc_doubles(size_t(smg_cholesky_aux_doubles(n)));
-  // check_symmetric fused with the factorisation's copy of A (one pass)
-  amd::check(smg_cholesky_fwd_checked(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
+  // check_symmetric fused with the factorisation's copy of A (one pass); the
+  // status is read at the mark after the panels, so the block inverses that
+  // follow run while the host builds the next node
+  amd::check(smg_cholesky_fwd_checked_mark(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
   int st = 0;
-  amd::check(smg_status(c, &st), fn);
+  amd::check(smg_status_mark_wait(c, &st), fn);
   if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
   if (st) amd::throw_status(st, fn, "m");
   new internal::cholesky_dev_vari(A.vi_, L);
