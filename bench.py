@@ -282,7 +282,9 @@ class MulChol(Workload):
 
     data = "synthetic (reference harness config-2 input: A = U(-1,1) sqrt(3/N), generated in HBM)"
 
-    eval_flops_expr = "7N^3 (fwd GEMM 2N^3 + rev 2 GEMM 4N^3 + chol N^3), SURVEY.md §8(d)"
+    eval_flops_expr = ("7N^3 (fwd GEMM 2N^3 + rev 2 GEMM 4N^3 + chol N^3), SURVEY.md §8(d): the reference "
+                       "algorithm's work; this build executes 4N^3 (the Gram product A A^T lower-only "
+                       "forward, one reverse GEMM) + chol N^3")
 
     def eval_flops(self):
         return 7.0 * float(self.N) ** 3

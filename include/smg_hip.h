@@ -437,6 +437,10 @@ int smg_sum(smg_ctx* ctx, const double* x, long long n, double* out);
 /* B(i,j) = A(j,i) style copy helpers */
 int smg_copy_matrix(smg_ctx* ctx, int m, int n, const double* A, int lda,
                     double* B, int ldb, int trans, int uplo_zero_upper);
+/* A (n x n, in place): strict upper triangle <- the transpose of the strict
+ * lower one (multiply(A, transpose(A)) forms the lower half of the Gram
+ * product on the GEMM, then mirrors it). */
+int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda);
 /* B (n x m) = A^T + beta B, A m x n (transpose(Matrix<var>): forward copy and
  * the reverse Aadj += Badj^T) */
 int smg_transpose(smg_ctx* ctx, int m, int n, const double* A, int lda,

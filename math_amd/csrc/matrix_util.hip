@@ -1,5 +1,6 @@
 // Small dense helpers behind the host layer's matrix functors:
 //   transpose  (rev/mat/fun/transpose / Eigen .transpose() in multiply(A, A^T))
+//   sym_from_lower (the upper half of a Gram product A A^T computed lower-only)
 //   shift      (sum(Matrix<var>) reverse: every operand adjoint += adj,
 //               rev/mat/fun/sum.hpp:18-60)
 //   dot        (dot_product / the scalar side of multiply(var, Matrix<var>),
@@ -34,6 +35,29 @@ __global__ __launch_bounds__(256) void k_transpose(int m, int n, const double* _
       const double v = t[r][c];
       *d = beta == 0.0 ? v : v + beta * *d;
     }
+  }
+}
+
+// A (n x n, in place): strict upper <- transpose of the strict lower.  Tile
+// (bx, by), bx >= by, of the lower triangle is read through LDS and written
+// to its mirror tile; on a diagonal tile only the strict upper entries are
+// written (every read precedes the barrier)
+__global__ __launch_bounds__(256) void k_sym_from_lower(int n, double* __restrict__ A, int lda) {
+  const int bx = blockIdx.x, by = blockIdx.y;
+  if (bx < by) return;
+  __shared__ double t[TT][TT + 1];
+  const int i0 = bx * TT, j0 = by * TT;
+  const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    const int i = i0 + r, j = j0 + c;
+    t[c][r] = (i < n && j < n) ? A[i + (size_t)j * lda] : 0.0;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    const int bi = j0 + r, bj = i0 + c;  // A(bi, bj) = A(bj, bi), bi < bj
+    if (bi < n && bj < n && bi < bj) A[bi + (size_t)bj * lda] = t[r][c];
   }
 }
 
@@ -133,6 +157,16 @@ int smg_transpose(smg_ctx* ctx, int m, int n, const double* A, int lda, double* 
   if (!A || !B || lda < m || ldb < n) return SMG_ERR_ARG;
   hipLaunchKernelGGL(k_transpose, dim3(smg_ceil_div(m, TT), smg_ceil_div(n, TT)), dim3(256), 0,
                      ctx->stream, m, n, A, lda, B, ldb, beta);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n <= 1) return SMG_OK;
+  if (!A || lda < n) return SMG_ERR_ARG;
+  const int t = smg_ceil_div(n, TT);
+  hipLaunchKernelGGL(k_sym_from_lower, dim3(t, t), dim3(256), 0, ctx->stream, n, A, lda);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -107,6 +107,7 @@ _SIGS = {
     "smg_sum": (_I, [_P, _P, _L, _P]),
     "smg_copy_matrix": (_I, [_P, _I, _I, _P, _I, _P, _I, _I, _I]),
     "smg_transpose": (_I, [_P, _I, _I, _P, _I, _P, _I, _D]),
+    "smg_sym_from_lower": (_I, [_P, _I, _P, _I]),
     "smg_shift": (_I, [_P, _I, _I, _D, _P, _I, _I]),
     "smg_dot": (_I, [_P, _P, _P, _L, _P]),
     "smg_check_domain": (_I, [_P, _P, _L, _I, _P]),

@@ -40,6 +40,9 @@ class dev_matrix_vari {
   double* adj_;  // device, column-major, registered with the tape
   dev_structure structure_;
   double* aux_;  // node-specific device side data (e.g. Cholesky diagonal-block inverses)
+  // set on transpose(A)'s output: multiply(A, transpose(A)) recognises the
+  // Gram product (one lower GEMM forward, one GEMM reverse)
+  dev_matrix_vari* transpose_of_ = nullptr;
 
   dev_matrix_vari(int rows, int cols, dev_structure s = dev_structure::general)
       : rows_(rows),

@@ -57,16 +57,41 @@ class multiply_dev_vari : public vari {
  public:
   dev_operand A_, B_;
   dev_matrix_vari* C_;
+  // B = transpose(A) of the same var node: C = A A^T is formed as its lower
+  // half (one triangular GEMM on A itself) mirrored, and the reverse is ONE
+  // GEMM, Aadj += (Cadj + Cadj^T) A, instead of Aadj += Cadj B^T plus
+  // Badj += A^T Cadj folded back through the transpose node (whose own
+  // reverse then adds this node's share of nothing).  Same derivative as the
+  // reference's two products (rev/mat/fun/multiply.hpp:65-135).
+  bool gram_;
   multiply_dev_vari(const dev_operand& A, const dev_operand& B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A.rows, B.cols)) {
-    amd::check(smg_multiply_fwd(amd::ctx(), A_.val(), A_.rows, B_.val(), B_.rows, A_.rows, A_.cols,
-                                B_.cols, C_->val_, C_->rows_),
+      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A.rows, B.cols)),
+        gram_(A.vi && B.vi && B.vi->transpose_of_ == A.vi) {
+    smg_ctx* c = amd::ctx();
+    if (gram_) {
+      amd::check(smg_gemm(c, 0, 1, 1, A_.rows, A_.rows, A_.cols, 1.0, A_.val(), A_.rows, A_.val(), A_.rows, 0.0,
+                          C_->val_, C_->rows_),
+                 "multiply");
+      amd::check(smg_sym_from_lower(c, C_->rows_, C_->val_, C_->rows_), "multiply");
+      return;
+    }
+    amd::check(smg_multiply_fwd(c, A_.val(), A_.rows, B_.val(), B_.rows, A_.rows, A_.cols, B_.cols, C_->val_,
+                                C_->rows_),
                "multiply");
   }
   void chain() override {
-    amd::check(smg_multiply_rev(amd::ctx(), A_.val(), A_.rows, B_.val(), B_.rows, C_->adj_,
-                                C_->rows_, A_.rows, A_.cols, B_.cols, A_.adj(), A_.rows, B_.adj(),
-                                B_.rows),
+    smg_ctx* c = amd::ctx();
+    if (gram_) {
+      const int m = C_->rows_;
+      double* S = amd::alloc_doubles(size_t(m) * m);  // Cadj + Cadj^T
+      amd::check(smg_memcpy_d2d(c, S, C_->adj_, size_t(m) * m * sizeof(double)), "multiply");
+      amd::check(smg_transpose(c, m, m, C_->adj_, m, S, m, 1.0), "multiply");
+      amd::check(smg_gemm(c, 0, 0, 0, m, A_.cols, m, 1.0, S, m, A_.val(), A_.rows, 1.0, A_.adj(), A_.rows),
+                 "multiply");
+      return;
+    }
+    amd::check(smg_multiply_rev(c, A_.val(), A_.rows, B_.val(), B_.rows, C_->adj_, C_->rows_, A_.rows, A_.cols,
+                                B_.cols, A_.adj(), A_.rows, B_.adj(), B_.rows),
                "multiply");
   }
 };
@@ -104,6 +129,7 @@ class transpose_dev_vari : public vari {
   dev_matrix_vari* B_;
   explicit transpose_dev_vari(dev_matrix_vari* A)
       : vari(0.0), A_(A), B_(new dev_matrix_vari(A->cols_, A->rows_)) {
+    B_->transpose_of_ = A;
     amd::check(smg_transpose(amd::ctx(), A_->rows_, A_->cols_, A_->val_, A_->rows_, B_->val_,
                              B_->rows_, 0.0),
                "transpose");
