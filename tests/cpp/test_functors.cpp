@@ -112,6 +112,31 @@ static void cmd_mulchol() {
   }
 }
 
+// the Gram product multiply(A, transpose(A)) with the transpose ALSO used
+// elsewhere (its adjoint nonzero): f = sum(A A^T) + w sum(transpose(A)) +
+// sum(multiply(transpose(A), A)) over an N x M matrix A (host values)
+static void cmd_gram_shared() {
+  int N, M;
+  double w;
+  std::cin >> N >> M >> w;
+  std::vector<double> a = read_vec(size_t(N) * M);
+  smg_ctx* c = amd::ctx();
+  const size_t nm = size_t(N) * M;
+  double* G = amd::alloc_doubles(nm);
+  dev_data<double> A = to_dev_data(a.data(), nm, N, M);
+  auto f = [w](const dev_var_matrix& x) {
+    dev_var_matrix t = transpose(x);
+    return sum(multiply(x, t)) + w * sum(t) + sum(multiply(t, x));
+  };
+  double fx;
+  gradient(f, A, fx, G);
+  std::vector<double> g(nm);
+  amd::to_host(g.data(), G, nm);
+  (void)c;
+  print1("fx", fx);
+  print("grad", g);
+}
+
 static void cmd_mulchol_eigen() {
   int N;
   std::cin >> N;
@@ -1203,6 +1228,7 @@ int main() {
   try {
     if (cmd == "mulchol") cmd_mulchol();
     else if (cmd == "mulchol_eigen") cmd_mulchol_eigen();
+    else if (cmd == "gram_shared") cmd_gram_shared();
     else if (cmd == "multiply") cmd_multiply();
     else if (cmd == "mdivide") cmd_mdivide();
     else if (cmd == "lse") cmd_lse();
