@@ -77,6 +77,13 @@ int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src_host, size_t bytes);
 int smg_memcpy_d2h(smg_ctx* ctx, void* dst_host, const void* src, size_t bytes);
 int smg_memcpy_d2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes);
 int smg_memset(smg_ctx* ctx, void* dst, int value, size_t bytes);
+/* Zero `bytes` at dst on the context's zeroing stream, after everything
+ * already enqueued on the main stream, overlapping what is enqueued there
+ * next; smg_join_async makes the main stream wait for every such zeroing
+ * (the tape zeroes large adjoint buffers this way and joins before the
+ * reverse sweep, grad.hpp). */
+int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes);
+int smg_join_async(smg_ctx* ctx);
 int smg_sync(smg_ctx* ctx);
 /* synchronise, return the latched status bits (0 = ok) and clear them */
 int smg_status(smg_ctx* ctx, int* status_host);

@@ -140,6 +140,9 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->comm = nullptr;
   ctx->status_ev = nullptr;
   ctx->status_mark = 0;
+  ctx->zero_stream = nullptr;
+  ctx->zero_ev_main = ctx->zero_ev_done = nullptr;
+  ctx->zero_pending = 0;
   ctx->side = nullptr;
   ctx->main_stream = nullptr;
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
@@ -195,6 +198,12 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   for (auto e : ctx->prof_pool) hipEventDestroy(e);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->status_ev) hipEventDestroy(ctx->status_ev);
+  if (ctx->zero_stream) {
+    hipStreamSynchronize(ctx->zero_stream);
+    hipEventDestroy(ctx->zero_ev_main);
+    hipEventDestroy(ctx->zero_ev_done);
+    hipStreamDestroy(ctx->zero_stream);
+  }
   if (ctx->side) {
     hipStreamSynchronize(ctx->side);
     hipStreamDestroy(ctx->side);
@@ -348,6 +357,38 @@ int smg_memcpy_d2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
 int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
   if (!bytes) return SMG_OK;
   SMG_HIP_TRY(hipMemsetAsync(dst, v, bytes, ctx->stream));
+  return SMG_OK;
+}
+
+int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes) {
+  if (!ctx) return SMG_ERR_ARG;
+  if (!bytes) return SMG_OK;
+  if (!dst) return SMG_ERR_ARG;
+  if (!ctx->zero_stream) {
+    if (hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->zero_ev_main, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->zero_ev_done, hipEventDisableTiming) != hipSuccess) {
+      hipGetLastError();
+      ctx->zero_stream = nullptr;
+      SMG_HIP_TRY(hipMemsetAsync(dst, 0, bytes, ctx->stream));  // no second stream: in order
+      return SMG_OK;
+    }
+  }
+  // after everything already enqueued on the main stream (the memory may have
+  // belonged to a recovered tape whose kernels are still queued there)
+  SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_main, ctx->stream));
+  SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_ev_main, 0));
+  SMG_HIP_TRY(hipMemsetAsync(dst, 0, bytes, ctx->zero_stream));
+  SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_done, ctx->zero_stream));
+  ctx->zero_pending = 1;
+  return SMG_OK;
+}
+
+int smg_join_async(smg_ctx* ctx) {
+  if (!ctx) return SMG_ERR_ARG;
+  if (!ctx->zero_pending) return SMG_OK;
+  SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->zero_ev_done, 0));
+  ctx->zero_pending = 0;
   return SMG_OK;
 }
 

@@ -49,6 +49,12 @@ struct smg_ctx {
   // with an event the host waits on instead of the whole stream
   hipEvent_t status_ev;
   int status_mark;
+  // zeroing stream (smg_memset_async / smg_join_async): large adjoint buffers
+  // are cleared there, overlapping the forward pass, and joined into `stream`
+  // before the reverse sweep
+  hipStream_t zero_stream;
+  hipEvent_t zero_ev_main, zero_ev_done;
+  int zero_pending;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;

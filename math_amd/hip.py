@@ -39,6 +39,8 @@ _SIGS = {
     "smg_memcpy_d2h": (_I, [_P, _P, _P, _S]),
     "smg_memcpy_d2d": (_I, [_P, _P, _P, _S]),
     "smg_memset": (_I, [_P, _P, _I, _S]),
+    "smg_memset_async": (_I, [_P, _P, _S]),
+    "smg_join_async": (_I, [_P]),
     "smg_sync": (_I, [_P]),
     "smg_status": (_I, [_P, ctypes.POINTER(_I)]),
     "smg_status_armed": (_I, [_P, ctypes.POINTER(_I)]),

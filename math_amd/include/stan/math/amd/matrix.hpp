@@ -83,6 +83,7 @@ class dev_var_matrix {
   }
   /** Column-major host copy of the adjoints (synchronising). */
   std::vector<double> adj() const {
+    join_device_adjoints();
     std::vector<double> h(size());
     amd::to_host(h.data(), vi_->adj_, size());
     return h;

@@ -23,10 +23,21 @@ namespace stan {
 namespace math {
 
 /** Register a device adjoint buffer with the tape (zeroed now and by
- * set_zero_all_adjoints). */
+ * set_zero_all_adjoints).  A large buffer is zeroed on the context's zeroing
+ * stream, overlapping the rest of the forward pass; only a reverse sweep (or
+ * a host read of the adjoint) touches it, and both join that stream first
+ * (join_device_adjoints). */
 inline void register_device_adjoint(double* p, size_t n) {
-  amd::zero(p, n);
+  if (n >= (size_t(1) << 17))
+    amd::check(smg_memset_async(amd::ctx(), p, n * sizeof(double)), "zero");
+  else
+    amd::zero(p, n);
   ChainableStack::instance_->dev_adj_stack_.push_back({p, n});
+}
+
+/** The main stream waits for every adjoint zeroing still in flight. */
+inline void join_device_adjoints() {
+  if (amd::has_ctx()) amd::check(smg_join_async(amd::ctx()), "grad");
 }
 
 /** Queue target->adj_ += *src (src: device scalar) for the next flush. */
@@ -75,6 +86,7 @@ static inline size_t nested_size() {
 static void grad(vari* vi) {
   using it_t = std::vector<vari*>::reverse_iterator;
   auto* st = ChainableStack::instance_;
+  join_device_adjoints();
   vi->init_dependent();
   it_t begin = st->var_stack_.rbegin();
   it_t end = empty_nested() ? st->var_stack_.rend() : begin + nested_size();
