@@ -319,6 +319,8 @@ class HVP(GP):
         # no reference value at N=4096 (the reference's O(N^3) fvar tape is infeasible there);
         # parity is pinned at N<=256 (tests/test_cpp_functors.py); here: value = the GP's,
         # and two products bitwise equal (deterministic)
+        if not np.any(self.hv):  # --warmup 0: no product has run yet
+            self.step()
         h0 = self.hv.copy()
         self.step()
         ok = (abs(self.fx[0] - self.gold["fx"]) < 1e-9 * abs(self.gold["fx"])

@@ -17,6 +17,7 @@
 // Split-K writes fixed-order partial slabs reduced by a second kernel, so the
 // result is bitwise deterministic run to run.
 #include "smg_internal.h"
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -575,6 +576,10 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
     return smg_scale_impl(ctx, m, n, beta, C, ldc, uplo);
   }
   smg_prof_scope prof(ctx, SMG_FAM_GEMM);
+  {  // dev shape log (SMG_GEMM_LOG=1): one stderr line per product
+    static const bool log = getenv("SMG_GEMM_LOG") != nullptr;
+    if (log) fprintf(stderr, "gemm ta=%d tb=%d uplo=%d m=%d n=%d k=%d tri=%d\n", ta, tb, uplo, m, n, k, tri);
+  }
   if (ctx->prof_on)
     ctx->prof_flops[SMG_FAM_GEMM] +=
         uplo ? 2.0 * k * ((double)m * n - (double)n * (n - 1) / 2) : 2.0 * m * n * k;
