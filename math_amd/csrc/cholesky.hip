@@ -213,7 +213,7 @@ __device__ inline void panel_gstore_tri(const double* D, double* A, int ld, int 
 
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status) {
+                                                    int* flags, int epoch, int* status, int early) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -235,24 +235,38 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     // it with L_{j+1,j} only after seeing diag[j].
     double* Dc = D;  // current diagonal block (LDS)
     double* Zn = Z;  // next one
+    __shared__ double Tch[3 * 256];  // lds_trtri64_mfma scratch
     lds_load_block(Dc, L + J + (size_t)J * ldl, ldl, min(SMG_NB, K - J), true);
     __syncthreads();
     for (int j = 0; j < nb; ++j) {
       const int cj = J + SMG_NB * j;
       const int bj = min(SMG_NB, K - cj);
       PANEL_EV((j << 16) | (j << 8) | 2);
-      lds_potrf_inv64_blk(Dc, X, bj, nullptr, 0, nullptr, 0, status, true);
-      __syncthreads();
-      PANEL_EV((j << 16) | (j << 8) | 10);
       const bool more = j + 1 < nb;
       const int t = j + 1, rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
       const int bt = min(SMG_NB, K - rt0);
       panel_regs Ra, Rz;
-      if (more) {
+      auto load_next = [&] {
         if (j >= 1) panel_wait(&done[(j - 1) * S + t], epoch, status);
         PANEL_EV((j << 16) | (t << 8) | 11);
         panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
         panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
+      };
+      if (early) {
+        // the next tile's operands are loaded between the factorisation and
+        // the inverse: their latency hides behind the inverse instead of
+        // sitting between the publish and the next products
+        lds_potrf64_lookahead(Dc, status);
+        __syncthreads();
+        if (more) load_next();
+        lds_trtri64_mfma(Dc, X, Tch);
+        __syncthreads();
+        PANEL_EV((j << 16) | (j << 8) | 10);
+      } else {
+        lds_potrf_inv64_blk(Dc, X, bj, nullptr, 0, nullptr, 0, status, true);
+        __syncthreads();
+        PANEL_EV((j << 16) | (j << 8) | 10);
+        if (more) load_next();
       }
       // Dinv_j is what the other tiles wait for; L_jj is read by no one in
       // the launch, so it is stored after the publish (off the chain)
@@ -764,8 +778,12 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int grid = T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID;  // chain + owners of tiles 1..T-1
       const int epoch = ++ctx->flag_epoch;
       ctx->status_armed = 1;
+      static const int early = [] {  // dev A/B switch: SMG_CHAIN_EARLY=0 loads after the inverse
+        const char* e = getenv("SMG_CHAIN_EARLY");
+        return !e || atoi(e) != 0 ? 1 : 0;
+      }();
       hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, early);
     }
     if (K >= n) break;
     const int m = n - K;
