@@ -39,6 +39,8 @@
 //   k_glm_reg   16 rows x 256 threads            4.75 TB/s (128-byte column segments)
 //   k_glm_reg   16 rows x 512 threads            4.04 TB/s
 //   k_glm_reg   32 x 512 with two tiles in flight (3 register buffers): no gain
+//   k_glm_reg   32 x 512, x read with nontemporal loads (x is streamed once,
+//               it should not displace other lines): 5.61-5.73 -> 5.81 TB/s
 // The first k_glm_reg build ran at 1.7 TB/s: a branch or a select next to a
 // load, a loop-carried register copy and a y load issued after x each made
 // the compiler wait for the loads within the tile that issued them.
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
 // thread (summed over the 32 rows of a column group once, at the end, by
 // lane shuffles).  A load instruction still covers two 256-byte column
 // segments per wave.
-template <int KIND, int RB, int NT>
+template <int KIND, int RB, int NT, bool NTL = false>
 __global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, const double* __restrict__ x,
                                                 long long R, int M, long long ldx, const double* __restrict__ ab,
                                                 double* __restrict__ part) {
@@ -210,7 +212,8 @@ __global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, con
     for (int q = 0; q < Q; ++q) {
       const int c = g + G * q;
       const int cc = c < M ? c : M - 1;
-      v[q] = x[rc + (size_t)cc * ldx];
+      const double* px = x + rc + (size_t)cc * ldx;
+      v[q] = NTL ? __builtin_nontemporal_load(px) : *px;
     }
   };
   // one tile's work on the registers cur / cy (the other buffer's loads
@@ -325,7 +328,8 @@ int glm_blocks(long long R) {
 }
 
 // dev A/B switches: SMG_GLM_REG selects the streaming kernel (0: LDS-staged
-// k_glm_fused; 1: k_glm_reg 32 rows x 512 threads; 2: 16 x 256; 3: 16 x 512),
+// k_glm_fused; 1: k_glm_reg 32 rows x 512 threads, nontemporal x loads;
+// 2: 16 x 256; 3: 16 x 512; 4: as 1 with ordinary loads),
 // SMG_GLM_NB caps the number of workgroups (<= glm_blocks(R), the workspace size)
 inline int glm_env(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -349,8 +353,11 @@ int glm_launch(hipStream_t st, const void* y, const double* x, long long R, int 
     case 3:
       hipLaunchKernelGGL((k_glm_reg<KIND, 16, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
       break;
-    default:
+    case 4:
       hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
+      break;
+    default:
+      hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512, true>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
   }
   return nb;
 }
