@@ -167,6 +167,31 @@ __device__ int g_panel_trace_n[PANEL_MAX_GRID];
 
 // hand-off primitives (st_dev / panel_publish / panel_wait): smg_sync.h
 
+// The chain's LDS phases out of line: each compiles with its own register
+// budget instead of under the whole kernel's pressure (228 VGPRs, ~110 SGPR
+// spills inlined); the LDS pointers are typed address_space(3) so the
+// callees keep ds_ instructions (a generic pointer would turn them into flat
+// accesses).  Same arithmetic in the same order as inlined.
+// SMG_CHAIN_INLINE restores the inlined phases (A/B builds).
+#ifndef SMG_CHAIN_INLINE
+typedef __attribute__((address_space(3))) double lds_dbl;
+__device__ __noinline__ void chain_factor(lds_dbl* D, int* status) { lds_potrf64_lookahead(D, status); }
+__device__ __noinline__ void chain_inverse(const lds_dbl* D, lds_dbl* X, lds_dbl* T) { lds_trtri64_mfma(D, X, T); }
+__device__ __noinline__ void chain_ltj(lds_dbl* Y, const lds_dbl* X) {
+  lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Y, Y, X);
+}
+__device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }
+#define CHAIN_FACTOR(D, st) chain_factor((lds_dbl*)(D), (st))
+#define CHAIN_INVERSE(D, X, T) chain_inverse((const lds_dbl*)(D), (lds_dbl*)(X), (lds_dbl*)(T))
+#define CHAIN_LTJ(Y, X) chain_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
+#define CHAIN_SYRK(Zn, Y, b) chain_syrk((lds_dbl*)(Zn), (const lds_dbl*)(Y), (b))
+#else
+#define CHAIN_FACTOR(D, st) lds_potrf64_lookahead((D), (st))
+#define CHAIN_INVERSE(D, X, T) lds_trtri64_mfma((D), (X), (T))
+#define CHAIN_LTJ(Y, X) lds_mma64_8w<false, true>((Y), (Y), (X))
+#define CHAIN_SYRK(Zn, Y, b) lds_syrk64_8w_next((Zn), (Y), (b))
+#endif
+
 // rows x cols block of a col-major matrix -> registers (8 per thread, 512
 // threads); branch-free: clamped addresses, out-of-range (and, with lower,
 // strict-upper) elements masked at the LDS store
@@ -256,10 +281,10 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         // the next tile's operands are loaded between the factorisation and
         // the inverse: their latency hides behind the inverse instead of
         // sitting between the publish and the next products
-        lds_potrf64_lookahead(Dc, status);
+        CHAIN_FACTOR(Dc, status);
         __syncthreads();
         if (more) load_next();
-        lds_trtri64_mfma(Dc, X, Tch);
+        CHAIN_INVERSE(Dc, X, Tch);
         __syncthreads();
         PANEL_EV((j << 16) | (j << 8) | 10);
       } else {
@@ -280,11 +305,11 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       panel_lstore(Zn, Rz);
       __syncthreads();
       PANEL_EV((j << 16) | (t << 8) | 12);
-      lds_mma64_8w<false, true>(Y, Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T (private)
+      CHAIN_LTJ(Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T (private)
       PANEL_EV((j << 16) | (t << 8) | 13);
       // A_tt -= L_tj L_tj^T, written as the factorisation's input: lower
       // triangle, zero strict upper, identity padding beyond bt
-      lds_syrk64_8w_next(Zn, Y, bt);
+      CHAIN_SYRK(Zn, Y, bt);
       double* tmp = Dc;
       Dc = Zn;
       Zn = tmp;

@@ -68,9 +68,8 @@ __device__ inline void lds_mma64(double* C, const double* A, const double* B, do
 
 // C (64x64) = alpha op(A) op(B) + beta C with NW = 8 waves: wave w owns row
 // stripe w & 3 and column tiles 2 (w >> 2) .. +1.  Safe when C aliases A or B.
-template <bool TA, bool TB>
-__device__ inline void lds_mma64_8w(double* C, const double* A, const double* B,
-                                    double alpha = 1.0, double beta = 0.0) {
+template <bool TA, bool TB, typename P = double*, typename CP = const double*>
+__device__ inline void lds_mma64_8w(P C, CP A, CP B, double alpha = 1.0, double beta = 0.0) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int fr = l & 15, fk = l >> 4;
   const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
@@ -93,7 +92,7 @@ __device__ inline void lds_mma64_8w(double* C, const double* A, const double* B,
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      double* c = &C[(16 * (w & 3) + fk + 4 * r) * SMG_NBP + 16 * (t0 + t) + fr];
+      auto c = &C[(16 * (w & 3) + fk + 4 * r) * SMG_NBP + 16 * (t0 + t) + fr];
       *c = beta == 0.0 ? alpha * acc[t][r] : alpha * acc[t][r] + beta * *c;
     }
   __syncthreads();
@@ -103,7 +102,8 @@ __device__ inline void lds_mma64_8w(double* C, const double* A, const double* B,
 // LDS), written straight in the factorisation's input form -- lower triangle,
 // zero strict upper, identity padding beyond row / column b -- so no separate
 // pass over C follows
-__device__ inline void lds_syrk64_8w_next(double* C, const double* A, int b) {
+template <typename P, typename CP>
+__device__ inline void lds_syrk64_8w_next(P C, CP A, int b) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int fr = l & 15, fk = l >> 4;
   const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
@@ -126,7 +126,7 @@ __device__ inline void lds_syrk64_8w_next(double* C, const double* A, int b) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * (w & 3) + fk + 4 * r, col = 16 * (t0 + t) + fr;
-      double* c = &C[row * SMG_NBP + col];
+      auto c = &C[row * SMG_NBP + col];
       *c = col > row ? 0.0 : (row == col && row >= b ? 1.0 : *c - acc[t][r]);
     }
   __syncthreads();
@@ -664,7 +664,8 @@ __device__ __forceinline__ void wave_panel8_local(double* D, int j0, bool& bad) 
   }
 }
 
-__device__ __forceinline__ void wave_store8(double* D, const double (&a)[8], int j0) {
+template <typename P>
+__device__ __forceinline__ void wave_store8(P D, const double (&a)[8], int j0) {
   const int i = threadIdx.x & 63;
   if (i >= j0)
 #pragma unroll
@@ -673,7 +674,8 @@ __device__ __forceinline__ void wave_store8(double* D, const double (&a)[8], int
 }
 
 // wave 0: load, factor (v_readlane broadcasts), store panel j0..j0+7
-__device__ __forceinline__ void wave_panel8_rl(double* D, int j0, bool& bad) {
+template <typename P>
+__device__ __forceinline__ void wave_panel8_rl(P D, int j0, bool& bad) {
   const int i = threadIdx.x & 63;
   double a[8];
 #pragma unroll
@@ -682,7 +684,10 @@ __device__ __forceinline__ void wave_panel8_rl(double* D, int j0, bool& bad) {
   wave_store8(D, a, j0);
 }
 
-__device__ inline void lds_potrf64_lookahead(double* D, int* status) {
+// (templated on the pointer type: double* when inlined into a kernel, an
+// address_space(3) pointer when called out of line)
+template <typename P>
+__device__ inline void lds_potrf64_lookahead(P D, int* status) {
   const int i = threadIdx.x & 63;
   const int g = threadIdx.x >> 6;
   bool bad = false;
@@ -745,7 +750,8 @@ __device__ inline void lds_potrf64_lookahead(double* D, int* status) {
 //   block rows p = 1..3:  T = -L[p, 0:p] X[0:p, 0:p]  (wave q < p: tile (p, q)),
 //                         X[p, 0:p] = X_pp T          (wave q < p)
 // X: LDS [64][SMG_NBP], fully written (upper zeros); T: LDS >= 3 * 256 doubles.
-__device__ inline void lds_trtri64_mfma(const double* D, double* X, double* T) {
+template <typename CP, typename P>
+__device__ inline void lds_trtri64_mfma(CP D, P X, P T) {
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < 64 * SMG_NBP; e += blockDim.x) X[e] = 0.0;
