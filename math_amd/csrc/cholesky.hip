@@ -181,15 +181,20 @@ __device__ __noinline__ void chain_ltj(lds_dbl* Y, const lds_dbl* X) {
   lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Y, Y, X);
 }
 __device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }
+__device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const lds_dbl* B) {
+  lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
+}
 #define CHAIN_FACTOR(D, st) chain_factor((lds_dbl*)(D), (st))
 #define CHAIN_INVERSE(D, X, T) chain_inverse((const lds_dbl*)(D), (lds_dbl*)(X), (lds_dbl*)(T))
 #define CHAIN_LTJ(Y, X) chain_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
 #define CHAIN_SYRK(Zn, Y, b) chain_syrk((lds_dbl*)(Zn), (const lds_dbl*)(Y), (b))
+#define OWNER_UPDATE(Z, D, B) owner_update((lds_dbl*)(Z), (const lds_dbl*)(D), (const lds_dbl*)(B))
 #else
 #define CHAIN_FACTOR(D, st) lds_potrf64_lookahead((D), (st))
 #define CHAIN_INVERSE(D, X, T) lds_trtri64_mfma((D), (X), (T))
 #define CHAIN_LTJ(Y, X) lds_mma64_8w<false, true>((Y), (Y), (X))
 #define CHAIN_SYRK(Zn, Y, b) lds_syrk64_8w_next((Zn), (Y), (b))
+#define OWNER_UPDATE(Z, D, B) lds_mma64_8w<false, true>((Z), (D), (B), -1.0, 1.0)
 #endif
 
 // rows x cols block of a col-major matrix -> registers (8 per thread, 512
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       panel_lstore(D, Ra);
       panel_lstore(X, Rd);
       __syncthreads();
-      lds_mma64_8w<false, true>(D, D, X);  // L_tj = A_tj Dinv_j^T
+      CHAIN_LTJ(D, X);  // L_tj = A_tj Dinv_j^T (the chain's own product: the same bits)
       panel_gstore(D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
       PANEL_EV((j << 16) | (t << 8) | 7);
       if (t < nb) panel_publish(&row[j * S + t], epoch);
@@ -369,7 +374,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         panel_lstore(Z, Rzn);
         __syncthreads();
         if (c + 1 <= clast) issue(c + 1);  // in flight during this product
-        lds_mma64_8w<false, true>(Z, D, own ? D : Y, -1.0, 1.0);
+        OWNER_UPDATE(Z, D, own ? D : Y);
         panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
         PANEL_EV((j << 16) | (t << 8) | (16 + c));
       }
