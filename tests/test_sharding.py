@@ -74,6 +74,21 @@ def _free_port():
     return port
 
 
+def _spawn(fn, world, *args):
+    """mp.start_processes with a fresh rendezvous port: fn(rank, world, port, *args).
+    The port is free when probed but can be taken by another process on a
+    shared host before rank 0 binds it (EADDRINUSE); only that case is retried,
+    with a new port."""
+    for attempt in range(3):
+        try:
+            mp.start_processes(fn, args=(world, _free_port()) + args, nprocs=world, join=True,
+                               start_method="spawn")
+            return
+        except mp.ProcessRaisedException as e:
+            if "EADDRINUSE" not in str(e) or attempt == 2:
+                raise
+
+
 def test_partition_tiles_rows():
     for R in (0, 1, 7, 100000, 10_000_000):
         for world in (1, 2, 3, 8):
@@ -98,8 +113,7 @@ def test_glm_two_ranks_gloo_matches_reference(tmp_path):
     d = golden("glm_R100000_M256")
     R, M = int(d["R"]), int(d["M"])
     out = str(tmp_path / "r0.npy")
-    mp.start_processes(_rank_main, args=(2, _free_port(), R, M, out), nprocs=2, join=True,
-                       start_method="spawn")
+    _spawn(_rank_main, 2, R, M, out)
     res = np.load(out)
     near_rel(res[0], d["fx"], 1e-12, what="fx")
     near_rel(res[1:], d["grad"], 1e-10, what="grad")
@@ -178,8 +192,7 @@ def test_map_rect_executor_gloo(tmp_path, world):
     throws on one rank makes every rank throw the reference's
     "Error during MPI evaluation."."""
     out = str(tmp_path / "mr")
-    mp.start_processes(_maprect_rank, args=(world, _free_port(), MAPRECT_CASES, out), nprocs=world, join=True,
-                       start_method="spawn")
+    _spawn(_maprect_rank, world, MAPRECT_CASES, out)
     ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(world)]
     lib = _maprect_lib()
     cb = _AG(lambda *a: None)
@@ -287,7 +300,7 @@ def test_glm_reducers_two_ranks_product_path(tmp_path):
     rank makes BOTH ranks throw domain_error (the owner with the reference's
     message and the global index)."""
     out = str(tmp_path / "gd")
-    mp.start_processes(_glm_dist_rank, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    _spawn(_glm_dist_rank, 2, out)
     ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(2)]
     for kind, name, bad in GLM_DIST_CASES:
         key = f"{kind}_{bad}"
