@@ -21,6 +21,9 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef SMG_GEMM_KS2_MAX
+#define SMG_GEMM_KS2_MAX 1536  // largest 64 x 64 tile count that takes the 8-wave variant
+#endif
 #ifndef SMG_GEMM_NR64
 #define SMG_GEMM_NR64 2
 #endif
@@ -529,7 +532,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   // (and a 64 x 64 grid below 256 tiles, split over K or not, loses to 32 x 32:
   // (3584,256,256) 18.6 vs 28 us)
   if (mid_tiles >= 512) {
-    if (mid_tiles <= 1536)
+    if (mid_tiles <= SMG_GEMM_KS2_MAX)
       return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   }
