@@ -243,7 +243,7 @@ __device__ inline void panel_gstore_tri(const double* D, double* A, int ld, int 
 
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status, int early) {
+                                                    int* flags, int epoch, int* status) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -282,22 +282,15 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
         panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
       };
-      if (early) {
-        // the next tile's operands are loaded between the factorisation and
-        // the inverse: their latency hides behind the inverse instead of
-        // sitting between the publish and the next products
-        CHAIN_FACTOR(Dc, status);
-        __syncthreads();
-        if (more) load_next();
-        CHAIN_INVERSE(Dc, X, Tch);
-        __syncthreads();
-        PANEL_EV((j << 16) | (j << 8) | 10);
-      } else {
-        lds_potrf_inv64_blk(Dc, X, bj, nullptr, 0, nullptr, 0, status, true);
-        __syncthreads();
-        PANEL_EV((j << 16) | (j << 8) | 10);
-        if (more) load_next();
-      }
+      // the next tile's operands are loaded between the factorisation and
+      // the inverse: their latency hides behind the inverse instead of
+      // sitting between the publish and the next products
+      CHAIN_FACTOR(Dc, status);
+      __syncthreads();
+      if (more) load_next();
+      CHAIN_INVERSE(Dc, X, Tch);
+      __syncthreads();
+      PANEL_EV((j << 16) | (j << 8) | 10);
       // Dinv_j is what the other tiles wait for; L_jj is read by no one in
       // the launch, so it is stored after the publish (off the chain)
       panel_gstore_tri(X, Dinv + cj, ldd, bj);
@@ -808,12 +801,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int grid = T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID;  // chain + owners of tiles 1..T-1
       const int epoch = ++ctx->flag_epoch;
       ctx->status_armed = 1;
-      static const int early = [] {  // dev A/B switch: SMG_CHAIN_EARLY=0 loads after the inverse
-        const char* e = getenv("SMG_CHAIN_EARLY");
-        return !e || atoi(e) != 0 ? 1 : 0;
-      }();
       hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, early);
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);
     }
     if (K >= n) break;
     const int m = n - K;
