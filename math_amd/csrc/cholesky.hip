@@ -241,9 +241,14 @@ __device__ inline void panel_gstore_tri(const double* D, double* A, int ld, int 
   }
 }
 
+// column block c of panel tile t is updated by t's helper workgroup
+__device__ __forceinline__ bool panel_helped(int t, int c, int nb, int nh) {
+  return t < nb && t >= 3 && t - 3 < nh && (c & 1) && c <= t - 2;
+}
+
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status) {
+                                                    int* flags, int epoch, int* status, int gown) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -252,8 +257,49 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   int* diag = flags;           // diag[j]: L_jj, Dinv_j stored
   int* row = flags + S;        // row[j S + t]: L_tj stored (panel tiles t < nb)
   int* done = flags + S + S * S;  // done[j S + t]: tile t's step-j updates stored
+  int* hflag = flags + S + 2 * S * S;  // hflag[j S + t]: tile t's helper finished step j
   const int nb = (K - J + SMG_NB - 1) / SMG_NB;
   const int T = (n - J + SMG_NB - 1) / SMG_NB;
+  // Column helpers: panel tile t >= 3 (t < nb) gets workgroup gown + t - 3,
+  // which applies the updates of its odd column blocks c <= t - 2 (panel_helped);
+  // the owner of t does the rest, its L_tj, and waits hflag[(j-1) S + t]
+  // before reading a helped column j.  The owners of the last panel tiles
+  // were the chain's bottleneck (their seven column updates per step).
+  const int nh = gridDim.x - gown;
+
+  if (blockIdx.x >= gown) {
+    const int t = 3 + (blockIdx.x - gown);
+    if (t >= nb) return;
+    const int rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
+    for (int j = 0; j + 2 <= t; ++j) {
+      const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
+      int c0 = j + 1;
+      while (c0 <= t - 2 && !panel_helped(t, c0, nb, nh)) ++c0;
+      if (c0 <= t - 2) {
+        panel_wait(&row[j * S + t], epoch, status);  // the owner's L_tj
+        panel_regs Rl;
+        panel_gload(Rl, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+        panel_wait_all(row + j * S, c0, t - 2, 1, epoch, status);
+        __syncthreads();
+        panel_lstore(D, Rl);
+        for (int c = c0; c <= t - 2; ++c) {
+          if (!panel_helped(t, c, nb, nh)) continue;
+          const int cc = J + SMG_NB * c, bc = min(SMG_NB, K - cc);
+          panel_regs Ry, Rz;
+          panel_gload(Rz, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, false);
+          panel_gload(Ry, L + cc + (size_t)cj * ldl, ldl, bc, bj, false);
+          __syncthreads();  // previous product's Y / Z consumed (and D stored)
+          panel_lstore(Y, Ry);
+          panel_lstore(Z, Rz);
+          __syncthreads();
+          OWNER_UPDATE(Z, D, Y);
+          panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, false);
+        }
+      }
+      panel_publish(&hflag[j * S + t], epoch);
+    }
+    return;
+  }
 
   if (blockIdx.x == 0) {
     // the diagonal chain: factor block j, then apply step j to tile j + 1
@@ -323,7 +369,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
-    for (int t = 1 + (blockIdx.x - 1); t < T; t += gridDim.x - 1) {
+    for (int t = 1 + (blockIdx.x - 1); t < T; t += gown - 1) {
       if (t <= j) continue;  // done
       const bool next = t == j + 1 && t < nb;  // the chain's next diagonal tile
       const int rt0 = J + SMG_NB * t;
@@ -331,6 +377,8 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       __syncthreads();  // LDS of the previous item fully consumed
       PANEL_EV((j << 16) | (t << 8) | 5);
       panel_regs Ra, Rd;
+      // a helped column is final once the helper has finished step j - 1
+      if (panel_helped(t, j, nb, nh)) panel_wait(&hflag[(j - 1) * S + t], epoch, status);
       panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);  // own data, final
       panel_wait(&diag[j], epoch, status);
       PANEL_EV((j << 16) | (t << 8) | 6);
@@ -357,8 +405,13 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         panel_gload(Rzn, L + rt0 + (size_t)cc * ldl, ldl, rt, min(SMG_NB, K - cc), own);
         if (!own) panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
       };
-      if (j + 1 <= clast) issue(j + 1);
-      for (int c = j + 1; c <= clast; ++c) {
+      auto next_col = [&](int c) {  // the next column from c on that this workgroup updates
+        while (c <= clast && panel_helped(t, c, nb, nh)) ++c;
+        return c;
+      };
+      int cfirst = next_col(j + 1);
+      if (cfirst <= clast) issue(cfirst);
+      for (int c = cfirst; c <= clast; c = next_col(c + 1)) {
         const int cc = J + SMG_NB * c;
         const int bc = min(SMG_NB, K - cc);
         const bool own = c == t;  // L_cj is L_tj itself; A_tt: lower triangle
@@ -366,7 +419,8 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         if (!own) panel_lstore(Y, Ryn);
         panel_lstore(Z, Rzn);
         __syncthreads();
-        if (c + 1 <= clast) issue(c + 1);  // in flight during this product
+        const int cn = next_col(c + 1);
+        if (cn <= clast) issue(cn);  // in flight during this product
         OWNER_UPDATE(Z, D, own ? D : Y);
         panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
         PANEL_EV((j << 16) | (t << 8) | (16 + c));
@@ -801,8 +855,16 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int grid = T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID;  // chain + owners of tiles 1..T-1
       const int epoch = ++ctx->flag_epoch;
       ctx->status_armed = 1;
-      hipLaunchKernelGGL(k_chol_panel, dim3(grid), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d);
+      // column helpers for panel tiles 3 .. nb-1 (SMG_PANEL_HELPERS=0: none)
+      static const bool use_helpers = [] {
+        const char* e = getenv("SMG_PANEL_HELPERS");
+        return !e || atoi(e) != 0;
+      }();
+      const int nbp = smg_ceil_div(K - J, SMG_NB);
+      int nh = use_helpers && nbp > 3 ? nbp - 3 : 0;
+      if (grid + nh > PANEL_MAX_GRID || nbp > T) nh = 0;
+      hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
     }
     if (K >= n) break;
     const int m = n - K;

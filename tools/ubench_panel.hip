@@ -47,7 +47,7 @@ int main() {
     hipEventCreate(&e1);
     hipEventRecord(e0);
     hipLaunchKernelGGL(k_chol_panel, dim3(T), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
-                       status);
+                       status, T);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
