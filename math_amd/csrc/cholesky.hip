@@ -277,9 +277,11 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       while (c0 <= t - 2 && !panel_helped(t, c0, nb, nh)) ++c0;
       if (c0 <= t - 2) {
         panel_wait(&row[j * S + t], epoch, status);  // the owner's L_tj
+        PANEL_EV((j << 16) | (t << 8) | 20);
         panel_regs Rl;
         panel_gload(Rl, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
         panel_wait_all(row + j * S, c0, t - 2, 1, epoch, status);
+        PANEL_EV((j << 16) | (t << 8) | 21);
         __syncthreads();
         panel_lstore(D, Rl);
         for (int c = c0; c <= t - 2; ++c) {
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         }
       }
       panel_publish(&hflag[j * S + t], epoch);
+      PANEL_EV((j << 16) | (t << 8) | 22);
     }
     return;
   }

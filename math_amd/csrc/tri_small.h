@@ -589,10 +589,17 @@ __device__ inline void lds_trtri64_blocked(const double* D, double* X, double* T
 // right of panel p+1.  The serial pivot chain (wave 0) overlaps the bulk of
 // the trailing work; one barrier per panel.
 // wave 0: factor the 8 columns held in a[] (lane i = row i, rows < j0 hold 0)
+// The column's entries of rows j0+c are broadcast BEFORE the pivot's
+// reciprocal root and scaled by it on every lane (the same product lane j0+c
+// forms, so the same bits as broadcasting l_{j0+c}): one readlane less on
+// the pivot chain
 __device__ __forceinline__ void wave_factor8_reg(double (&a)[8], int j0, bool& bad) {
   const int i = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
+    double sc[8];
+#pragma unroll
+    for (int c = t + 1; c < 8; ++c) sc[c] = bcast(a[t], j0 + c);
     const double piv = bcast(a[t], j0 + t);
     bad |= !(piv > 0.0 && piv < INFINITY);
     double r = __builtin_amdgcn_rsq(piv);
@@ -601,7 +608,7 @@ __device__ __forceinline__ void wave_factor8_reg(double (&a)[8], int j0, bool& b
     const double li = (i == j0 + t) ? piv * r : a[t] * r;
     a[t] = li;
 #pragma unroll
-    for (int c = t + 1; c < 8; ++c) a[c] -= li * bcast(li, j0 + c);
+    for (int c = t + 1; c < 8; ++c) a[c] -= li * (sc[c] * r);
   }
 }
 
@@ -745,60 +752,93 @@ __device__ inline void lds_potrf64_lookahead(P D, int* status) {
   if (bad) atomicOr(status, (int)SMG_ERR_NOT_PD);
 }
 
+// Pieces of X = L^{-1} (64x64) on 16x16 blocks, shared by lds_trtri64_mfma
+// and the fused lds_potrf_trtri64 (same arithmetic, same order: same bits).
+// Leaf k (one wave, lane c < 16 owns column c): X_kk = L_kk^{-1} by
+// right-looking elimination -- each x[q] still accumulates its terms in
+// ascending order, but only one FMA per row sits on the dependency chain.
+template <typename CP, typename P>
+__device__ __forceinline__ void trtri_leaf16(CP D, P X, int k) {
+  const int l = threadIdx.x & 63;
+  const int r0 = 16 * k;
+  double x[16], rv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    x[r] = (l == r) ? 1.0 : 0.0;
+    const double dd = D[(r0 + r) * SMG_NBP + r0 + r];
+    double rr = __builtin_amdgcn_rcp(dd);
+    rr = rr * (2.0 - dd * rr);
+    rv[r] = rr * (2.0 - dd * rr);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    x[r] = x[r] * rv[r];
+#pragma unroll
+    for (int q = r + 1; q < 16; ++q) x[q] -= D[(r0 + q) * SMG_NBP + r0 + r] * x[r];
+  }
+  if (l < 16)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) X[(r0 + r) * SMG_NBP + r0 + l] = x[r];
+}
+// T_q = -L[p, q:p] X[q:p, q] accumulated over k in [kb, ke) (multiples of 8,
+// from 16q): two MFMA chains (even / odd k-steps of 4), summed at the store
+template <typename CP, typename XP>
+__device__ __forceinline__ void trtri_t_acc(CP D, XP X, int p, int q, int kb, int ke, d4& acc,
+                                            d4& acc2) {
+  const int l = threadIdx.x & 63;
+  const int fr = l & 15, fk = l >> 4;
+  for (int k0 = kb; k0 < ke; k0 += 8) {
+    const double a = D[(16 * p + fr) * SMG_NBP + k0 + fk];
+    const double b = X[(k0 + fk) * SMG_NBP + 16 * q + fr];
+    const double a2 = D[(16 * p + fr) * SMG_NBP + k0 + 4 + fk];
+    const double b2 = X[(k0 + 4 + fk) * SMG_NBP + 16 * q + fr];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc2, 0, 0, 0);
+  }
+}
+template <typename P>
+__device__ __forceinline__ void trtri_t_store(P T, int q, const d4& acc, const d4& acc2) {
+  const int l = threadIdx.x & 63;
+  const int fr = l & 15, fk = l >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) T[q * 256 + (fk + 4 * r) * 16 + fr] = -(acc[r] + acc2[r]);
+}
+// X[p, q] = X_pp T_q
+template <typename P>
+__device__ __forceinline__ void trtri_x_tile(P X, P T, int p, int q) {
+  const int l = threadIdx.x & 63;
+  const int fr = l & 15, fk = l >> 4;
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    const double a = X[(16 * p + fr) * SMG_NBP + 16 * p + k0 + fk];
+    const double b = T[q * 256 + (k0 + fk) * 16 + fr];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) X[(16 * p + fk + 4 * r) * SMG_NBP + 16 * q + fr] = acc[r];
+}
+
 // X = L^{-1} (64x64) with 16x16 blocks on the fp64 matrix cores:
-//   leaves: wave w < 4 inverts diagonal block w (lane c < 16 owns column c);
+//   leaves: wave w < 4 inverts diagonal block w (trtri_leaf16)
 //   block rows p = 1..3:  T = -L[p, 0:p] X[0:p, 0:p]  (wave q < p: tile (p, q)),
 //                         X[p, 0:p] = X_pp T          (wave q < p)
 // X: LDS [64][SMG_NBP], fully written (upper zeros); T: LDS >= 3 * 256 doubles.
 template <typename CP, typename P>
 __device__ inline void lds_trtri64_mfma(CP D, P X, P T) {
-  const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < 64 * SMG_NBP; e += blockDim.x) X[e] = 0.0;
   __syncthreads();
-  if (w < 4) {
-    const int r0 = 16 * w;
-    double x[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      double s = (l == r) ? 1.0 : 0.0;
-#pragma unroll
-      for (int t = 0; t < r; ++t) s -= D[(r0 + r) * SMG_NBP + r0 + t] * x[t];
-      const double dd = D[(r0 + r) * SMG_NBP + r0 + r];
-      double rr = __builtin_amdgcn_rcp(dd);
-      rr = rr * (2.0 - dd * rr);
-      rr = rr * (2.0 - dd * rr);
-      x[r] = s * rr;
-    }
-    if (l < 16)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) X[(r0 + r) * SMG_NBP + r0 + l] = x[r];
-  }
+  if (w < 4) trtri_leaf16(D, X, w);
   __syncthreads();
-  const int fr = l & 15, fk = l >> 4;
   for (int p = 1; p < 4; ++p) {
-    if (w < p) {  // T_q = -sum_{k < 16p} L[16p + r][k] X[k][16q + c]
-      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-      for (int k0 = 16 * w; k0 < 16 * p; k0 += 4) {  // X[k][16w..] = 0 for k < 16w
-        const double a = D[(16 * p + fr) * SMG_NBP + k0 + fk];
-        const double b = X[(k0 + fk) * SMG_NBP + 16 * w + fr];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) T[w * 256 + (fk + 4 * r) * 16 + fr] = -acc[r];
+    if (w < p) {
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0}, acc2 = acc;
+      trtri_t_acc(D, X, p, w, 16 * w, 16 * p, acc, acc2);
+      trtri_t_store(T, w, acc, acc2);
     }
     __syncthreads();
-    if (w < p) {  // X[16p + r][16w + c] = sum_t Xpp[r][t] T_w[t][c]
-      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int k0 = 0; k0 < 16; k0 += 4) {
-        const double a = X[(16 * p + fr) * SMG_NBP + 16 * p + k0 + fk];
-        const double b = T[w * 256 + (k0 + fk) * 16 + fr];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) X[(16 * p + fk + 4 * r) * SMG_NBP + 16 * w + fr] = acc[r];
-    }
+    if (w < p) trtri_x_tile(X, T, p, w);
     __syncthreads();
   }
 }

@@ -7,7 +7,8 @@
 #include <vector>
 #include <cmath>
 
-int main() {
+int main(int argc, char** argv) {
+  const int nh = argc > 1 ? atoi(argv[1]) : 5;  // column helper workgroups
   const int n = 4096, J = 0, K = 512;
   std::vector<double> A((size_t)n * n);
   for (int j = 0; j < n; ++j)
@@ -46,7 +47,7 @@ int main() {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    hipLaunchKernelGGL(k_chol_panel, dim3(T), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
+    hipLaunchKernelGGL(k_chol_panel, dim3(T + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
                        status, T);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
@@ -88,9 +89,10 @@ int main() {
     hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_panel_trace), tr.size() * 8);
     hipMemcpyFromSymbol(cnt.data(), HIP_SYMBOL(g_panel_trace_n), cnt.size() * 4);
     unsigned long long t0 = ~0ull;
-    for (int w = 0; w < T; ++w)
+    for (int w = 0; w < T + nh; ++w)
       for (int k = 0; k < cnt[w] && k < 64; ++k) t0 = std::min(t0, tr[w * 128 + 2 * k]);
-    for (int w : {0, 5, 6, 7, 10, 62}) {
+    for (int w : {0, 5, 6, 7, 10, T + 3, T + 4}) {
+      if (w >= T + nh) continue;
       printf("WG %d:", w);
       for (int k = 0; k < cnt[w] && k < 64; ++k) {
         const unsigned long long c = tr[w * 128 + 2 * k + 1];
