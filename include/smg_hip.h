@@ -81,7 +81,10 @@ int smg_memset(smg_ctx* ctx, void* dst, int value, size_t bytes);
  * already enqueued on the main stream, overlapping what is enqueued there
  * next; smg_join_async makes the main stream wait for every such zeroing
  * (the tape zeroes large adjoint buffers this way and joins before the
- * reverse sweep, grad.hpp). */
+ * reverse sweep, grad.hpp).  The zeroing may be issued later than the call:
+ * at the next latency-bound entry (Cholesky panels, persistent solves), at
+ * smg_join_async or at an arena rewind / recover, whichever comes first; the
+ * buffer must not be touched on the main stream before smg_join_async. */
 int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes);
 int smg_join_async(smg_ctx* ctx);
 int smg_sync(smg_ctx* ctx);

@@ -95,6 +95,62 @@ __global__ __launch_bounds__(256) void k_check_symmetric_copy(const double* __re
   if (__any(bad) && lane == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
 }
 
+// The same pass for n % 64 == 0 with 16-byte aligned columns: each lane moves
+// two rows per 16-byte access, and all sixteen loads of a lane (eight from the
+// mirror tile U = A[j0.., i0..], eight from the tile itself) are issued before
+// the first use.  U(r, c) sits in LDS at c*64 + (r ^ (c & 62)): the 16-byte
+// stores of a column and the transposed reads of a row are both bank-spread.
+__global__ __launch_bounds__(256) void k_check_symmetric_copy2(const double* __restrict__ A,
+                                                               int lda, int n, int* status,
+                                                               double* __restrict__ L, int ldl) {
+  __shared__ double T[64 * 64];
+  int bi, bj;
+  {
+    const int t = blockIdx.x;
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    bi = r;
+    bj = t - r * (r + 1) / 2;
+  }
+  const int i0 = 64 * bi, j0 = 64 * bj;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rr = 2 * (lane & 31), cb = 2 * w + (lane >> 5);
+  double2 u[8], a[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int c = 8 * p + cb;
+    u[p] = *reinterpret_cast<const double2*>(A + (j0 + rr) + (size_t)(i0 + c) * lda);
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int c = 8 * p + cb;
+    a[p] = *reinterpret_cast<const double2*>(A + (i0 + rr) + (size_t)(j0 + c) * lda);
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int c = 8 * p + cb;
+    *reinterpret_cast<double2*>(&T[c * 64 + (rr ^ (c & 62))]) = u[p];
+  }
+  __syncthreads();
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int c = 8 * p + cb;
+    const int gc = j0 + c;
+    const double t0 = T[rr * 64 + (c ^ rr)], t1 = T[(rr + 1) * 64 + (c ^ rr)];
+    double2 v = a[p];
+    if (i0 + rr > gc) bad |= !(fabs(v.x - t0) <= 1e-8);
+    if (i0 + rr + 1 > gc) bad |= !(fabs(v.y - t1) <= 1e-8);
+    if (i0 + rr < gc) v.x = 0.0;
+    if (i0 + rr + 1 < gc) v.y = 0.0;
+    *reinterpret_cast<double2*>(L + (i0 + rr) + (size_t)gc * ldl) = v;
+    if (bi != bj)
+      *reinterpret_cast<double2*>(L + (j0 + rr) + (size_t)(i0 + c) * ldl) = make_double2(0.0, 0.0);
+  }
+  if (__any(bad) && lane == 0) atomicOr(status, (int)SMG_ERR_NOT_SYMMETRIC);
+}
+
 __global__ void k_copy_lower(const double* __restrict__ A, int lda, int n,
                              double* __restrict__ L, int ldl) {
   for (smg_mn it(n, n); it.ok(); it.next()) {
@@ -818,7 +874,11 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   Dinv = aux;  // the SMG_NB level comes first
   const int tb = smg_ceil_div(n, 64);
   if (A != L || lda != ldl) {
-    if (check_sym)
+    if (check_sym && n % 64 == 0 && lda % 2 == 0 && ldl % 2 == 0 &&
+        ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(L)) & 15) == 0)
+      hipLaunchKernelGGL(k_check_symmetric_copy2, dim3(tb * (tb + 1) / 2), dim3(256), 0,
+                         ctx->stream, A, lda, n, ctx->status_d, L, ldl);
+    else if (check_sym)
       hipLaunchKernelGGL(k_check_symmetric_copy, dim3(tb * (tb + 1) / 2), dim3(256), 0, ctx->stream, A,
                          lda, n, ctx->status_d, L, ldl);
     else
@@ -828,6 +888,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     hipLaunchKernelGGL(k_check_symmetric, dim3(tb * (tb + 1) / 2), dim3(256), 0, ctx->stream, A, lda,
                        n, ctx->status_d);
   }
+  // queued adjoint zeroings overlap the latency-bound panels, not the copy
+  if (int e = smg_zero_flush(ctx)) return e;
   // Two-level right-looking: panels of SMG_NBF columns factored with SMG_NB
   // steps whose updates stay inside the panel (all rows below), then ONE
   // rank-SMG_NBF update of the trailing matrix per panel (compute-bound, vs a

@@ -266,12 +266,16 @@ size_t smg_arena_mark(smg_ctx* ctx) {
 int smg_arena_rewind(smg_ctx* ctx, size_t mark) {
   size_t blk = mark >> 48, off = mark & ((1ull << 48) - 1);
   if (blk >= ctx->blocks.size()) return SMG_ERR_ARG;
+  // the freed memory is handed out again: no zeroing of it may still be
+  // queued or running behind the main stream
+  if (int e = smg_join_async(ctx)) return e;
   ctx->cur_block = blk;
   ctx->offset = off;
   return SMG_OK;
 }
 
 int smg_arena_recover_all(smg_ctx* ctx) {
+  if (int e = smg_join_async(ctx)) return e;
   ctx->cur_block = 0;
   ctx->offset = 0;
   return SMG_OK;
@@ -374,18 +378,29 @@ int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes) {
       return SMG_OK;
     }
   }
+  // issued by smg_zero_flush: at the next latency-bound entry, the join, or a
+  // rewind (the memory then still belongs to this tape)
+  ctx->zero_queue.emplace_back(dst, bytes);
+  return SMG_OK;
+}
+
+int smg_zero_flush(smg_ctx* ctx) {
+  if (ctx->zero_queue.empty()) return SMG_OK;
   // after everything already enqueued on the main stream (the memory may have
   // belonged to a recovered tape whose kernels are still queued there)
-  SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_main, ctx->stream));
+  hipStream_t main = (ctx->side && ctx->stream == ctx->side) ? ctx->main_stream : ctx->stream;
+  SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_main, main));
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_ev_main, 0));
-  SMG_HIP_TRY(hipMemsetAsync(dst, 0, bytes, ctx->zero_stream));
+  for (const auto& z : ctx->zero_queue) SMG_HIP_TRY(hipMemsetAsync(z.first, 0, z.second, ctx->zero_stream));
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_done, ctx->zero_stream));
+  ctx->zero_queue.clear();
   ctx->zero_pending = 1;
   return SMG_OK;
 }
 
 int smg_join_async(smg_ctx* ctx) {
   if (!ctx) return SMG_ERR_ARG;
+  if (int e = smg_zero_flush(ctx)) return e;
   if (!ctx->zero_pending) return SMG_OK;
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->zero_ev_done, 0));
   ctx->zero_pending = 0;

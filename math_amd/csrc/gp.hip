@@ -94,6 +94,79 @@ __global__ void k_add_diag_fwd(const double* __restrict__ A, int lda, int n, dou
   }
 }
 
+// Column forms of k_gp_fwd / k_add_diag_fwd for 16-byte aligned operands with
+// even n and leading dimensions (the N=4096 GP): a workgroup walks whole
+// columns, each lane moves two rows with one 16-byte access, four accesses in
+// flight per lane.  Same per-element expressions as above (the same bits).
+__global__ __launch_bounds__(256) void k_gp_fwd_col2(const double* __restrict__ x, int n, double s2,
+                                                     double inv_half_sq_l, double* __restrict__ K,
+                                                     int ldk) {
+  const int np = n >> 1;
+  const double2* x2 = reinterpret_cast<const double2*>(x);
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double xj = x[j];
+    double2* col = reinterpret_cast<double2*>(K + (size_t)j * ldk);
+    for (int p0 = threadIdx.x; p0 < np; p0 += 4 * 256) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          const double2 xi = x2[p];
+          const int i = 2 * p;
+          double2 v;
+          if (i == j) {
+            v.x = s2;
+          } else {
+            const double d = (i > j) ? xi.x - xj : xj - xi.x;
+            v.x = s2 * exp(-(d * d) * inv_half_sq_l);
+          }
+          if (i + 1 == j) {
+            v.y = s2;
+          } else {
+            const double d = (i + 1 > j) ? xi.y - xj : xj - xi.y;
+            v.y = s2 * exp(-(d * d) * inv_half_sq_l);
+          }
+          col[p] = v;
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_add_diag_fwd_col2(const double* __restrict__ A, int lda,
+                                                           int n, double d,
+                                                           const double* __restrict__ dv,
+                                                           double* __restrict__ B, int ldb) {
+  const int np = n >> 1;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double2* a = reinterpret_cast<const double2*>(A + (size_t)j * lda);
+    double2* b = reinterpret_cast<double2*>(B + (size_t)j * ldb);
+    const double dj = dv ? dv[j] : d;
+    for (int p0 = threadIdx.x; p0 < np; p0 += 4 * 256) {
+      double2 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) v[k] = a[p];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          if (2 * p == j) v[k].x += dj;
+          if (2 * p + 1 == j) v[k].y += dj;
+          b[p] = v[k];
+        }
+      }
+    }
+  }
+}
+
+// Both column forms need 16-byte aligned columns.
+inline bool col2_ok(const void* p, int ld, int n) {
+  return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (ld % 2 == 0) && (n % 2 == 0);
+}
+
 __global__ void k_add_full(const double* __restrict__ X, int ldx, int n, double* __restrict__ Y,
                            int ldy) {
   for (smg_mn it(n, n); it.ok(); it.next()) {
@@ -215,6 +288,12 @@ int smg_gp_exp_quad_cov_fwd(smg_ctx* ctx, const double* x, int n, double sigma, 
   smg_prof_scope prof(ctx, SMG_FAM_GP);
   const double s2 = sigma * sigma;
   const double ihl = 0.5 / (l * l);
+  if (col2_ok(x, 2, n) && col2_ok(K, ldk, n)) {
+    hipLaunchKernelGGL(k_gp_fwd_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, x, n,
+                       s2, ihl, K, ldk);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
   dim3 grid(smg_ceil_div(n, 256) > 16 ? 16 : smg_ceil_div(n, 256), n);
   hipLaunchKernelGGL(k_gp_fwd, grid, dim3(256), 0, ctx->stream, x, n, s2, ihl, K, ldk);
   SMG_LAUNCH_CHECK();
@@ -272,6 +351,12 @@ int smg_add_diag_fwd(smg_ctx* ctx, const double* A, int lda, int n, double d, co
                      double* B, int ldb) {
   if (!ctx || n < 0 || (n > 0 && (!A || !B || lda < n || ldb < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
+  if (col2_ok(A, lda, n) && col2_ok(B, ldb, n)) {
+    hipLaunchKernelGGL(k_add_diag_fwd_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream,
+                       A, lda, n, d, dv, B, ldb);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
   hipLaunchKernelGGL(k_add_diag_fwd, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, A,
                      lda, n, d, dv, B, ldb);
   SMG_LAUNCH_CHECK();

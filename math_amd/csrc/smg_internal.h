@@ -4,6 +4,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "../../include/smg_hip.h"
@@ -55,6 +56,11 @@ struct smg_ctx {
   hipStream_t zero_stream;
   hipEvent_t zero_ev_main, zero_ev_done;
   int zero_pending;
+  // zeroings requested but not yet issued: they are issued at the next
+  // latency-bound entry (the Cholesky panels, the persistent solves) so they
+  // overlap those rather than the HBM-bound element-wise kernels before them,
+  // and at the latest by smg_join_async / an arena rewind (smg_zero_flush)
+  std::vector<std::pair<void*, size_t>> zero_queue;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;
@@ -147,6 +153,8 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
 int smg_status_mark_impl(smg_ctx* ctx);
+// issue the queued smg_memset_async zeroings on the zeroing stream (ctx.hip)
+extern "C" int smg_zero_flush(smg_ctx* ctx);
 int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);
 int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux, int n);
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,

@@ -425,6 +425,8 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
                         const double* W256, const double* W512, int ldw, const double* x, double* y,
                         double* r, int n) {
   if (n <= 0) return SMG_OK;
+  // queued adjoint zeroings overlap this latency-bound solve
+  if (int e = smg_zero_flush(ctx)) return e;
   const bool fits = n / 64 <= 256 && TRSV_FLAG_OFFSET + 2 * (n / 64) <= 4096;
   // forward only: the backward's 512-row form needs 32 more VGPRs per lane
   // than two waves per SIMD leave and spills (100 vs 83 us at n = 4096);

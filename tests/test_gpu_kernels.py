@@ -121,7 +121,25 @@ def test_mfma_layout_asymmetric(ctx):
 
 
 # ------------------------------------------------------- gp_exp_quad_cov
-@pytest.mark.parametrize("n", [1, 2, 33, 300])
+@pytest.mark.parametrize("n,ld", [(1, 1), (33, 35), (300, 300), (301, 302), (2050, 2050), (300, 301)])
+@pytest.mark.parametrize("vec", [0, 1])
+def test_add_diag_fwd(ctx, n, ld, vec):
+    """add_diag (prim/mat/fun/add_diag.hpp:20-55) bit for bit, through the
+    16-byte column form (even n and ld) and the element form."""
+    rng = np.random.default_rng(n + ld + vec)
+    A = rng.uniform(-1, 1, (n, n))
+    d = rng.uniform(0, 2, n)
+    Ap = np.zeros((n, ld)); Ap[:, :n] = A.T        # column-major with leading dimension ld
+    B = np.full(n * ld, 5.0)
+    dB = ctx.put(B)
+    ctx.call("smg_add_diag_fwd", ctx.put(Ap.ravel()), ld, n, 0.25, ctx.put(d) if vec else None, dB, ld)
+    out = ctx.get(dB, n * ld).reshape(n, ld)
+    ref = A + np.diag(d if vec else np.full(n, 0.25))
+    assert np.array_equal(out[:, :n].T, ref)
+    assert np.all(out[:, n:] == 5.0)
+
+
+@pytest.mark.parametrize("n", [1, 2, 33, 300, 2050, 4096])
 def test_gp_cov(ctx, n):
     x = gen.unif(11 + n, n, -10, 10)
     K_ref = np.zeros(n * n)
@@ -649,11 +667,15 @@ def test_handoff_stress_repeat_under_load(ctx):
         other.close()
 
 
-@pytest.mark.parametrize("N", [70, 300, 1000])
-def test_cholesky_fwd_checked(ctx, N):
+@pytest.mark.parametrize("N,bad", [(70, (69, 35)), (300, (299, 150)), (1000, (999, 500)),
+                                   (256, (255, 128)), (1024, (1023, 512)), (1024, (130, 129)),
+                                   (512, (511, 0)), (512, (3, 2))])
+def test_cholesky_fwd_checked(ctx, N, bad):
     """check_symmetric fused with the factorisation's copy: the same L and aux
     as smg_cholesky_fwd on a symmetric input; NOT_SYMMETRIC latched (and the
-    upper triangle of L still zero) on an asymmetric one."""
+    upper triangle of L still zero) on an asymmetric one.  N % 64 == 0 takes
+    the 16-byte form (k_check_symmetric_copy2); the perturbed entry `bad` sits
+    in an off-diagonal tile or inside a diagonal tile."""
     rng = np.random.default_rng(N + 5)
     B = rng.uniform(-1, 1, (N, N))
     A = B @ B.T / N + np.eye(N)
@@ -667,7 +689,9 @@ def test_cholesky_fwd_checked(ctx, N):
     assert ctx.status() == 0
     assert np.array_equal(ctx.get(L1, N * N), ctx.get(L2, N * N))
     assert np.array_equal(ctx.get(D1, na), ctx.get(D2, na))
-    A[N - 1, N // 2] += 1e-6
+    Lref = np.linalg.cholesky(A)
+    assert np.allclose(ctx.get(L2, N * N).reshape(N, N, order="F"), Lref, rtol=0, atol=1e-12)
+    A[bad] += 1e-6
     dA = ctx.put(F(A))
     L3 = ctx.put(np.full(N * N, 7.0))
     ctx.call("smg_cholesky_fwd_checked", dA, N, N, L3, N, ctx.zeros(na))
