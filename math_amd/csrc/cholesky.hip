@@ -169,6 +169,38 @@ __global__ void k_add_lower(const double* __restrict__ X, int ldx, int n,
   }
 }
 
+// k_add_lower in the column form (16-byte accesses, whole columns per
+// workgroup, only the row pairs at or below the diagonal touched)
+__global__ __launch_bounds__(256) void k_add_lower_col2(const double* __restrict__ X, int ldx, int n,
+                                                        double* __restrict__ Y, int ldy) {
+  const int np = n >> 1;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double2* x = reinterpret_cast<const double2*>(X + (size_t)j * ldx);
+    double2* y = reinterpret_cast<double2*>(Y + (size_t)j * ldy);
+    const int p1 = j >> 1;  // first pair holding a row >= j
+    for (int p0 = p1 + threadIdx.x; p0 < np; p0 += 4 * 256) {
+      double2 a[4], b[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          a[k] = x[p];
+          b[k] = y[p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          if (2 * p >= j) b[k].x += a[k].x;
+          b[k].y += a[k].y;  // row 2p + 1 >= j for every p >= j / 2
+          y[p] = b[k];
+        }
+      }
+    }
+  }
+}
+
 // factor the diagonal block in place and write its inverse (dense, upper
 // zeros, so GEMMs may read it as a plain matrix); ONE wave
 __global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int ldl, int b,
@@ -1006,8 +1038,13 @@ int smg_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* Dinv,
   int rc = n > 2 * SMG_NBR ? chol_rev_two_level(ctx, L, ldl, aux, n, La, ldla)
                            : chol_rev_blocks(ctx, L, ldl, aux, n, La, ldla, n);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_add_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
-                     La, ldla, n, Aadj, ldaa);
+  if (n % 2 == 0 && ldla % 2 == 0 && ldaa % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(La) | reinterpret_cast<uintptr_t>(Aadj)) & 15) == 0)
+    hipLaunchKernelGGL(k_add_lower_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, La,
+                       ldla, n, Aadj, ldaa);
+  else
+    hipLaunchKernelGGL(k_add_lower, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream,
+                       La, ldla, n, Aadj, ldaa);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

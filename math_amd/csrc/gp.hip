@@ -66,6 +66,60 @@ __global__ __launch_bounds__(256) void k_gp_rev_partials(const double* __restric
   }
 }
 
+// k_gp_rev_partials in the column form (16-byte reads of Kadj and x; a
+// workgroup walks whole columns); the same per-element terms, fixed order.
+__global__ __launch_bounds__(256) void k_gp_rev_partials_col2(const double* __restrict__ x, int n,
+                                                              double s2, double inv_half_sq_l,
+                                                              const double* __restrict__ Ka,
+                                                              int lda, double* __restrict__ part) {
+  __shared__ double lds[16];
+  const int np = n >> 1;
+  const double2* x2 = reinterpret_cast<const double2*>(x);
+  double al = 0.0, as = 0.0;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double xj = x[j];
+    const double2* col = reinterpret_cast<const double2*>(Ka + (size_t)j * lda);
+    for (int p0 = threadIdx.x; p0 < np; p0 += 4 * 256) {
+      double2 a[4], xi[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          a[k] = col[p];
+          xi[k] = x2[p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          const int i = 2 * p;
+          const double av[2] = {a[k].x, a[k].y}, xv[2] = {xi[k].x, xi[k].y};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (i + h == j) {
+              as += av[h] * s2;
+            } else {
+              const double d = (i + h > j) ? xv[h] - xj : xj - xv[h];
+              const double dist = d * d;
+              const double prod = av[h] * (s2 * exp(-dist * inv_half_sq_l));
+              al += prod * dist;
+              as += prod;
+            }
+          }
+        }
+      }
+    }
+  }
+  const double sl = block_sum(al, lds);
+  __syncthreads();
+  const double ss = block_sum(as, lds);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x + 0] = ss;
+    part[2 * blockIdx.x + 1] = sl;
+  }
+}
+
 __global__ void k_gp_rev_final(const double* __restrict__ part, int nparts, double sigma, double l,
                                double* out2) {
   __shared__ double lds[16];
@@ -306,12 +360,18 @@ int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma, 
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_GP);
   const long long tot = (long long)n * n;
-  int nb = grid_for(tot);
+  const bool col2 = col2_ok(x, 2, n) && col2_ok(Kadj, ldka, n);
+  int nb = col2 ? n : grid_for(tot);
   if (nb > GP_BLOCKS) nb = GP_BLOCKS;
   double* part = smg_ws(ctx, SMG_WS_RED, 2 * (size_t)nb);
   if (!part) return SMG_ERR_OOM;
-  hipLaunchKernelGGL(k_gp_rev_partials, dim3(nb), dim3(256), 0, ctx->stream, x, n, sigma * sigma,
-                     0.5 / (l * l), Kadj, ldka, part);
+  if (col2) {
+    hipLaunchKernelGGL(k_gp_rev_partials_col2, dim3(nb), dim3(256), 0, ctx->stream, x, n,
+                       sigma * sigma, 0.5 / (l * l), Kadj, ldka, part);
+  } else {
+    hipLaunchKernelGGL(k_gp_rev_partials, dim3(nb), dim3(256), 0, ctx->stream, x, n, sigma * sigma,
+                       0.5 / (l * l), Kadj, ldka, part);
+  }
   hipLaunchKernelGGL(k_gp_rev_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, sigma, l, out2);
   SMG_LAUNCH_CHECK();
   return SMG_OK;

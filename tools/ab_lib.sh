@@ -12,10 +12,10 @@ cp $LIB /tmp/ab_base.so || exit 1
 rc=0
 for r in 1 2 3; do
   cp /tmp/ab_base.so $LIB
-  timeout -k 10 200 python bench.py --workload $W --no-cpu-baseline --steps 40 > gpurun_out/ab_base.json || { rc=1; break; }
+  timeout -k 10 200 python bench.py --workload $W --no-cpu-baseline --steps ${STEPS:-40} > gpurun_out/ab_base.json || { rc=1; break; }
   python -c "import json;d=json.load(open('gpurun_out/ab_base.json'));print('base', round(d['value'],2), round(d['ms_per_step'],4))"
   cp $GRAFT_REPO_ROOT/var/$V/libsmg_hip.so $LIB
-  timeout -k 10 200 python bench.py --workload $W --no-cpu-baseline --steps 40 > gpurun_out/ab_var.json || { rc=1; break; }
+  timeout -k 10 200 python bench.py --workload $W --no-cpu-baseline --steps ${STEPS:-40} > gpurun_out/ab_var.json || { rc=1; break; }
   python -c "import json;d=json.load(open('gpurun_out/ab_var.json'));print('$V', round(d['value'],2), round(d['ms_per_step'],4))"
 done
 cp /tmp/ab_base.so $LIB
