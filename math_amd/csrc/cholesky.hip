@@ -813,12 +813,15 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
       double* S = G + bb;
       double* T = S + bb;
       const int gb = grid_for((long long)bb);
-      hipLaunchKernelGGL(k_tril_copy, dim3(gb), dim3(256), 0, ctx->stream, Da, ldla, bs, G);
-      // the operands' triangles bound each tile's K range (gemm tri flags):
+      // D^T tril(Dadj) read straight from Dadj, no tril copy: for an output
+      // entry (i, j), i >= j, an entry Dadj_kj of the strict upper (k < j,
+      // written by the [R_adj | D_adj] update) meets (D^T)_ik = D_ki, a stored
+      // zero of L since k < j <= i (finite times zero: the same sums).
+      // The operands' triangles bound each tile's K range (gemm tri flags):
       // D^T upper (2) x tril(Dadj) lower (4), lower output only (mirrored
       // next); D^{-T} upper (2); D^{-1} lower (4).  Measured on MI355X (GP
       // N = 4096, same-box A/B): 221.3 -> 225.4 evals/s
-      rc = smg_gemm_impl(ctx, 1, 0, 1, bs, bs, bs, 1.0, Ld, ldl, G, bs, 0.0, S, bs, 6);  // D^T tril(Dadj)
+      rc = smg_gemm_impl(ctx, 1, 0, 1, bs, bs, bs, 1.0, Ld, ldl, Da, ldla, 0.0, S, bs, 6);
       if (rc) return rc;
       hipLaunchKernelGGL(k_mirror_lower, dim3(gb), dim3(256), 0, ctx->stream, S, bs);
       rc = smg_gemm_impl(ctx, 1, 0, 0, bs, bs, bs, 1.0, Wp, n, S, bs, 0.0, T, bs, 2);  // D^{-T} S
