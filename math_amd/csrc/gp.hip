@@ -221,6 +221,36 @@ inline bool col2_ok(const void* p, int ld, int n) {
   return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (ld % 2 == 0) && (n % 2 == 0);
 }
 
+// Y += X over whole columns, 16-byte accesses (add_diag's reverse, A's adjoint)
+__global__ __launch_bounds__(256) void k_add_full_col2(const double* __restrict__ X, int ldx, int n,
+                                                       double* __restrict__ Y, int ldy) {
+  const int np = n >> 1;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double2* x = reinterpret_cast<const double2*>(X + (size_t)j * ldx);
+    double2* y = reinterpret_cast<double2*>(Y + (size_t)j * ldy);
+    for (int p0 = threadIdx.x; p0 < np; p0 += 4 * 256) {
+      double2 a[4], b[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          a[k] = x[p];
+          b[k] = y[p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          b[k].x += a[k].x;
+          b[k].y += a[k].y;
+          y[p] = b[k];
+        }
+      }
+    }
+  }
+}
+
 __global__ void k_add_full(const double* __restrict__ X, int ldx, int n, double* __restrict__ Y,
                            int ldy) {
   for (smg_mn it(n, n); it.ok(); it.next()) {
@@ -427,7 +457,10 @@ int smg_add_diag_rev(smg_ctx* ctx, const double* Ba, int ldb, int n, double* Aa,
                      double* dadj, int vec) {
   if (!ctx || n < 0 || (n > 0 && !Ba)) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
-  if (Aa)
+  if (Aa && col2_ok(Ba, ldb, n) && col2_ok(Aa, ldaa, n))
+    hipLaunchKernelGGL(k_add_full_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, Ba,
+                       ldb, n, Aa, ldaa);
+  else if (Aa)
     hipLaunchKernelGGL(k_add_full, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, Ba,
                        ldb, n, Aa, ldaa);
   if (dadj)

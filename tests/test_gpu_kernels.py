@@ -139,6 +139,22 @@ def test_add_diag_fwd(ctx, n, ld, vec):
     assert np.all(out[:, n:] == 5.0)
 
 
+@pytest.mark.parametrize("n,ld", [(1, 1), (33, 35), (300, 300), (301, 302), (2050, 2050)])
+def test_add_diag_rev(ctx, n, ld):
+    """add_diag's reverse: A's adjoint += B's adjoint (column form for even n
+    and ld, element form otherwise), the scalar diagonal's adjoint = trace."""
+    rng = np.random.default_rng(3 * n + ld)
+    Ba = rng.uniform(-1, 1, n * ld)
+    Aa0 = rng.uniform(-1, 1, n * ld)
+    dAa, dd = ctx.put(Aa0), ctx.zeros(1)
+    ctx.call("smg_add_diag_rev", ctx.put(Ba), ld, n, dAa, ld, dd, 0)
+    out = ctx.get(dAa, n * ld).reshape(n, ld)
+    ref = (Aa0 + Ba).reshape(n, ld)
+    assert np.array_equal(out[:, :n], ref[:, :n])
+    assert np.array_equal(out[:, n:], Aa0.reshape(n, ld)[:, n:])
+    near_rel(ctx.get(dd, 1)[0], np.trace(Ba.reshape(n, ld)[:, :n]), 1e-13, what="diag adj")
+
+
 @pytest.mark.parametrize("n", [1, 2, 33, 300, 2050, 4096])
 def test_gp_cov(ctx, n):
     x = gen.unif(11 + n, n, -10, 10)
