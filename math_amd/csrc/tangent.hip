@@ -70,6 +70,36 @@ __global__ void k_copy_tril(int m, int n, const double* __restrict__ X, int ldx,
     if (it.i >= it.j) Y[it.i + (size_t)it.j * ldy] = X[it.i + (size_t)it.j * ldx];
 }
 
+// k_copy_tril over whole columns with 16-byte accesses (even ld, 16-byte
+// aligned): only the row pairs at or below the diagonal are touched
+__global__ __launch_bounds__(256) void k_copy_tril_col2(int m, int n, const double* __restrict__ X,
+                                                        int ldx, double* __restrict__ Y, int ldy) {
+  const int mp = m >> 1;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double2* x = reinterpret_cast<const double2*>(X + (size_t)j * ldx);
+    double2* y = reinterpret_cast<double2*>(Y + (size_t)j * ldy);
+    for (int p0 = (j >> 1) + threadIdx.x; p0 < mp; p0 += 4 * 256) {
+      double2 a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < mp) a[k] = x[p];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < mp) {
+          if (2 * p >= j) {
+            y[p] = a[k];
+          } else {  // the pair straddles the diagonal: row 2p + 1 == j only
+            Y[(2 * p + 1) + (size_t)j * ldy] = a[k].y;
+          }
+        }
+      }
+    }
+  }
+}
+
 // out = [lse(x), sum_i exp(x_i - lse) x'_i]
 __global__ __launch_bounds__(TT) void k_lse_tangent_fwd(const double* __restrict__ x, const double* __restrict__ xd,
                                                        long long n, double* __restrict__ out) {
@@ -192,8 +222,13 @@ int smg_copy_tril(smg_ctx* ctx, int m, int n, const double* X, int ldx, double* 
   if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
   if (m == 0 || n == 0) return SMG_OK;
   if (!X || !Y || ldx < m || ldy < m) return SMG_ERR_ARG;
-  hipLaunchKernelGGL(k_copy_tril, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n, X, ldx, Y,
-                     ldy);
+  if (m % 2 == 0 && ldx % 2 == 0 && ldy % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) == 0)
+    hipLaunchKernelGGL(k_copy_tril_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, m, n,
+                       X, ldx, Y, ldy);
+  else
+    hipLaunchKernelGGL(k_copy_tril, dim3(grid_for((long long)m * n)), dim3(256), 0, ctx->stream, m, n,
+                       X, ldx, Y, ldy);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

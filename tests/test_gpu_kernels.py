@@ -139,6 +139,23 @@ def test_add_diag_fwd(ctx, n, ld, vec):
     assert np.all(out[:, n:] == 5.0)
 
 
+@pytest.mark.parametrize("m,n,ld", [(1, 1, 1), (33, 20, 35), (300, 300, 300), (300, 301, 302),
+                                    (2050, 2050, 2050), (64, 200, 64), (301, 300, 301)])
+def test_copy_tril(ctx, m, n, ld):
+    """Y's lower trapezoid <- X's (column form for even m and ld), the rest of
+    Y untouched."""
+    rng = np.random.default_rng(m + 7 * n + ld)
+    X = rng.uniform(-1, 1, n * ld)
+    Y0 = rng.uniform(-1, 1, n * ld)
+    dY = ctx.put(Y0)
+    ctx.call("smg_copy_tril", m, n, ctx.put(X), ld, dY, ld)
+    out = ctx.get(dY, n * ld).reshape(n, ld).T          # out[i, j] = Y(i, j)
+    Xm, Ym = X.reshape(n, ld).T, Y0.reshape(n, ld).T
+    i, j = np.indices((ld, n))
+    ref = np.where((i >= j) & (i < m), Xm, Ym)
+    assert np.array_equal(out, ref)
+
+
 @pytest.mark.parametrize("n,ld", [(1, 1), (33, 35), (300, 300), (301, 302), (2050, 2050)])
 def test_add_diag_rev(ctx, n, ld):
     """add_diag's reverse: A's adjoint += B's adjoint (column form for even n
