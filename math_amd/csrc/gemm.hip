@@ -531,6 +531,20 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   //   (512,512,512) 11.5 (32x32) / 10.2 (32x32 KS=2)
   // (and a 64 x 64 grid below 256 tiles, split over K or not, loses to 32 x 32:
   // (3584,256,256) 18.6 vs 28 us)
+  {  // dev: the tile of the large triangle outputs (HVP's N x N lower products)
+    static const int tri_tile = [] {
+      const char* e = getenv("SMG_GEMM_TRI");
+      return e ? atoi(e) : 0;
+    }();
+    if (MODE != 0 && mid_tiles > SMG_GEMM_KS2_MAX && tri_tile) {
+      if (tri_tile == 12864)
+        return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+      if (tri_tile == 128)
+        return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+      if (tri_tile == 6402)
+        return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
+    }
+  }
   if (mid_tiles >= 512) {
     if (mid_tiles <= SMG_GEMM_KS2_MAX)
       return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
