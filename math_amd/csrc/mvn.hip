@@ -60,6 +60,48 @@ __global__ void k_mvn_rev_lower(const double* __restrict__ L, int ldl, int n,
   }
 }
 
+// k_mvn_rev_lower over whole columns with 16-byte accesses (even n and ldla,
+// 16-byte aligned La and sd); the same per-element expression
+__global__ __launch_bounds__(256) void k_mvn_rev_lower_col2(const double* __restrict__ L, int ldl,
+                                                            int n, const double* __restrict__ w,
+                                                            const double* __restrict__ sd,
+                                                            double adj, double* __restrict__ La,
+                                                            int ldla) {
+  const int np = n >> 1;
+  const double2* sd2 = reinterpret_cast<const double2*>(sd);
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double wj = w[j];
+    double2* col = reinterpret_cast<double2*>(La + (size_t)j * ldla);
+    for (int p0 = (j >> 1) + threadIdx.x; p0 < np; p0 += 4 * 256) {
+      double2 a[4], s[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          a[k] = col[p];
+          s[k] = sd2[p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          const int i = 2 * p;
+          if (i >= j) {
+            double g = s[k].x * wj;
+            if (i == j) g -= 1.0 / L[i + (size_t)i * ldl];
+            a[k].x += adj * g;
+          }
+          double g = s[k].y * wj;
+          if (i + 1 == j) g -= 1.0 / L[(i + 1) + (size_t)(i + 1) * ldl];
+          a[k].y += adj * g;
+          col[p] = a[k];
+        }
+      }
+    }
+  }
+}
+
 // Ladj += adj*(sd w^T - Linv^T) over every entry; Linv given (lower, dense)
 __global__ void k_mvn_rev_full(const double* __restrict__ Linv, int n, const double* __restrict__ w,
                                const double* __restrict__ sd, double adj, double* __restrict__ La,
@@ -142,8 +184,13 @@ int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl, const double* D
   if (muadj) hipLaunchKernelGGL(k_axpy_vec, dim3(grid_for(n)), dim3(256), 0, ctx->stream, n, adj, sd, muadj);
   if (Ladj) {
     if (lower_only) {
-      hipLaunchKernelGGL(k_mvn_rev_lower, dim3(grid_for((long long)n * n)), dim3(256), 0,
-                         ctx->stream, L, ldl, n, w, sd, adj, Ladj, ldla);
+      if (n % 2 == 0 && ldla % 2 == 0 &&
+          ((reinterpret_cast<uintptr_t>(Ladj) | reinterpret_cast<uintptr_t>(sd)) & 15) == 0)
+        hipLaunchKernelGGL(k_mvn_rev_lower_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0,
+                           ctx->stream, L, ldl, n, w, sd, adj, Ladj, ldla);
+      else
+        hipLaunchKernelGGL(k_mvn_rev_lower, dim3(grid_for((long long)n * n)), dim3(256), 0,
+                           ctx->stream, L, ldl, n, w, sd, adj, Ladj, ldla);
     } else {
       double* Linv = smg_ws(ctx, SMG_WS_TMP, (size_t)n * n);
       if (!Linv) return SMG_ERR_OOM;
