@@ -155,6 +155,17 @@ int smg_gp_exp_quad_cov_fwd(smg_ctx* ctx, const double* x, int n, double sigma,
 int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma,
                             double l, const double* Kadj, int ldka, double* out2);
 
+/* gp_exp_quad_cov(std::vector<VectorXd> x, var|double sigma, var l) with
+ * D-dimensional points (rev/mat/fun/gp_exp_quad_cov.hpp:158-184 forward via
+ * squared_distance, :96-112 chain, :211-286 the overloads): x is D x n
+ * column-major (point i at x + i D), K_ij = sigma^2 exp(-|x_i - x_j|^2 / (2 l^2)).
+ * Same outputs as the scalar-x pair above (D == 1 is that pair); D x n
+ * doubles of one point are staged in LDS (D <= 8192). */
+int smg_gp_exp_quad_cov_nd_fwd(smg_ctx* ctx, const double* x, int D, int n, double sigma,
+                               double l, double* K, int ldk);
+int smg_gp_exp_quad_cov_nd_rev(smg_ctx* ctx, const double* x, int D, int n, double sigma,
+                               double l, const double* Kadj, int ldka, double* out2);
+
 /* Tangent of the same covariance along (sigma', l') -- what the fvar<var>
  * instantiation of gp_exp_quad_cov computes inside hessian_times_vector
  * (mix/mat/functor/hessian_times_vector.hpp:13-40):
@@ -271,9 +282,10 @@ int smg_log_determinant_rev(smg_ctx* ctx, const double* LU, const int* piv,
  *     eta_i + alpha (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:117-123).
  *     rev: eta_adj += adj d'(theta) (etad + alphad), etad_adj += adj d;
  *     out[0], out[1] = their sums (alpha's and alphad's adjoints). */
-/* Y(i >= j) = X(i >= j) (m x n); Y's strict upper triangle is left alone.
- * The work copy of L's adjoint that smg_cholesky_rev overwrites (it reads the
- * lower triangle only): half of a full copy's traffic. */
+/* Y = tril(X) (m x n): Y(i >= j) = X(i >= j), Y's strict upper triangle is
+ * stored as zeros (write-only).  The work copy of L's adjoint that
+ * smg_cholesky_rev overwrites: it reads the lower triangle of X only, and the
+ * Murray reverse may read the work matrix's strict upper as stored zeros. */
 int smg_copy_tril(smg_ctx* ctx, int m, int n, const double* X, int ldx, double* Y, int ldy);
 int smg_add_tril(smg_ctx* ctx, int m, int n, double alpha, const double* X,
                  int ldx, double* Y, int ldy);

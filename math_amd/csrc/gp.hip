@@ -354,6 +354,71 @@ __global__ void k_gp_tan_final(const double* __restrict__ part, int nparts, doub
   }
 }
 
+
+// D-dimensional inputs (gp_exp_quad_cov(std::vector<T_x> x, ...) with T_x an
+// Eigen vector, rev/mat/fun/gp_exp_quad_cov.hpp:158-184,211-242): x is D x n
+// column-major (point i at x + i D), d_ij^2 = squared_distance(x_i, x_j)
+// summed over the D coordinates in order.  A workgroup walks whole columns j;
+// x_j is staged in LDS, the row points are read from L2 (x is n D doubles).
+__global__ __launch_bounds__(256) void k_gp_nd_fwd(const double* __restrict__ x, int D, int n, double s2,
+                                                   double inv_half_sq_l, double* __restrict__ K, int ldk) {
+  extern __shared__ double xj[];
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x) xj[d] = x[(size_t)j * D + d];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      double v = s2;
+      if (i != j) {
+        const double* xi = x + (size_t)i * D;
+        double d2 = 0.0;
+        for (int d = 0; d < D; ++d) {
+          const double t = xi[d] - xj[d];
+          d2 += t * t;
+        }
+        v = s2 * exp(-d2 * inv_half_sq_l);
+      }
+      K[i + (size_t)j * ldk] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gp_nd_rev_partials(const double* __restrict__ x, int D, int n, double s2,
+                                                            double inv_half_sq_l, const double* __restrict__ Ka,
+                                                            int lda, double* __restrict__ part) {
+  extern __shared__ double xj[];
+  __shared__ double lds[16];
+  double al = 0.0, as = 0.0;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x) xj[d] = x[(size_t)j * D + d];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const double a = Ka[i + (size_t)j * lda];
+      if (i == j) {
+        as += a * s2;
+      } else {
+        const double* xi = x + (size_t)i * D;
+        double d2 = 0.0;
+        for (int d = 0; d < D; ++d) {
+          const double t = xi[d] - xj[d];
+          d2 += t * t;
+        }
+        const double prod = a * (s2 * exp(-d2 * inv_half_sq_l));
+        al += prod * d2;
+        as += prod;
+      }
+    }
+  }
+  const double sl = block_sum(al, lds);
+  __syncthreads();
+  const double ss = block_sum(as, lds);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x + 0] = ss;
+    part[2 * blockIdx.x + 1] = sl;
+  }
+}
+
 inline int grid_for(long long tot) {
   long long g = (tot + 255) / 256;
   if (g > 8192) g = 8192;
@@ -402,6 +467,34 @@ int smg_gp_exp_quad_cov_rev(smg_ctx* ctx, const double* x, int n, double sigma, 
     hipLaunchKernelGGL(k_gp_rev_partials, dim3(nb), dim3(256), 0, ctx->stream, x, n, sigma * sigma,
                        0.5 / (l * l), Kadj, ldka, part);
   }
+  hipLaunchKernelGGL(k_gp_rev_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, sigma, l, out2);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_gp_exp_quad_cov_nd_fwd(smg_ctx* ctx, const double* x, int D, int n, double sigma, double l, double* K,
+                               int ldk) {
+  if (!ctx || n < 0 || D < 1 || D > 8192 || (n > 0 && (!x || !K || ldk < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (D == 1) return smg_gp_exp_quad_cov_fwd(ctx, x, n, sigma, l, K, ldk);
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  hipLaunchKernelGGL(k_gp_nd_fwd, dim3(n < 2048 ? n : 2048), dim3(256), D * sizeof(double), ctx->stream, x, D, n,
+                     sigma * sigma, 0.5 / (l * l), K, ldk);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_gp_exp_quad_cov_nd_rev(smg_ctx* ctx, const double* x, int D, int n, double sigma, double l,
+                               const double* Kadj, int ldka, double* out2) {
+  if (!ctx || n < 0 || D < 1 || D > 8192 || (n > 0 && (!x || !Kadj || !out2 || ldka < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (D == 1) return smg_gp_exp_quad_cov_rev(ctx, x, n, sigma, l, Kadj, ldka, out2);
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  const int nb = n < GP_BLOCKS ? n : GP_BLOCKS;
+  double* part = smg_ws(ctx, SMG_WS_RED, 2 * (size_t)nb);
+  if (!part) return SMG_ERR_OOM;
+  hipLaunchKernelGGL(k_gp_nd_rev_partials, dim3(nb), dim3(256), D * sizeof(double), ctx->stream, x, D, n,
+                     sigma * sigma, 0.5 / (l * l), Kadj, ldka, part);
   hipLaunchKernelGGL(k_gp_rev_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, sigma, l, out2);
   SMG_LAUNCH_CHECK();
   return SMG_OK;

@@ -65,20 +65,25 @@ __global__ void k_add_tril(int m, int n, double alpha, const double* __restrict_
     if (it.i >= it.j) Y[it.i + (size_t)it.j * ldy] += alpha * X[it.i + (size_t)it.j * ldx];
 }
 
+// Y = tril(X): the strict upper triangle of Y is written with zeros (Y is a
+// fresh arena buffer whose upper half the Murray reverse reads as stored
+// zeros of the work matrix; recycled arena memory may hold NaN / Inf there)
 __global__ void k_copy_tril(int m, int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy) {
   for (smg_mn it(m, n); it.ok(); it.next())
-    if (it.i >= it.j) Y[it.i + (size_t)it.j * ldy] = X[it.i + (size_t)it.j * ldx];
+    Y[it.i + (size_t)it.j * ldy] = it.i >= it.j ? X[it.i + (size_t)it.j * ldx] : 0.0;
 }
 
 // k_copy_tril over whole columns with 16-byte accesses (even ld, 16-byte
-// aligned): only the row pairs at or below the diagonal are touched
+// aligned): row pairs above the diagonal are stored as zeros without a read
 __global__ __launch_bounds__(256) void k_copy_tril_col2(int m, int n, const double* __restrict__ X,
                                                         int ldx, double* __restrict__ Y, int ldy) {
   const int mp = m >> 1;
   for (int j = blockIdx.x; j < n; j += gridDim.x) {
     const double2* x = reinterpret_cast<const double2*>(X + (size_t)j * ldx);
     double2* y = reinterpret_cast<double2*>(Y + (size_t)j * ldy);
-    for (int p0 = (j >> 1) + threadIdx.x; p0 < mp; p0 += 4 * 256) {
+    const int pz = j >> 1;  // pairs p < pz lie wholly above the diagonal
+    for (int p = threadIdx.x; p < (pz < mp ? pz : mp); p += 256) y[p] = make_double2(0.0, 0.0);
+    for (int p0 = pz + threadIdx.x; p0 < mp; p0 += 4 * 256) {
       double2 a[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -89,11 +94,8 @@ __global__ __launch_bounds__(256) void k_copy_tril_col2(int m, int n, const doub
       for (int k = 0; k < 4; ++k) {
         const int p = p0 + 256 * k;
         if (p < mp) {
-          if (2 * p >= j) {
-            y[p] = a[k];
-          } else {  // the pair straddles the diagonal: row 2p + 1 == j only
-            Y[(2 * p + 1) + (size_t)j * ldy] = a[k].y;
-          }
+          if (2 * p < j) a[k].x = 0.0;  // the pair straddles the diagonal: row 2p + 1 == j only
+          y[p] = a[k];
         }
       }
     }

@@ -136,8 +136,10 @@ inline void check(int rc, const char* function, const char* what = "") {
 }
 
 /** After a status word read with smg_status_enqueue: a timed-out hand-off
- * (SMG_ERR_SYNC) throws here, after clearing the latch; other latched bits
- * (domain errors) stay for the functor that checks them (smg_status). */
+ * (SMG_ERR_SYNC) throws here.  smg_status clears the WHOLE latch first, so
+ * any domain bits latched with it are dropped: the evaluation is abandoned
+ * (its values are not trustworthy after a failed hand-off) and the next one
+ * starts from a clean status word. */
 inline void throw_if_sync(int st, const char* function, const char* what) {
   if (__builtin_expect(!(st & SMG_ERR_SYNC), 1)) return;
   int cleared = 0;

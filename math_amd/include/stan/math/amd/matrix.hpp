@@ -16,10 +16,14 @@
 //   dev_data         a device copy of constant data (double or int)
 
 #include <stan/math/amd/device.hpp>
+#include <stan/math/amd/host_parallel.hpp>
 #include <stan/math/rev/core/grad.hpp>
 #include <stan/math/rev/core/var.hpp>
 #include <stan/math/rev/core/vari.hpp>
 
+#include <cmath>
+#include <new>
+#include <sstream>
 #include <stdexcept>
 #include <vector>
 
@@ -125,6 +129,20 @@ inline dev_data<int> to_dev_data(const std::vector<int>& v) {
   return dev_data<int>(d, v.size(), int(v.size()), 1);
 }
 
+namespace internal {
+/** One operand of a matrix functor: a device var node or constant device data. */
+struct dev_operand {
+  dev_matrix_vari* vi = nullptr;  // null for data
+  const double* data = nullptr;
+  int rows = 0, cols = 0;
+  const double* val() const { return vi ? vi->val_ : data; }
+  double* adj() const { return vi ? vi->adj_ : nullptr; }
+  size_t size() const { return size_t(rows) * size_t(cols); }
+};
+inline dev_operand operand(const dev_var_matrix& m) { return dev_operand{m.vi_, nullptr, m.rows(), m.cols()}; }
+inline dev_operand operand(const dev_data<double>& d) { return dev_operand{nullptr, d.data(), d.rows(), d.cols()}; }
+}  // namespace internal
+
 /** A fresh device matrix of vars initialised from host values (a leaf:
  * its adjoint is read back by the caller, like x_var in gradient()). */
 inline dev_var_matrix to_dev_var_matrix(const double* host_colmajor, int rows, int cols) {
@@ -134,37 +152,147 @@ inline dev_var_matrix to_dev_var_matrix(const double* host_colmajor, int rows, i
 }
 
 namespace internal {
-// device -> host varis (reverse: host adjoints -> device adjoint)
+
+/** The host block (if any) that vari pointer range d[0..n) mirrors exactly:
+ * element i is block.first + i (a lower-structured node: the block's dummy
+ * above the diagonal).  The full pointer check runs on every call (a caller
+ * may have replaced single elements); it is one parallel read of n pointers. */
+inline dev_matrix_vari* recognise_block(const var* d, size_t n, int rows, int cols) {
+  if (n == 0) return nullptr;
+  auto& blocks = ChainableStack::instance_->host_blocks_;
+  const vari* v0 = d[0].vi_;
+  for (size_t k = blocks.size(); k-- > 0;) {
+    const host_block& b = blocks[k];
+    if (b.first != v0) continue;
+    if (b.n != n || b.rows != rows || b.cols != cols) return nullptr;
+    const vari* first = b.first;
+    const vari* dummy = b.dummy;
+    const size_t r = size_t(rows);
+    const bool ok = host_parallel_all(n, [&](size_t lo, size_t hi) {
+      if (!dummy) {
+        for (size_t i = lo; i < hi; ++i)
+          if (d[i].vi_ != first + i) return false;
+        return true;
+      }
+      for (size_t i = lo; i < hi; ++i) {
+        const size_t row = i % r, col = i / r;
+        if (d[i].vi_ != (row >= col ? first + i : dummy)) return false;
+      }
+      return true;
+    });
+    return ok ? static_cast<dev_matrix_vari*>(b.node) : nullptr;
+  }
+  return nullptr;
+}
+
+// The bridge of a host block: in the reverse sweep, the host adjoints of the
+// block's varis are gathered into the device node's adjoint -- unless no node
+// chained after the block touched them (device consumers of the recognised
+// node add into its device adjoint directly) and no device->host pending
+// adjoint landed in it, in which case they are all still zero.
 class dev_to_host_vari : public vari {
  public:
-  dev_matrix_vari* src_;
-  vari** elems_;
-  double* stage_;  // device scratch for the gathered adjoints
-  dev_to_host_vari(dev_matrix_vari* src, vari** elems)
-      : vari(0.0), src_(src), elems_(elems), stage_(amd::alloc_doubles(src->size())) {}
+  size_t blk_;  // index in host_blocks_
+  size_t pos_;  // this node's index in var_stack_
+  explicit dev_to_host_vari(size_t blk)
+      : vari(0.0), blk_(blk), pos_(ChainableStack::instance_->var_stack_.size() - 1) {}
   bool reads_other_adjoints() const override { return true; }
+  bool touches_adjoints_in(const vari*, const vari*) const override { return false; }
   void chain() override {
-    const size_t n = src_->size();
-    std::vector<double> h(n);
-    for (size_t i = 0; i < n; ++i) h[i] = elems_[i]->adj_;
-    amd::to_device(stage_, h.data(), n);
-    amd::check(smg_axpy(amd::ctx(), (long long)n, 1.0, stage_, 1, src_->adj_, 1), "to_host");
+    auto* st = ChainableStack::instance_;
+    const host_block b = st->host_blocks_[blk_];
+    const vari* lo = b.first;
+    const vari* hi = b.first + b.n;
+    bool touched = b.dirty;
+    for (size_t i = pos_ + 1; !touched && i < st->var_stack_.size(); ++i)
+      touched = st->var_stack_[i]->touches_adjoints_in(lo, hi);
+    if (!touched) return;
+    smg_ctx* c = amd::ctx();
+    double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
+    if (!stage) throw std::bad_alloc();
+    const size_t r = size_t(b.rows);
+    const bool lower = b.dummy != nullptr;
+    host_parallel_for(b.n, [&](size_t s, size_t e) {
+      for (size_t i = s; i < e; ++i) stage[i] = (!lower || i % r >= i / r) ? b.first[i].adj_ : 0.0;
+    });
+    double* dst = amd::alloc_doubles(b.n);
+    auto* node = static_cast<dev_matrix_vari*>(b.node);
+    amd::check(smg_memcpy_h2d(c, dst, stage, b.n * sizeof(double)), "to_host");
+    amd::check(smg_axpy(c, (long long)b.n, 1.0, dst, 1, node->adj_, 1), "to_host");
+    amd::check(smg_sync(c), "to_host");  // the staging buffer is reused by the next host copy
   }
 };
 
+/**
+ * Materialise device node m as n contiguous host varis (off every stack; the
+ * tape's host_blocks_ owns them) plus one bridge vari on var_stack_.  The
+ * values come down in one copy; the varis are constructed in parallel.
+ * Returns the block (element i = first + i; a lower-structured node's strict
+ * upper triangle is the one dummy vari, like cholesky_decompose.hpp:34-48).
+ */
+inline const host_block& materialise(dev_matrix_vari* m) {
+  auto* st = ChainableStack::instance_;
+  const size_t n = m->size();
+  vari* first = static_cast<vari*>(st->memalloc_.alloc((n ? n : 1) * sizeof(vari)));
+  const bool lower = m->structure_ == dev_structure::lower;
+  vari* dummy = lower ? new vari(0.0, vari::unstacked_tag{}) : nullptr;
+  if (n) {
+    smg_ctx* c = amd::ctx();
+    int armed = 0;
+    amd::check(smg_status_armed(c, &armed), "to_host");
+    double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
+    if (!stage) throw std::bad_alloc();
+    amd::check(smg_memcpy_d2h(c, stage, m->val_, n * sizeof(double)), "to_host");
+    if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(stage + n)), "to_host");
+    amd::check(smg_sync(c), "to_host");
+    if (armed) amd::throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
+    host_parallel_for(n, [&](size_t s, size_t e) {
+      for (size_t i = s; i < e; ++i) ::new (static_cast<void*>(first + i)) vari(stage[i], vari::unstacked_tag{});
+    });
+  }
+  st->host_blocks_.push_back(host_block{first, n, m, dummy, m->rows_, m->cols_, false});
+  new dev_to_host_vari(st->host_blocks_.size() - 1);
+  return st->host_blocks_.back();
+}
+
 // host varis -> device (reverse: device adjoint -> host adjoints)
-class host_to_dev_vari : public vari {
+class host_to_dev_vari : public local_adjoint_vari {
  public:
   dev_matrix_vari* dst_;
   vari** elems_;
-  host_to_dev_vari(dev_matrix_vari* dst, vari** elems) : vari(0.0), dst_(dst), elems_(elems) {}
+  host_to_dev_vari(dev_matrix_vari* dst, vari** elems) : local_adjoint_vari(0.0), dst_(dst), elems_(elems) {}
+  bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
+    const size_t n = dst_->size();
+    return !host_parallel_all(n, [&](size_t s, size_t e) {
+      for (size_t i = s; i < e; ++i)
+        if (elems_[i] >= lo && elems_[i] < hi) return false;
+      return true;
+    });
+  }
   void chain() override {
     const size_t n = dst_->size();
-    std::vector<double> h(n);
-    amd::to_host(h.data(), dst_->adj_, n);
+    if (!n) return;
+    smg_ctx* c = amd::ctx();
+    int armed = 0;
+    amd::check(smg_status_armed(c, &armed), "to_dev");
+    double* h = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
+    if (!h) throw std::bad_alloc();
+    amd::check(smg_memcpy_d2h(c, h, dst_->adj_, n * sizeof(double)), "to_dev");
+    if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(h + n)), "to_dev");
+    amd::check(smg_sync(c), "to_dev");
+    if (armed) amd::throw_if_sync(*reinterpret_cast<int*>(h + n), "to_dev", "a persistent solve");
+    // elements may alias one vari (e.g. a broadcast mean): a serial scatter
     for (size_t i = 0; i < n; ++i) elems_[i]->adj_ += h[i];
   }
 };
+
+/** Host vars d[0..n) (column-major rows x cols) -> device node: the node a
+ * host block mirrors when d is exactly that block, else a gathered copy
+ * bridged by host_to_dev_vari.  nan_fn != null: the reference's
+ * check_not_nan(nan_fn, nan_name, x) on the values first (throws before the
+ * tape is touched; a recognised node is checked on the device). */
+inline dev_var_matrix to_dev_vars(const var* d, size_t n, int rows, int cols, const char* nan_fn = nullptr,
+                                  const char* nan_name = nullptr);
 }  // namespace internal
 
 /** Host vars (column-major; a column vector by default) -> device node
@@ -173,31 +301,63 @@ inline dev_var_matrix to_dev(const std::vector<var>& v, int rows = -1, int cols 
   const size_t n = v.size();
   if (rows < 0) rows = int(n);
   if (size_t(rows) * size_t(cols) != n) throw std::invalid_argument("to_dev: rows * cols != size");
-  auto* d = new dev_matrix_vari(rows, cols);
-  std::vector<double> vals(n);
-  vari** elems = ChainableStack::instance_->memalloc_.alloc_array<vari*>(n ? n : 1);
-  for (size_t i = 0; i < n; ++i) {
-    vals[i] = v[i].val();
-    elems[i] = v[i].vi_;
-  }
-  amd::to_device(d->val_, vals.data(), n);
-  new internal::host_to_dev_vari(d, elems);
-  return dev_var_matrix(d);
+  return internal::to_dev_vars(v.data(), n, rows, cols);
 }
 
 /** Device node -> host vars, column-major (bridged in the reverse sweep). */
 inline std::vector<var> to_var_vector(const dev_var_matrix& m) {
-  const size_t n = m.size();
-  std::vector<double> vals = m.val();
-  vari** elems = ChainableStack::instance_->memalloc_.alloc_array<vari*>(n ? n : 1);
-  std::vector<var> out(n);
-  for (size_t i = 0; i < n; ++i) {
-    elems[i] = new vari(vals[i], false);
-    out[i] = var(elems[i]);
-  }
-  new internal::dev_to_host_vari(m.vi_, elems);
+  const host_block& b = internal::materialise(m.vi_);
+  std::vector<var> out(b.n);
+  const size_t r = size_t(b.rows);
+  for (size_t i = 0; i < b.n; ++i) out[i] = var((b.dummy && i % r < i / r) ? b.dummy : b.first + i);
   return out;
 }
+
+namespace internal {
+inline void throw_not_nan(const char* fn, const char* name, size_t i) {
+  std::ostringstream m;
+  m << fn << ": " << name << "[" << i + 1 << "] is nan, but must not be nan!";
+  throw std::domain_error(m.str());
+}
+
+inline dev_var_matrix to_dev_vars(const var* d, size_t n, int rows, int cols, const char* nan_fn,
+                                  const char* nan_name) {
+  if (dev_matrix_vari* node = recognise_block(d, n, rows, cols)) {
+    if (nan_fn) {  // check_not_nan on the device values (one flag read back)
+      smg_ctx* c = amd::ctx();
+      double* flag = amd::alloc_doubles(1);
+      amd::check(smg_memset(c, flag, 0, sizeof(double)), nan_fn);
+      amd::check(smg_check_domain(c, node->val_, (long long)n, 0, flag), nan_fn);
+      double f = 0;
+      amd::to_host(&f, flag, 1);
+      if (f != 0.0)
+        for (size_t i = 0; i < n; ++i)
+          if (std::isnan(d[i].vi_->val_)) throw_not_nan(nan_fn, nan_name, i);
+    }
+    return dev_var_matrix(node);
+  }
+  smg_ctx* c = amd::ctx();
+  double* stage = n ? static_cast<double*>(smg_host_scratch(c, n * sizeof(double))) : nullptr;
+  if (n && !stage) throw std::bad_alloc();
+  vari** elems = ChainableStack::instance_->memalloc_.alloc_array<vari*>(n ? n : 1);
+  host_parallel_for(n, [&](size_t s, size_t e) {
+    for (size_t i = s; i < e; ++i) {
+      elems[i] = d[i].vi_;
+      stage[i] = d[i].vi_->val_;
+    }
+  });
+  if (nan_fn)
+    for (size_t i = 0; i < n; ++i)
+      if (std::isnan(stage[i])) throw_not_nan(nan_fn, nan_name, i);
+  auto* node = new dev_matrix_vari(rows, cols);
+  if (n) {
+    amd::check(smg_memcpy_h2d(c, node->val_, stage, n * sizeof(double)), "to_dev");
+    amd::check(smg_sync(c), "to_dev");
+  }
+  new host_to_dev_vari(node, elems);
+  return dev_var_matrix(node);
+}
+}  // namespace internal
 
 }  // namespace math
 }  // namespace stan

@@ -77,13 +77,13 @@ namespace internal {
 // tiles, K ranges cut to the triangles, N^3/3 flops); the reverse reads only
 // the lower triangle of C's adjoint and writes only the lower triangles of
 // L's and Phi's (both lower-structured: their upper adjoints are never read).
-class multiply_lower_dev_vari : public vari {
+class multiply_lower_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* B_;
   dev_matrix_vari* C_;
   multiply_lower_dev_vari(dev_matrix_vari* A, dev_matrix_vari* B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, B->cols_, dev_structure::lower)) {
+      : device_vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, B->cols_, dev_structure::lower)) {
     const int n = A->rows_;
     amd::check(smg_multiply_lower_fwd(amd::ctx(), A_->val_, n, B_->val_, n, n, C_->val_, n), "multiply");
   }
@@ -99,13 +99,13 @@ class multiply_lower_dev_vari : public vari {
 
 namespace internal {
 // C = A + B (same shape)
-class add_dev_vari : public vari {
+class add_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* B_;
   dev_matrix_vari* C_;
   add_dev_vari(dev_matrix_vari* A, dev_matrix_vari* B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, A->cols_)) {
+      : device_vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A->rows_, A->cols_)) {
     smg_ctx* c = amd::ctx();
     amd::check(smg_copy_matrix(c, A->rows_, A->cols_, A->val_, A->rows_, C_->val_, C_->rows_, 0, 0), "add");
     amd::check(smg_axpy(c, (long long)C_->size(), 1.0, B->val_, 1, C_->val_, 1), "add");
@@ -118,12 +118,12 @@ class add_dev_vari : public vari {
 };
 
 // C = tril(A): the lower triangle (diagonal included), zeros above
-class tril_dev_vari : public vari {
+class tril_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* C_;
   explicit tril_dev_vari(dev_matrix_vari* A)
-      : vari(0.0), A_(A), C_(new dev_matrix_vari(A->rows_, A->cols_, dev_structure::lower)) {
+      : device_vari(0.0), A_(A), C_(new dev_matrix_vari(A->rows_, A->cols_, dev_structure::lower)) {
     smg_ctx* c = amd::ctx();
     amd::zero(C_->val_, C_->size());
     amd::check(smg_add_tril(c, A->rows_, A->cols_, 1.0, A->val_, A->rows_, C_->val_, C_->rows_), "tril");
@@ -135,13 +135,13 @@ class tril_dev_vari : public vari {
 };
 
 // t = softmax(x) . x' (a var of x and x')
-class lse_tangent_dev_vari : public vari {
+class lse_tangent_dev_vari : public device_vari {
  public:
   dev_matrix_vari* x_;
   dev_matrix_vari* xd_;
   double lse_;
   lse_tangent_dev_vari(double t, double lse, dev_matrix_vari* x, dev_matrix_vari* xd)
-      : vari(t), x_(x), xd_(xd), lse_(lse) {}
+      : device_vari(t), x_(x), xd_(xd), lse_(lse) {}
   void chain() override {
     amd::check(smg_lse_tangent_rev(amd::ctx(), x_->val_, xd_->val_, (long long)x_->size(), lse_, val_, adj_,
                                    x_->adj_, xd_->adj_),
@@ -150,7 +150,7 @@ class lse_tangent_dev_vari : public vari {
 };
 
 // t = sum_i d(eta_i + alpha) (eta'_i + alpha') of the bernoulli logit GLM
-class glm_tangent_dev_vari : public vari {
+class glm_tangent_dev_vari : public device_vari {
  public:
   dev_matrix_vari* eta_;
   dev_matrix_vari* etad_;
@@ -161,7 +161,7 @@ class glm_tangent_dev_vari : public vari {
   double* out2_;
   glm_tangent_dev_vari(double t, dev_matrix_vari* eta, dev_matrix_vari* etad, vari* alpha, vari* alphad, double a,
                        double ad, const int* y)
-      : vari(t), eta_(eta), etad_(etad), alpha_(alpha), alphad_(alphad), a_(a), ad_(ad), y_(y),
+      : device_vari(t), eta_(eta), etad_(etad), alpha_(alpha), alphad_(alphad), a_(a), ad_(ad), y_(y),
         out2_(amd::alloc_doubles(2)) {}
   void chain() override {
     amd::check(smg_glm_tangent_rev(amd::ctx(), eta_->val_, a_, etad_->val_, ad_, y_, (long long)eta_->size(), adj_,

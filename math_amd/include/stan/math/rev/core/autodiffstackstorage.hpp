@@ -18,6 +18,8 @@
 //   nested_dev_marks_   device-arena marks per nesting level
 //   pending_            device -> host adjoint contributions that must land in
 //                       host vari::adj_ before the next host chain() runs.
+//   host_blocks_        device nodes materialised as contiguous host varis at
+//                       an Eigen boundary (recognised again by to_dev).
 
 #include <stan/math/memory/stack_alloc.hpp>
 
@@ -37,6 +39,17 @@ struct dev_buffer {
 struct pending_adjoint {
   vari* target;       // host vari whose adj_ receives the value
   const double* src;  // device scalar
+};
+/** A device matrix node materialised as host varis (stan/math/eigen/bridge.hpp):
+ * n contiguous nochain varis in the arena, column-major, registered here
+ * instead of on var_nochain_stack_ (zeroed by set_zero_all_adjoints). */
+struct host_block {
+  vari* first;   // element i is first + i (a lower-structured node: i on or below the diagonal)
+  size_t n;
+  void* node;    // the dev_matrix_vari it mirrors
+  vari* dummy;   // the shared vari of a lower-structured node's upper triangle, else null
+  int rows, cols;
+  bool dirty;    // a landed device->host pending adjoint targeted one of its varis
 };
 
 template <typename ChainableT, typename ChainableAllocT>
@@ -60,6 +73,8 @@ struct AutodiffStackSingleton {
     std::vector<size_t> nested_dev_adj_sizes_;
     std::vector<size_t> nested_dev_marks_;
     std::vector<pending_adjoint> pending_;
+    std::vector<host_block> host_blocks_;
+    std::vector<size_t> nested_host_block_sizes_;
   };
 
   AutodiffStackSingleton() : own_instance_(init()) {}
@@ -72,10 +87,18 @@ struct AutodiffStackSingleton {
   AutodiffStackSingleton(const AutodiffStackSingleton_t&) = delete;
   AutodiffStackSingleton& operator=(const AutodiffStackSingleton_t&) = delete;
 
-  // initial-exec TLS: the tape pointer is read on every var construction and
-  // every chain() of the sweep; in a shared library the default
-  // (general-dynamic) model would make each read a __tls_get_addr call
+  // The tape pointer is read on every var construction and every chain() of
+  // the sweep.  Executables get the local-exec model by default; a shared
+  // library built with STAN_MATH_AMD_TLS_INITIAL_EXEC uses initial-exec, which
+  // avoids a __tls_get_addr call per read but draws on glibc's small static
+  // TLS surplus (a library dlopen'ed late can then fail with "cannot allocate
+  // memory in static TLS block"), so it is opt-in: our bench library, loaded
+  // first by bench.py, opts in; other shared builds keep the default model.
+#ifdef STAN_MATH_AMD_TLS_INITIAL_EXEC
   static inline thread_local AutodiffStackStorage* instance_ __attribute__((tls_model("initial-exec"))) = nullptr;
+#else
+  static inline thread_local AutodiffStackStorage* instance_ = nullptr;
+#endif
 
  private:
   static bool init() {

@@ -16,6 +16,7 @@
 #include <stan/math/rev/core/vari.hpp>
 
 #include <cstdint>
+#include <typeinfo>
 #include <stdexcept>
 #include <vector>
 
@@ -64,7 +65,13 @@ inline void flush_pending(bool status = false) {
   int* st = reinterpret_cast<int*>(stage + n);
   if (armed) amd::check(smg_status_enqueue(c, st), "grad");
   amd::check(smg_sync(c), "flush_pending");
-  for (size_t i = 0; i < n; ++i) pend[i].target->adj_ += stage[i];
+  auto& blocks = ChainableStack::instance_->host_blocks_;
+  for (size_t i = 0; i < n; ++i) {
+    vari* t = pend[i].target;
+    t->adj_ += stage[i];
+    for (auto& b : blocks)  // a host block's bridge must then gather (bridge.hpp)
+      if (t >= b.first && t < b.first + b.n) b.dirty = true;
+  }
   pend.clear();
   if (armed) amd::throw_if_sync(*st, "grad", "the reverse sweep");
 }
@@ -88,6 +95,8 @@ static void grad(vari* vi) {
   auto* st = ChainableStack::instance_;
   join_device_adjoints();
   vi->init_dependent();
+  for (auto& b : st->host_blocks_)  // the root itself may be an element of a host block
+    if (vi >= b.first && vi < b.first + b.n) b.dirty = true;
   it_t begin = st->var_stack_.rbegin();
   it_t end = empty_nested() ? st->var_stack_.rend() : begin + nested_size();
   for (it_t it = begin; it < end; ++it) {
@@ -95,7 +104,8 @@ static void grad(vari* vi) {
     // its adj_; nodes that are not a target run without a synchronisation
     // (device nodes keep streaming)
     if (__builtin_expect(!st->pending_.empty(), 0)) {
-      bool need = (*it)->reads_other_adjoints();
+      // (a plain vari -- a leaf such as var(double)'s -- has an empty chain())
+      bool need = (*it)->reads_other_adjoints() && typeid(**it) != typeid(vari);
       for (size_t i = 0; !need && i < st->pending_.size(); ++i) need = st->pending_[i].target == *it;
       if (need) flush_pending();
     }
@@ -111,6 +121,7 @@ static inline void start_nested() {
   st->nested_var_alloc_stack_starts_.push_back(st->var_alloc_stack_.size());
   st->nested_dev_adj_sizes_.push_back(st->dev_adj_stack_.size());
   st->nested_dev_marks_.push_back(amd::has_ctx() ? smg_arena_mark(amd::ctx()) : SIZE_MAX);
+  st->nested_host_block_sizes_.push_back(st->host_blocks_.size());
   st->memalloc_.start_nested();
 }
 
@@ -131,6 +142,8 @@ static inline void recover_memory_nested() {
   const size_t mark = st->nested_dev_marks_.back();
   st->nested_dev_marks_.pop_back();
   st->pending_.clear();
+  st->host_blocks_.resize(st->nested_host_block_sizes_.back());
+  st->nested_host_block_sizes_.pop_back();
   if (amd::has_ctx()) {
     if (mark == SIZE_MAX)
       smg_arena_recover_all(amd::ctx());
@@ -150,8 +163,21 @@ static inline void recover_memory() {
   st->var_alloc_stack_.clear();
   st->dev_adj_stack_.clear();
   st->pending_.clear();
+  st->host_blocks_.clear();
   if (amd::has_ctx()) smg_arena_recover_all(amd::ctx());
   st->memalloc_.recover_all();
+}
+
+/** Zero the adjoints of the host blocks from index `from` on (their varis
+ * are on no stack; stan/math/amd/matrix.hpp materialise). */
+static inline void zero_host_blocks(size_t from) {
+  auto& blocks = ChainableStack::instance_->host_blocks_;
+  for (size_t k = from; k < blocks.size(); ++k) {
+    host_block& b = blocks[k];
+    for (size_t i = 0; i < b.n; ++i) b.first[i].adj_ = 0.0;
+    if (b.dummy) b.dummy->adj_ = 0.0;
+    b.dirty = false;
+  }
 }
 
 static inline void set_zero_all_adjoints() {
@@ -159,6 +185,7 @@ static inline void set_zero_all_adjoints() {
   for (auto* v : st->var_stack_) v->set_zero_adjoint();
   for (auto* v : st->var_nochain_stack_) v->set_zero_adjoint();
   for (auto& b : st->dev_adj_stack_) amd::zero(b.ptr, b.n);
+  zero_host_blocks(0);
   st->pending_.clear();
 }
 
@@ -175,6 +202,7 @@ static inline void set_zero_all_adjoints_nested() {
     st->var_nochain_stack_[i]->set_zero_adjoint();
   for (size_t i = st->nested_dev_adj_sizes_.back(); i < st->dev_adj_stack_.size(); ++i)
     amd::zero(st->dev_adj_stack_[i].ptr, st->dev_adj_stack_[i].n);
+  zero_host_blocks(st->nested_host_block_sizes_.back());
   st->pending_.clear();
 }
 

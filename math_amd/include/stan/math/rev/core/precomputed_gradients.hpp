@@ -13,7 +13,7 @@
 namespace stan {
 namespace math {
 
-class precomputed_gradients_vari : public vari {
+class precomputed_gradients_vari : public local_adjoint_vari {
  protected:
   const size_t size_;
   vari** varis_;
@@ -21,11 +21,11 @@ class precomputed_gradients_vari : public vari {
 
  public:
   precomputed_gradients_vari(double val, size_t size, vari** varis, double* gradients)
-      : vari(val), size_(size), varis_(varis), gradients_(gradients) {}
+      : local_adjoint_vari(val), size_(size), varis_(varis), gradients_(gradients) {}
 
   precomputed_gradients_vari(double val, const std::vector<var>& vars,
                              const std::vector<double>& gradients)
-      : vari(val),
+      : local_adjoint_vari(val),
         size_(vars.size()),
         varis_(ChainableStack::instance_->memalloc_.alloc_array<vari*>(vars.size())),
         gradients_(ChainableStack::instance_->memalloc_.alloc_array<double>(vars.size())) {
@@ -40,6 +40,11 @@ class precomputed_gradients_vari : public vari {
 
   void chain() override {
     for (size_t i = 0; i < size_; ++i) varis_[i]->adj_ += adj_ * gradients_[i];
+  }
+  bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
+    for (size_t i = 0; i < size_; ++i)
+      if (varis_[i] >= lo && varis_[i] < hi) return true;
+    return false;
   }
 };
 

@@ -33,14 +33,35 @@ class vari {
       ChainableStack::instance_->var_nochain_stack_.push_back(this);
   }
 
+  /** A vari on no stack: an element of a host block (the tape's
+   * host_blocks_ holds the whole block; stan/math/eigen/bridge.hpp). */
+  struct unstacked_tag {};
+  vari(double x, unstacked_tag) : val_(x), adj_(0.0) {}
+
   virtual ~vari() {}
 
   virtual void chain() {}
 
-  /** True for a node whose chain() reads the adjoints of OTHER varis (not
-   * only its own adj_): the reverse sweep lands pending device->host
-   * contributions before such a node runs (grad.hpp). */
-  virtual bool reads_other_adjoints() const { return false; }
+  /** True for a node whose chain() may read the adjoints of OTHER varis
+   * (not only its own adj_): the reverse sweep lands every pending
+   * device->host contribution before such a node runs (grad.hpp).  The
+   * default is true, so a user vari written in the reference's style (an
+   * output-element vari read by a base vari's chain(), e.g.
+   * rev/mat/fun/multiply.hpp:107-135) always sees complete adjoints; the
+   * library's own nodes derive from local_adjoint_vari (audited: chain()
+   * reads only this->adj_ and device buffers) and skip that synchronisation. */
+  virtual bool reads_other_adjoints() const { return true; }
+
+  /** False only when chain() provably adds nothing to the adj_ of any vari
+   * in [lo, hi) directly (a device->host pending adjoint is tracked
+   * separately).  A host block materialised from a device node
+   * (stan/math/eigen/bridge.hpp) skips gathering its N^2 host adjoints when
+   * no node chained after it touches them.  Conservative default: true. */
+  virtual bool touches_adjoints_in(const vari* lo, const vari* hi) const {
+    (void)lo;
+    (void)hi;
+    return true;
+  }
 
   void init_dependent() { adj_ = 1.0; }
 
@@ -54,6 +75,24 @@ class vari {
     return ChainableStack::instance_->memalloc_.alloc(nbytes);
   }
   static inline void operator delete(void* /* ignored */) {}
+};
+
+/** Base of the library's own nodes: chain() reads no host adjoint but its
+ * own adj_ (device adjoints are stream-ordered), so a pending device->host
+ * contribution need only land before it when it targets this node. */
+class local_adjoint_vari : public vari {
+ public:
+  using vari::vari;
+  bool reads_other_adjoints() const override { return false; }
+};
+
+/** Base of the library's device nodes: chain() reads only this->adj_ and
+ * writes only device adjoint buffers (host scalars receive device results
+ * through add_pending_adjoint), so it touches no host vari's adj_ directly. */
+class device_vari : public local_adjoint_vari {
+ public:
+  using local_adjoint_vari::local_adjoint_vari;
+  bool touches_adjoints_in(const vari*, const vari*) const override { return false; }
 };
 
 /** Objects with destructors living as long as the tape

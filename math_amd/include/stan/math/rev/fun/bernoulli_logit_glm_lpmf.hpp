@@ -56,7 +56,7 @@ inline void row_partition(long long R, int world, int rank, long long* begin, lo
 
 namespace internal {
 
-class glm_dev_vari : public vari {
+class glm_dev_vari : public local_adjoint_vari {
  public:
   vari* alpha_vi_;
   vari** beta_vi_;           // host varis of beta (null when beta is data / on device)
@@ -65,7 +65,15 @@ class glm_dev_vari : public vari {
   const double* g_dev_;      // beta' on device
   int M_;
   glm_dev_vari(double lp, vari* a, vari** b, dev_matrix_vari* bd, double* g, const double* gd, int M)
-      : vari(lp), alpha_vi_(a), beta_vi_(b), beta_dev_(bd), g_(g), g_dev_(gd), M_(M) {}
+      : local_adjoint_vari(lp), alpha_vi_(a), beta_vi_(b), beta_dev_(bd), g_(g), g_dev_(gd), M_(M) {}
+  bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
+    auto in = [&](const vari* v) { return v && v >= lo && v < hi; };
+    if (in(alpha_vi_)) return true;
+    if (beta_vi_)
+      for (int j = 0; j < M_; ++j)
+        if (in(beta_vi_[j])) return true;
+    return false;
+  }
   void chain() override {
     if (alpha_vi_) alpha_vi_->adj_ += adj_ * g_[0];
     if (beta_vi_)

@@ -95,13 +95,13 @@ inline void glm_throw_out_of_support(const char* fn, const int* y, long long n, 
 
 /** One node over device alpha (C) and beta (M x C); out = [lp, alpha', beta']
  * on the device. */
-class glm_cat_dev_vari : public vari {
+class glm_cat_dev_vari : public device_vari {
  public:
   dev_operand alpha_, beta_;
   const double* g_dev_;
   int C_, M_;
   glm_cat_dev_vari(double lp, const dev_operand& a, const dev_operand& b, const double* g, int C, int M)
-      : vari(lp), alpha_(a), beta_(b), g_dev_(g), C_(C), M_(M) {}
+      : device_vari(lp), alpha_(a), beta_(b), g_dev_(g), C_(C), M_(M) {}
   void chain() override {
     smg_ctx* c = amd::ctx();
     if (alpha_.adj()) amd::check(smg_axpy(c, C_, adj_, g_dev_ + 1, 1, alpha_.adj(), 1), "categorical_logit_glm_lpmf");

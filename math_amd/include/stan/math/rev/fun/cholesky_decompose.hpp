@@ -27,36 +27,55 @@ namespace math {
 
 namespace internal {
 
-class add_diag_dev_vari : public vari {
+/** B = A + diag(d) over the min(m, n) leading diagonal (prim/mat/fun/add_diag.hpp:20-55):
+ * A a device var node or data; d a scalar (var or double) or a device vector
+ * (var node or data). */
+class add_diag_dev_vari : public device_vari {
  public:
-  dev_matrix_vari* A_;
+  dev_operand A_;
   dev_matrix_vari* B_;
-  vari* d_vi_;     // scalar var diagonal (null when data)
-  double* dadj_;   // device scalar
+  vari* d_vi_;    // scalar var diagonal (null otherwise)
+  double* dadj_;  // its device adjoint
+  dev_operand dv_;  // vector diagonal (dv_.rows == 0 when scalar)
 
-  add_diag_dev_vari(dev_matrix_vari* A, double d, vari* d_vi)
-      : vari(0.0), A_(A), B_(new dev_matrix_vari(A->rows_, A->cols_)), d_vi_(d_vi),
-        dadj_(d_vi ? amd::alloc_doubles(1) : nullptr) {
-    amd::check(smg_add_diag_fwd(amd::ctx(), A_->val_, A_->rows_, A_->rows_, d, nullptr, B_->val_,
-                                B_->rows_),
-               "add_diag");
+  add_diag_dev_vari(const dev_operand& A, double d, vari* d_vi, const dev_operand& dv)
+      : device_vari(0.0), A_(A), B_(new dev_matrix_vari(A.rows, A.cols)), d_vi_(d_vi),
+        dadj_(d_vi ? amd::alloc_doubles(1) : nullptr), dv_(dv) {
+    smg_ctx* c = amd::ctx();
+    const int m = A.rows, n = A.cols, k = m < n ? m : n;
+    const double* dvec = dv_.rows ? dv_.val() : nullptr;
+    if (m == n) {
+      amd::check(smg_add_diag_fwd(c, A_.val(), m, m, d, dvec, B_->val_, m), "add_diag");
+    } else if (m && n) {  // copy, then the k x k leading block in place
+      amd::check(smg_memcpy_d2d(c, B_->val_, A_.val(), size_t(m) * n * sizeof(double)), "add_diag");
+      amd::check(smg_add_diag_fwd(c, B_->val_, m, k, d, dvec, B_->val_, m), "add_diag");
+    }
   }
   void chain() override {
     smg_ctx* c = amd::ctx();
+    const int m = A_.rows, n = A_.cols, k = m < n ? m : n;
+    if (!m || !n) return;
+    double* dadj = dv_.rows ? dv_.adj() : dadj_;
     if (dadj_) amd::check(smg_memset(c, dadj_, 0, sizeof(double)), "add_diag");
-    amd::check(smg_add_diag_rev(c, B_->adj_, B_->rows_, B_->rows_, A_->adj_, A_->rows_, dadj_, 0),
-               "add_diag");
+    const int vec = dv_.rows ? 1 : 0;
+    if (m == n) {
+      amd::check(smg_add_diag_rev(c, B_->adj_, m, m, A_.adj(), m, dadj, vec), "add_diag");
+    } else {
+      if (A_.adj())
+        amd::check(smg_axpy(c, (long long)m * n, 1.0, B_->adj_, 1, A_.adj(), 1), "add_diag");
+      amd::check(smg_add_diag_rev(c, B_->adj_, m, k, nullptr, 0, dadj, vec), "add_diag");
+    }
     if (d_vi_) add_pending_adjoint(d_vi_, dadj_);
   }
 };
 
-class cholesky_dev_vari : public vari {
+class cholesky_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* L_;
   int n_;
 
-  cholesky_dev_vari(dev_matrix_vari* A, dev_matrix_vari* L) : vari(0.0), A_(A), L_(L), n_(A->rows_) {}
+  cholesky_dev_vari(dev_matrix_vari* A, dev_matrix_vari* L) : device_vari(0.0), A_(A), L_(L), n_(A->rows_) {}
 
   void chain() override {
     smg_ctx* c = amd::ctx();
@@ -86,17 +105,43 @@ inline void throw_not_symmetric_dev(const char* fn, const char* name, const doub
   amd::throw_not_symmetric_host(fn, name, h.data(), n);
 }
 
-}  // namespace internal
 
-inline dev_var_matrix add_diag(const dev_var_matrix& A, const var& d) {
-  internal::check_square("add_diag", "mat", A.rows(), A.cols());
-  auto* node = new internal::add_diag_dev_vari(A.vi_, d.val(), d.vi_);
+inline dev_var_matrix add_diag_dev(const dev_operand& A, double d, vari* d_vi, const dev_operand& dv) {
+  if (dv.rows || dv.cols) {  // check_consistent_size(fn, "number of elements of to_add", to_add, min(rows, cols))
+    const size_t k = size_t(A.rows < A.cols ? A.rows : A.cols);
+    if (dv.size() != k) {
+      std::ostringstream m;
+      m << "add_diag: number of elements of to_add has dimension = " << dv.size() << ", expecting dimension = " << k
+        << "; a function was called with arguments of different scalar, array, vector, or matrix types, and they "
+           "were not consistently sized;  all arguments must be scalars or multidimensional values of the same shape.";
+      throw std::invalid_argument(m.str());
+    }
+  }
+  auto* node = new add_diag_dev_vari(A, d, d_vi, dv);
   return dev_var_matrix(node->B_);
 }
+
+}  // namespace internal
+
+/** add_diag(mat, to_add) (prim/mat/fun/add_diag.hpp:20-55) on device operands:
+ * a scalar or a vector to_add, any var / data combination, rectangular mat. */
+inline dev_var_matrix add_diag(const dev_var_matrix& A, const var& d) {
+  return internal::add_diag_dev(internal::operand(A), d.val(), d.vi_, {});
+}
 inline dev_var_matrix add_diag(const dev_var_matrix& A, double d) {
-  internal::check_square("add_diag", "mat", A.rows(), A.cols());
-  auto* node = new internal::add_diag_dev_vari(A.vi_, d, nullptr);
-  return dev_var_matrix(node->B_);
+  return internal::add_diag_dev(internal::operand(A), d, nullptr, {});
+}
+inline dev_var_matrix add_diag(const dev_data<double>& A, const var& d) {
+  return internal::add_diag_dev(internal::operand(A), d.val(), d.vi_, {});
+}
+inline dev_var_matrix add_diag(const dev_var_matrix& A, const dev_var_matrix& d) {
+  return internal::add_diag_dev(internal::operand(A), 0.0, nullptr, internal::operand(d));
+}
+inline dev_var_matrix add_diag(const dev_var_matrix& A, const dev_data<double>& d) {
+  return internal::add_diag_dev(internal::operand(A), 0.0, nullptr, internal::operand(d));
+}
+inline dev_var_matrix add_diag(const dev_data<double>& A, const dev_var_matrix& d) {
+  return internal::add_diag_dev(internal::operand(A), 0.0, nullptr, internal::operand(d));
 }
 
 inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {

@@ -1,7 +1,9 @@
 #ifndef STAN_MATH_REV_FUN_GP_EXP_QUAD_COV_HPP
 #define STAN_MATH_REV_FUN_GP_EXP_QUAD_COV_HPP
 
-// gp_exp_quad_cov(x, sigma, length_scale) for scalar inputs x.
+// gp_exp_quad_cov(x, sigma, length_scale) for scalar inputs x (the
+// D-dimensional std::vector<Eigen vector> forms are in eigen/interop.hpp and
+// share this node: x on the device as D x n).
 // Reference: rev/mat/fun/gp_exp_quad_cov.hpp:32-286.  Same checks
 // (check_positive sigma / length_scale, check_not_nan x, :216-221), same
 // value K_ij = sigma^2 exp(-(x_i - x_j)^2 / (2 l^2)) and adjoint
@@ -28,48 +30,58 @@ inline void gp_check_positive(const char* fn, const char* name, double v) {
   }
 }
 
-class gp_exp_quad_cov_dev_vari : public vari {
+class gp_exp_quad_cov_dev_vari : public device_vari {
  public:
-  const double* x_;
+  const double* x_;  // D x n column-major (point i at x_ + i D)
   const int n_;
+  const int D_;
   const double sigma_d_, l_d_;
   vari* sigma_vi_;  // null when sigma is data
   vari* l_vi_;      // null when l is data
   dev_matrix_vari* K_;
   double* out2_;
 
-  gp_exp_quad_cov_dev_vari(const double* x, int n, double sigma, vari* sigma_vi, double l,
-                           vari* l_vi)
-      : vari(0.0),
+  gp_exp_quad_cov_dev_vari(const double* x, int n, int D, double sigma, vari* sigma_vi, double l, vari* l_vi)
+      : device_vari(0.0),
         x_(x),
         n_(n),
+        D_(D),
         sigma_d_(sigma),
         l_d_(l),
         sigma_vi_(sigma_vi),
         l_vi_(l_vi),
         K_(new dev_matrix_vari(n, n)),
         out2_(amd::alloc_doubles(2)) {
-    amd::check(smg_gp_exp_quad_cov_fwd(amd::ctx(), x_, n_, sigma_d_, l_d_, K_->val_, n_),
-               "gp_exp_quad_cov");
+    amd::check(smg_gp_exp_quad_cov_nd_fwd(amd::ctx(), x_, D_, n_, sigma_d_, l_d_, K_->val_, n_), "gp_exp_quad_cov");
   }
 
   void chain() override {
+    if (!sigma_vi_ && !l_vi_) return;
     smg_ctx* c = amd::ctx();
     amd::check(smg_memset(c, out2_, 0, 2 * sizeof(double)), "gp_exp_quad_cov");
-    amd::check(smg_gp_exp_quad_cov_rev(c, x_, n_, sigma_d_, l_d_, K_->adj_, n_, out2_),
-               "gp_exp_quad_cov");
+    amd::check(smg_gp_exp_quad_cov_nd_rev(c, x_, D_, n_, sigma_d_, l_d_, K_->adj_, n_, out2_), "gp_exp_quad_cov");
     if (sigma_vi_) add_pending_adjoint(sigma_vi_, out2_);
     if (l_vi_) add_pending_adjoint(l_vi_, out2_ + 1);
   }
 };
 
-inline dev_var_matrix gp_exp_quad_cov_dev(const dev_data<double>& x, double sigma,
-                                          vari* sigma_vi, double l, vari* l_vi) {
+/** names: the checked argument names of the overload (rev: "sigma" /
+ * "length_scale" for (var, var), "marginal variance" / "length-scale" for
+ * (double, var), :216-221,254-259; prim: "magnitude" / "length scale",
+ * prim/mat/fun/gp_exp_quad_cov.hpp:180-181). */
+inline dev_var_matrix gp_exp_quad_cov_dev(const dev_data<double>& x, int D, double sigma, vari* sigma_vi, double l,
+                                          vari* l_vi, const char* sigma_name = nullptr,
+                                          const char* l_name = nullptr) {
   const char* fn = "gp_exp_quad_cov";
-  gp_check_positive(fn, sigma_vi ? "sigma" : "marginal variance", sigma);
-  gp_check_positive(fn, l_vi ? "length_scale" : "length-scale", l);
-  auto* node = new gp_exp_quad_cov_dev_vari(x.data(), int(x.size()), sigma, sigma_vi, l, l_vi);
+  gp_check_positive(fn, sigma_name ? sigma_name : sigma_vi ? "sigma" : "marginal variance", sigma);
+  gp_check_positive(fn, l_name ? l_name : l_vi ? "length_scale" : "length-scale", l);
+  const int n = D > 0 ? int(x.size() / size_t(D)) : 0;
+  auto* node = new gp_exp_quad_cov_dev_vari(x.data(), n, D, sigma, sigma_vi, l, l_vi);
   return dev_var_matrix(node->K_);
+}
+inline dev_var_matrix gp_exp_quad_cov_dev(const dev_data<double>& x, double sigma, vari* sigma_vi, double l,
+                                          vari* l_vi) {
+  return gp_exp_quad_cov_dev(x, 1, sigma, sigma_vi, l, l_vi);
 }
 
 inline dev_data<double> gp_x_to_device(const std::vector<double>& x) {
@@ -103,6 +115,12 @@ inline dev_var_matrix gp_exp_quad_cov(const dev_data<double>& x, const var& sigm
 inline dev_var_matrix gp_exp_quad_cov(const dev_data<double>& x, double sigma,
                                       const var& length_scale) {
   return internal::gp_exp_quad_cov_dev(x, sigma, nullptr, length_scale.val(), length_scale.vi_);
+}
+/** (var sigma, double length_scale): the reference's prim template
+ * (prim/mat/fun/gp_exp_quad_cov.hpp:175-198, names "magnitude" / "length scale"). */
+inline dev_var_matrix gp_exp_quad_cov(const std::vector<double>& x, const var& sigma, double length_scale) {
+  return internal::gp_exp_quad_cov_dev(internal::gp_x_to_device(x), 1, sigma.val(), sigma.vi_, length_scale,
+                                       nullptr, "magnitude", "length scale");
 }
 
 }  // namespace math

@@ -32,12 +32,12 @@ class digamma_vari : public op_v_vari {
 };
 
 template <int OP>  // 0 = lgamma, 1 = digamma
-class unary_special_dev_vari : public vari {
+class unary_special_dev_vari : public device_vari {
  public:
   dev_matrix_vari* x_;
   dev_matrix_vari* y_;
   explicit unary_special_dev_vari(dev_matrix_vari* x)
-      : vari(0.0), x_(x), y_(new dev_matrix_vari(x->rows_, x->cols_)) {
+      : device_vari(0.0), x_(x), y_(new dev_matrix_vari(x->rows_, x->cols_)) {
     const long long n = (long long)x_->size();
     amd::check(OP == 0 ? smg_lgamma_fwd(amd::ctx(), x_->val_, n, y_->val_)
                        : smg_digamma_fwd(amd::ctx(), x_->val_, n, y_->val_),

@@ -18,13 +18,13 @@ namespace stan {
 namespace math {
 namespace internal {
 
-class log_determinant_dev_vari : public vari {
+class log_determinant_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   double* LU_;
   int* piv_;
   log_determinant_dev_vari(double v, dev_matrix_vari* A, double* LU, int* piv)
-      : vari(v), A_(A), LU_(LU), piv_(piv) {}
+      : device_vari(v), A_(A), LU_(LU), piv_(piv) {}
   void chain() override {
     const int n = A_->rows_;
     double* ws = amd::alloc_doubles(3 * size_t(n) * n);

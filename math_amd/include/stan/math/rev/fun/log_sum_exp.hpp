@@ -17,10 +17,10 @@ namespace stan {
 namespace math {
 
 namespace internal {
-class log_sum_exp_dev_vari : public vari {
+class log_sum_exp_dev_vari : public device_vari {
  public:
   dev_matrix_vari* x_;
-  log_sum_exp_dev_vari(double v, dev_matrix_vari* x) : vari(v), x_(x) {}
+  log_sum_exp_dev_vari(double v, dev_matrix_vari* x) : device_vari(v), x_(x) {}
   void chain() override {
     amd::check(smg_log_sum_exp_rev(amd::ctx(), x_->val_, (long long)x_->size(), val_, adj_,
                                    x_->adj_),

@@ -20,13 +20,13 @@ namespace math {
 
 namespace internal {
 
-class mdivide_left_tri_dev_vari : public vari {
+class mdivide_left_tri_dev_vari : public device_vari {
  public:
   const int lower_;
   dev_operand A_, B_;
   dev_matrix_vari* C_;
   mdivide_left_tri_dev_vari(int lower, const dev_operand& A, const dev_operand& B)
-      : vari(0.0), lower_(lower), A_(A), B_(B), C_(new dev_matrix_vari(B.rows, B.cols)) {
+      : device_vari(0.0), lower_(lower), A_(A), B_(B), C_(new dev_matrix_vari(B.rows, B.cols)) {
     amd::check(smg_mdivide_left_tri_fwd(amd::ctx(), lower_, A_.val(), A_.rows, B_.val(), B_.rows,
                                         B_.rows, B_.cols, C_->val_, C_->rows_),
                "mdivide_left_tri");

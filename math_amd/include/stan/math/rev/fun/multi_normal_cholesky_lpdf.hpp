@@ -15,6 +15,7 @@
 
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/core.hpp>
+#include <stan/math/rev/fun/multiply.hpp>
 
 #include <cmath>
 #include <sstream>
@@ -26,7 +27,7 @@ namespace math {
 
 namespace internal {
 
-class mvn_cholesky_dev_vari : public vari {
+class mvn_cholesky_dev_vari : public device_vari {
  public:
   dev_matrix_vari* L_;
   const double* ws_;  // [w, sd] on device
@@ -36,7 +37,7 @@ class mvn_cholesky_dev_vari : public vari {
 
   mvn_cholesky_dev_vari(double lp, dev_matrix_vari* L, const double* ws,
                         dev_matrix_vari* y = nullptr, dev_matrix_vari* mu = nullptr)
-      : vari(lp), L_(L), ws_(ws), n_(L->rows_), y_(y), mu_(mu) {}
+      : device_vari(lp), L_(L), ws_(ws), n_(L->rows_), y_(y), mu_(mu) {}
 
   void chain() override {
     const int lower_only = L_->structure_ == dev_structure::lower ? 1 : 0;
@@ -109,6 +110,69 @@ inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const 
   return var(new mvn_cholesky_dev_vari(lp, L.vi_, ws, y_vi, mu_vi));
 }
 
+
+/** One observation of the multi-observation form: device pointers of y_i and
+ * mu_i (mu null: zero mean) and their adjoints (null: data). */
+struct mvn_obs {
+  const double* y;
+  double* yadj;
+  const double* mu;
+  double* muadj;
+};
+
+// The array forms (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:59-80,
+// vector_seq_view): the observations share L; each contributes its own
+// quadratic term and the -log|L| term, so the partials of L sum over them
+// (:139-155: size_vec * inv_L^T).  L may be a var node or data.
+class mvn_multi_dev_vari : public device_vari {
+ public:
+  dev_operand L_;
+  const double* aux_;
+  int n_, k_, lower_only_;
+  const double* ws_;  // k blocks of 2n doubles: [w_i, sd_i]
+  mvn_obs* obs_;
+  mvn_multi_dev_vari(double lp, const dev_operand& L, const double* aux, int lower_only, const double* ws,
+                     mvn_obs* obs, int k)
+      : device_vari(lp), L_(L), aux_(aux), n_(L.rows), k_(k), lower_only_(lower_only), ws_(ws), obs_(obs) {}
+  void chain() override {
+    smg_ctx* c = amd::ctx();
+    for (int i = 0; i < k_; ++i)
+      amd::check(smg_mvn_cholesky_rev(c, L_.val(), n_, aux_, n_, ws_ + 2 * size_t(n_) * i, adj_, lower_only_,
+                                      obs_[i].yadj, obs_[i].muadj, L_.adj(), n_),
+                 "multi_normal_cholesky_lpdf");
+  }
+};
+
+/**
+ * Sum over k observations of log N(y_i | mu_i, L L^T) on the device, as one
+ * node.  Value terms: include_const (-n log sqrt(2 pi)), include_logdet
+ * (-log|L|, from the device lp minus host_logdet when dropped); the
+ * quadratic term is always there (the caller returns early when all of y,
+ * mu, L are data under propto).  Returns the node (null when nothing is a
+ * var) and the value in *lp_out.
+ */
+inline vari* mvn_cholesky_multi(const dev_operand& L, const double* aux, bool lower_only, mvn_obs* obs, int k,
+                                bool include_const, bool include_logdet, double host_logdet, double* lp_out) {
+  const char* fn = "multi_normal_cholesky_lpdf";
+  const int n = L.rows;
+  smg_ctx* c = amd::ctx();
+  double* ws = amd::alloc_doubles(2 * size_t(n) * size_t(k) + size_t(k));
+  double* lp_d = ws + 2 * size_t(n) * size_t(k);
+  for (int i = 0; i < k; ++i)
+    amd::check(smg_mvn_cholesky_fwd(c, obs[i].y, obs[i].mu, L.val(), n, aux, n, ws + 2 * size_t(n) * i, lp_d + i),
+               fn);
+  std::vector<double> lps(static_cast<size_t>(k));
+  amd::to_host(lps.data(), lp_d, lps.size());
+  double lp = 0.0;
+  for (double v : lps) lp += v;
+  if (!include_const) lp -= -std::log(std::sqrt(2.0 * 3.14159265358979323846)) * n * k;
+  if (!include_logdet) lp -= host_logdet * k;
+  *lp_out = lp;
+  bool any_adj = L.adj() != nullptr;
+  for (int i = 0; i < k; ++i) any_adj = any_adj || obs[i].yadj || obs[i].muadj;
+  if (!any_adj) return nullptr;
+  return new mvn_multi_dev_vari(lp, L, aux, lower_only ? 1 : 0, ws, obs, k);
+}
 
 }  // namespace internal
 

@@ -38,22 +38,7 @@ inline void check_multiplicable(const char* fn, int a_rows, int a_cols, int b_ro
   }
 }
 
-/** One operand of a matrix functor: a device var node or constant device data. */
-struct dev_operand {
-  dev_matrix_vari* vi = nullptr;  // null for data
-  const double* data = nullptr;
-  int rows = 0, cols = 0;
-  const double* val() const { return vi ? vi->val_ : data; }
-  double* adj() const { return vi ? vi->adj_ : nullptr; }
-};
-inline dev_operand operand(const dev_var_matrix& m) {
-  return dev_operand{m.vi_, nullptr, m.rows(), m.cols()};
-}
-inline dev_operand operand(const dev_data<double>& d) {
-  return dev_operand{nullptr, d.data(), d.rows(), d.cols()};
-}
-
-class multiply_dev_vari : public vari {
+class multiply_dev_vari : public device_vari {
  public:
   dev_operand A_, B_;
   dev_matrix_vari* C_;
@@ -65,7 +50,7 @@ class multiply_dev_vari : public vari {
   // reference's two products (rev/mat/fun/multiply.hpp:65-135).
   bool gram_;
   multiply_dev_vari(const dev_operand& A, const dev_operand& B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A.rows, B.cols)),
+      : device_vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A.rows, B.cols)),
         gram_(A.vi && B.vi && B.vi->transpose_of_ == A.vi) {
     smg_ctx* c = amd::ctx();
     if (gram_) {
@@ -96,7 +81,7 @@ class multiply_dev_vari : public vari {
   }
 };
 
-class scale_dev_vari : public vari {
+class scale_dev_vari : public device_vari {
  public:
   dev_operand A_;
   double c_;
@@ -104,7 +89,7 @@ class scale_dev_vari : public vari {
   double* cadj_;  // device scalar
   dev_matrix_vari* B_;
   scale_dev_vari(const dev_operand& A, double c, vari* c_vi)
-      : vari(0.0), A_(A), c_(c), c_vi_(c_vi), cadj_(c_vi ? amd::alloc_doubles(1) : nullptr),
+      : device_vari(0.0), A_(A), c_(c), c_vi_(c_vi), cadj_(c_vi ? amd::alloc_doubles(1) : nullptr),
         B_(new dev_matrix_vari(A.rows, A.cols)) {
     smg_ctx* x = amd::ctx();
     const long long n = (long long)A.rows * A.cols;
@@ -123,12 +108,12 @@ class scale_dev_vari : public vari {
   }
 };
 
-class transpose_dev_vari : public vari {
+class transpose_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* B_;
   explicit transpose_dev_vari(dev_matrix_vari* A)
-      : vari(0.0), A_(A), B_(new dev_matrix_vari(A->cols_, A->rows_)) {
+      : device_vari(0.0), A_(A), B_(new dev_matrix_vari(A->cols_, A->rows_)) {
     B_->transpose_of_ = A;
     amd::check(smg_transpose(amd::ctx(), A_->rows_, A_->cols_, A_->val_, A_->rows_, B_->val_,
                              B_->rows_, 0.0),
@@ -141,13 +126,30 @@ class transpose_dev_vari : public vari {
   }
 };
 
-class sum_dev_vari : public vari {
+class sum_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
-  sum_dev_vari(double v, dev_matrix_vari* A) : vari(v), A_(A) {}
+  sum_dev_vari(double v, dev_matrix_vari* A) : device_vari(v), A_(A) {}
   void chain() override {
     const int uplo = A_->structure_ == dev_structure::lower ? 1 : 0;
     amd::check(smg_shift(amd::ctx(), A_->rows_, A_->cols_, adj_, A_->adj_, A_->rows_, uplo), "sum");
+  }
+};
+
+// sum(std::vector<var>) (rev/arr/fun/sum.hpp:14-57): a host node, the
+// values summed in order on the host like the reference's sum_of_val
+class sum_v_vari : public local_adjoint_vari {
+ public:
+  vari** v_;
+  size_t n_;
+  sum_v_vari(double s, vari** v, size_t n) : local_adjoint_vari(s), v_(v), n_(n) {}
+  void chain() override {
+    for (size_t i = 0; i < n_; ++i) v_[i]->adj_ += adj_;
+  }
+  bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
+    for (size_t i = 0; i < n_; ++i)
+      if (v_[i] >= lo && v_[i] < hi) return true;
+    return false;
   }
 };
 
@@ -186,6 +188,22 @@ inline dev_var_matrix multiply(const var& c, const dev_data<double>& A) {
 inline dev_var_matrix transpose(const dev_var_matrix& A) {
   auto* node = new internal::transpose_dev_vari(A.vi_);
   return dev_var_matrix(node->B_);
+}
+
+inline var sum(const std::vector<var>& v) {
+  if (v.empty()) return var(0.0);
+  vari** p = ChainableStack::instance_->memalloc_.alloc_array<vari*>(v.size());
+  double s = 0.0;
+  for (size_t i = 0; i < v.size(); ++i) {
+    p[i] = v[i].vi_;
+    s += v[i].vi_->val_;
+  }
+  return var(new internal::sum_v_vari(s, p, v.size()));
+}
+inline double sum(const std::vector<double>& v) {
+  double s = 0.0;
+  for (double x : v) s += x;
+  return s;
 }
 
 inline var sum(const dev_var_matrix& A) {

@@ -34,7 +34,7 @@ namespace internal {
 
 /** One node over (alpha, beta, sigma): partials g = [alpha', beta'(M), sigma']
  * on the host (arena), beta' also on the device for device-resident beta. */
-class glm_sigma_dev_vari : public vari {
+class glm_sigma_dev_vari : public local_adjoint_vari {
  public:
   vari* alpha_vi_;
   vari** beta_vi_;
@@ -45,7 +45,15 @@ class glm_sigma_dev_vari : public vari {
   int M_;
   glm_sigma_dev_vari(double lp, vari* a, vari** b, dev_matrix_vari* bd, vari* s, double* g,
                      const double* gd, int M)
-      : vari(lp), alpha_vi_(a), beta_vi_(b), beta_dev_(bd), sigma_vi_(s), g_(g), g_dev_(gd), M_(M) {}
+      : local_adjoint_vari(lp), alpha_vi_(a), beta_vi_(b), beta_dev_(bd), sigma_vi_(s), g_(g), g_dev_(gd), M_(M) {}
+  bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
+    auto in = [&](const vari* v) { return v && v >= lo && v < hi; };
+    if (in(alpha_vi_) || in(sigma_vi_)) return true;
+    if (beta_vi_)
+      for (int j = 0; j < M_; ++j)
+        if (in(beta_vi_[j])) return true;
+    return false;
+  }
   void chain() override {
     if (alpha_vi_) alpha_vi_->adj_ += adj_ * g_[0];
     if (beta_vi_)

@@ -57,14 +57,14 @@ inline void check_symmetric_dev(const char* fn, const char* name, const double* 
 }
 
 // ---------------------------------------------------------------- mdivide_left_spd
-class mdivide_left_spd_dev_vari : public vari {
+class mdivide_left_spd_dev_vari : public device_vari {
  public:
   dev_operand A_, B_;
   double* L_;
   double* aux_;
   dev_matrix_vari* C_;
   mdivide_left_spd_dev_vari(const dev_operand& A, const dev_operand& B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(B.rows, B.cols)) {
+      : device_vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(B.rows, B.cols)) {
     static const char* fn = "mdivide_left_spd";
     const int m = A.rows;
     smg_ctx* c = amd::ctx();
@@ -99,13 +99,13 @@ inline dev_var_matrix mdivide_left_spd_dev(const dev_operand& A, const dev_opera
 }
 
 // ---------------------------------------------------------------- log_determinant_spd
-class log_determinant_spd_dev_vari : public vari {
+class log_determinant_spd_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   double* L_;
   double* aux_;
   log_determinant_spd_dev_vari(double v, dev_matrix_vari* A, double* L, double* aux)
-      : vari(v), A_(A), L_(L), aux_(aux) {}
+      : device_vari(v), A_(A), L_(L), aux_(aux) {}
   void chain() override {
     const int n = A_->rows_;
     double* ws = amd::alloc_doubles(size_t(n) * n);
@@ -115,12 +115,12 @@ class log_determinant_spd_dev_vari : public vari {
 };
 
 // ---------------------------------------------------------------- multiply_lower_tri_self_transpose
-class mlt_self_transpose_dev_vari : public vari {
+class mlt_self_transpose_dev_vari : public device_vari {
  public:
   dev_matrix_vari* L_;
   dev_matrix_vari* C_;
   explicit mlt_self_transpose_dev_vari(dev_matrix_vari* L)
-      : vari(0.0), L_(L), C_(new dev_matrix_vari(L->rows_, L->rows_)) {
+      : device_vari(0.0), L_(L), C_(new dev_matrix_vari(L->rows_, L->rows_)) {
     const int K = L->rows_, J = L->cols_;
     double* ws = amd::alloc_doubles(size_t(K) * (J > 0 ? J : 1));
     amd::check(smg_multiply_lower_tri_self_transpose_fwd(amd::ctx(), L_->val_, K, K, J, C_->val_, K, ws),
@@ -136,13 +136,13 @@ class mlt_self_transpose_dev_vari : public vari {
 };
 
 // ---------------------------------------------------------------- quad_form_sym
-class quad_form_sym_dev_vari : public vari {
+class quad_form_sym_dev_vari : public device_vari {
  public:
   dev_operand A_, B_;
   dev_matrix_vari* C_;
   const int sym_adj_;
   quad_form_sym_dev_vari(const dev_operand& A, const dev_operand& B)
-      : vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(B.cols, B.cols)),
+      : device_vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(B.cols, B.cols)),
         sym_adj_(A.vi && B.vi ? 1 : 0) {
     const int M = B.rows, N = B.cols;
     double* ws = amd::alloc_doubles(size_t(M) * N + size_t(N) * N);

@@ -17,7 +17,7 @@ namespace math {
 
 namespace internal {
 
-class gp_tangent_dev_vari : public vari {
+class gp_tangent_dev_vari : public device_vari {
  public:
   const double* x_;
   int n_;
@@ -27,7 +27,7 @@ class gp_tangent_dev_vari : public vari {
   double* out4_;
   gp_tangent_dev_vari(const double* x, int n, const var& s, const var& l, const var& ds,
                       const var& dl)
-      : vari(0.0), x_(x), n_(n), s_(s.val()), l_(l.val()), ds_(ds.val()), dl_(dl.val()),
+      : device_vari(0.0), x_(x), n_(n), s_(s.val()), l_(l.val()), ds_(ds.val()), dl_(dl.val()),
         vis_{s.vi_, l.vi_, ds.vi_, dl.vi_}, K_(new dev_matrix_vari(n, n)),
         out4_(amd::alloc_doubles(4)) {
     amd::check(smg_gp_exp_quad_cov_tangent_fwd(amd::ctx(), x_, n_, s_, l_, ds_, dl_, K_->val_, n_),
@@ -43,12 +43,12 @@ class gp_tangent_dev_vari : public vari {
   }
 };
 
-class phi_dev_vari : public vari {
+class phi_dev_vari : public device_vari {
  public:
   dev_matrix_vari* X_;
   dev_matrix_vari* Y_;
   explicit phi_dev_vari(dev_matrix_vari* X)
-      : vari(0.0), X_(X), Y_(new dev_matrix_vari(X->rows_, X->cols_, dev_structure::lower)) {
+      : device_vari(0.0), X_(X), Y_(new dev_matrix_vari(X->rows_, X->cols_, dev_structure::lower)) {
     amd::check(smg_phi(amd::ctx(), X_->rows_, X_->val_, X_->rows_, Y_->val_, Y_->rows_, 0), "phi");
   }
   void chain() override {
@@ -56,11 +56,11 @@ class phi_dev_vari : public vari {
   }
 };
 
-class dot_dev_vari : public vari {
+class dot_dev_vari : public device_vari {
  public:
   dev_matrix_vari* x_;
   dev_matrix_vari* y_;
-  dot_dev_vari(double v, dev_matrix_vari* x, dev_matrix_vari* y) : vari(v), x_(x), y_(y) {}
+  dot_dev_vari(double v, dev_matrix_vari* x, dev_matrix_vari* y) : device_vari(v), x_(x), y_(y) {}
   void chain() override {
     smg_ctx* c = amd::ctx();
     const long long n = (long long)x_->size();
@@ -69,11 +69,11 @@ class dot_dev_vari : public vari {
   }
 };
 
-class diag_ratio_dev_vari : public vari {
+class diag_ratio_dev_vari : public device_vari {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* B_;
-  diag_ratio_dev_vari(double v, dev_matrix_vari* A, dev_matrix_vari* B) : vari(v), A_(A), B_(B) {}
+  diag_ratio_dev_vari(double v, dev_matrix_vari* A, dev_matrix_vari* B) : device_vari(v), A_(A), B_(B) {}
   void chain() override {
     amd::check(smg_diag_ratio_rev(amd::ctx(), A_->rows_, A_->val_, A_->rows_, B_->val_, B_->rows_,
                                   adj_, A_->adj_, A_->rows_, B_->adj_, B_->rows_),

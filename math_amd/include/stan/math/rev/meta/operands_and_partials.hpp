@@ -263,7 +263,7 @@ class ops_partials_edge<double, dev_var_matrix> {
 
 /** The node build() puts on the tape: host operands (precomputed-gradients
  * form) plus up to five device edges (one axpy each). */
-class ops_partials_vari : public vari {
+class ops_partials_vari : public local_adjoint_vari {
  public:
   size_t size_;
   vari** varis_;
@@ -271,8 +271,13 @@ class ops_partials_vari : public vari {
   dev_edge dev_[5];
   int ndev_;
   ops_partials_vari(double v, size_t size, vari** varis, double* partials, const dev_edge* dev, int ndev)
-      : vari(v), size_(size), varis_(varis), partials_(partials), ndev_(ndev) {
+      : local_adjoint_vari(v), size_(size), varis_(varis), partials_(partials), ndev_(ndev) {
     for (int i = 0; i < ndev; ++i) dev_[i] = dev[i];
+  }
+  bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
+    for (size_t i = 0; i < size_; ++i)
+      if (varis_[i] >= lo && varis_[i] < hi) return true;
+    return false;
   }
   void chain() override {
     for (size_t i = 0; i < size_; ++i) varis_[i]->adj_ += adj_ * partials_[i];

@@ -40,6 +40,8 @@
  *   map_rect                 stan/math/prim/mat/functor/map_rect.hpp:120-177
  *   hessian_times_vector     stan/math/mix/mat/functor/hessian_times_vector.hpp:13-40
  *   hessian                  stan/math/mix/mat/functor/hessian.hpp:39-72
+ *   the boundary call forms  tests/cpp/boundary_cases.hpp (multiply / add_diag / sum /
+ *                            multi_normal_cholesky_lpdf / D-dimensional gp_exp_quad_cov)
  */
 #define STAN_MATH_REV_CORE_INIT_CHAINABLESTACK_HPP
 #include <stan/math/mix/mat.hpp>
@@ -56,6 +58,7 @@
 #include <vector>
 
 #include "gen.h"
+#include "../tests/cpp/boundary_cases.hpp"  // the call forms, shared with tests/cpp/test_boundary.cpp
 
 stan::math::ChainableStack main_thread_tape;  // owns the main-thread tape
 
@@ -1388,6 +1391,128 @@ static void fix_hvp() {
   }
 }
 
+
+// The reference's call forms at the drop-in boundary (tests/cpp/boundary_cases.hpp,
+// compiled here against the reference and in tests/cpp/test_boundary.cpp
+// against math_amd): multiply row x col / matrix x vector / scalar forms,
+// add_diag with a vector, sum(std::vector<var>), every var / double mix and
+// the array forms of multi_normal_cholesky_lpdf, the D-dimensional GP.
+static bnd::form_inputs boundary_inputs() {
+  bnd::form_inputs in;
+  in.A = unif(SEED + 2000, (size_t)in.m * in.k, -1, 1);
+  in.B = unif(SEED + 2001, (size_t)in.k * in.n, -1, 1);
+  in.v = unif(SEED + 2002, in.k, -1, 1);
+  in.r = unif(SEED + 2003, in.k, -1, 1);
+  in.r5 = unif(SEED + 2004, in.m, -1, 1);
+  MatrixXd S = spd(in.s, SEED + 2005);
+  in.S.assign(S.data(), S.data() + S.size());
+  in.d = unif(SEED + 2006, in.s, 0.5, 1.5);
+  MatrixXd L = spd(in.s, SEED + 2007).llt().matrixL();
+  in.L.assign(L.data(), L.data() + L.size());
+  in.ys = unif(SEED + 2008, (size_t)in.s * in.nobs, -2, 2);
+  in.mu = unif(SEED + 2009, in.s, -1, 1);
+  in.W = unif(SEED + 2010, 64, -1, 1);
+  in.c = 0.7;
+  return in;
+}
+
+static void gp_nd_inputs(int N, int D, int nobs, std::vector<VectorXd>& x, std::vector<VectorXd>& ys) {
+  std::vector<double> xv = unif(SEED + 2100, (size_t)N * D, -5.0, 5.0);
+  x.assign(N, VectorXd(D));
+  for (int i = 0; i < N; ++i)
+    for (int d = 0; d < D; ++d) x[i](d) = xv[(size_t)i * D + d];
+  ys.assign(nobs, VectorXd(N));
+  for (int j = 0; j < nobs; ++j) {
+    std::vector<double> e = normals(SEED + 2101 + j, N);
+    for (int i = 0; i < N; ++i) {
+      double t = 0;
+      for (int d = 0; d < D; ++d) t += (d % 2 ? -0.5 : 1.0) * x[i](d);
+      ys[j](i) = std::sin(t) + 0.3 * e[i];
+    }
+  }
+}
+
+static void fix_boundary() {
+  {
+    bnd::form_inputs in = boundary_inputs();
+    Json j;
+    j.put_str("what", "the reference's boundary call forms (tests/cpp/boundary_cases.hpp): per case f and the gradient of every var input in argument order");
+    j.put_int("m", in.m);
+    j.put_int("k", in.k);
+    j.put_int("n", in.n);
+    j.put_int("s", in.s);
+    j.put_int("nobs", in.nobs);
+    j.put_vec("A", in.A);
+    j.put_vec("B", in.B);
+    j.put_vec("v", in.v);
+    j.put_vec("r", in.r);
+    j.put_vec("r5", in.r5);
+    j.put_vec("S", in.S);
+    j.put_vec("d", in.d);
+    j.put_vec("L", in.L);
+    j.put_vec("ys", in.ys);
+    j.put_vec("mu", in.mu);
+    j.put_vec("W", in.W);
+    j.put("c", in.c);
+    bnd::run_form_cases(in, [&](const std::string& name, double f, const std::vector<double>& g) {
+      j.put(name + "_fx", f);
+      j.put_vec(name + "_grad", g);
+    });
+    write_fixture("boundary_forms", j);
+  }
+  {
+    Json j;
+    bnd::run_error_cases([&](const std::string& name, const std::function<void()>& f) {
+      std::string out;
+      try {
+        f();
+        out = "nothrow";
+      } catch (const std::domain_error& e) {
+        out = std::string("domain_error ") + e.what();
+      } catch (const std::invalid_argument& e) {
+        out = std::string("invalid_argument ") + e.what();
+      } catch (const std::exception& e) {
+        out = std::string("other ") + e.what();
+      }
+      stan::math::recover_memory();
+      j.put_str(name, out);
+    });
+    write_fixture("boundary_errors", j);
+  }
+  for (int N : {64, 256}) {
+    const int D = 3, nobs = 5;
+    std::vector<VectorXd> x, ys;
+    gp_nd_inputs(N, D, nobs, x, ys);
+    Json j;
+    j.put_str("what", "Stan-codegen-shaped GP marginal with D-dimensional x (std::vector<VectorXd>): form 0 gp_exp_quad_cov(x, alpha, rho); form 1 gp_exp_quad_cov(x, 1.3, rho); form 2 form 0 with nobs observations and a var mean theta(3)");
+    j.put_int("N", N);
+    j.put_int("D", D);
+    j.put_int("nobs", nobs);
+    std::vector<double> xf, yf;
+    for (auto& p : x) xf.insert(xf.end(), p.data(), p.data() + D);
+    for (auto& y : ys) yf.insert(yf.end(), y.data(), y.data() + N);
+    j.put_vec("x", xf);
+    j.put_vec("ys", yf);
+    const double th0[] = {1.0, 1.5, 0.3, 0.2};
+    for (int form = 0; form < 3; ++form) {
+      const int P = form == 1 ? 2 : form == 2 ? 4 : 3;
+      VectorXd th(P);
+      if (form == 1)
+        th << 1.5, 0.3;
+      else
+        for (int i = 0; i < P; ++i) th(i) = th0[i];
+      double fx;
+      VectorXd g;
+      stan::math::gradient(bnd::gp_marginal<VectorXd>{x, ys, form}, th, fx, g);
+      const std::string f = "_f" + std::to_string(form);
+      j.put_vec("theta" + f, th);
+      j.put("fx" + f, fx);
+      j.put_vec("grad" + f, g);
+    }
+    write_fixture("gp_nd_D3_N" + std::to_string(N), j);
+  }
+}
+
 // ------------------------------------------------------------------ bench
 static double now() {
   return std::chrono::duration<double>(
@@ -1475,6 +1600,7 @@ int main(int argc, char** argv) {
     if (want("hvp")) fix_hvp();
     if (want("mulchol")) fix_mulchol();
     if (want("gp")) fix_gp();
+    if (want("boundary")) fix_boundary();
     return 0;
   }
   if (argc >= 5 && std::string(argv[1]) == "bench")

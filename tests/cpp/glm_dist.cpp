@@ -60,4 +60,10 @@ int glm_dist_eval(int nranks, int rank, amd::allgather_fn ag, amd::allreduce_fn 
   return rc;
 }
 
+/* stan::math::row_partition, from this library (a process that has
+ * dlopen'ed it need not load a second one) */
+void glm_dist_row_partition(long long R, int world, int rank, long long* b0, long long* b1) {
+  stan::math::row_partition(R, world, rank, b0, b1);
+}
+
 }  // extern "C"

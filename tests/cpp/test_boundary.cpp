@@ -1,0 +1,213 @@
+// The drop-in boundary's call forms (tests/cpp/boundary_cases.hpp, the same
+// source the reference harness compiles to write the fixtures) against
+// math_amd.  Compiling this file is the compile probe: every reference call
+// form must resolve to a math_amd overload.  Commands (stdin):
+//   forms <inputs of tests/golden/boundary_forms.json>   per case: "<name> f g..."
+//   errors                                               "<name> <kind> <what()>"
+//   gp_nd N D nobs x(N*D) ys(nobs*N) form P theta(P) reps
+//                                                        the Stan-codegen-shaped GP
+//                                                        (Eigen::Matrix<var> K / L) through gradient()
+//   bridge N touch                                       host-block bookkeeping of the
+//                                                        device <-> Eigen round trip
+//   chol_nan_arena N                                     cholesky gradient after NaN-poisoned arena
+#include <stan/math.hpp>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "boundary_cases.hpp"
+
+using namespace stan::math;
+
+static std::vector<double> read_vec(size_t n) {
+  std::vector<double> v(n);
+  std::string t;
+  for (auto& x : v) {
+    std::cin >> t;
+    x = std::strtod(t.c_str(), nullptr);
+  }
+  return v;
+}
+static void print(const std::string& tag, double f, const std::vector<double>& v) {
+  std::printf("%s %.17g", tag.c_str(), f);
+  for (double x : v) std::printf(" %.17g", x);
+  std::printf("\n");
+}
+
+static void cmd_forms() {
+  bnd::form_inputs in;
+  std::cin >> in.m >> in.k >> in.n >> in.s >> in.nobs;
+  in.A = read_vec(size_t(in.m) * in.k);
+  in.B = read_vec(size_t(in.k) * in.n);
+  in.v = read_vec(in.k);
+  in.r = read_vec(in.k);
+  in.r5 = read_vec(in.m);
+  in.S = read_vec(size_t(in.s) * in.s);
+  in.d = read_vec(in.s);
+  in.L = read_vec(size_t(in.s) * in.s);
+  in.ys = read_vec(size_t(in.s) * in.nobs);
+  in.mu = read_vec(in.s);
+  in.W = read_vec(64);
+  in.c = read_vec(1)[0];
+  bnd::run_form_cases(in, [](const std::string& name, double f, const std::vector<double>& g) { print(name, f, g); });
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->host_blocks_.size());
+}
+
+static void cmd_errors() {
+  bnd::run_error_cases([](const std::string& name, const std::function<void()>& f) {
+    std::string out;
+    try {
+      f();
+      out = "nothrow";
+    } catch (const std::domain_error& e) {
+      out = std::string("domain_error ") + e.what();
+    } catch (const std::invalid_argument& e) {
+      out = std::string("invalid_argument ") + e.what();
+    } catch (const std::exception& e) {
+      out = std::string("other ") + e.what();
+    }
+    recover_memory();
+    std::printf("%s %s\n", name.c_str(), out.c_str());
+  });
+}
+
+static void cmd_gp_nd() {
+  int N, D, nobs, form, P, reps;
+  std::cin >> N >> D >> nobs;
+  std::vector<double> xf = read_vec(size_t(N) * D), yf = read_vec(size_t(N) * nobs);
+  std::cin >> form >> P;
+  std::vector<double> th = read_vec(P);
+  std::cin >> reps;
+  std::vector<Eigen::VectorXd> x(N, Eigen::VectorXd(D)), ys(nobs, Eigen::VectorXd(N));
+  for (int i = 0; i < N; ++i)
+    for (int d = 0; d < D; ++d) x[i](d) = xf[size_t(i) * D + d];
+  for (int j = 0; j < nobs; ++j)
+    for (int i = 0; i < N; ++i) ys[j](i) = yf[size_t(j) * N + i];
+  Eigen::VectorXd t = Eigen::Map<Eigen::VectorXd>(th.data(), P), g;
+  double fx = 0;
+  double best = 1e30;
+  for (int r = 0; r < reps; ++r) {
+    auto t0 = std::chrono::steady_clock::now();
+    gradient(bnd::gp_marginal<Eigen::VectorXd>{x, ys, form}, t, fx, g);
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (dt < best) best = dt;
+  }
+  print("gp_nd", fx, std::vector<double>(g.data(), g.data() + g.size()));
+  std::printf("seconds %.9g\n", best);
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->host_blocks_.size());
+}
+
+// The round trip device -> Eigen -> device: the second crossing hands back the
+// same node (no gather, no upload), a copy with one element replaced does
+// not, and the reverse sweep skips the N^2 host gather unless a host node
+// touched the block.  Prints the facts; tests/test_boundary.py checks them.
+static void cmd_bridge() {
+  int N;
+  std::cin >> N;
+  std::vector<double> a(size_t(N) * N);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) a[size_t(j) * N + i] = (i == j ? 2.0 : 0.0) + 1.0 / (1.0 + i + j);
+  start_nested();
+  dev_var_matrix A = to_dev_var_matrix(a.data(), N, N);
+  matrix_v K = add_diag(A, 1.0);  // materialised: one host block
+  const size_t h2d_stack = ChainableStack::instance_->var_stack_.size();
+  dev_var_matrix back = to_dev(K);
+  std::printf("same_node %d\n",
+              int(static_cast<void*>(back.vi_) == ChainableStack::instance_->host_blocks_.back().node));
+  std::printf("no_bridge_pushed %d\n", int(ChainableStack::instance_->var_stack_.size() == h2d_stack));
+  matrix_v K2 = K;
+  K2(0, 1) = var(5.0);
+  dev_var_matrix other = to_dev(K2);
+  std::printf("modified_copy_new_node %d\n",
+              int(static_cast<void*>(other.vi_) != ChainableStack::instance_->host_blocks_.back().node));
+  matrix_v L = cholesky_decompose(K);  // recognised K, lower block
+  const host_block& lb = ChainableStack::instance_->host_blocks_.back();
+  int dummy_ok = 1;
+  for (int j = 1; j < N; ++j)
+    for (int i = 0; i < j; ++i) dummy_ok &= int(L(i, j).vi_ == lb.dummy);
+  std::printf("lower_dummy %d\n", dummy_ok);
+  // touch == 0: only device consumers (the bridges skip their gathers);
+  // touch == 1: a host node reads K(0,0) and L(1,0) too (the gathers run)
+  int touch;
+  std::cin >> touch;
+  var f = sum(cholesky_decompose(K)) + 0.5 * sum(to_dev(L));
+  if (touch) f += 2.0 * K(0, 0) + 3.0 * L(1, 0) + 7.0 * L(0, 1);  // L(0,1): the dummy (dropped)
+  f.grad();
+  print("grad_eigen", f.val(), A.adj());
+  std::printf("blocks %zu\n", ChainableStack::instance_->host_blocks_.size());
+  recover_memory_nested();
+  std::printf("blocks_after %zu\n", ChainableStack::instance_->host_blocks_.size());
+  // the same function on device nodes only, K = A + I, L = chol(K)
+  start_nested();
+  dev_var_matrix A2 = to_dev_var_matrix(a.data(), N, N);
+  dev_var_matrix Kd = add_diag(A2, 1.0);
+  dev_var_matrix Ld = cholesky_decompose(Kd);
+  var g = 1.5 * sum(Ld);
+  g.grad();
+  print("grad_device", g.val(), A2.adj());
+  std::vector<double> lv = Ld.val();
+  std::printf("L10 %.17g\n", lv[1]);
+  recover_memory_nested();
+}
+
+// the Murray reverse reads its work matrix's strict upper as
+// stored zeros; recycled arena memory may hold NaN there.  Poison the arena,
+// recover it, take the gradient again: it must equal the clean one.
+static void cmd_chol_nan_arena() {
+  int N;
+  std::cin >> N;
+  std::vector<double> a(size_t(N) * N);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) a[size_t(j) * N + i] = (i == j ? double(N) : 0.0) + std::cos(0.37 * (i + j));
+  auto run = [&]() {
+    start_nested();
+    dev_var_matrix A = to_dev_var_matrix(a.data(), N, N);
+    var f = sum(cholesky_decompose(A));
+    f.grad();
+    std::vector<double> g = A.adj();
+    recover_memory_nested();
+    return g;
+  };
+  const size_t used0 = smg_arena_used(amd::ctx());
+  std::vector<double> g1 = run();
+  // poison everything the evaluation used (and more) with NaN bytes
+  start_nested();
+  const size_t span = size_t(64) * N * N + (size_t(1) << 20);
+  double* p = amd::alloc_doubles(span);
+  amd::check(smg_memset(amd::ctx(), p, 0xFF, span * sizeof(double)), "poison");
+  amd::check(smg_sync(amd::ctx()), "poison");
+  recover_memory_nested();
+  std::vector<double> g2 = run();
+  size_t nan2 = 0, diff = 0;
+  for (size_t i = 0; i < g1.size(); ++i) {
+    nan2 += std::isnan(g2[i]) ? 1 : 0;
+    diff += g1[i] != g2[i] ? 1 : 0;
+  }
+  std::printf("arena_used0 %zu\n", used0);
+  std::printf("nan_entries %zu\n", nan2);
+  std::printf("diff_entries %zu\n", diff);
+}
+
+int main() {
+  std::string cmd;
+  while (std::cin >> cmd) {
+    if (cmd == "forms") cmd_forms();
+    else if (cmd == "errors") cmd_errors();
+    else if (cmd == "gp_nd") cmd_gp_nd();
+    else if (cmd == "bridge") cmd_bridge();
+    else if (cmd == "chol_nan_arena") cmd_chol_nan_arena();
+    else {
+      std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
+      return 2;
+    }
+    std::fflush(stdout);
+  }
+  return 0;
+}

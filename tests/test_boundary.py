@@ -1,0 +1,132 @@
+"""The drop-in boundary's overload sets, on the device.
+
+tests/cpp/boundary_cases.hpp holds the reference's call forms once; the
+reference harness compiled it against Stan Math 3.0.0 to write
+tests/golden/boundary_forms.json / boundary_errors.json / gp_nd_D3_N*.json,
+and tests/cpp/test_boundary.cpp compiles the SAME source against math_amd
+(the compile probe, built by __graft_entry__.build()).  Values at 1e-12
+relative, gradients at 1e-10 (expect_near_rel semantics), error messages
+character for character.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from _util import ROOT, golden, near_rel
+
+BIN = os.path.join(ROOT, "tests", "cpp", "_bin", "test_boundary")
+RTOL = 1e-10
+
+
+def _run(stdin, timeout=600):
+    p = subprocess.run([BIN], input=stdin, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return p.stdout
+
+
+def _num(vals):
+    return " ".join(repr(float(v)) for v in np.ravel(vals))
+
+
+def _parse(out):
+    res = {}
+    for line in out.strip().splitlines():
+        tag, *vals = line.split()
+        res[tag] = np.array([float(v) for v in vals])
+    return res
+
+
+EIGEN = "/root/reference/lib/eigen_3.3.3"
+
+
+@pytest.mark.skipif(not os.path.isdir(EIGEN), reason="Eigen (vendored with the reference) not present")
+def test_compile_probe():
+    """Every reference call form of boundary_cases.hpp compiles against
+    math_amd/include (a missing or ambiguous overload fails here)."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_boundary.cpp")
+    p = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I" + os.path.join(ROOT, "math_amd", "include"),
+                        "-I" + os.path.join(ROOT, "include"), "-isystem", EIGEN, src],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+
+
+@pytest.mark.gpu
+def test_boundary_forms():
+    d = golden("boundary_forms")
+    inp = [int(d["m"]), int(d["k"]), int(d["n"]), int(d["s"]), int(d["nobs"])]
+    stdin = "forms " + " ".join(map(str, inp)) + " " + " ".join(
+        _num(d[k]) for k in ("A", "B", "v", "r", "r5", "S", "d", "L", "ys", "mu", "W")) + " " + repr(d["c"]) + "\n"
+    res = _parse(_run(stdin))
+    names = sorted(k[:-3] for k in d if k.endswith("_fx"))
+    assert len(names) >= 28, names
+    for name in names:
+        got = res[name]
+        near_rel(got[0], d[name + "_fx"], 1e-12, what=name + " f")
+        want = np.atleast_1d(d[name + "_grad"]) if len(np.atleast_1d(d[name + "_grad"])) else np.zeros(0)
+        near_rel(got[1:], want, RTOL, what=name + " grad")
+    assert list(res["stack"]) == [0.0, 0.0]  # every case recovered its tape and host blocks
+
+
+@pytest.mark.gpu
+def test_boundary_errors():
+    want = golden("boundary_errors")
+    out = _run("errors\n")
+    got = {}
+    for line in out.strip().splitlines():
+        tag, _, rest = line.partition(" ")
+        got[tag] = rest
+    for k, v in want.items():
+        assert got.get(k) == v, (k, got.get(k), v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [64, 256])
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_gp_nd_codegen_shape(N, form):
+    """The Stan-codegen-shaped GP marginal (Eigen::Matrix<var> K, Kd, L) with
+    D = 3 inputs: (var, var), (double, var) and 5 observations with a var
+    mean, against the reference's gradient()."""
+    d = golden(f"gp_nd_D3_N{N}")
+    th = d[f"theta_f{form}"]
+    stdin = (f"gp_nd {N} 3 5 {_num(d['x'])} {_num(d['ys'])} {form} {len(th)} {_num(th)} 2\n")
+    res = _parse(_run(stdin))
+    near_rel(res["gp_nd"][0], d[f"fx_f{form}"], 1e-12, what="fx")
+    near_rel(res["gp_nd"][1:], d[f"grad_f{form}"], RTOL, what="grad")
+    assert list(res["stack"]) == [0.0, 0.0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("touch", [0, 1])
+def test_bridge_round_trip(touch):
+    """device -> Eigen -> device hands back the materialised node (no bridge
+    vari, no upload); a modified copy is gathered; L's upper triangle is the
+    one dummy vari; the gradient equals the all-device one, plus the closed
+    form of the host-side terms when a host node touches the blocks (their
+    gathers then run; the dummy's adjoint is dropped like the reference's)."""
+    N = 40
+    r = _parse(_run(f"bridge {N} {touch}\n"))
+    for k in ("same_node", "no_bridge_pushed", "modified_copy_new_node", "lower_dummy"):
+        assert r[k][0] == 1.0, k
+    assert r["blocks_after"][0] == 0.0
+    g_eig, g_dev = r["grad_eigen"][1:], r["grad_device"][1:].copy()
+    if touch:
+        i, j = np.indices((N, N))
+        a = (np.where(i == j, 2.0, 0.0) + 1.0 / (1.0 + i + j)).T.ravel()  # column-major like the C++ side
+        K00, K10 = a[0] + 1.0, a[1]
+        g_dev[0] += 2.0 + 3.0 * (-K10 / (2.0 * K00 ** 1.5))  # dL10/dK00
+        g_dev[1] += 3.0 / np.sqrt(K00)                          # dL10/dK10
+        near_rel(r["L10"][0], K10 / np.sqrt(K00), 1e-15, what="L10")
+    near_rel(g_eig, g_dev, 1e-12, what="grad")
+
+
+@pytest.mark.gpu
+def test_cholesky_gradient_after_nan_poisoned_arena():
+    """the Murray reverse reads its work matrix's strict
+    upper triangle as stored zeros; with the arena pre-filled with NaN bytes
+    and recovered, the gradient at n > 2 * 512 (the two-level reverse) must
+    be finite and bit-identical to the clean one."""
+    r = _parse(_run("chol_nan_arena 1100\n"))
+    assert r["nan_entries"][0] == 0
+    assert r["diff_entries"][0] == 0

@@ -142,18 +142,20 @@ def test_add_diag_fwd(ctx, n, ld, vec):
 @pytest.mark.parametrize("m,n,ld", [(1, 1, 1), (33, 20, 35), (300, 300, 300), (300, 301, 302),
                                     (2050, 2050, 2050), (64, 200, 64), (301, 300, 301)])
 def test_copy_tril(ctx, m, n, ld):
-    """Y's lower trapezoid <- X's (column form for even m and ld), the rest of
-    Y untouched."""
+    """Y = tril(X) over the m x n block (column form for even m and ld): the
+    lower trapezoid copied, the strict upper stored as zeros even where Y held
+    NaN (recycled arena memory), the rows past m untouched."""
     rng = np.random.default_rng(m + 7 * n + ld)
     X = rng.uniform(-1, 1, n * ld)
     Y0 = rng.uniform(-1, 1, n * ld)
+    Y0[::3] = np.nan
     dY = ctx.put(Y0)
     ctx.call("smg_copy_tril", m, n, ctx.put(X), ld, dY, ld)
     out = ctx.get(dY, n * ld).reshape(n, ld).T          # out[i, j] = Y(i, j)
     Xm, Ym = X.reshape(n, ld).T, Y0.reshape(n, ld).T
     i, j = np.indices((ld, n))
-    ref = np.where((i >= j) & (i < m), Xm, Ym)
-    assert np.array_equal(out, ref)
+    ref = np.where(i >= m, Ym, np.where(i >= j, Xm, 0.0))
+    assert np.array_equal(out, ref, equal_nan=True)
 
 
 @pytest.mark.parametrize("n,ld", [(1, 1), (33, 35), (300, 300), (301, 302), (2050, 2050)])
@@ -187,6 +189,36 @@ def test_gp_cov(ctx, n):
     ctx.call("smg_gp_exp_quad_cov_rev", dx, n, 1.3, 0.7, dW, n, dout)
     out = ctx.get(dout, 2)
     near_rel(out, [ga[0], gl[0]], 1e-11, what="gp rev")
+
+
+@pytest.mark.parametrize("n,D", [(1, 3), (2, 2), (33, 3), (300, 1), (300, 5), (2051, 3), (64, 200)])
+def test_gp_cov_nd(ctx, n, D):
+    """D-dimensional gp_exp_quad_cov (rev/mat/fun/gp_exp_quad_cov.hpp:158-184,
+    96-112) against float64 numpy over the same squared distances (summed in
+    coordinate order) and, for D = 1, bit-equal to the scalar-x entries."""
+    X = gen.unif(31 + n + D, n * D, -5, 5).reshape(n, D)  # point i = row i (device: D x n column-major)
+    s, l = 1.3, 0.9
+    d2 = np.zeros((n, n))
+    for d in range(D):
+        d2 = d2 + (X[:, d][:, None] - X[:, d][None, :]) ** 2
+    K_ref = s * s * np.exp(-d2 * (0.5 / (l * l)))
+    np.fill_diagonal(K_ref, s * s)
+    dx, dK = ctx.put(X.ravel()), ctx.zeros(n * n)
+    ctx.call("smg_gp_exp_quad_cov_nd_fwd", dx, D, n, s, l, dK, n)
+    near_rel(ctx.get(dK, n * n), F(K_ref), 1e-13, atol=1e-300, what="K")
+    W = gen.unif(32 + n, n * n, -1, 1)
+    Wm = W.reshape(n, n).T
+    off = ~np.eye(n, dtype=bool)
+    prod = Wm * K_ref
+    g_s = 2.0 / s * (prod[off].sum() + np.trace(Wm) * s * s)
+    g_l = (prod * d2)[off].sum() / l ** 3
+    dW, dout = ctx.put(W), ctx.zeros(2)
+    ctx.call("smg_gp_exp_quad_cov_nd_rev", dx, D, n, s, l, dW, n, dout)
+    near_rel(ctx.get(dout, 2), [g_s, g_l], 1e-11, what="gp nd rev")
+    if D == 1:
+        dK1 = ctx.zeros(n * n)
+        ctx.call("smg_gp_exp_quad_cov_fwd", dx, n, s, l, dK1, n)
+        assert np.array_equal(ctx.get(dK1, n * n), ctx.get(dK, n * n))
 
 
 # ------------------------------------------------------------- cholesky

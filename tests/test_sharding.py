@@ -28,10 +28,15 @@ GOLDEN_INC = 0x9E3779B97F4A7C15
 BENCH_LIB = os.path.join(ROOT, "math_amd", "lib", "libsmg_bench.so")
 
 
-def _partition(R, world, rank):
-    lib = ctypes.CDLL(BENCH_LIB)
+def _partition(R, world, rank, lib=None):
+    """stan::math::row_partition, through the bench library or (in a process
+    that already loaded it) the glm_dist test library."""
     b0, b1 = ctypes.c_longlong(), ctypes.c_longlong()
-    lib.smg_bench_row_partition(ctypes.c_longlong(R), world, rank, ctypes.byref(b0), ctypes.byref(b1))
+    if lib is None:
+        ctypes.CDLL(BENCH_LIB).smg_bench_row_partition(ctypes.c_longlong(R), world, rank, ctypes.byref(b0),
+                                                       ctypes.byref(b1))
+    else:
+        lib.glm_dist_row_partition(ctypes.c_longlong(R), world, rank, ctypes.byref(b0), ctypes.byref(b1))
     return b0.value, b1.value
 
 
@@ -271,7 +276,7 @@ def _glm_dist_rank(rank, world, port, out):
     res = {}
     for kind, name, bad in GLM_DIST_CASES:
         R = int(golden(name)["R"])
-        b0, b1 = _partition(R, world, rank)
+        b0, b1 = _partition(R, world, rank, lib)
         R, M, x, y, th = _glm_case_block(kind, name, b0, b1)
         if b0 <= bad < b1:
             y[bad - b0] = 2 if kind == 0 else -1
