@@ -20,6 +20,10 @@ generated in HBM before the timed region, ONE RCCL all-reduce of the M+2
 --workload mulchol (config 2): gradient of sum(cholesky_decompose(add_diag(
 multiply(A, A^T), N))) wrt all N^2 entries of A, N=2048, A resident in HBM.
 
+--workload gp_eigen: config 3 through the Eigen::Matrix<var> signatures
+Stan-generated code uses (K, Kd, L materialised as host varis at every
+stage and recognised again by the next functor), with the per-crossing cost.
+
 --workload normal (config 1): gradient of normal_lpdf(theta | 0, 1), N=1024,
 theta a host std::vector<var>: below the size gate (16384 elements) evaluated
 on the host, as the reference keeps small calls off its device; the forced
@@ -173,6 +177,48 @@ class GP(Workload):
         return {"value": r["evals_per_sec"], "unit": "gradient evals/s", "cores": 1, "kind": "reference",
                 "sample": f"1 gradient eval of the GP marginal at N={self.N} (Stan Math 3.0.0 compiled "
                           f"from /root/reference by oracle/Makefile; {r['seconds_per_eval']:.2f} s)"}
+
+
+class GPEigen(GP):
+    """config 3 exactly as Stan-generated code declares it: `matrix[N,N] K`,
+    Kd and L are Eigen::Matrix<var,-1,-1>, x a host std::vector, y and mu
+    Eigen vectors (the reference harness's gp_functor, the CPU baseline's
+    own code), so each stage crosses the Eigen boundary: every device output
+    is materialised as N^2 host varis and recognised again by the next
+    functor (stan/math/eigen/interop.hpp)."""
+    metric = "gradient evals/sec (fp64), GP-marginal log-density N=4096, Eigen::Matrix<var> (Stan-codegen) signatures"
+
+    def init(self):
+        rc = super().init()
+        self.bl.smg_bench_gp_eigen_step.argtypes = [D, D, D]
+        self.bl.smg_bench_malloc_tuning.argtypes = [ctypes.c_int]
+        self.bl.smg_bench_bridge_cost.argtypes = [ctypes.c_int, ctypes.c_int, D]
+        self.malloc_tuning = int(os.environ.get("SMG_BENCH_MALLOC_TUNING", "1"))
+        self.bl.smg_bench_malloc_tuning(self.malloc_tuning)
+        return rc
+
+    def step(self):
+        return self.bl.smg_bench_gp_eigen_step(ptr(self.theta), ptr(self.fx), ptr(self.g))
+
+    def config(self):
+        c = super().config()
+        c["workload"] = "gp_marginal_gradient_eigen_signatures"
+        c["path"] = ("stan::math::gradient over Eigen::VectorXd theta; K, Kd, L declared Eigen::Matrix<var,-1,-1> "
+                     "(3 materialisations of N^2 host varis + 3 recognitions per eval)")
+        c["malloc_tuning"] = bool(self.malloc_tuning)
+        return c
+
+    def extra(self, timed, steps):
+        out = np.zeros(5)
+        if self.bl.smg_bench_bridge_cost(self.N, 3, ptr(out)) != 0:
+            raise SystemExit(f"bridge cost failed: {self.bl.smg_bench_error().decode()}")
+        return {"bridge_cost_ms": {"to_host_matrix": out[0] * 1e3, "to_dev_recognised": out[1] * 1e3,
+                                   "to_dev_gathered_copy": out[2] * 1e3, "reverse_gather_touched": out[3] * 1e3,
+                                   "reverse_untouched_sweep": out[4] * 1e3,
+                                   "note": f"one crossing of an N={self.N} matrix, best of 3 "
+                                           "(smg_bench_bridge_cost): the reverse sweeps of sum(A) + sum(B) with "
+                                           "B = to_dev(to_host_matrix(A)), with / without a host node "
+                                           "reading one element of the block"}}
 
 
 class GLM(Workload):
@@ -434,7 +480,7 @@ class Normal(Workload):
                           f"{r['seconds_per_eval'] * 1e6:.2f} us each)"}
 
 
-WORKLOADS = {"gp": GP, "glm": GLM, "mulchol": MulChol, "hvp": HVP, "normal": Normal}
+WORKLOADS = {"gp": GP, "gp_eigen": GPEigen, "glm": GLM, "mulchol": MulChol, "hvp": HVP, "normal": Normal}
 
 
 def _free_port():

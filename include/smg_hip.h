@@ -88,6 +88,12 @@ int smg_memset(smg_ctx* ctx, void* dst, int value, size_t bytes);
 int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes);
 int smg_join_async(smg_ctx* ctx);
 int smg_sync(smg_ctx* ctx);
+/* Host-side pipelining: record marker `slot` (0..63) on the context stream
+ * after the work enqueued so far; smg_marker_wait blocks the host until the
+ * stream reaches it (e.g. a large device->host copy issued in chunks whose
+ * host-side consumption overlaps the next chunk's transfer). */
+int smg_marker_record(smg_ctx* ctx, int slot);
+int smg_marker_wait(smg_ctx* ctx, int slot);
 /* synchronise, return the latched status bits (0 = ok) and clear them */
 int smg_status(smg_ctx* ctx, int* status_host);
 /* 1 when a launch that can latch the status word asynchronously (a persistent

@@ -4,6 +4,10 @@
 // stan::math::gradient() call (stan/math/rev/mat/functor/gradient.hpp:41-57).
 #include <stan/math.hpp>
 
+#include <malloc.h>
+
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <exception>
@@ -26,11 +30,34 @@ struct gp_functor {
     auto K = gp_exp_quad_cov(x, th[0], th[1]);
     auto Kd = add_diag(K, square(th[2]));
     auto L = cholesky_decompose(Kd);
-    return multi_normal_cholesky_lpdf(y, L);
+    return multi_normal_cholesky_lpdf(y, mu0, L);
+  }
+  const dev_data<double>& mu0;
+};
+
+// config 3 exactly as Stan-generated code declares it (and as the reference
+// harness times it, oracle/ref_harness.cpp gp_functor): host std::vector x,
+// Eigen y / mu, and `matrix[N,N] K = ...` as Eigen::Matrix<var,-1,-1>, so
+// every stage crosses the Eigen boundary (materialised host blocks,
+// recognised again by the next functor).
+struct gp_eigen_functor {
+  const std::vector<double>& x;
+  const Eigen::VectorXd& y;
+  template <typename T>
+  T operator()(const Eigen::Matrix<T, -1, 1>& th) const {
+    using namespace stan::math;
+    const int N = int(x.size());
+    Eigen::Matrix<T, -1, -1> K = gp_exp_quad_cov(x, th(0), th(1));
+    Eigen::Matrix<T, -1, -1> Kd = add_diag(K, square(th(2)));
+    Eigen::Matrix<T, -1, -1> L = cholesky_decompose(Kd);
+    Eigen::VectorXd mu = Eigen::VectorXd::Zero(N);
+    return multi_normal_cholesky_lpdf(y, mu, L);
   }
 };
 
-dev_data<double> g_x, g_y;
+dev_data<double> g_x, g_y, g_mu0;
+std::vector<double> g_xh;
+Eigen::VectorXd g_yh;
 int g_n = 0;
 char g_err[512];
 
@@ -67,6 +94,10 @@ int smg_bench_gp_init(int device, int n, const double* x, const double* y) {
     // nested gradient() scopes never rewind it)
     g_x = stan::math::to_dev_data(x, size_t(n));
     g_y = stan::math::to_dev_data(y, size_t(n));
+    const std::vector<double> zeros(size_t(n), 0.0);
+    g_mu0 = stan::math::to_dev_data(zeros);
+    g_xh.assign(x, x + n);
+    g_yh = Eigen::Map<const Eigen::VectorXd>(y, n);
     g_n = n;
     return 0;
   } catch (const std::exception& e) {
@@ -77,8 +108,87 @@ int smg_bench_gp_init(int device, int n, const double* x, const double* y) {
 int smg_bench_gp_step(const double* theta, double* fx, double* grad) {
   try {
     std::vector<double> th(theta, theta + 3), g;
-    stan::math::gradient(gp_functor{g_x, g_y}, th, *fx, g);
+    stan::math::gradient(gp_functor{g_x, g_y, g_mu0}, th, *fx, g);
     for (int i = 0; i < 3; ++i) grad[i] = g[i];
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+/* config 3 through the Eigen-typed boundary (gp_eigen_functor); data from
+ * smg_bench_gp_init.  malloc_tuning != 0 keeps Eigen's N^2 heap buffers in
+ * the brk heap (M_MMAP_MAX = 0, no trimming) so they are reused without page
+ * faults: the application's allocator choice, reported with the bench line. */
+int smg_bench_gp_eigen_step(const double* theta, double* fx, double* grad) {
+  try {
+    Eigen::VectorXd th = Eigen::Map<const Eigen::VectorXd>(theta, 3), g;
+    stan::math::gradient(gp_eigen_functor{g_xh, g_yh}, th, *fx, g);
+    for (int i = 0; i < 3; ++i) grad[i] = g(i);
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+void smg_bench_malloc_tuning(int on) {
+  if (on) {
+    mallopt(M_MMAP_MAX, 0);
+    mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    mallopt(M_TOP_PAD, 64 << 20);
+  } else {
+    mallopt(M_MMAP_MAX, 65536);
+  }
+}
+
+/* The Eigen boundary's cost per crossing of an n x n device matrix (seconds,
+ * best of `reps`): out[0] to_host_matrix (one D2H of the values, n^2 varis
+ * constructed in one arena block, the Eigen pointer array), out[1] to_dev of
+ * that matrix (recognised: a parallel pointer check), out[2] to_dev of a copy
+ * with one element replaced (gathered and uploaded), out[3] the reverse
+ * sweep's gather of the block's host adjoints (a host node touched it),
+ * out[4] the same sweep when nothing touched it (skipped). */
+int smg_bench_bridge_cost(int n, int reps, double* out) {
+  try {
+    using namespace stan::math;
+    const size_t nn = size_t(n) * n;
+    for (int k = 0; k < 5; ++k) out[k] = 1e30;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto sec = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
+    for (int r = 0; r < reps; ++r) {
+      for (int touch = 0; touch < 2; ++touch) {
+        start_nested();
+        auto* node = new dev_matrix_vari(n, n);
+        amd::check(smg_fill_unif(amd::ctx(), node->val_, (long long)nn, SEED + 7, -1.0, 1.0, 1.0), "bridge");
+        dev_var_matrix A(node);
+        var f0 = sum(A);  // a device consumer below the block (the sweep's common part)
+        auto t0 = now();
+        Eigen::Matrix<var, -1, -1> M = to_host_matrix(A);
+        auto t1 = now();
+        dev_var_matrix B = to_dev(M);
+        auto t2 = now();
+        if (B.vi_ != A.vi_) throw std::runtime_error("bridge: the round trip did not recognise its block");
+        var f = f0 + sum(B);
+        if (touch) f += 2.0 * M(1, 1);
+        amd::check(smg_sync(amd::ctx()), "bridge");
+        auto t4 = now();
+        f.grad();  // the block's bridge runs inside: gathers when touched, skips otherwise
+        auto t5 = now();
+        out[0] = std::min(out[0], sec(t0, t1));
+        out[1] = std::min(out[1], sec(t1, t2));
+        out[touch ? 3 : 4] = std::min(out[touch ? 3 : 4], sec(t4, t5));
+        recover_memory_nested();
+      }
+      start_nested();  // a copy with one element replaced is not the block: gathered and uploaded
+      auto* node = new dev_matrix_vari(n, n);
+      amd::check(smg_fill_unif(amd::ctx(), node->val_, (long long)nn, SEED + 7, -1.0, 1.0, 1.0), "bridge");
+      Eigen::Matrix<var, -1, -1> M2 = to_host_matrix(dev_var_matrix(node));
+      M2(0, 0) = var(1.0);
+      auto t3 = now();
+      dev_var_matrix C = to_dev(M2);
+      auto t4 = now();
+      out[2] = std::min(out[2], sec(t3, t4));
+      recover_memory_nested();
+    }
     return 0;
   } catch (const std::exception& e) {
     return fail(e);
@@ -146,7 +256,7 @@ int smg_bench_glm_step(const double* theta, double* fx, double* grad) {
 int smg_bench_hvp_step(const double* theta, const double* v, double* fx, double* hv) {
   try {
     std::vector<double> th(theta, theta + 3), vv(v, v + 3), h;
-    stan::math::hessian_times_vector(gp_functor{g_x, g_y}, th, vv, *fx, h);
+    stan::math::hessian_times_vector(gp_functor{g_x, g_y, g_mu0}, th, vv, *fx, h);
     for (int i = 0; i < 3; ++i) hv[i] = h[i];
     return 0;
   } catch (const std::exception& e) {

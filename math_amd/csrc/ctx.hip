@@ -197,6 +197,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   for (auto& b : ctx->blocks) hipFree(b.base);
   for (auto e : ctx->prof_pool) hipEventDestroy(e);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  for (auto e : ctx->marker_ev) hipEventDestroy(e);
   if (ctx->status_ev) hipEventDestroy(ctx->status_ev);
   if (ctx->zero_stream) {
     hipStreamSynchronize(ctx->zero_stream);
@@ -404,6 +405,26 @@ int smg_join_async(smg_ctx* ctx) {
   if (!ctx->zero_pending) return SMG_OK;
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->zero_ev_done, 0));
   ctx->zero_pending = 0;
+  return SMG_OK;
+}
+
+int smg_marker_record(smg_ctx* ctx, int slot) {
+  if (!ctx || slot < 0 || slot >= 64) return SMG_ERR_ARG;
+  while ((int)ctx->marker_ev.size() <= slot) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      ctx->host_status |= SMG_ERR_HIP;
+      return SMG_ERR_HIP;
+    }
+    ctx->marker_ev.push_back(e);
+  }
+  SMG_HIP_TRY(hipEventRecord(ctx->marker_ev[slot], ctx->stream));
+  return SMG_OK;
+}
+
+int smg_marker_wait(smg_ctx* ctx, int slot) {
+  if (!ctx || slot < 0 || slot >= (int)ctx->marker_ev.size()) return SMG_ERR_ARG;
+  SMG_HIP_TRY(hipEventSynchronize(ctx->marker_ev[slot]));
   return SMG_OK;
 }
 

@@ -326,12 +326,16 @@ __global__ void __launch_bounds__(1024) k_normal_fused(
   if (gridDim.x > 1) {
     if (threadIdx.x < 7)
       __hip_atomic_store(part + 7 * blockIdx.x + threadIdx.x, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this block's partial vectors
+    // every wave's partial-vector (gy / gmu / gs) and part stores have left
+    // it before the barrier; then ONE system-scope release by thread 0 makes
+    // them all visible (pinned host memory included) ahead of the ticket, and
+    // the ticket's acquire orders the last block's reads of every part
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-      last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
     __syncthreads();
     if (!last) return;
     if (threadIdx.x < 7) {

@@ -33,6 +33,7 @@ struct smg_ctx {
   hipStream_t side;
   hipStream_t main_stream;  // saved while `stream` temporarily points at `side`
   std::vector<hipEvent_t> ev_pool;
+  std::vector<hipEvent_t> marker_ev;  // smg_marker_record / smg_marker_wait (host pipelining)
   // device bump arena: blocks double in size (memory/stack_alloc.hpp:94-119)
   std::vector<smg_arena_block> blocks;
   size_t cur_block;

@@ -4,12 +4,17 @@
 // Host-side data parallelism for the O(N^2) passes at the Eigen boundary
 // (materialising a device matrix as N^2 host varis, recognising it again,
 // gathering its host adjoints).  These are pure memory passes over disjoint
-// index ranges, so they split across threads with no synchronisation beyond
-// the join.  Small passes stay on the calling thread.
+// index ranges, so they split across a small persistent pool of worker
+// threads with no synchronisation beyond the join.  Small passes stay on the
+// calling thread.
 //   SMG_HOST_THREADS   worker count (default: hardware threads, at most 16)
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -26,8 +31,70 @@ inline int host_threads() {
   return t;
 }
 
-/** f(begin, end) over a partition of [0, n) (in order on one thread below
- * `grain` elements per thread). */
+/** A persistent pool: run(f) calls f(0..n-1), f(0) on the caller, and
+ * returns when all have finished.  Workers sleep on a condition variable
+ * between jobs.  One job at a time (callers from several tape threads take
+ * turns). */
+class host_pool {
+ public:
+  explicit host_pool(int n) : n_(n) {
+    for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~host_pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return n_; }
+  void run(const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> one(run_m_);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &f;
+      left_.store(n_ - 1, std::memory_order_relaxed);
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    while (left_.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+  }
+
+ private:
+  void loop(int i) {
+    long long seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(i);
+      left_.fetch_sub(1, std::memory_order_release);
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_, run_m_;
+  std::condition_variable cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  long long gen_ = 0;
+  std::atomic<int> left_{0};
+  bool stop_ = false;
+};
+
+inline host_pool& the_host_pool() {
+  static host_pool p(host_threads());
+  return p;
+}
+
+/** f(begin, end) over a partition of [0, n) (in order on the calling thread
+ * below `grain` elements per thread). */
 template <typename F>
 inline void host_parallel_for(size_t n, F&& f, size_t grain = size_t(1) << 18) {
   const size_t want = n / grain;
@@ -36,36 +103,26 @@ inline void host_parallel_for(size_t n, F&& f, size_t grain = size_t(1) << 18) {
     if (n) f(size_t(0), n);
     return;
   }
-  std::vector<std::thread> pool;
-  pool.reserve(size_t(t - 1));
-  const size_t step = (n + size_t(t) - 1) / size_t(t);
-  for (int k = 1; k < t; ++k) {
+  host_pool& pool = the_host_pool();
+  const int parts = pool.size();
+  const size_t step = (n + size_t(parts) - 1) / size_t(parts);
+  pool.run([&](int k) {
     const size_t b = size_t(k) * step, e = std::min(n, b + step);
-    if (b < e) pool.emplace_back([&f, b, e] { f(b, e); });
-  }
-  f(size_t(0), std::min(n, step));
-  for (auto& th : pool) th.join();
+    if (b < e) f(b, e);
+  });
 }
 
 /** True when pred(begin, end) holds on every range of the partition. */
 template <typename P>
 inline bool host_parallel_all(size_t n, P&& pred, size_t grain = size_t(1) << 18) {
-  const size_t want = n / grain;
-  const int t = int(std::min<size_t>(size_t(host_threads()), want));
-  if (t <= 1) return n == 0 || pred(size_t(0), n);
-  std::vector<char> ok(size_t(t), 1);
+  std::atomic<bool> ok{true};
   host_parallel_for(
-      size_t(t), [&](size_t b, size_t e) {
-        const size_t step = (n + size_t(t) - 1) / size_t(t);
-        for (size_t k = b; k < e; ++k) {
-          const size_t lo = k * step, hi = std::min(n, lo + step);
-          ok[k] = lo >= hi || pred(lo, hi);
-        }
+      n,
+      [&](size_t b, size_t e) {
+        if (!pred(b, e)) ok.store(false, std::memory_order_relaxed);
       },
-      1);
-  for (char c : ok)
-    if (!c) return false;
-  return true;
+      grain);
+  return ok.load();
 }
 
 }  // namespace internal

@@ -21,7 +21,9 @@
 #include <stan/math/rev/core/var.hpp>
 #include <stan/math/rev/core/vari.hpp>
 
+#include <algorithm>
 #include <cmath>
+#include <functional>
 #include <new>
 #include <sstream>
 #include <stdexcept>
@@ -226,11 +228,15 @@ class dev_to_host_vari : public vari {
 /**
  * Materialise device node m as n contiguous host varis (off every stack; the
  * tape's host_blocks_ owns them) plus one bridge vari on var_stack_.  The
- * values come down in one copy; the varis are constructed in parallel.
- * Returns the block (element i = first + i; a lower-structured node's strict
- * upper triangle is the one dummy vari, like cholesky_decompose.hpp:34-48).
+ * values come down in chunks (one marker each); the host constructs chunk k's
+ * varis in parallel while chunk k+1 is in flight, after running `overlap`
+ * (work that needs the block's addresses but not its values: the caller's
+ * pointer array) while the first chunk transfers.  Returns the block
+ * (element i = first + i; a lower-structured node's strict upper triangle is
+ * the one dummy vari, like cholesky_decompose.hpp:34-48).
  */
-inline const host_block& materialise(dev_matrix_vari* m) {
+inline const host_block& materialise(dev_matrix_vari* m,
+                                     const std::function<void(vari* first, vari* dummy)>& overlap = nullptr) {
   auto* st = ChainableStack::instance_;
   const size_t n = m->size();
   vari* first = static_cast<vari*>(st->memalloc_.alloc((n ? n : 1) * sizeof(vari)));
@@ -242,13 +248,25 @@ inline const host_block& materialise(dev_matrix_vari* m) {
     amd::check(smg_status_armed(c, &armed), "to_host");
     double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
     if (!stage) throw std::bad_alloc();
-    amd::check(smg_memcpy_d2h(c, stage, m->val_, n * sizeof(double)), "to_host");
+    const int nch = n >= (size_t(1) << 21) ? 8 : 1;
+    const size_t chunk = (n + size_t(nch) - 1) / size_t(nch);
     if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(stage + n)), "to_host");
-    amd::check(smg_sync(c), "to_host");
-    if (armed) amd::throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
-    host_parallel_for(n, [&](size_t s, size_t e) {
-      for (size_t i = s; i < e; ++i) ::new (static_cast<void*>(first + i)) vari(stage[i], vari::unstacked_tag{});
-    });
+    for (int k = 0; k < nch; ++k) {
+      const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
+      amd::check(smg_memcpy_d2h(c, stage + b, m->val_ + b, (e - b) * sizeof(double)), "to_host");
+      amd::check(smg_marker_record(c, k), "to_host");
+    }
+    if (overlap) overlap(first, dummy);
+    for (int k = 0; k < nch; ++k) {
+      const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
+      amd::check(smg_marker_wait(c, k), "to_host");
+      if (k == 0 && armed) amd::throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
+      host_parallel_for(e - b, [&](size_t s0, size_t s1) {
+        for (size_t i = b + s0; i < b + s1; ++i) ::new (static_cast<void*>(first + i)) vari(stage[i], vari::unstacked_tag{});
+      });
+    }
+  } else if (overlap) {
+    overlap(first, dummy);
   }
   st->host_blocks_.push_back(host_block{first, n, m, dummy, m->rows_, m->cols_, false});
   new dev_to_host_vari(st->host_blocks_.size() - 1);

@@ -168,17 +168,18 @@ inline dev_operand commit(const eig_in& e) {
 /** Materialise a device matrix of vars as an Eigen matrix of host varis. */
 template <int R = Eigen::Dynamic, int C = Eigen::Dynamic>
 inline Eigen::Matrix<var, R, C> to_host_matrix(const dev_var_matrix& m) {
-  const host_block& b = internal::materialise(m.vi_);
   Eigen::Matrix<var, R, C> out(m.rows(), m.cols());
   var* d = out.data();
-  const size_t r = size_t(b.rows);
-  vari* first = b.first;
-  vari* dummy = b.dummy;
-  internal::host_parallel_for(b.n, [&](size_t s, size_t e) {
-    if (!dummy)
-      for (size_t i = s; i < e; ++i) d[i].vi_ = first + i;
-    else
-      for (size_t i = s; i < e; ++i) d[i].vi_ = i % r >= i / r ? first + i : dummy;
+  const size_t n = m.size(), r = size_t(m.rows());
+  // the pointer array needs only the block's addresses: filled while the
+  // values are in flight
+  internal::materialise(m.vi_, [&](vari* first, vari* dummy) {
+    internal::host_parallel_for(n, [&](size_t s, size_t e) {
+      if (!dummy)
+        for (size_t i = s; i < e; ++i) d[i].vi_ = first + i;
+      else
+        for (size_t i = s; i < e; ++i) d[i].vi_ = i % r >= i / r ? first + i : dummy;
+    });
   });
   return out;
 }

@@ -349,6 +349,23 @@ inline fvar<var> multi_normal_cholesky_lpdf(const dev_data<double>& y, const dev
   return lp;
 }
 
+/** y and mu device-resident (the residual y - mu formed on the device). */
+template <bool propto = false>
+inline fvar<var> multi_normal_cholesky_lpdf(const dev_data<double>& y, const dev_data<double>& mu,
+                                            const dev_fvar_matrix& L) {
+  internal::mvn_check_sizes(int(y.size()), int(mu.size()), L.val_);
+  fvar<var> lp;
+  lp.val_ = multi_normal_cholesky_lpdf<propto>(y, mu, L.val_);
+  const size_t n = y.size();
+  if (n == 0) return lp;
+  smg_ctx* c = amd::ctx();
+  double* r = amd::alloc_doubles(n);
+  amd::check(smg_memcpy_d2d(c, r, y.data(), n * sizeof(double)), "multi_normal_cholesky_lpdf");
+  amd::check(smg_axpy(c, (long long)n, -1.0, mu.data(), 1, r, 1), "multi_normal_cholesky_lpdf");
+  lp.d_ = internal::mvn_cholesky_tangent(L, dev_data<double>(r, n, int(n), 1));
+  return lp;
+}
+
 template <bool propto = false>
 inline fvar<var> multi_normal_cholesky_lpdf(const std::vector<double>& y,
                                             const std::vector<double>& mu,

@@ -13,6 +13,8 @@
 //   special_vec X(200) W(200)     f = sum(W .* (lgamma(X) + 0.5 digamma(X))), Matrix<var> 10x20
 //   normal N theta                gradient of normal_lpdf(theta | 0, 1)
 //   normal_vec y mu sigma (9)     all var vectors; f, f(propto), gradients
+//   normal_big N y mu sigma       n > 4096: the fused kernel's multi-block path (host vars,
+//                                 scalar var mu, device operands)
 //   normal_known y mu sigma (4)   double arguments -> values
 //   glm R M nb beta               device-filled (x, y); single call and 32 row shards
 //   glm_data R M x y theta        explicit data (cutoff branches)
@@ -20,6 +22,7 @@
 //   errors                        the reference's exceptions
 //   hvp N theta v x y             hessian_times_vector of the GP marginal (config 5)
 //   hessian N theta x y           hessian() of the GP marginal (3 fwd-over-rev sweeps)
+//   hvp_fd N theta v x y h        H v at full size vs the extrapolated central difference of the gradient
 //   map_rect_glm R M shards beta  map_rect over GLM row blocks (vs the reference's map_rect32)
 //   spd kind n k args... W        mdivide_left_spd / log_determinant_spd /
 //                                 multiply_lower_tri_self_transpose / quad_form_sym through the
@@ -337,6 +340,48 @@ static void cmd_normal() {
   print1("fx_dev", f.val());
   print("grad_dev", d.adj());
   recover_memory_nested();
+}
+
+// The fused kernel's multi-block path (n > 4096): host vars (zero-copy pinned
+// operands above the host gate), mixed scalar var / vector data, and
+// dev_var_matrix operands.  Prints f and every gradient for the closed form.
+static void cmd_normal_big() {
+  int N;
+  std::cin >> N;
+  auto y = read_vec(N), mu = read_vec(N), s = read_vec(N);
+  {  // all vectors host vars
+    start_nested();
+    std::vector<var> yv = vars(y), mv = vars(mu), sv = vars(s);
+    var f = normal_lpdf(yv, mv, sv);
+    f.grad();
+    print1("fx_vvv", f.val());
+    print("gy_vvv", adjs(yv));
+    print("gmu_vvv", adjs(mv));
+    print("gs_vvv", adjs(sv));
+    recover_memory_nested();
+  }
+  {  // y host vars, mu scalar var, sigma vector data
+    start_nested();
+    std::vector<var> yv = vars(y);
+    var m0 = 0.25;
+    var f = normal_lpdf(yv, m0, s);
+    f.grad();
+    print1("fx_vsd", f.val());
+    print("gy_vsd", adjs(yv));
+    print1("gmu_vsd", m0.adj());
+    recover_memory_nested();
+  }
+  {  // device-resident y and sigma, mu data vector
+    start_nested();
+    auto yd = to_dev_var_matrix(y.data(), N, 1);
+    auto sd = to_dev_var_matrix(s.data(), N, 1);
+    var f = normal_lpdf(yd, mu, sd);
+    f.grad();
+    print1("fx_dev", f.val());
+    print("gy_dev", yd.adj());
+    print("gs_dev", sd.adj());
+    recover_memory_nested();
+  }
 }
 
 static void cmd_normal_vec() {
@@ -776,6 +821,38 @@ static void cmd_hvp() {
   print("Hv_std", hv);
   std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
               ChainableStack::instance_->dev_adj_stack_.size());
+}
+
+// config 5 at full size: H v against the Richardson-extrapolated central
+// difference of the (pinned) gradient along v:
+//   D(h) = (g(th + h v) - g(th - h v)) / 2h,  Hv ~ (4 D(h/2) - D(h)) / 3
+static void cmd_hvp_fd() {
+  int N;
+  double h;
+  std::cin >> N;
+  auto th = read_vec(3), v = read_vec(3), x = read_vec(N), y = read_vec(N);
+  std::cin >> h;
+  std::vector<double> hv;
+  double fx;
+  hessian_times_vector(gp_functor{x, y}, th, v, fx, hv);
+  print1("fx", fx);
+  print("Hv", hv);
+  auto grad_at = [&](double t) {
+    std::vector<double> p(3), g;
+    for (int i = 0; i < 3; ++i) p[i] = th[i] + t * v[i];
+    double f;
+    gradient(gp_functor{x, y}, p, f, g);
+    return g;
+  };
+  auto D = [&](double s) {
+    std::vector<double> a = grad_at(s), b = grad_at(-s), d(3);
+    for (int i = 0; i < 3; ++i) d[i] = (a[i] - b[i]) / (2 * s);
+    return d;
+  };
+  std::vector<double> d1 = D(h), d2 = D(h / 2), r(3);
+  for (int i = 0; i < 3; ++i) r[i] = (4 * d2[i] - d1[i]) / 3;
+  print("Hv_fd", r);
+  print("Hv_fd_plain", d2);
 }
 
 static void cmd_hessian() {
@@ -1237,6 +1314,7 @@ int main() {
     else if (cmd == "special_vec") cmd_special_vec();
     else if (cmd == "normal") cmd_normal();
     else if (cmd == "normal_vec") cmd_normal_vec();
+    else if (cmd == "normal_big") cmd_normal_big();
     else if (cmd == "normal_known") cmd_normal_known();
     else if (cmd == "glm") cmd_glm();
     else if (cmd == "glm_data") cmd_glm_data();
@@ -1250,6 +1328,7 @@ int main() {
     else if (cmd == "errors_hot") cmd_errors_hot();
     else if (cmd == "hvp") cmd_hvp();
     else if (cmd == "hessian") cmd_hessian();
+    else if (cmd == "hvp_fd") cmd_hvp_fd();
     else if (cmd == "hessian2") cmd_hessian2();
     else if (cmd == "map_rect_glm") cmd_map_rect_glm();
     else if (cmd == "status") cmd_status();
