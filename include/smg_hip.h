@@ -130,7 +130,8 @@ int smg_fill_bernoulli(smg_ctx* ctx, int* out, long long n, unsigned long long s
 /* --------------------------------------------------------------- BLAS-3 ---
  * C = alpha op(A) op(B) + beta C  (op = transpose when trans != 0), fp64 MFMA
  * (v_mfma_f64_16x16x4_f64).  uplo: 0 = full C, 1 = only the lower triangle of
- * C (i >= j) is computed and written (SYRK-style).  Replaces the Eigen GEMMs
+ * C (i >= j) is computed and written (SYRK-style), 2 = only the upper, 3 = the
+ * lower triangle computed and written to both triangles (a symmetric C).  Replaces the Eigen GEMMs
  * in multiply_mat_vari (rev/mat/fun/multiply.hpp:65-135) and
  * cholesky_block::chain (rev/mat/fun/cholesky_decompose.hpp:135-158). */
 int smg_gemm(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n, int k,

@@ -821,14 +821,16 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
       // D^T upper (2) x tril(Dadj) lower (4), lower output only (mirrored
       // next); D^{-T} upper (2); D^{-1} lower (4).  Measured on MI355X (GP
       // N = 4096, same-box A/B): 221.3 -> 225.4 evals/s
-      rc = smg_gemm_impl(ctx, 1, 0, 1, bs, bs, bs, 1.0, Ld, ldl, Da, ldla, 0.0, S, bs, 6);
+      // (uplo 3: the lower half computed and stored mirrored, the
+      // sym_from_lower pass folded into the epilogue; the last product also
+      // writes D_adj = tril(P) with halved diagonal from its epilogue)
+      rc = smg_gemm_impl(ctx, 1, 0, 3, bs, bs, bs, 1.0, Ld, ldl, Da, ldla, 0.0, S, bs, 6);
       if (rc) return rc;
-      hipLaunchKernelGGL(k_mirror_lower, dim3(gb), dim3(256), 0, ctx->stream, S, bs);
       rc = smg_gemm_impl(ctx, 1, 0, 0, bs, bs, bs, 1.0, Wp, n, S, bs, 0.0, T, bs, 2);  // D^{-T} S
       if (rc) return rc;
-      rc = smg_gemm_impl(ctx, 0, 0, 0, bs, bs, bs, 1.0, T, bs, Wp, n, 0.0, S, bs, 4);  // ... D^{-1}
+      rc = smg_gemm_dual_impl(ctx, 0, 0, bs, bs, bs, 1.0, T, bs, Wp, n, 0.0, S, bs, Da, ldla, 4);  // ... D^{-1}
       if (rc) return rc;
-      hipLaunchKernelGGL(k_half_lower, dim3(gb), dim3(256), 0, ctx->stream, S, bs, Da, ldla);
+      (void)gb;
       Pm = S;
     } else {
       rc = chol_rev_blocks(ctx, Ld, ldl, Dv + J, ldd, Da, ldla, bs);

@@ -128,7 +128,14 @@ __device__ __forceinline__ void tri_decode(int t, int& bi, int& bj) {
   bj = t - r * (r + 1) / 2;
 }
 
-// MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n)
+// MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n),
+//   3 = the lower triangle computed and stored mirrored too (a symmetric C
+//       from its lower half: no separate sym_from_lower pass),
+//   4 = full C plus a second output C2 = tril(C) with halved diagonal (the
+//       Murray reverse's D_adj image of its symbolic step: no separate pass).
+// Split-K (slab != null): partial tiles into fixed-order slabs, summed by
+// k_splitk_reduce (an in-kernel last-workgroup fixup measured slower: the
+// tail reduction ran on one CU per tile, 90 -> 172 us for 512 x 2560 x 1536).
 // KS: waves per output sub-tile (KS = 2: 8 waves, the two 4-wave groups take
 // alternate halves of every K stage and their accumulators are summed in the
 // epilogue -- twice the waves per CU for grids that cover the CUs only once
@@ -138,7 +145,10 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
     int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab, long long sA,
-    long long sB, long long sC, int px, int ntp, int tri) {
+    long long sB, long long sC, int px, int ntp, int tri, double* __restrict__ C2, int ldc2) {
+  constexpr bool LOWT = MODE == 1 || MODE == 3;  // lower-triangle tiles
+  constexpr bool UPT = MODE == 2;
+  constexpr bool TRIC = LOWT || UPT;
   // strided batch over blockIdx.y (sA = sB = sC = 0 for a single product)
   A += blockIdx.y * sA;
   B += blockIdx.y * sB;
@@ -185,17 +195,17 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
   // triangle modes: square C -> only the tiles of the triangle are launched
   // (tri_decode); trapezoidal C (m != n, the panel updates of the two-level
   // Cholesky) -> the full grid, tiles wholly outside the triangle exit
-  const bool tri_sq = MODE != 0 && m == n && BM == BN;
-  if (MODE == 1 && tri_sq) {
+  const bool tri_sq = TRIC && m == n && BM == BN;
+  if (LOWT && tri_sq) {
     tri_decode(tile, bi, bj);
-  } else if (MODE == 2 && tri_sq) {
+  } else if (UPT && tri_sq) {
     tri_decode(tile, bj, bi);
   } else {
     bi = tile % tiles_m;
     bj = tile / tiles_m;
   }
-  if (MODE == 1 && !tri_sq && bj * BN > bi * BM + BM - 1) return;
-  if (MODE == 2 && !tri_sq && bi * BM > bj * BN + BN - 1) return;
+  if (LOWT && !tri_sq && bj * BN > bi * BM + BM - 1) return;
+  if (UPT && !tri_sq && bi * BM > bj * BN + BN - 1) return;
   const int i0 = bi * BM, j0 = bj * BN;
   int kbeg = split * kchunk;
   int kend = min(k, kbeg + kchunk);
@@ -342,18 +352,24 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
       const int il = e % BM, jl = e / BM;
       const int i = i0 + il, j = j0 + c0 + jl;
       if (i >= m || j >= n) continue;
-      if (MODE == 1 && i < j) continue;
-      if (MODE == 2 && i > j) continue;
+      if (LOWT && i < j) continue;
+      if (UPT && i > j) continue;
       const double v = pool[jl * (BM + 1) + il];
       if (slab) {
         slab[(size_t)split * m * n + (size_t)j * m + i] = v;
-      } else if (!use_c) {
-        C[i + (size_t)j * ldc] = alpha * v;
       } else {
-        double cv;
-        if (PREFETCH_C) cv = cpre[(c0 / ECH) * (BM * ECH / NT) + q];
-        else cv = C[i + (size_t)j * ldc];
-        C[i + (size_t)j * ldc] = alpha * v + beta * cv;
+        double out;
+        if (!use_c) {
+          out = alpha * v;
+        } else {
+          double cv;
+          if (PREFETCH_C) cv = cpre[(c0 / ECH) * (BM * ECH / NT) + q];
+          else cv = C[i + (size_t)j * ldc];
+          out = alpha * v + beta * cv;
+        }
+        C[i + (size_t)j * ldc] = out;
+        if (MODE == 3 && i > j) C[j + (size_t)i * ldc] = out;
+        if (MODE == 4 && i >= j) C2[i + (size_t)j * ldc2] = i == j ? 0.5 * out : out;
       }
     }
     if (c0 + ECH < BN) __syncthreads();
@@ -374,12 +390,18 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
   *c = (beta == 0.0) ? alpha * s : alpha * s + beta * *c;
 }
 
+// the second output of MODE 4 (launch reads it from here: one product at a
+// time per host thread issues a MODE-4 GEMM)
+thread_local double* t_c2 = nullptr;
+thread_local int t_ldc2 = 0;
+
 template <int BM, int BN, int BK, bool TA, bool TB, int MODE, int KS = 1>
 int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
            int lda, const double* B, int ldb, double beta, double* C, int ldc, int batch = 1,
            long long sA = 0, long long sB = 0, long long sC = 0, int tri = 0) {
+  constexpr bool TRIC = MODE == 1 || MODE == 2 || MODE == 3;
   const int tm = smg_ceil_div(m, BM), tn = smg_ceil_div(n, BN);
-  const int ntiles = (MODE != 0 && m == n && BM == BN) ? tm * (tm + 1) / 2 : tm * tn;
+  const int ntiles = (TRIC && m == n && BM == BN) ? tm * (tm + 1) / 2 : tm * tn;
   // split K when the tile grid cannot fill the 256 CUs and K is long
   int splits = 1;
   const int target = 512;
@@ -390,7 +412,10 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   // in two plus the reduction)
   const bool covers = ntiles >= 256 && k <= 1024;
   // (triangular operands: every tile has its own K range, no split)
-  if (!nosplit && !tri && batch == 1 && ntiles < target && !covers && k >= 2 * KMIN) {
+  // (MODE 3 / 4 products -- the symbolic step's, with triangular operands --
+  // never split)
+  if (!nosplit && !tri && MODE != 3 && MODE != 4 && batch == 1 && ntiles < target && !covers &&
+      k >= 2 * KMIN) {
     splits = smg_ceil_div(target, ntiles);
     const int maxs = k / KMIN;
     if (splits > maxs) splits = maxs;
@@ -410,7 +435,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   // operand footprint (rows of A + columns of B, in tiles); triangle grids
   // (tri_decode order) and grids too small to split keep the linear order
   int px = 0, ntp = ntiles;
-  if (!(MODE != 0 && m == n && BM == BN) && ntiles >= 64) {
+  if (!(TRIC && m == n && BM == BN) && ntiles >= 64) {
     long long best = -1;
     for (int p = 1; p <= 8; p *= 2) {
       const int q = 8 / p;
@@ -426,7 +451,8 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   }
   hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE, KS>), dim3(ntp * splits, batch), dim3(256 * KS), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
-                     ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri);
+                     ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri, MODE == 4 ? t_c2 : nullptr,
+                     MODE == 4 ? t_ldc2 : 0);
   if (splits > 1) {
     const long long tot = (long long)m * n;
     hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
@@ -460,12 +486,14 @@ constexpr int BK64 = 16;
 template <bool TA, bool TB, int MODE>
 int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
                   int lda, const double* B, int ldb, double beta, double* C, int ldc, int tri) {
+  constexpr bool FULLC = MODE == 0 || MODE == 4;  // every tile of C computed
   // In-place products (C aliases an operand: the blocked TRSMs C = C Dinv,
   // L21 = A21 Dinv^T, X_p = W_p B_p) are race-free only when every workgroup
   // owns whole rows (C aliases A) or whole columns (C aliases B) of C.
   const bool alias_a = overlaps(A, lda, TA ? k : m, TA ? m : k, C, ldc, m, n);
   const bool alias_b = overlaps(B, ldb, TB ? n : k, TB ? k : n, C, ldc, m, n);
   if (alias_a || alias_b) {
+    if (MODE == 3 || MODE == 4) return SMG_ERR_ARG;  // (the symbolic step's products never alias)
     if (MODE == 0 && alias_a && !alias_b && n <= 64)
       return launch<32, 64, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (MODE == 0 && alias_b && !alias_a && m <= 64)
@@ -489,7 +517,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   const long long big_tiles = (long long)smg_ceil_div(m, 128) * smg_ceil_div(n, 128);
   const long long t64 = smg_ceil_div(m, 64);
   const long long mid_tiles =
-      (MODE != 0 && m == n) ? t64 * (t64 + 1) / 2 : t64 * smg_ceil_div(n, 64);
+      (!FULLC && m == n) ? t64 * (t64 + 1) / 2 : t64 * smg_ceil_div(n, 64);
   {  // dev override for tile studies (tools/ubench_gemm): SMG_GEMM_TILE=128|12864|64|32
     static const int forced = [] {
       const char* e = getenv("SMG_GEMM_TILE");
@@ -512,7 +540,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   // the diagonal, and the split-K those few tiles need costs a reduction; at
   // N = K = 4096 the 528-tile 128 triangle -- 2.06 waves over the CUs -- ran
   // 1692 vs 1416 us for the 64 grid)
-  if (MODE == 0 && big_tiles >= 256 && k > 128)
+  if (FULLC && big_tiles >= 256 && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   // long-K transposed-A products with a small output (the Murray reverse's
   // [R_adj | D_adj] -= C_adj^T [B | C]: 512 x K x m, m >= 1536): 128 x 64
@@ -536,7 +564,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
       const char* e = getenv("SMG_GEMM_TRI");
       return e ? atoi(e) : 0;
     }();
-    if (MODE != 0 && mid_tiles > SMG_GEMM_KS2_MAX && tri_tile) {
+    if (!FULLC && mid_tiles > SMG_GEMM_KS2_MAX && tri_tile) {
       if (tri_tile == 12864)
         return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
       if (tri_tile == 128)
@@ -554,7 +582,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   if (mid_tiles >= 256 && !tall_nn)
     return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   const long long t32 = smg_ceil_div(m, 32);
-  const long long small_tiles = (MODE != 0 && m == n) ? t32 * (t32 + 1) / 2 : t32 * smg_ceil_div(n, 32);
+  const long long small_tiles = (!FULLC && m == n) ? t32 * (t32 + 1) / 2 : t32 * smg_ceil_div(n, 32);
   if (small_tiles <= 256)
     return launch<32, 32, 32, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
@@ -606,6 +634,12 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
     if (!ta && !tb) return dispatch_tile<false, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
     return dispatch_tile<true, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   }
+  if (uplo == 3) {  // lower half computed, stored mirrored (symmetric C)
+    if (ta && !tb) return dispatch_tile<true, false, 3>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    if (!ta && !tb) return dispatch_tile<false, false, 3>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    if (!ta && tb) return dispatch_tile<false, true, 3>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+    return dispatch_tile<true, true, 3>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  }
   if (uplo == 2) {
     if (!ta && tb) return dispatch_tile<false, true, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
     if (ta && !tb) return dispatch_tile<true, false, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
@@ -616,6 +650,24 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
   if (!ta && tb) return dispatch_tile<false, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   if (ta && !tb) return dispatch_tile<true, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   return dispatch_tile<true, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+}
+
+// C = alpha op(A) op(B) + beta C (full) and C2 = tril(C) with halved diagonal
+int smg_gemm_dual_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda,
+                       const double* B, int ldb, double beta, double* C, int ldc, double* C2, int ldc2, int tri) {
+  if (m <= 0 || n <= 0) return SMG_OK;
+  if (k <= 0 || alpha == 0.0 || !C2) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GEMM);
+  if (ctx->prof_on) ctx->prof_flops[SMG_FAM_GEMM] += 2.0 * m * n * k;
+  t_c2 = C2;
+  t_ldc2 = ldc2;
+  int rc;
+  if (!ta && !tb) rc = dispatch_tile<false, false, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  else if (ta && !tb) rc = dispatch_tile<true, false, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  else if (!ta && tb) rc = dispatch_tile<false, true, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  else rc = dispatch_tile<true, true, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  t_c2 = nullptr;
+  return rc;
 }
 
 extern "C" int smg_gemm_tri(smg_ctx* ctx, int ta, int tb, int uplo, int tri, int m, int n, int k,

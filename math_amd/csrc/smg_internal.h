@@ -170,6 +170,11 @@ int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
                   int k, double alpha, const double* A, int lda, const double* B,
                   int ldb, double beta, double* C, int ldc, int tri = 0);
 
+// C = alpha op(A) op(B) + beta C and C2 = tril(C) with halved diagonal (one pass)
+int smg_gemm_dual_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda,
+                       const double* B, int ldb, double beta, double* C, int ldc, double* C2, int ldc2,
+                       int tri = 0);
+
 int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha,
                           const double* A, int lda, long long sA, const double* B, int ldb,
                           long long sB, double beta, double* C, int ldc, long long sC, int batch);

@@ -70,6 +70,39 @@ def test_gemm_triangle(ctx, uplo):
     assert np.array_equal(out[~mask], C[~mask])  # other triangle untouched
 
 
+@pytest.mark.parametrize("n,k", [(64, 64), (200, 77), (512, 512), (1000, 300)])
+def test_gemm_symmetric_output(ctx, n, k):
+    """uplo 3: the lower half of C = A A^T - C0 computed, written mirrored."""
+    rng = np.random.default_rng(n + k)
+    A = rng.standard_normal((n, k))
+    C0 = rng.standard_normal((n, n))
+    C0 = C0 + C0.T
+    ref = A @ A.T - C0
+    dA, dC = ctx.put(F(A)), ctx.put(F(C0))
+    ctx.call("smg_gemm", 0, 1, 3, n, n, k, 1.0, dA, n, dA, n, -1.0, dC, n)
+    out = ctx.get(dC, n * n).reshape(n, n).T
+    assert np.array_equal(out, out.T)
+    assert np.abs(out - ref).max() < 1e-12 * (np.abs(A).max() ** 2 * k + np.abs(C0).max())
+
+
+@pytest.mark.parametrize("m,n,k,ta", [(512, 512, 3584, 1), (512, 2560, 1536, 1), (130, 70, 5000, 0), (64, 64, 4096, 1)])
+def test_gemm_split_k_deterministic(ctx, m, n, k, ta):
+    """Split-K products (small output grid, long K): fixed-order partial slabs,
+    three runs bitwise equal."""
+    rng = np.random.default_rng(m + n + k)
+    A = rng.standard_normal((k, m) if ta else (m, k))
+    B = rng.standard_normal((k, n))
+    C0 = rng.standard_normal((m, n))
+    ref = -(A.T if ta else A) @ B + C0
+    outs = []
+    for _ in range(3):
+        dA, dB, dC = ctx.put(F(A)), ctx.put(F(B)), ctx.put(F(C0))
+        ctx.call("smg_gemm", ta, 0, 0, m, n, k, -1.0, dA, A.shape[0], dB, k, 1.0, dC, m)
+        outs.append(ctx.get(dC, m * n).reshape(n, m).T)
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+    assert np.abs(outs[0] - ref).max() <= 1e-13 * (np.abs(A).max() * np.abs(B).max() * k + np.abs(C0).max())
+
+
 @pytest.mark.parametrize("case", ["c_is_a_right", "c_is_b_left", "c_in_a_general", "disjoint_blocks"])
 def test_gemm_in_place(ctx, case):
     """In-place products of the blocked TRSMs (C = C W, C = W C) and general
