@@ -277,11 +277,16 @@ class GLM(Workload):
         avg = ms / max(n, 1)
         ach = byts / (avg * 1e-3) / 1e9 if avg > 0 else None
         traffic, src = pmc_traffic("glm")
+        step_ms = t_prof * 1e3 / steps
         return {"bound": "hbm", "kernel": "k_glm_reg (one pass over x)", "achieved": ach,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS if ach else None,
                 "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
                 "bytes_per_launch": byts, "avg_launch_ms": avg,
-                "launches_per_step": n / steps}
+                "launches_per_step": n / steps,
+                "step_minus_glm_kernels_us": (step_ms - ms / steps) * 1e3,
+                "note_overhead": "profiled step time minus the GLM family's HIP-event time: host work "
+                                 "(gradient() tape, one staged upload / download, one sync) + the "
+                                 "partials reduction + launch gaps"}
 
     def cpu_baseline(self):
         rs = 1000000

@@ -421,6 +421,15 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x,
                             long long R, int M, long long ldx,
                             const double* alpha_beta, double* ws, double* out);
 
+/* smg_bernoulli_logit_glm with the reference's check_bounded(y, 0, 1)
+ * (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:75) fused into the same pass:
+ * out (M + 3 doubles) = [logp, sum theta', x^T theta' (M), number of y
+ * outside {0, 1}].  Replaces smg_check_bounded_int + smg_bernoulli_logit_glm
+ * (one launch and one pass over y fewer per evaluation). */
+int smg_bernoulli_logit_glm_checked(smg_ctx* ctx, const int* y, const double* x,
+                                    long long R, int M, long long ldx,
+                                    const double* alpha_beta, double* ws, double* out);
+
 /* normal_id_glm_lpdf<false>(y | x, alpha, beta, sigma), scalar alpha and
  * sigma (prim/mat/prob/normal_id_glm_lpdf.hpp:40-150), ONE fused pass over x:
  *   abs = [alpha, beta(M), sigma] (device);

@@ -179,10 +179,14 @@ __global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
 // thread (summed over the 32 rows of a column group once, at the end, by
 // lane shuffles).  A load instruction still covers two 256-byte column
 // segments per wave.
+// check_y (KIND 0): also count the rows whose y is outside {0, 1} (the
+// reference's check_bounded(y, 0, 1), prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:75)
+// into partial slot M + 2 -- the pass reads y anyway, so the check costs no
+// extra launch and no extra pass over y.
 template <int KIND, int RB, int NT, bool NTL = false>
 __global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, const double* __restrict__ x,
                                                 long long R, int M, long long ldx, const double* __restrict__ ab,
-                                                double* __restrict__ part) {
+                                                double* __restrict__ part, int check_y = 0) {
   constexpr int G = NT / RB, Q = MMAX / G;
   const int* __restrict__ y = static_cast<const int*>(yv);
   const double* __restrict__ yd = static_cast<const double*>(yv);
@@ -254,6 +258,7 @@ __global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, con
       if (g == 0) {  // one thread per row accumulates the row's terms
         lp_acc += lp;
         ga_acc += th;
+        if (KIND == 0) c_acc += (cy != 0.0 && cy != 1.0) ? 1.0 : 0.0;
       }
     }
 #pragma unroll
@@ -287,21 +292,22 @@ __global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, con
 #pragma unroll
   for (int q = 0; q < Q; ++q)
     for (int off = RB / 2; off > 0; off >>= 1) gacc[q] += __shfl_xor(gacc[q], off, RB);
-  const int W = M + 2 + (KIND == 2);
+  const bool extra = KIND == 2 || (KIND == 0 && check_y);
+  const int W = M + 2 + (extra ? 1 : 0);
   double* p = part + (size_t)blockIdx.x * W;
   __syncthreads();
   const double lp = block_sum(lp_acc, lds);
   __syncthreads();
   const double ga = block_sum(ga_acc, lds);
   double cs = 0.0;
-  if (KIND == 2) {
+  if (extra) {
     __syncthreads();
     cs = block_sum(c_acc, lds);
   }
   if (t == 0) {
     p[0] = lp;
     p[1] = ga;
-    if (KIND == 2) p[M + 2] = cs;
+    if (extra) p[M + 2] = cs;
   }
   if (r == 0)
 #pragma unroll
@@ -338,7 +344,7 @@ inline int glm_env(const char* name, int dflt) {
 
 template <int KIND>
 int glm_launch(hipStream_t st, const void* y, const double* x, long long R, int M, long long ldx,
-               const double* ab, double* ws) {
+               const double* ab, double* ws, int check_y = 0) {
   static const int variant = glm_env("SMG_GLM_REG", 1);
   static const int nb_cap = glm_env("SMG_GLM_NB", 0);
   int nb = glm_blocks(R);
@@ -357,7 +363,8 @@ int glm_launch(hipStream_t st, const void* y, const double* x, long long R, int 
       hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
       break;
     default:
-      hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512, true>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
+      hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512, true>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws,
+                         check_y);
   }
   return nb;
 }
@@ -568,6 +575,25 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x, long lo
   rc = smg_gemm_impl(ctx, 1, 0, 0, M, 1, (int)R, 1.0, x, (int)ldx, th, (int)R, 0.0, out + 2, M);
   SMG_LAUNCH_CHECK();
   return rc;
+}
+
+int smg_bernoulli_logit_glm_checked(smg_ctx* ctx, const int* y, const double* x, long long R, int M,
+                                    long long ldx, const double* ab, double* ws, double* out) {
+  if (!ctx || R < 0 || M < 0 || !ab || !ws || !out) return SMG_ERR_ARG;
+  if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
+  static const int variant = glm_env("SMG_GLM_REG", 1);
+  if (M > MMAX || variant != 1 || R == 0) {  // the other variants: a separate bound check
+    int rc = smg_memset(ctx, out + M + 2, 0, sizeof(double));
+    if (!rc) rc = smg_check_bounded_int(ctx, y, R, 0, 1, out + M + 2);
+    if (!rc) rc = R > 0 ? smg_bernoulli_logit_glm(ctx, y, x, R, M, ldx, ab, ws, out)
+                        : smg_memset(ctx, out, 0, sizeof(double) * (M + 2));
+    return rc;
+  }
+  smg_prof_scope prof(ctx, SMG_FAM_GLM);
+  const int nb = glm_launch<0>(ctx->stream, y, x, R, M, ldx, ab, ws, 1);
+  smg_reduce_partials(ctx, ws, nb, M + 3, out, 0);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
 }
 
 long long smg_glm_categorical_ws_doubles(long long R, int M, int C) {

@@ -56,6 +56,7 @@ _SIGS = {
     "smg_gemm_tri": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _D, _P, _I, _P, _I, _D, _P, _I]),
     "smg_gp_exp_quad_cov_fwd": (_I, [_P, _P, _I, _D, _D, _P, _I]),
     "smg_gp_exp_quad_cov_rev": (_I, [_P, _P, _I, _D, _D, _P, _I, _P]),
+    "smg_bernoulli_logit_glm_checked": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
     "smg_marker_record": (_I, [_P, _I]),
     "smg_marker_wait": (_I, [_P, _I]),
     "smg_gp_exp_quad_cov_nd_fwd": (_I, [_P, _P, _I, _I, _D, _D, _P, _I]),

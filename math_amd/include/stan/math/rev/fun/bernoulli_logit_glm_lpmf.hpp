@@ -159,24 +159,31 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
     throw std::invalid_argument(m.str());
   }
   smg_ctx* c = amd::ctx();
-  // [alpha, beta(M) | out: logp, alpha', beta'(M) | flag]
-  double* buf = amd::alloc_doubles(size_t(2 * M + 4));
+  // [alpha, beta(M) | out: logp, alpha', beta'(M), y flag]: the parameters go
+  // up and the results come down through ONE pinned staging buffer with ONE
+  // synchronisation per evaluation (stream order keeps the upload ahead of
+  // the download into the same buffer)
+  const size_t nb = size_t(2 * M + 4);
+  double* buf = amd::alloc_doubles(nb);
   double* ab = buf;
   double* out = buf + M + 1;
-  double* flag = buf + 2 * M + 3;
-  std::vector<double> h(size_t(2 * M + 4), 0.0);
+  double* h = static_cast<double*>(smg_host_scratch(c, (nb + 1) * sizeof(double)));
+  if (!h) throw std::bad_alloc();
   h[0] = p.alpha;
   for (int j = 0; j < M; ++j) h[1 + j] = p.beta[j];
-  amd::to_device(buf, h.data(), h.size());
-  amd::check(smg_check_bounded_int(c, s.y, s.rows, 0, 1, flag), fn);
-  if (s.rows > 0) {
-    double* ws = amd::alloc_doubles(size_t(smg_glm_ws_doubles(s.rows, M)));
-    amd::check(smg_bernoulli_logit_glm(c, s.y, s.x, s.rows, M, s.ldx, ab, ws, out), fn);
-  }
+  amd::check(smg_memcpy_h2d(c, buf, h, size_t(M + 1) * sizeof(double)), fn);
+  double* ws = amd::alloc_doubles(size_t(smg_glm_ws_doubles(s.rows > 0 ? s.rows : 1, M)));
+  // the fused pass also counts y outside {0, 1} (out[M + 2])
+  amd::check(smg_bernoulli_logit_glm_checked(c, s.y, s.x, s.rows, M, s.ldx, ab, ws, out), fn);
   // [logp, alpha', beta'(M) | flag] are contiguous: the y-support flag is
   // summed with them, so a bad y on any rank makes every rank throw
   if (s.distributed) amd::allreduce_sum(out, M + 3, fn);
-  amd::to_host(h.data(), buf, h.size());
+  int armed = 0;
+  amd::check(smg_status_armed(c, &armed), fn);
+  amd::check(smg_memcpy_d2h(c, h + M + 1, out, size_t(M + 3) * sizeof(double)), fn);
+  if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(h + nb)), fn);
+  amd::check(smg_sync(c), fn);
+  if (armed) amd::throw_if_sync(*reinterpret_cast<int*>(h + nb), fn, "a persistent solve");
   if (h[2 * M + 3] != 0.0) glm_throw_y_bounds(fn, s.y, s.rows, 0, 1, s.row0);
   if (s.total_rows == 0 || !(p.any_var() || !propto)) return glm_result{};
   const double lp = h[M + 1];
