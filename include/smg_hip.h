@@ -429,6 +429,17 @@ int smg_bernoulli_logit_glm(smg_ctx* ctx, const int* y, const double* x,
 int smg_bernoulli_logit_glm_checked(smg_ctx* ctx, const int* y, const double* x,
                                     long long R, int M, long long ldx,
                                     const double* alpha_beta, double* ws, double* out);
+/* The latency-bound form: alpha and beta (M doubles, host memory) are passed
+ * in the launch's kernel arguments (no upload), and the pass's last
+ * workgroup writes out (device, M + 3 doubles: [logp, alpha', beta'(M),
+ * count of y outside {0, 1}]) and, when out_h is non-null (pinned host
+ * memory from smg_pinned_io), the same values to out_h, then returns once
+ * they have landed (the host spins on a completion word, no stream
+ * synchronisation).  With out_h null the call returns without waiting.
+ * ws: smg_glm_ws_doubles(R, M) doubles.  Other variants / M > 256 / R == 0
+ * take the general path (upload, smg_bernoulli_logit_glm_checked, copy back). */
+int smg_bernoulli_logit_glm_io(smg_ctx* ctx, const int* y, const double* x, long long R, int M, long long ldx,
+                               double alpha, const double* beta, double* ws, double* out, double* out_h);
 
 /* normal_id_glm_lpdf<false>(y | x, alpha, beta, sigma), scalar alpha and
  * sigma (prim/mat/prob/normal_id_glm_lpdf.hpp:40-150), ONE fused pass over x:
@@ -519,6 +530,13 @@ int smg_comm_allreduce_sum(smg_ctx* ctx, double* buf, long long count);
  * per-job [value; partials] columns (replaces the gatherv of
  * prim/mat/functor/mpi_parallel_call.hpp:374-382). */
 int smg_comm_allgather(smg_ctx* ctx, const double* send, long long count, double* recv);
+/* recv (device, counts[my rank] doubles) <- my block of the root's send
+ * (device, the blocks of ranks 0, 1, ... back to back; read on the root
+ * only): the distributed map_rect's one-time scatter of each rank's job data
+ * per call_id (replaces boost::mpi::scatterv in
+ * prim/mat/functor/mpi_parallel_call.hpp:423-450). counts: nranks entries,
+ * the same on every rank. */
+int smg_comm_scatterv(smg_ctx* ctx, const double* send, const long long* counts, double* recv, int root);
 int smg_comm_destroy(smg_ctx* ctx);
 
 #ifdef __cplusplus

@@ -1,7 +1,8 @@
 // RCCL (xGMI) communicator for the row-sharded reducers.
 // One communicator per process/device.  The row-sharded reducers' one
 // collective is a single fp64 sum all-reduce of [logp, alpha', beta'(M)] per
-// gradient; the distributed map_rect executor all-gathers per-job results.
+// gradient; the distributed map_rect executor all-gathers per-job results and
+// scatters each rank's block of the job data once per call_id (scatterv).
 // Replaces map_rect's Boost.MPI reduce/gatherv
 // (prim/mat/functor/mpi_parallel_call.hpp:320-392).
 #include <hip/hip_runtime.h>
@@ -48,6 +49,45 @@ int smg_comm_allgather(smg_ctx* ctx, const double* send, long long count, double
   if (count == 0) return SMG_OK;
   if (ncclAllGather(send, recv, (size_t)count, ncclDouble, (ncclComm_t)ctx->comm, ctx->stream) != ncclSuccess)
     return SMG_ERR_HIP;
+  return SMG_OK;
+}
+
+int smg_comm_scatterv(smg_ctx* ctx, const double* send, const long long* counts, double* recv, int root) {
+  if (!ctx || !ctx->comm || !counts) return SMG_ERR_ARG;
+  ncclComm_t c = (ncclComm_t)ctx->comm;
+  int n = 0, me = 0;
+  if (ncclCommCount(c, &n) != ncclSuccess || ncclCommUserRank(c, &me) != ncclSuccess) return SMG_ERR_HIP;
+  if (root < 0 || root >= n) return SMG_ERR_ARG;
+  long long total = 0;
+  for (int r = 0; r < n; ++r) {
+    if (counts[r] < 0) return SMG_ERR_ARG;
+    total += counts[r];
+  }
+  if ((me == root && total > 0 && !send) || (counts[me] > 0 && !recv)) return SMG_ERR_ARG;
+  // point-to-point: the root sends rank r its block, each rank receives its own
+  if (ncclGroupStart() != ncclSuccess) return SMG_ERR_HIP;
+  long long off = 0;
+  for (int r = 0; r < n; ++r) {
+    if (me == root && r != root && counts[r] > 0 &&
+        ncclSend(send + off, (size_t)counts[r], ncclDouble, r, c, ctx->stream) != ncclSuccess) {
+      ncclGroupEnd();
+      return SMG_ERR_HIP;
+    }
+    off += counts[r];
+  }
+  if (me != root && counts[me] > 0 &&
+      ncclRecv(recv, (size_t)counts[me], ncclDouble, root, c, ctx->stream) != ncclSuccess) {
+    ncclGroupEnd();
+    return SMG_ERR_HIP;
+  }
+  if (ncclGroupEnd() != ncclSuccess) return SMG_ERR_HIP;
+  if (me == root && counts[me] > 0) {
+    long long o = 0;
+    for (int r = 0; r < root; ++r) o += counts[r];
+    if (hipMemcpyAsync(recv, send + o, (size_t)counts[me] * sizeof(double), hipMemcpyDeviceToDevice,
+                       ctx->stream) != hipSuccess)
+      return SMG_ERR_HIP;
+  }
   return SMG_OK;
 }
 

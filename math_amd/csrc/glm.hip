@@ -183,10 +183,10 @@ __global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
 // reference's check_bounded(y, 0, 1), prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:75)
 // into partial slot M + 2 -- the pass reads y anyway, so the check costs no
 // extra launch and no extra pass over y.
-template <int KIND, int RB, int NT, bool NTL = false>
-__global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, const double* __restrict__ x,
-                                                long long R, int M, long long ldx, const double* __restrict__ ab,
-                                                double* __restrict__ part, int check_y = 0) {
+template <int KIND, int RB, int NT, bool NTL>
+__device__ __forceinline__ void glm_reg_body(const void* __restrict__ yv, const double* __restrict__ x, long long R,
+                                             int M, long long ldx, const double* __restrict__ ab,
+                                             double* __restrict__ part, int check_y) {
   constexpr int G = NT / RB, Q = MMAX / G;
   const int* __restrict__ y = static_cast<const int*>(yv);
   const double* __restrict__ yd = static_cast<const double*>(yv);
@@ -315,6 +315,55 @@ __global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, con
       const int c = g + G * q;
       if (c < M) p[2 + c] = gacc[q];
     }
+}
+
+template <int KIND, int RB, int NT, bool NTL = false>
+__global__ __launch_bounds__(NT) void k_glm_reg(const void* __restrict__ yv, const double* __restrict__ x,
+                                                long long R, int M, long long ldx, const double* __restrict__ ab,
+                                                double* __restrict__ part, int check_y = 0) {
+  glm_reg_body<KIND, RB, NT, NTL>(yv, x, R, M, ldx, ab, part, check_y);
+}
+
+// [alpha, beta(M)] as a kernel argument: the launch carries the parameters,
+// no host-to-device copy ahead of it
+struct glm_ab_arg {
+  double v[MMAX + 1];
+};
+
+// The latency-bound form of k_glm_reg (KIND 0, y-bounds count on) takes the
+// parameters from the kernel arguments of a one-workgroup copy ahead of it
+// (no host-to-device copy).  The kernel arguments live in host memory: the
+// streaming kernel reading them directly (every workgroup, 8 B at a time
+// over the bus) measured 0.44 -> 0.53 ms at 1.25e6 rows.
+__global__ __launch_bounds__(256) void k_glm_params(glm_ab_arg a, int n, double* __restrict__ dst) {
+  for (int i = threadIdx.x; i < n; i += 256) dst[i] = a.v[i];
+}
+
+// ...and its finish: one workgroup per output column c sums column c of the
+// per-workgroup partials (the order of k_reduce_partials: the same bits as
+// the staged path), writes out[c] (device) and out_h[c] (pinned host), and
+// takes a ticket; the last workgroup publishes seq to the host completion
+// word, so the host spins on it instead of a copy back and a stream
+// synchronisation.  (One workgroup summing all M + 3 columns measured 84 us
+// at M = 256 -- 1 MB of partials through one CU -- against 4.7 us here.)
+__global__ __launch_bounds__(256) void k_glm_io_final(const double* __restrict__ part, int nb, int W, double* out,
+                                                      double* out_h, unsigned int* counter, long long* done,
+                                                      long long seq) {
+  __shared__ double lds[16];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[(size_t)i * W + c];
+  s = block_sum(s, lds);
+  if (threadIdx.x != 0) return;
+  out[c] = s;
+  if (!out_h) return;
+  // a system-scope store goes to host memory directly; the ticket's
+  // system-scope release orders it (and out[c]) before this workgroup's
+  // arrival, the last arrival's acquire orders every column before done
+  __hip_atomic_store(out_h + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (__hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) != gridDim.x - 1) return;
+  __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // rows per tile (measured on MI355X: 16 rows 4.3 TB/s, 32 rows 5.1, 64 rows 4.0).
@@ -594,6 +643,44 @@ int smg_bernoulli_logit_glm_checked(smg_ctx* ctx, const int* y, const double* x,
   smg_reduce_partials(ctx, ws, nb, M + 3, out, 0);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
+}
+
+int smg_bernoulli_logit_glm_io(smg_ctx* ctx, const int* y, const double* x, long long R, int M, long long ldx,
+                               double alpha, const double* beta, double* ws, double* out, double* out_h) {
+  if (!ctx || R < 0 || M < 0 || !ws || !out || (M > 0 && !beta)) return SMG_ERR_ARG;
+  if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
+  static const int variant = glm_env("SMG_GLM_REG", 1);
+  static const int nb_cap = glm_env("SMG_GLM_NB", 0);
+  static const int io = glm_env("SMG_GLM_IO", 1);  // dev A/B switch: 0 = always the general path
+  if (M > MMAX || variant != 1 || R == 0 || !io) {  // the general path, then one copy back and a synchronisation
+    double* ab = smg_ws(ctx, SMG_WS_TMP2, (size_t)M + 1);
+    double* h = (double*)smg_host_scratch(ctx, sizeof(double) * (M + 1));
+    if (!ab || !h) return SMG_ERR_OOM;
+    h[0] = alpha;
+    for (int j = 0; j < M; ++j) h[1 + j] = beta[j];
+    int rc = smg_memcpy_h2d(ctx, ab, h, sizeof(double) * (M + 1));
+    if (!rc) rc = smg_bernoulli_logit_glm_checked(ctx, y, x, R, M, ldx, ab, ws, out);
+    if (!rc && out_h) rc = smg_memcpy_d2h(ctx, out_h, out, sizeof(double) * (M + 3));
+    if (!rc) rc = smg_sync(ctx);  // the scratch upload has been read
+    return rc;
+  }
+  glm_ab_arg a;
+  a.v[0] = alpha;
+  for (int j = 0; j < M; ++j) a.v[1 + j] = beta[j];
+  int nb = glm_blocks(R);
+  if (nb_cap > 0 && nb_cap < nb) nb = nb_cap;
+  const long long seq = out_h ? ++ctx->done_seq : 0;
+  {  // (the profiling scope closes before the host waits)
+    smg_prof_scope prof(ctx, SMG_FAM_GLM);
+    double* ab = smg_ws(ctx, SMG_WS_TMP2, MMAX + 1);
+    if (!ab) return SMG_ERR_OOM;
+    hipLaunchKernelGGL(k_glm_params, dim3(1), dim3(256), 0, ctx->stream, a, M + 1, ab);
+    hipLaunchKernelGGL((k_glm_reg<0, GLM_RB, 512, true>), dim3(nb), dim3(512), 0, ctx->stream, y, x, R, M, ldx, ab, ws, 1);
+    hipLaunchKernelGGL(k_glm_io_final, dim3(M + 3), dim3(256), 0, ctx->stream, ws, nb, M + 3, out, out_h,
+                       ctx->red_counter_d + 1, out_h ? ctx->done_h : nullptr, seq);
+    SMG_LAUNCH_CHECK();
+  }
+  return out_h ? smg_wait_done(ctx, seq) : SMG_OK;
 }
 
 long long smg_glm_categorical_ws_doubles(long long R, int M, int C) {

@@ -57,6 +57,7 @@ _SIGS = {
     "smg_gp_exp_quad_cov_fwd": (_I, [_P, _P, _I, _D, _D, _P, _I]),
     "smg_gp_exp_quad_cov_rev": (_I, [_P, _P, _I, _D, _D, _P, _I, _P]),
     "smg_bernoulli_logit_glm_checked": (_I, [_P, _P, _P, _L, _I, _L, _P, _P, _P]),
+    "smg_bernoulli_logit_glm_io": (_I, [_P, _P, _P, _L, _I, _L, _D, _P, _P, _P, _P]),
     "smg_marker_record": (_I, [_P, _I]),
     "smg_marker_wait": (_I, [_P, _I]),
     "smg_gp_exp_quad_cov_nd_fwd": (_I, [_P, _P, _I, _I, _D, _D, _P, _I]),
@@ -129,6 +130,7 @@ _SIGS = {
     "smg_comm_init": (_I, [_P, _I, _I, ctypes.c_char_p]),
     "smg_comm_allreduce_sum": (_I, [_P, _P, _L]),
     "smg_comm_allgather": (_I, [_P, _P, _L, _P]),
+    "smg_comm_scatterv": (_I, [_P, _P, _P, _P, _I]),
     "smg_comm_destroy": (_I, [_P]),
 }
 

@@ -7,11 +7,13 @@
 // sum all-reduce of device doubles.  Both run over RCCL unless a host
 // collective is installed with set_host_collective (a test harness's gloo
 // process group, or any transport of the caller's); the map_rect executor
-// (rev/functor/map_rect.hpp) only ever calls amd::allgather, the row-sharded
-// reducers (*_glm_*) only amd::allreduce_sum.
+// (rev/functor/map_rect.hpp) calls amd::allgather (results) and amd::scatterv
+// (its job data, once per call_id), the row-sharded reducers (*_glm_*) only
+// amd::allreduce_sum.
 
 #include <stan/math/amd/device.hpp>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -24,6 +26,9 @@ namespace amd {
 using allgather_fn = void (*)(const double* send, long long count, double* recv, void* user);
 /** buf[i] = sum over ranks of buf[i] (in place, host doubles); every rank calls it. */
 using allreduce_fn = void (*)(double* buf, long long count, void* user);
+/** recv <- rank r's block of rank 0's send (blocks of counts[0], counts[1],
+ * ... doubles back to back; send is read on rank 0 only); every rank calls it. */
+using scatterv_fn = void (*)(const double* send, const long long* counts, double* recv, void* user);
 
 struct comm_state {
   int nranks = 1;
@@ -31,6 +36,7 @@ struct comm_state {
   bool rccl = false;
   allgather_fn host_allgather = nullptr;
   allreduce_fn host_allreduce = nullptr;
+  scatterv_fn host_scatterv = nullptr;
   void* user = nullptr;
 };
 inline comm_state& comm_info() {
@@ -57,12 +63,13 @@ inline void comm_destroy() {
  * all-reduce the row-sharded reducers use (optional; without it they need
  * RCCL). */
 inline void set_host_collective(int nranks, int rank, allgather_fn fn, void* user,
-                                allreduce_fn ar = nullptr) {
+                                allreduce_fn ar = nullptr, scatterv_fn sc = nullptr) {
   if (fn && (nranks < 1 || rank < 0 || rank >= nranks))
     throw std::invalid_argument("set_host_collective: rank outside [0, nranks)");
   comm_state& s = comm_info();
   s.host_allgather = fn;
   s.host_allreduce = fn ? ar : nullptr;
+  s.host_scatterv = fn ? sc : nullptr;
   s.user = user;
   s.nranks = fn ? nranks : (s.rccl ? s.nranks : 1);
   s.rank = fn ? rank : (s.rccl ? s.rank : 0);
@@ -95,6 +102,43 @@ inline void allgather(const double* send, long long count, double* recv) {
   to_device(d, send, size_t(count));
   check(smg_comm_allgather(ctx(), d, count, d + count), "allgather");
   to_host(recv, d + count, size_t(count) * s.nranks);
+}
+
+/** Scatter from rank 0: recv (host, counts[my rank] doubles) <- my block of
+ * rank 0's send (host; blocks of counts[0], counts[1], ... back to back).
+ * RCCL: point-to-point sends from the root (smg_comm_scatterv); a host
+ * collective: its scatterv hook, or -- without one -- an all-gather of the
+ * root's whole buffer. */
+inline void scatterv(const double* send, const std::vector<long long>& counts, double* recv) {
+  comm_state& s = comm_info();
+  const int W = s.nranks, me = s.rank;
+  if (int(counts.size()) != W) throw std::invalid_argument("scatterv: one count per rank");
+  long long total = 0, off = 0;
+  for (int r = 0; r < W; ++r) {
+    if (r < me) off += counts[size_t(r)];
+    total += counts[size_t(r)];
+  }
+  if (W == 1 || (!s.host_allgather && !s.rccl)) {
+    if (W != 1) throw std::logic_error("scatterv: no collective for a multi-rank job");
+    for (long long i = 0; i < counts[0]; ++i) recv[i] = send[i];
+    return;
+  }
+  if (s.host_allgather) {
+    if (s.host_scatterv) {
+      s.host_scatterv(send, counts.data(), recv, s.user);
+      return;
+    }
+    std::vector<double> mine(size_t(total), 0.0), all(size_t(total) * W);
+    if (me == 0) std::copy(send, send + total, mine.begin());
+    s.host_allgather(mine.data(), total, all.data(), s.user);
+    std::copy(all.begin() + off, all.begin() + off + counts[size_t(me)], recv);
+    return;
+  }
+  if (total == 0) return;
+  double* d = alloc_doubles(size_t(total) + size_t(counts[size_t(me)]));
+  if (me == 0) to_device(d, send, size_t(total));
+  check(smg_comm_scatterv(ctx(), d, counts.data(), d + total, 0), "scatterv");
+  to_host(recv, d + total, size_t(counts[size_t(me)]));
 }
 
 /** Sum all-reduce of `count` device doubles in place, on the tape's stream

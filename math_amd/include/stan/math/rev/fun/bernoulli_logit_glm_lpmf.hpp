@@ -3,8 +3,10 @@
 
 // bernoulli_logit_glm_lpmf<propto>(y | x, alpha, beta), scalar intercept
 // (prim/mat/prob/bernoulli_logit_glm_lpmf.hpp:46-144), with x and y resident
-// on the device: ONE fused pass over x yields [logp, sum theta', x^T theta']
-// (smg_bernoulli_logit_glm), read back with the y-bounds flag in one copy.
+// on the device: ONE fused pass over x yields [logp, sum theta', x^T theta',
+// y-bounds count] (smg_bernoulli_logit_glm_io: parameters in the kernel
+// arguments, results written to pinned host memory by the pass's last
+// workgroup).
 // Semantics kept: check_consistent_size of y / beta (:63-64), check_bounded(y,
 // 0, 1) (:69), size_zero -> 0 (:71-73), include_summand<propto, x, alpha,
 // beta> (:75-77), the non-finite logp checks of beta, alpha, then the linear
@@ -159,34 +161,38 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
     throw std::invalid_argument(m.str());
   }
   smg_ctx* c = amd::ctx();
-  // [alpha, beta(M) | out: logp, alpha', beta'(M), y flag]: the parameters go
-  // up and the results come down through ONE pinned staging buffer with ONE
-  // synchronisation per evaluation (stream order keeps the upload ahead of
-  // the download into the same buffer)
-  const size_t nb = size_t(2 * M + 4);
-  double* buf = amd::alloc_doubles(nb);
-  double* ab = buf;
-  double* out = buf + M + 1;
-  double* h = static_cast<double*>(smg_host_scratch(c, (nb + 1) * sizeof(double)));
-  if (!h) throw std::bad_alloc();
-  h[0] = p.alpha;
-  for (int j = 0; j < M; ++j) h[1 + j] = p.beta[j];
-  amd::check(smg_memcpy_h2d(c, buf, h, size_t(M + 1) * sizeof(double)), fn);
+  // (alpha, beta) travel in the launch's kernel arguments; the fused pass also
+  // counts y outside {0, 1}, and its last workgroup writes [logp, alpha',
+  // beta'(M), bad-y count] to `out` (device) and -- on one GPU with no
+  // latched-status launch outstanding -- straight to pinned host memory,
+  // publishing a completion word the host spins on (no copy, no stream sync)
+  double* out = amd::alloc_doubles(size_t(M + 3));
   double* ws = amd::alloc_doubles(size_t(smg_glm_ws_doubles(s.rows > 0 ? s.rows : 1, M)));
-  // the fused pass also counts y outside {0, 1} (out[M + 2])
-  amd::check(smg_bernoulli_logit_glm_checked(c, s.y, s.x, s.rows, M, s.ldx, ab, ws, out), fn);
-  // [logp, alpha', beta'(M) | flag] are contiguous: the y-support flag is
-  // summed with them, so a bad y on any rank makes every rank throw
-  if (s.distributed) amd::allreduce_sum(out, M + 3, fn);
   int armed = 0;
   amd::check(smg_status_armed(c, &armed), fn);
-  amd::check(smg_memcpy_d2h(c, h + M + 1, out, size_t(M + 3) * sizeof(double)), fn);
-  if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(h + nb)), fn);
-  amd::check(smg_sync(c), fn);
-  if (armed) amd::throw_if_sync(*reinterpret_cast<int*>(h + nb), fn, "a persistent solve");
-  if (h[2 * M + 3] != 0.0) glm_throw_y_bounds(fn, s.y, s.rows, 0, 1, s.row0);
+  const double* h;
+  if (!s.distributed && !armed) {
+    double* o = static_cast<double*>(smg_pinned_io(c, size_t(M + 3) * sizeof(double)));
+    if (!o) throw std::bad_alloc();
+    amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out, o), fn);
+    h = o;
+  } else {
+    amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out,
+                                          nullptr), fn);
+    // the y-support count is summed with the rest, so a bad y on any rank
+    // makes every rank throw
+    if (s.distributed) amd::allreduce_sum(out, M + 3, fn);
+    double* o = static_cast<double*>(smg_host_scratch(c, size_t(M + 4) * sizeof(double)));
+    if (!o) throw std::bad_alloc();
+    amd::check(smg_memcpy_d2h(c, o, out, size_t(M + 3) * sizeof(double)), fn);
+    if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(o + M + 3)), fn);
+    amd::check(smg_sync(c), fn);
+    if (armed) amd::throw_if_sync(*reinterpret_cast<int*>(o + M + 3), fn, "a persistent solve");
+    h = o;
+  }
+  if (h[M + 2] != 0.0) glm_throw_y_bounds(fn, s.y, s.rows, 0, 1, s.row0);
   if (s.total_rows == 0 || !(p.any_var() || !propto)) return glm_result{};
-  const double lp = h[M + 1];
+  const double lp = h[0];
   if (!std::isfinite(lp)) {
     for (int j = 0; j < M; ++j)
       if (!std::isfinite(p.beta[j])) {
@@ -204,7 +210,7 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
   }
   if (!p.any_var()) return glm_result{lp, nullptr};
   double* g = ChainableStack::instance_->memalloc_.alloc_array<double>(size_t(M + 1));
-  for (int j = 0; j <= M; ++j) g[j] = h[M + 2 + j];
+  for (int j = 0; j <= M; ++j) g[j] = h[1 + j];
   return glm_result{lp, new glm_dev_vari(lp, p.alpha_vi, p.beta_vi, p.beta_dev, g, out + 2, M)};
 }
 

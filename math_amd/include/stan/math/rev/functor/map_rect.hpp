@@ -23,7 +23,17 @@
 // to ranks 1, 2, ...) on its own GPU, and two all-gathers exchange
 //   (1) [status, outputs per job] of every rank, then
 //   (2) every job's [value; d/d shared; d/d job] columns,
-// after which every rank combines the same full result.  The per-job values
+// after which every rank combines the same full result.
+//
+// Job data cache (prim/mat/functor/mpi_parallel_call.hpp:170-181, 423-450):
+// the first distributed call of a call_id fixes each rank's block of x_r /
+// x_i -- sliced locally when every rank passed the data, scattered from rank
+// 0 (amd::scatterv) when only the root holds it (the other ranks may pass
+// empty x_r / x_i) -- and every later call of that call_id uses the cached
+// block without exchanging any data, as the reference's workers do (the
+// x_r / x_i passed to a later call are then not read for the evaluation:
+// the reference's cache semantics).  map_rect_clear_cache() forgets every
+// call_id's block.  The per-job values
 // and partials are the ones a single process computes, so the result is
 // bit-identical to the serial path.  A job that throws on any rank makes
 // every rank throw std::domain_error("Error during MPI evaluation."), as the
@@ -103,6 +113,29 @@ Eigen::MatrixXd map_rect_reduce_job(const Eigen::VectorXd& shared, const Eigen::
   return out;
 }
 
+/** One call_id's cached job data: this rank's block of jobs (the reference
+ * keeps one cache per call_id, mpi_parallel_call_cache<call_id, ...>). */
+struct map_rect_data {
+  bool valid = false;
+  int world = 0;
+  size_t J = 0, nr = 0, ni = 0;
+  std::vector<std::vector<double>> x_r;
+  std::vector<std::vector<int>> x_i;
+};
+inline std::vector<map_rect_data*>& map_rect_caches() {
+  static std::vector<map_rect_data*> all;
+  return all;
+}
+template <int call_id>
+map_rect_data& map_rect_cache() {
+  static map_rect_data* d = [] {
+    auto* p = new map_rect_data();
+    map_rect_caches().push_back(p);
+    return p;
+  }();
+  return *d;
+}
+
 /** Jobs per rank: J / W each, the remainder one by one to ranks 1, 2, ...
  * (from rank 0 when J < W) -- mpi_map_chunks. */
 inline std::vector<int> map_rect_chunks(size_t J, int W) {
@@ -112,14 +145,75 @@ inline std::vector<int> map_rect_chunks(size_t J, int W) {
   return c;
 }
 
-/** Evaluate this rank's chunk of jobs, then all-gather every job's output
- * columns (rows = 1 + shared partials + job partials, or 1 for values). */
+/** Fill `c` with this rank's block of the job data: one all-gather of
+ * [J, x_r length, x_i length, holds data] per rank, then either a local slice
+ * (every rank holds the data) or two scatters from rank 0 (x_r, then x_i as
+ * doubles: exact for every int).  The root's sizes are the job's. */
+inline void map_rect_fill_cache(map_rect_data& c, size_t J, const std::vector<std::vector<double>>& x_r,
+                                const std::vector<std::vector<int>>& x_i) {
+  const int W = amd::world_size(), rank = amd::world_rank();
+  const bool have = x_r.size() == J && x_i.size() == J;
+  double hdr[4] = {double(J), have && J ? double(x_r[0].size()) : 0.0, have && J ? double(x_i[0].size()) : 0.0,
+                   have ? 1.0 : 0.0};
+  std::vector<double> all(size_t(4) * W);
+  amd::allgather(hdr, 4, all.data());
+  if (all[3] != 1.0)  // (every rank sees the root's flag: all of them throw)
+    throw std::invalid_argument("map_rect: the root (rank 0) must hold the job data");
+  const size_t nr = size_t(all[1]), ni = size_t(all[2]);
+  bool everyone = true;
+  for (int r = 0; r < W; ++r) {
+    everyone = everyone && all[size_t(4 * r + 3)] == 1.0;
+    if (size_t(all[size_t(4 * r)]) != J)
+      throw std::invalid_argument("map_rect: every rank must pass the same number of jobs");
+  }
+  const std::vector<int> chunks = map_rect_chunks(J, W);
+  size_t first = 0;
+  for (int r = 0; r < rank; ++r) first += size_t(chunks[size_t(r)]);
+  const size_t mine = size_t(chunks[size_t(rank)]);
+  c.x_r.assign(mine, std::vector<double>(nr));
+  c.x_i.assign(mine, std::vector<int>(ni));
+  if (everyone) {
+    for (size_t i = 0; i < mine; ++i) {
+      c.x_r[i] = x_r[first + i];
+      c.x_i[i] = x_i[first + i];
+    }
+  } else {
+    std::vector<long long> cr(static_cast<size_t>(W)), ci(static_cast<size_t>(W));
+    for (int r = 0; r < W; ++r) {
+      cr[size_t(r)] = (long long)chunks[size_t(r)] * (long long)nr;
+      ci[size_t(r)] = (long long)chunks[size_t(r)] * (long long)ni;
+    }
+    std::vector<double> fr, fi;
+    if (rank == 0) {
+      fr.reserve(J * nr);
+      fi.reserve(J * ni);
+      for (size_t j = 0; j < J; ++j) {
+        fr.insert(fr.end(), x_r[j].begin(), x_r[j].end());
+        for (int v : x_i[j]) fi.push_back(double(v));
+      }
+    }
+    std::vector<double> lr(mine * nr), li(mine * ni);
+    amd::scatterv(fr.data(), cr, lr.data());
+    amd::scatterv(fi.data(), ci, li.data());
+    for (size_t i = 0; i < mine; ++i) {
+      std::copy(lr.begin() + i * nr, lr.begin() + (i + 1) * nr, c.x_r[i].begin());
+      for (size_t k = 0; k < ni; ++k) c.x_i[i][k] = int(li[i * ni + k]);
+    }
+  }
+  c.J = J;
+  c.nr = nr;
+  c.ni = ni;
+  c.world = W;
+  c.valid = true;
+}
+
+/** Evaluate this rank's chunk of jobs on its cached block of the job data,
+ * then all-gather every job's output columns (rows = 1 + shared partials +
+ * job partials, or 1 for values). */
 template <typename F, bool SV, bool JV, typename T_job>
 std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_d,
                                                   const std::vector<Eigen::Matrix<T_job, Eigen::Dynamic, 1>>& job_params,
-                                                  const std::vector<std::vector<double>>& x_r,
-                                                  const std::vector<std::vector<int>>& x_i, std::ostream* msgs,
-                                                  Eigen::Index rows) {
+                                                  const map_rect_data& data, std::ostream* msgs, Eigen::Index rows) {
   const int W = amd::world_size(), rank = amd::world_rank();
   const size_t J = job_params.size();
   const std::vector<int> chunks = map_rect_chunks(J, W);
@@ -136,9 +230,10 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
       const size_t j = size_t(first + i);
       const Eigen::VectorXd job_d = map_rect_values(job_params[j]);
       if constexpr (SV || JV) {
-        local[size_t(i)] = map_rect_reduce_job<F, SV, JV>(shared_d, job_d, x_r[j], x_i[j], msgs);
+        local[size_t(i)] = map_rect_reduce_job<F, SV, JV>(shared_d, job_d, data.x_r[size_t(i)], data.x_i[size_t(i)],
+                                                          msgs);
       } else {
-        Eigen::VectorXd v = F()(shared_d, job_d, x_r[j], x_i[j], msgs);
+        Eigen::VectorXd v = F()(shared_d, job_d, data.x_r[size_t(i)], data.x_i[size_t(i)], msgs);
         local[size_t(i)] = v.transpose();
       }
     }
@@ -184,6 +279,12 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
 
 }  // namespace internal
 
+/** Forget every call_id's cached job data (the next distributed map_rect of
+ * each call_id distributes its data again). */
+inline void map_rect_clear_cache() {
+  for (auto* c : internal::map_rect_caches()) *c = internal::map_rect_data{};
+}
+
 template <int call_id, typename F, typename T_shared, typename T_job>
 Eigen::Matrix<typename std::conditional<std::is_same<T_shared, var>::value ||
                                             std::is_same<T_job, var>::value,
@@ -197,14 +298,20 @@ map_rect(const Eigen::Matrix<T_shared, Eigen::Dynamic, 1>& shared_params,
   constexpr bool JV = std::is_same<T_job, var>::value;
   using R = typename std::conditional<SV || JV, var, double>::type;
   using result_t = Eigen::Matrix<R, Eigen::Dynamic, 1>;
-  internal::map_rect_size_match("job parameters", job_params.size(), "real data", x_r.size());
-  internal::map_rect_size_match("job parameters", job_params.size(), "int data", x_i.size());
   const size_t J = job_params.size();
+  // a non-root rank of a distributed job may leave the job data to the root
+  // (empty x_r and x_i; its block then comes from the cache / the scatter)
+  const bool data_elsewhere = amd::distributed() && amd::world_rank() != 0 && x_r.empty() && x_i.empty();
+  if (!data_elsewhere) {
+    internal::map_rect_size_match("job parameters", job_params.size(), "real data", x_r.size());
+    internal::map_rect_size_match("job parameters", job_params.size(), "int data", x_i.size());
+  }
   for (size_t i = 1; i < J; ++i) {
     internal::map_rect_size_match("Size of one of the vectors of the job specific parameters",
                                   job_params[i].size(),
                                   "size of another vector of the job specifc parameters",
                                   job_params[0].size());
+    if (data_elsewhere) continue;
     internal::map_rect_size_match("Size of one of the arrays of the job specific real data",
                                   x_r[i].size(),
                                   "size of another array of the job specifc real data",
@@ -219,7 +326,11 @@ map_rect(const Eigen::Matrix<T_shared, Eigen::Dynamic, 1>& shared_params,
   std::vector<Eigen::MatrixXd> outs(J);
   if (amd::distributed()) {
     const Eigen::Index rows = 1 + (SV ? shared_params.size() : 0) + (JV ? job_params[0].size() : 0);
-    outs = internal::map_rect_distributed<F, SV, JV>(shared_d, job_params, x_r, x_i, msgs, rows);
+    internal::map_rect_data& data = internal::map_rect_cache<call_id>();
+    if (!data.valid) internal::map_rect_fill_cache(data, J, x_r, x_i);
+    if (data.J != J || data.world != amd::world_size())
+      throw std::invalid_argument("map_rect: the number of jobs of a call_id must not change between calls");
+    outs = internal::map_rect_distributed<F, SV, JV>(shared_d, job_params, data, msgs, rows);
   } else {
     for (size_t j = 0; j < J; ++j) {
       const Eigen::VectorXd job_d = internal::map_rect_values(job_params[j]);

@@ -53,14 +53,19 @@ extern "C" {
 /* mode 0: phi and theta var; 1: phi var, theta data; 2: phi data, theta var;
  * 3: all data.  f = sum_i (1 + 0.1 i) out_i.  grad: (phi(2), theta(J)) (zeros
  * for data).  vals: the concatenated outputs; *nvals their count.
+ * fresh: forget the cached job data first (map_rect_clear_cache); root_only:
+ * ranks other than 0 pass empty x_r / x_i (their blocks come from rank 0's
+ * scatter, sc: the scatterv hook or null).
  * Returns 0, 1 (domain_error; message in err) or 2 (other exception). */
-int maprect_hier(int nranks, int rank, amd::allgather_fn fn, void* user, int J, const double* xr_flat, int nr,
-                 const int* xi_flat, const double* th, int mode, double* fx, double* grad, double* vals, int* nvals,
-                 char* err, int errlen) {
-  amd::set_host_collective(nranks, rank, nranks > 1 ? fn : nullptr, user);
-  std::vector<std::vector<double>> xr(static_cast<size_t>(J));
-  std::vector<std::vector<int>> xi(static_cast<size_t>(J));
-  for (int j = 0; j < J; ++j) {
+int maprect_hier_ex(int nranks, int rank, amd::allgather_fn fn, amd::scatterv_fn sc, void* user, int J,
+                    const double* xr_flat, int nr, const int* xi_flat, const double* th, int mode, int fresh,
+                    int root_only, double* fx, double* grad, double* vals, int* nvals, char* err, int errlen) {
+  amd::set_host_collective(nranks, rank, nranks > 1 ? fn : nullptr, user, nullptr, sc);
+  if (fresh) map_rect_clear_cache();
+  const bool hold = !(root_only && rank != 0);
+  std::vector<std::vector<double>> xr(hold ? static_cast<size_t>(J) : 0);
+  std::vector<std::vector<int>> xi(hold ? static_cast<size_t>(J) : 0);
+  for (int j = 0; hold && j < J; ++j) {
     xr[size_t(j)].assign(xr_flat + size_t(j) * nr, xr_flat + size_t(j + 1) * nr);
     xi[size_t(j)].assign(xi_flat + 2 * j, xi_flat + 2 * j + 2);
   }
@@ -117,6 +122,14 @@ int maprect_hier(int nranks, int rank, amd::allgather_fn fn, void* user, int J, 
   recover_memory_nested();
   amd::set_host_collective(1, 0, nullptr, nullptr);
   return rc;
+}
+
+/* Every rank holds the data; the job data cache is cleared before the call. */
+int maprect_hier(int nranks, int rank, amd::allgather_fn fn, void* user, int J, const double* xr_flat, int nr,
+                 const int* xi_flat, const double* th, int mode, double* fx, double* grad, double* vals, int* nvals,
+                 char* err, int errlen) {
+  return maprect_hier_ex(nranks, rank, fn, nullptr, user, J, xr_flat, nr, xi_flat, th, mode, 1, 0, fx, grad, vals,
+                         nvals, err, errlen);
 }
 
 /* The same call over RCCL: joins a one-rank communicator on this process's

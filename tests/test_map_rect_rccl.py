@@ -82,3 +82,27 @@ def test_map_rect_rccl_failing_job():
     rc, fx, _, _, err = _call(lib, True, xr, xi, th, 0)
     assert rc == 0, err
     near_rel(fx, golden("map_rect_hier_J7")["fx"], 1e-12, what="fx after failure")
+
+
+def test_comm_scatterv_one_rank():
+    """smg_comm_scatterv on a one-rank communicator: the grouped point-to-point
+    calls (none to make) and the root's own block copied on the device --
+    the map_rect job data scatter's RCCL entry (W > 1 scatter logic: gloo in
+    tests/test_sharding.py::test_map_rect_job_data_cache_gloo)."""
+    from math_amd import hip
+    with hip.Context(0, 1 << 26) as c:
+        idb = ctypes.create_string_buffer(128)
+        assert c.lib.smg_comm_unique_id(idb) == 0
+        c.call("smg_comm_init", 1, 0, idb)
+        try:
+            a = np.arange(37, dtype=np.float64) * 0.5 - 3.0
+            src = c.put(a)
+            dst = c.alloc(a.nbytes)
+            counts = (ctypes.c_longlong * 1)(37)
+            c.call("smg_comm_scatterv", src, counts, dst, 0)
+            assert np.array_equal(c.get(dst, 37), a)
+            counts0 = (ctypes.c_longlong * 1)(0)
+            c.call("smg_comm_scatterv", src, counts0, dst, 0)  # an empty block is a no-op
+            assert c.lib.smg_comm_scatterv(c.ptr, src, counts, dst, 1) != 0  # root outside the job
+        finally:
+            c.call("smg_comm_destroy")

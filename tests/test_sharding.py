@@ -228,10 +228,111 @@ def test_map_rect_executor_gloo(tmp_path, world):
                 if mode == 3:
                     want[:] = 0.0
                 near_rel(g1, want, 1e-10, what=f"{key} grad")
-    # two all-gathers per call on every rank; a failed evaluation stops after the status exchange
+    # per call (each with a cleared job data cache): the cache's size exchange,
+    # then two all-gathers; a failed evaluation stops after the status exchange
     n_ok = sum(1 for _, fail in MAPRECT_CASES if fail < 0)
-    want = 4 * (2 * n_ok + (len(MAPRECT_CASES) - n_ok))
+    want = 4 * (3 * n_ok + 2 * (len(MAPRECT_CASES) - n_ok))
     assert all(rk["collectives"] == want for rk in ranks), [rk["collectives"] for rk in ranks]
+
+
+_SC = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                       ctypes.POINTER(ctypes.c_double), ctypes.c_void_p)
+
+
+def _maprect_ex(lib, world, rank, cb, sc, xr, xi, th, mode, fresh, root_only):
+    J = xr.shape[0]
+    fx = ctypes.c_double()
+    grad = np.zeros(2 + J)
+    vals = np.zeros(3 * J + 3)
+    nv = ctypes.c_int()
+    err = ctypes.create_string_buffer(512)
+    xrf = np.ascontiguousarray(xr, dtype=np.float64)
+    xif = np.ascontiguousarray(xi, dtype=np.int32)
+    thf = np.ascontiguousarray(th, dtype=np.float64)
+    lib.maprect_hier_ex.restype = ctypes.c_int
+    rc = lib.maprect_hier_ex(world, rank, cb, sc, None, J, xrf.ctypes.data_as(ctypes.c_void_p), xr.shape[1],
+                             xif.ctypes.data_as(ctypes.c_void_p), thf.ctypes.data_as(ctypes.c_void_p), mode, fresh,
+                             root_only, ctypes.byref(fx), grad.ctypes.data_as(ctypes.c_void_p),
+                             vals.ctypes.data_as(ctypes.c_void_p), ctypes.byref(nv), err, 512)
+    return rc, fx.value, grad, vals[:nv.value], err.value.decode()
+
+
+def _maprect_cache_rank(rank, world, port, use_hook, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    log = []
+
+    def allgather(send, count, recv, _user):
+        t = torch.from_numpy(np.ctypeslib.as_array(send, shape=(count,)).copy())
+        parts = [torch.empty(count, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, t)
+        np.ctypeslib.as_array(recv, shape=(count * world,))[:] = torch.cat(parts).numpy()
+        log.append(("ag", count))
+
+    def scatterv(send, counts, recv, _user):  # point to point from rank 0
+        cn = [counts[r] for r in range(world)]
+        if rank == 0:
+            flat = np.ctypeslib.as_array(send, shape=(sum(cn),)) if sum(cn) else np.zeros(0)
+            off = cn[0]
+            for r in range(1, world):
+                if cn[r]:
+                    dist.send(torch.from_numpy(flat[off:off + cn[r]].copy()), dst=r)
+                off += cn[r]
+            if cn[0]:
+                np.ctypeslib.as_array(recv, shape=(cn[0],))[:] = flat[:cn[0]]
+        elif cn[rank]:
+            t = torch.empty(cn[rank], dtype=torch.float64)
+            dist.recv(t, src=0)
+            np.ctypeslib.as_array(recv, shape=(cn[rank],))[:] = t.numpy()
+        log.append(("sc", cn[rank]))
+
+    cb, sc = _AG(allgather), _SC(scatterv)
+    lib = _maprect_lib()
+    res = {}
+    for J in (7, 16):
+        xr, xi, th = gen.maprect_inputs(J)
+        for mode in range(4):
+            for call in (0, 1):  # the first call fills the cache, the second reuses it
+                n0 = len(log)
+                got = _maprect_ex(lib, world, rank, cb, sc if use_hook else _SC(), xr, xi, th, mode,
+                                  int(call == 0 and mode == 0), 1)
+                res[f"{J}_{mode}_{call}"] = dict(rc=got[0], fx=got[1], grad=got[2], vals=got[3], err=got[4],
+                                                 log=log[n0:])
+    np.save(out + f".{rank}.npy", np.array(res, dtype=object), allow_pickle=True)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,use_hook", [(2, True), (3, True), (3, False)])
+def test_map_rect_job_data_cache_gloo(tmp_path, world, use_hook):
+    """The per-call_id job data cache (prim/mat/functor/mpi_parallel_call.hpp:
+    170-181, 423-450): only rank 0 holds x_r / x_i (the other ranks pass empty
+    arrays).  The first call of each call_id exchanges the sizes and scatters
+    each rank's block from rank 0 (a scatterv hook, or without one an
+    all-gather of the root's buffer); the second call exchanges NO job data --
+    only the two result all-gathers -- and both calls equal the one-process
+    executor bit for bit."""
+    out = str(tmp_path / "mc")
+    _spawn(_maprect_cache_rank, world, use_hook, out)
+    ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(world)]
+    lib = _maprect_lib()
+    cb = _AG(lambda *a: None)
+    for J in (7, 16):
+        xr, xi, th = gen.maprect_inputs(J)
+        for mode in range(4):
+            rc1, fx1, g1, v1, err1 = _maprect_call(lib, 1, 0, cb, xr, xi, th, mode)
+            assert rc1 == 0, err1
+            for r in range(world):
+                for call in (0, 1):
+                    got = ranks[r][f"{J}_{mode}_{call}"]
+                    assert got["rc"] == 0, (J, mode, call, r, got["err"])
+                    assert got["fx"] == fx1 and np.array_equal(got["grad"], g1) and np.array_equal(got["vals"], v1)
+                    kinds = [k for k, _ in got["log"]]
+                    if call == 1:
+                        assert kinds == ["ag", "ag"], (J, mode, r, got["log"])
+                    elif use_hook:
+                        assert kinds == ["ag", "sc", "sc", "ag", "ag"], (J, mode, r, got["log"])
+                    else:
+                        assert kinds == ["ag"] * 5, (J, mode, r, got["log"])
 
 
 # ---------------------------------------------------------------- product GLM reducers, W = 2
