@@ -234,6 +234,16 @@ class GLM(Workload):
         bl.smg_bench_glm_step.argtypes = [D, D, D]
         bl.smg_bench_glm_local_rows.restype = ctypes.c_longlong
         comm_id = None
+        # SMG_BENCH_GLM_RCCL1=1 at one GPU: a one-rank RCCL communicator, so the
+        # step is the sharded path one rank of W runs (the per-rank proxy of
+        # an 8-GPU run at --rows R/8)
+        self.rccl1 = self.world == 1 and os.environ.get("SMG_BENCH_GLM_RCCL1") == "1"
+        if self.rccl1:
+            from math_amd import hip
+            buf = ctypes.create_string_buffer(128)
+            if hip.lib().smg_comm_unique_id(buf) != 0:
+                raise SystemExit("smg_comm_unique_id failed")
+            comm_id = bytes(buf.raw)
         if self.world > 1:  # RCCL unique id from rank 0, shared over the gloo group
             from math_amd import hip
             buf = ctypes.create_string_buffer(128)
@@ -266,7 +276,8 @@ class GLM(Workload):
 
     def config(self):
         return {"workload": "bernoulli_logit_glm_gradient", "rows": self.R, "covariates": self.M,
-                "rows_per_rank": int(self.rows), "parallelism": f"rows{self.world}+rccl_allreduce",
+                "rows_per_rank": int(self.rows),
+                "parallelism": f"rows{self.world}+rccl_allreduce" + ("(one-rank communicator)" if self.rccl1 else ""),
                 "path": "stan::math::gradient + reduce_sum_bernoulli_logit_glm via header-only layer"}
 
     data = "synthetic (reference harness config-4 streams: x~U(-sqrt3,sqrt3), y~Bern(0.5), generated in HBM)"

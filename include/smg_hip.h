@@ -72,6 +72,12 @@ void* smg_host_scratch(smg_ctx* ctx, size_t bytes);
  * of the *_fused entries; coarse-grained: the kernels publish it with one
  * system-scope release); grown on demand, reused by the next call */
 void* smg_pinned_io(smg_ctx* ctx, size_t bytes);
+/* dst (pinned host memory from smg_pinned_io) <- n device doubles of src, in
+ * stream order, written by a one-workgroup kernel that then publishes a
+ * completion word; returns once they have landed (no copy-engine transfer,
+ * no stream synchronisation).  For small results read right after the work
+ * that produced them (the row-sharded reducers after their all-reduce). */
+int smg_publish_to_host(smg_ctx* ctx, const double* src, long long n, double* dst);
 
 int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src_host, size_t bytes);
 int smg_memcpy_d2h(smg_ctx* ctx, void* dst_host, const void* src, size_t bytes);

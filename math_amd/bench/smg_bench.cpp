@@ -204,7 +204,9 @@ int smg_bench_glm_init(int device, long long R, int M, int rank, int world, cons
     using namespace stan::math;
     amd::set_device(device);
     smg_ctx* c = amd::ctx();
-    if (world > 1) amd::comm_init(world, rank, comm_id);
+    // world == 1 with an id: a one-rank RCCL communicator, so the sharded
+    // path (all-reduce, zero-copy read of the sums) runs as on each of W ranks
+    if (world > 1 || comm_id) amd::comm_init(world, rank, comm_id);
     long long b0, b1;
     row_partition(R, world, rank, &b0, &b1);
     const long long rows = b1 - b0;
@@ -227,7 +229,7 @@ int smg_bench_glm_init(int device, long long R, int M, int rank, int world, cons
     g_shard.ldx = rows > 0 ? rows : 1;
     g_shard.row0 = b0;
     g_shard.total_rows = R;
-    g_shard.distributed = world > 1;
+    g_shard.distributed = world > 1 || comm_id;
     return 0;
   } catch (const std::exception& e) {
     return fail(e);

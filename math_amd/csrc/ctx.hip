@@ -22,6 +22,17 @@ __global__ void k_reduce_partials(const double* __restrict__ p, int nparts,
   if (threadIdx.x == 0) out[c] = accumulate ? out[c] + s : s;
 }
 
+// copy n device doubles to pinned host memory with system-scope stores, then
+// publish seq to the host completion word (smg_publish_to_host)
+__global__ __launch_bounds__(256) void k_publish(const double* __restrict__ src, long long n, double* dst,
+                                                 long long* done, long long seq) {
+  for (long long i = threadIdx.x; i < n; i += blockDim.x)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 smg_prof_scope::smg_prof_scope(smg_ctx* c, int f) : ctx(c), fam(f), on(c && c->prof_on) {
@@ -339,6 +350,14 @@ int smg_wait_done(smg_ctx* ctx, long long seq) {
     if (*d >= seq) return SMG_OK;
   SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
   return *d >= seq ? SMG_OK : SMG_ERR_HIP;
+}
+
+int smg_publish_to_host(smg_ctx* ctx, const double* src, long long n, double* dst) {
+  if (!ctx || n < 0 || (n > 0 && (!src || !dst))) return SMG_ERR_ARG;
+  const long long seq = ++ctx->done_seq;
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, src, n, dst, ctx->done_h, seq);
+  SMG_LAUNCH_CHECK();
+  return smg_wait_done(ctx, seq);
 }
 
 int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {

@@ -47,6 +47,7 @@ _SIGS = {
     "smg_status_enqueue": (_I, [_P, _P]),
     "smg_status_inject": (_I, [_P, _I]),
     "smg_pinned_io": (_P, [_P, _S]),
+    "smg_publish_to_host": (_I, [_P, _P, _L, _P]),
     "smg_profile_enable": (_I, [_P, _I]),
     "smg_profile_read": (_I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
     "smg_profile_flops": (_I, [_P, _I, ctypes.POINTER(_D)]),

@@ -176,11 +176,20 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
     if (!o) throw std::bad_alloc();
     amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out, o), fn);
     h = o;
+  } else if (!armed) {
+    // sharded: the local results, ONE all-reduce of the M + 3 doubles (the
+    // y-support count is summed with the rest, so a bad y on any rank makes
+    // every rank throw), then the same zero-copy read of the sums
+    amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out,
+                                          nullptr), fn);
+    amd::allreduce_sum(out, M + 3, fn);
+    double* o = static_cast<double*>(smg_pinned_io(c, size_t(M + 3) * sizeof(double)));
+    if (!o) throw std::bad_alloc();
+    amd::check(smg_publish_to_host(c, out, M + 3, o), fn);
+    h = o;
   } else {
     amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out,
                                           nullptr), fn);
-    // the y-support count is summed with the rest, so a bad y on any rank
-    // makes every rank throw
     if (s.distributed) amd::allreduce_sum(out, M + 3, fn);
     double* o = static_cast<double*>(smg_host_scratch(c, size_t(M + 4) * sizeof(double)));
     if (!o) throw std::bad_alloc();

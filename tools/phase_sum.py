@@ -30,3 +30,12 @@ for k, (i, j) in cuts.items():
     print(f"{k:8s} main busy {busy:7.1f} us  span {span:7.1f} us  kernels {len(main)}")
 other = sum((r[3] - r[2]) for n, r in ev if r[1] != q0) / 1e3
 print(f"total main busy {tot:.1f} us, eval span {(ev[-1][1][3] - t0) / 1e3:.1f} us, other queues busy {other:.1f} us")
+
+# per-kernel totals of the chosen evaluation (all queues), largest first
+agg = {}
+for n, r in ev:
+    k = re.sub(r"<.*", "", n) if len(sys.argv) < 3 else n
+    t, c_ = agg.get(k, (0.0, 0))
+    agg[k] = (t + (r[3] - r[2]) / 1e3, c_ + 1)
+for k, (t, c_) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:30]:
+    print(f"  {t:8.1f} us  {c_:4d}  {k}")
