@@ -257,7 +257,16 @@ class GLM(Workload):
         beta = unif(SEED + 43, self.M, -1.0, 1.0) * np.sqrt(3.0 / self.M)
         self.theta = np.concatenate([[0.1], beta])
         self.g = np.zeros(self.M + 1)
-        rc = bl.smg_bench_glm_init(self.local, self.R, self.M, self.rank, self.world, comm_id)
+        # RCCL prints a version banner on stdout when the communicator comes
+        # up: send it to stderr, so stdout carries only the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            rc = bl.smg_bench_glm_init(self.local, self.R, self.M, self.rank, self.world, comm_id)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         self.rows = bl.smg_bench_glm_local_rows()
         return rc
 

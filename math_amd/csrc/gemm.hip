@@ -390,6 +390,40 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
   *c = (beta == 0.0) ? alpha * s : alpha * s + beta * *c;
 }
 
+// the same reduction for an even m: a lane takes two rows of one column
+// (16-byte slab loads, every split's load issued before the sum), a 2-D
+// grid-stride walk instead of a 64-bit division per element, a bounded grid
+// (the per-element form spent most of its time on index arithmetic: 44 us for
+// four 512 x 2560 slabs)
+__global__ __launch_bounds__(256) void k_splitk_reduce2(int m, int n, int splits, const double* __restrict__ slab,
+                                                        double alpha, double beta, double* __restrict__ C, int ldc,
+                                                        int lower) {
+  const long long tot = (long long)m * n;
+  for (smg_mn w(m >> 1, n); w.ok(); w.next()) {
+    const int i = 2 * w.i, j = w.j;
+    if (lower == 1 && i + 1 < j) continue;
+    if (lower == 2 && i > j) continue;
+    const long long e = (long long)j * m + i;
+    d2v s = {0.0, 0.0};
+    int t = 0;
+    for (; t + 4 <= splits; t += 4) {
+      const d2v a0 = *reinterpret_cast<const d2v*>(slab + (size_t)t * tot + e);
+      const d2v a1 = *reinterpret_cast<const d2v*>(slab + (size_t)(t + 1) * tot + e);
+      const d2v a2 = *reinterpret_cast<const d2v*>(slab + (size_t)(t + 2) * tot + e);
+      const d2v a3 = *reinterpret_cast<const d2v*>(slab + (size_t)(t + 3) * tot + e);
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; t < splits; ++t) s += *reinterpret_cast<const d2v*>(slab + (size_t)t * tot + e);
+    double* c = C + i + (size_t)j * ldc;
+    const bool w0 = !(lower == 1 && i < j), w1 = !(lower == 2 && i + 1 > j);
+    if (w0) c[0] = (beta == 0.0) ? alpha * s[0] : alpha * s[0] + beta * c[0];
+    if (w1) c[1] = (beta == 0.0) ? alpha * s[1] : alpha * s[1] + beta * c[1];
+  }
+}
+
 // the second output of MODE 4 (launch reads it from here: one product at a
 // time per host thread issues a MODE-4 GEMM)
 thread_local double* t_c2 = nullptr;
@@ -455,8 +489,16 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
                      MODE == 4 ? t_ldc2 : 0);
   if (splits > 1) {
     const long long tot = (long long)m * n;
-    hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
-                       ctx->stream, m, n, splits, slab, alpha, beta, C, ldc, MODE);
+    static const bool old_reduce = getenv("SMG_SPLITK_REDUCE1") != nullptr;  // dev A/B
+    if ((m & 1) == 0 && !old_reduce) {
+      const long long pairs = tot / 2;
+      const int nb = (int)(pairs / 256 < 2048 ? (pairs + 255) / 256 : 2048);
+      hipLaunchKernelGGL(k_splitk_reduce2, dim3(nb), dim3(256), 0, ctx->stream, m, n, splits, slab, alpha, beta,
+                         C, ldc, MODE);
+    } else {
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
+                         ctx->stream, m, n, splits, slab, alpha, beta, C, ldc, MODE);
+    }
   }
   SMG_LAUNCH_CHECK();
   return SMG_OK;

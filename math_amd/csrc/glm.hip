@@ -653,7 +653,7 @@ int smg_bernoulli_logit_glm_io(smg_ctx* ctx, const int* y, const double* x, long
   static const int nb_cap = glm_env("SMG_GLM_NB", 0);
   static const int io = glm_env("SMG_GLM_IO", 1);  // dev A/B switch: 0 = always the general path
   if (M > MMAX || variant != 1 || R == 0 || !io) {  // the general path, then one copy back and a synchronisation
-    double* ab = smg_ws(ctx, SMG_WS_TMP2, (size_t)M + 1);
+    double* ab = smg_ws(ctx, SMG_WS_GLM, (size_t)M + 1);
     double* h = (double*)smg_host_scratch(ctx, sizeof(double) * (M + 1));
     if (!ab || !h) return SMG_ERR_OOM;
     h[0] = alpha;
@@ -672,7 +672,7 @@ int smg_bernoulli_logit_glm_io(smg_ctx* ctx, const int* y, const double* x, long
   const long long seq = out_h ? ++ctx->done_seq : 0;
   {  // (the profiling scope closes before the host waits)
     smg_prof_scope prof(ctx, SMG_FAM_GLM);
-    double* ab = smg_ws(ctx, SMG_WS_TMP2, MMAX + 1);
+    double* ab = smg_ws(ctx, SMG_WS_GLM, MMAX + 1);
     if (!ab) return SMG_ERR_OOM;
     hipLaunchKernelGGL(k_glm_params, dim3(1), dim3(256), 0, ctx->stream, a, M + 1, ab);
     hipLaunchKernelGGL((k_glm_reg<0, GLM_RB, 512, true>), dim3(nb), dim3(512), 0, ctx->stream, y, x, R, M, ldx, ab, ws, 1);

@@ -32,6 +32,7 @@
 #include <stan/math/fwd/core/fvar.hpp>
 #include <stan/math/rev/core.hpp>
 #include <stan/math/rev/fun/cholesky_decompose.hpp>
+#include <cstdlib>
 #include <stan/math/rev/fun/gp_exp_quad_cov.hpp>
 #include <stan/math/rev/fun/mdivide_left_tri.hpp>
 #include <stan/math/rev/fun/multi_normal_cholesky_lpdf.hpp>
@@ -307,9 +308,54 @@ inline fvar<var> bernoulli_logit_glm_lpmf(const dev_data<int>& y, const dev_data
   return bernoulli_logit_glm_lpmf<propto>(y, x, alpha, to_dev(beta));
 }
 
+namespace internal {
+// L' = L Phi(L^{-1} A' L^{-T}) as one node with a written-out reverse
+// (smg_chol_tangent_fwd / _rev, csrc/chol_tangent.hip): W = L^{-1}, Y and
+// Phi(Y) are kept for the reverse.  SMG_CHOL_TANGENT_COMPOSED=1 composes it
+// from the device functors instead (two triangular solves with N right-hand
+// sides, their reverses, L Phi).
+class chol_tangent_dev_vari : public device_vari {
+ public:
+  dev_matrix_vari* L_;
+  dev_matrix_vari* Ad_;
+  dev_matrix_vari* Ld_;
+  double* W_;
+  double* Y_;
+  double* P_;
+  chol_tangent_dev_vari(dev_matrix_vari* L, dev_matrix_vari* Ad)
+      : device_vari(0.0), L_(L), Ad_(Ad), Ld_(new dev_matrix_vari(L->rows_, L->cols_, dev_structure::lower)) {
+    const int n = L->rows_;
+    const size_t nn = size_t(n) * n;
+    W_ = amd::alloc_doubles(nn);
+    Y_ = amd::alloc_doubles(nn);
+    P_ = amd::alloc_doubles(nn);
+    amd::check(smg_chol_tangent_fwd(amd::ctx(), L_->val_, n, Ad_->val_, n, n, W_, Y_, P_, Ld_->val_, n),
+               "cholesky_decompose");
+  }
+  void chain() override {
+    const int n = L_->rows_;
+    double* ws = amd::alloc_doubles(2 * size_t(n) * n);
+    amd::check(smg_chol_tangent_rev(amd::ctx(), L_->val_, n, W_, Y_, P_, n, Ld_->adj_, n, n, L_->adj_, n,
+                                    Ad_->adj_, n, ws),
+               "cholesky_decompose");
+  }
+};
+inline bool chol_tangent_composed() {
+  static const bool c = [] {
+    const char* e = std::getenv("SMG_CHOL_TANGENT_COMPOSED");
+    return e && std::atoi(e) != 0;
+  }();
+  return c;
+}
+}  // namespace internal
+
 inline dev_fvar_matrix cholesky_decompose(const dev_fvar_matrix& A) {
   dev_fvar_matrix L;
-  L.val_ = cholesky_decompose(A.val_);                    // checks + L (structurally lower)
+  L.val_ = cholesky_decompose(A.val_);  // checks + L (structurally lower)
+  if (!internal::chol_tangent_composed()) {
+    L.d_ = dev_var_matrix((new internal::chol_tangent_dev_vari(L.val_.vi_, A.d_.vi_))->Ld_);
+    return L;
+  }
   dev_var_matrix X = mdivide_left_tri<1>(L.val_, A.d_);   // L^{-1} A'
   dev_var_matrix Y = mdivide_left_tri<1>(L.val_, transpose(X));  // L^{-1} A' L^{-T}
   // L' = L Phi(Y): lower times lower
