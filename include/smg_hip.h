@@ -246,6 +246,15 @@ int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda,
                              const double* C, int ldc, const double* Cadj,
                              int ldca, int m, int n, double* Aadj, int ldaa,
                              double* Badj, int ldba, double* ws);
+/* The same with A = a Cholesky factor and aux its smg_cholesky_fwd block
+ * inverses (n x SMG_AUX_COLS doubles, ld m; NULL: computed per call, as
+ * above): the solves reuse them instead of rebuilding them from A (lower
+ * only; upper ignores aux).  The fvar<var> MVN tangent's solves against L. */
+int smg_mdivide_left_tri_aux_fwd(smg_ctx* ctx, int lower, const double* A, int lda, const double* aux,
+                                 const double* B, int ldb, int m, int n, double* C, int ldc);
+int smg_mdivide_left_tri_aux_rev(smg_ctx* ctx, int lower, const double* A, int lda, const double* aux,
+                                 const double* C, int ldc, const double* Cadj, int ldca, int m, int n, double* Aadj,
+                                 int ldaa, double* Badj, int ldba, double* ws);
 
 /* mdivide_left_spd(A, B) (rev/mat/fun/mdivide_left_spd.hpp:20-150)
  *   fwd: L = chol(lower(A)) into L (m x m, ld m) and aux
@@ -354,18 +363,19 @@ int smg_multiply_lower_fwd(smg_ctx* ctx, const double* L, int ldl, const double*
 /* The tangent of a Cholesky factor, L' = L Phi(L^{-1} A' L^{-T}), as one
  * node (the fvar<var> cholesky_decompose of mix/fvar_functors.hpp; the
  * reference forms the same L' through Eigen's LLT on fvar<var> scalars,
- * prim/mat/fun/cholesky_decompose.hpp).  fwd: W = L^{-1} (lower, zeros
- * above), Y = W A' W^T (symmetric, full), P = Phi(Y), Ld = L P (lower);
- * W, Y, P: n x n, ld.  rev (Ld_adj lower): Ladj += tril(Ld_adj P^T)
+ * prim/mat/fun/cholesky_decompose.hpp).  aux: smg_cholesky_fwd's block
+ * inverses of L (NULL: rebuilt).  fwd: W = L^{-1} (lower, zeros
+ * above), Wt = W^T, Y = W A' W^T (symmetric, full), P = Phi(Y), Ld = L P
+ * (lower); W, Wt, Y, P: n x n, ld.  rev (Ld_adj lower): Ladj += tril(Ld_adj P^T)
  * - tril(W^T S Y), A'adj += (1/2) W^T S W (symmetric, both triangles), with
  * S = Phi(Padj) + Phi(Padj)^T, Padj = tril(L^T tril(Ld_adj)); NULL Ladj /
  * Adadj skip.  ws: 2 n^2 doubles.  ~5.3 n^3 flops for both against 7 n^3
  * through two N-column triangular solves. */
-int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* Ad, int ldad, int n, double* W,
-                         double* Y, double* P, double* Ld, int ld);
-int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Y, const double* P,
-                         int ld, const double* Ldadj, int ldla, int n, double* Ladj, int ldladj, double* Adadj,
-                         int ldaa, double* ws);
+int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* aux, const double* Ad, int ldad, int n,
+                         double* W, double* Wt, double* Y, double* P, double* Ld, int ld);
+int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Wt, const double* Y,
+                         const double* P, int ld, const double* Ldadj, int ldla, int n, double* Ladj, int ldladj,
+                         double* Adadj, int ldaa, double* ws);
 int smg_multiply_lower_rev(smg_ctx* ctx, const double* L, int ldl, const double* P, int ldp, const double* Cadj,
                            int ldca, int n, double* Ladj, int ldla, double* Padj, int ldpa, double* ws);
 int smg_multiply_fwd(smg_ctx* ctx, const double* A, int lda, const double* B,

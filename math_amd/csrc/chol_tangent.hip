@@ -13,7 +13,7 @@
 //             P = Phi(Y),  L' = L P (N^3/3)
 //   reverse   Ladj += tril(tril(Ld_adj) P^T),  Padj = tril(L^T tril(Ld_adj))  (2 N^3/3)
 //             S = Phi(Padj) + Phi(Padj)^T   (sym_from_lower of Padj)
-//             M = W^T S (N^3)
+//             M = W^T S (N^3; W^T stored by the forward: an NN product)
 //             Ladj -= tril(M Y) (N^3)
 //             A'adj += (1/2) W^T S W = (1/2) M W, symmetric (2 N^3 / 3)
 // from dY = W dA' W^T - W dL Y - Y dL^T W^T: <Ybar, dY> = <W^T Ybar W, dA'>
@@ -50,25 +50,32 @@ int inv_rec(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n, d
 
 extern "C" {
 
-int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* Ad, int ldad, int n, double* W,
-                         double* Y, double* P, double* Ld, int ld) {
+int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* aux, const double* Ad, int ldad, int n,
+                         double* W, double* Wt, double* Y, double* P, double* Ld, int ld) {
   if (!ctx || n < 0) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
-  if (!L || !Ad || !W || !Y || !P || !Ld || ldl < n || ldad < n || ld < n) return SMG_ERR_ARG;
+  if (!L || !Ad || !W || !Wt || !Y || !P || !Ld || ldl < n || ldad < n || ld < n) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_TRSV);
   // W = L^{-1} (lower, stored zeros above)
   int rc = smg_memset(ctx, W, 0, sizeof(double) * (size_t)ld * n);
   if (rc) return rc;
   if (n % SMG_NBR == 0 && n >= 2 * SMG_NBR) {
-    double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_AUX_COLS);
-    if (!w) return SMG_ERR_OOM;
-    if ((rc = smg_trtri_blocks_impl(ctx, L, ldl, n, w))) return rc;
-    if ((rc = smg_block_inverses_impl(ctx, L, ldl, w, n))) return rc;
+    const double* w = aux;  // the factorisation's block inverses, or rebuilt here
+    if (!w) {
+      double* wn = smg_ws(ctx, SMG_WS_TMP2, (size_t)n * SMG_AUX_COLS);
+      if (!wn) return SMG_ERR_OOM;
+      if ((rc = smg_trtri_blocks_impl(ctx, L, ldl, n, wn))) return rc;
+      if ((rc = smg_block_inverses_impl(ctx, L, ldl, wn, n))) return rc;
+      w = wn;
+    }
     if ((rc = inv_rec(ctx, L, ldl, w + (size_t)n * SMG_AUX_W512, n, W, ld, Y, 0, n))) return rc;
   } else {  // W = L^{-1} I by the blocked solve
     if ((rc = smg_add_diag_fwd(ctx, W, ld, n, 1.0, nullptr, W, ld))) return rc;  // W = I
-    if ((rc = smg_trsm_impl(ctx, 1, 0, L, ldl, nullptr, 0, W, ld, n, n))) return rc;
+    if ((rc = smg_trsm_impl(ctx, 1, 0, L, ldl, nullptr, 0, W, ld, n, n, nullptr, 0, aux))) return rc;
   }
+  // W^T stored for the reverse's M = W^T S (an NN product on the matrix
+  // cores: the TN form ran at 34 TF/s against 75 for NN at N = 4096)
+  if ((rc = smg_transpose(ctx, n, n, W, ld, Wt, ld, 0.0))) return rc;
   // T = W A' (in Ld's storage), Y = T W^T (lower computed, mirrored)
   if ((rc = smg_gemm_impl(ctx, 0, 0, 0, n, n, n, 1.0, W, ld, Ad, ldad, 0.0, Ld, ld, SMG_TRI_A_LOWER))) return rc;
   if ((rc = smg_gemm_impl(ctx, 0, 1, 3, n, n, n, 1.0, Ld, ld, W, ld, 0.0, Y, ld, SMG_TRI_B_UPPER))) return rc;
@@ -76,12 +83,12 @@ int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* A
   return smg_multiply_lower_fwd(ctx, L, ldl, P, ld, n, Ld, ld);
 }
 
-int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Y, const double* P,
-                         int ld, const double* Ldadj, int ldla, int n, double* Ladj, int ldladj, double* Adadj,
-                         int ldaa, double* ws) {
+int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Wt, const double* Y,
+                         const double* P, int ld, const double* Ldadj, int ldla, int n, double* Ladj, int ldladj,
+                         double* Adadj, int ldaa, double* ws) {
   if (!ctx || n < 0) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
-  if (!L || !W || !Y || !P || !Ldadj || !ws || ldl < n || ld < n || ldla < n) return SMG_ERR_ARG;
+  if (!L || !W || !Wt || !Y || !P || !Ldadj || !ws || ldl < n || ld < n || ldla < n) return SMG_ERR_ARG;
   if ((Ladj && ldladj < n) || (Adadj && ldaa < n)) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_TRSV);
   const size_t nn = (size_t)n * n;
@@ -92,7 +99,7 @@ int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W
   if ((rc = smg_multiply_lower_rev(ctx, L, ldl, P, ld, Ldadj, ldla, n, Ladj, ldladj, S, n, M))) return rc;
   if (!Ladj && !Adadj) return SMG_OK;
   if ((rc = smg_sym_from_lower(ctx, n, S, n))) return rc;
-  if ((rc = smg_gemm_impl(ctx, 1, 0, 0, n, n, n, 1.0, W, ld, S, n, 0.0, M, n, SMG_TRI_A_UPPER))) return rc;
+  if ((rc = smg_gemm_impl(ctx, 0, 0, 0, n, n, n, 1.0, Wt, ld, S, n, 0.0, M, n, SMG_TRI_A_UPPER))) return rc;
   if (Ladj && (rc = smg_gemm_impl(ctx, 0, 0, 1, n, n, n, -1.0, M, n, Y, ld, 1.0, Ladj, ldladj))) return rc;
   if (!Adadj) return SMG_OK;
   if ((rc = smg_gemm_impl(ctx, 0, 0, 3, n, n, n, 0.5, M, n, W, ld, 0.0, S, n, SMG_TRI_B_LOWER))) return rc;

@@ -152,7 +152,8 @@ int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, 
 // place (B is then the right-hand side's workspace, overwritten): each
 // block's X_p = W_p R_p is written straight to X, no in-place copy-back
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
-                  int ldw, double* B, int ldb, int m, int n, double* X = nullptr, int ldx = 0);
+                  int ldw, double* B, int ldb, int m, int n, double* X = nullptr, int ldx = 0,
+                  const double* aux = nullptr);
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
 int smg_status_mark_impl(smg_ctx* ctx);

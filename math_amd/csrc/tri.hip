@@ -86,9 +86,11 @@ int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double*
   return SMG_OK;
 }
 
-// W: inverse diagonal blocks (m x SMG_NB, ld m) or NULL (computed here)
+// W: inverse diagonal blocks (m x SMG_NB, ld m) or NULL (computed here, or
+// taken from aux: smg_cholesky_fwd's block inverses of a lower A, ld m)
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
-                  int ldw, double* B, int ldb, int m, int n, double* X, int ldx) {
+                  int ldw, double* B, int ldb, int m, int n, double* X, int ldx, const double* aux) {
+  if (!lower || W) aux = nullptr;
   if (m <= 0 || n <= 0) return SMG_OK;
   if (X == B) X = nullptr;
   int BSZ = SMG_NB;  // diagonal-block size of the solve
@@ -104,13 +106,18 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
   if (!W && n == 1 && lower && ldb >= m && m >= 512 && m % 256 == 0 && m / 64 <= 256) {
     // one right-hand side: the persistent solve (trsv.hip) on the 256- / 512-
     // row inverses, one launch instead of 2 m / 64 small GEMMs
-    double* w = smg_ws(ctx, SMG_WS_TMP2, (size_t)m * SMG_AUX_COLS);
+    const double* w = aux;
     double* xr = smg_ws(ctx, SMG_WS_CW, 2 * (size_t)m);
-    if (!w || !xr) return SMG_ERR_OOM;
-    hipLaunchKernelGGL(k_trtri_blocks, dim3(m / SMG_NB), dim3(SMG_DIAG_THREADS), 0, ctx->stream, A, lda,
-                       m, 0, w);
-    int rc = smg_block_inverses_impl(ctx, A, lda, w, m);
-    if (rc) return rc;
+    if (!xr) return SMG_ERR_OOM;
+    int rc;
+    if (!w) {
+      double* wn = smg_ws(ctx, SMG_WS_TMP2, (size_t)m * SMG_AUX_COLS);
+      if (!wn) return SMG_ERR_OOM;
+      hipLaunchKernelGGL(k_trtri_blocks, dim3(m / SMG_NB), dim3(SMG_DIAG_THREADS), 0, ctx->stream, A, lda,
+                         m, 0, wn);
+      if ((rc = smg_block_inverses_impl(ctx, A, lda, wn, m))) return rc;
+      w = wn;
+    }
     rc = smg_copy_impl(ctx, m, 1, B, ldb, xr, m, 1.0, 0);
     if (rc) return rc;
     return smg_trsv_lower_impl(ctx, trans, A, lda, w, w + (size_t)m * SMG_AUX_W256,
@@ -122,16 +129,22 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
     // doubled up from the 64-row ones, as the Cholesky aux), so the updates
     // are rank-512 GEMMs instead of rank-64 ones and the step count is m / 512
     const bool big = lower && m >= 4 * SMG_NBR && m % SMG_NBR == 0 && n >= SMG_NBR;
-    const size_t wd = big ? (size_t)m * SMG_AUX_COLS : (size_t)m * SMG_NB;
-    double* w = smg_ws(ctx, SMG_WS_TMP2, wd);
-    if (!w) return SMG_ERR_OOM;
-    hipLaunchKernelGGL(k_trtri_blocks, dim3((m + SMG_NB - 1) / SMG_NB), dim3(SMG_DIAG_THREADS), 0,
-                       ctx->stream, A, lda, m, lower ? 0 : 1, w);
+    const double* w = aux;
+    if (!w) {
+      const size_t wd = big ? (size_t)m * SMG_AUX_COLS : (size_t)m * SMG_NB;
+      double* wn = smg_ws(ctx, SMG_WS_TMP2, wd);
+      if (!wn) return SMG_ERR_OOM;
+      hipLaunchKernelGGL(k_trtri_blocks, dim3((m + SMG_NB - 1) / SMG_NB), dim3(SMG_DIAG_THREADS), 0,
+                         ctx->stream, A, lda, m, lower ? 0 : 1, wn);
+      if (big) {
+        const int rc = smg_block_inverses_impl(ctx, A, lda, wn, m);
+        if (rc) return rc;
+      }
+      w = wn;
+    }
     W = w;
     ldw = m;
     if (big) {
-      const int rc = smg_block_inverses_impl(ctx, A, lda, w, m);
-      if (rc) return rc;
       W = w + (size_t)m * SMG_AUX_W512;
       BSZ = SMG_NBR;
     }
@@ -234,6 +247,11 @@ int smg_copy_matrix(smg_ctx* ctx, int m, int n, const double* A, int lda, double
 
 int smg_mdivide_left_tri_fwd(smg_ctx* ctx, int lower, const double* A, int lda, const double* B,
                              int ldb, int m, int n, double* C, int ldc) {
+  return smg_mdivide_left_tri_aux_fwd(ctx, lower, A, lda, nullptr, B, ldb, m, n, C, ldc);
+}
+
+int smg_mdivide_left_tri_aux_fwd(smg_ctx* ctx, int lower, const double* A, int lda, const double* aux,
+                                 const double* B, int ldb, int m, int n, double* C, int ldc) {
   if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
   if (m == 0 || n == 0) return SMG_OK;
   if (!A || !B || !C || lda < m || ldb < m || ldc < m) return SMG_ERR_ARG;
@@ -243,16 +261,23 @@ int smg_mdivide_left_tri_fwd(smg_ctx* ctx, int lower, const double* A, int lda, 
     if (!R) return SMG_ERR_OOM;
     int rc = smg_copy_impl(ctx, m, n, B, ldb, R, m, 1.0, 0);
     if (rc) return rc;
-    return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, R, m, m, n, C, ldc);
+    return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, R, m, m, n, C, ldc, aux);
   }
   int rc = smg_copy_impl(ctx, m, n, B, ldb, C, ldc, 1.0, 0);
   if (rc) return rc;
-  return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, C, ldc, m, n);
+  return smg_trsm_impl(ctx, lower, 0, A, lda, nullptr, 0, C, ldc, m, n, nullptr, 0, aux);
 }
 
 int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda, const double* C,
                              int ldc, const double* Cadj, int ldca, int m, int n, double* Aadj,
                              int ldaa, double* Badj, int ldba, double* ws) {
+  return smg_mdivide_left_tri_aux_rev(ctx, lower, A, lda, nullptr, C, ldc, Cadj, ldca, m, n, Aadj, ldaa, Badj, ldba,
+                                      ws);
+}
+
+int smg_mdivide_left_tri_aux_rev(smg_ctx* ctx, int lower, const double* A, int lda, const double* aux,
+                                 const double* C, int ldc, const double* Cadj, int ldca, int m, int n, double* Aadj,
+                                 int ldaa, double* Badj, int ldba, double* ws) {
   if (!ctx || m < 0 || n < 0) return SMG_ERR_ARG;
   if (m == 0 || n == 0) return SMG_OK;
   if (!A || !C || !Cadj || !ws) return SMG_ERR_ARG;
@@ -264,11 +289,11 @@ int smg_mdivide_left_tri_rev(smg_ctx* ctx, int lower, const double* A, int lda, 
     if (!R) return SMG_ERR_OOM;
     rc = smg_copy_impl(ctx, m, n, Cadj, ldca, R, m, 1.0, 0);
     if (rc) return rc;
-    rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, R, m, m, n, ws, m);
+    rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, R, m, m, n, ws, m, aux);
   } else {
     rc = smg_copy_impl(ctx, m, n, Cadj, ldca, ws, m, 1.0, 0);
     if (rc) return rc;
-    rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, ws, m, m, n);
+    rc = smg_trsm_impl(ctx, lower, 1, A, lda, nullptr, 0, ws, m, m, n, nullptr, 0, aux);
   }
   if (rc) return rc;
   if (Aadj) {  // adjA = -adjB C^T on the triangle only (:108, :111-123)

@@ -74,8 +74,10 @@ _SIGS = {
     "smg_cholesky_rev": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_fwd": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_rev": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
-    "smg_chol_tangent_fwd": (_I, [_P, _P, _I, _P, _I, _I, _P, _P, _P, _P, _I]),
-    "smg_chol_tangent_rev": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
+    "smg_mdivide_left_tri_aux_fwd": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _P, _I]),
+    "smg_mdivide_left_tri_aux_rev": (_I, [_P, _I, _P, _I, _P, _P, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
+    "smg_chol_tangent_fwd": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I]),
+    "smg_chol_tangent_rev": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
     "smg_multiply_lower_fwd": (_I, [_P, _P, _I, _P, _I, _I, _P, _I]),
     "smg_multiply_lower_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
     "smg_multiply_fwd": (_I, [_P, _P, _I, _P, _I, _I, _I, _I, _P, _I]),

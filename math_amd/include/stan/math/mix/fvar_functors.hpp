@@ -320,6 +320,7 @@ class chol_tangent_dev_vari : public device_vari {
   dev_matrix_vari* Ad_;
   dev_matrix_vari* Ld_;
   double* W_;
+  double* Wt_;
   double* Y_;
   double* P_;
   chol_tangent_dev_vari(dev_matrix_vari* L, dev_matrix_vari* Ad)
@@ -327,15 +328,16 @@ class chol_tangent_dev_vari : public device_vari {
     const int n = L->rows_;
     const size_t nn = size_t(n) * n;
     W_ = amd::alloc_doubles(nn);
+    Wt_ = amd::alloc_doubles(nn);
     Y_ = amd::alloc_doubles(nn);
     P_ = amd::alloc_doubles(nn);
-    amd::check(smg_chol_tangent_fwd(amd::ctx(), L_->val_, n, Ad_->val_, n, n, W_, Y_, P_, Ld_->val_, n),
+    amd::check(smg_chol_tangent_fwd(amd::ctx(), L_->val_, n, L_->aux_, Ad_->val_, n, n, W_, Wt_, Y_, P_, Ld_->val_, n),
                "cholesky_decompose");
   }
   void chain() override {
     const int n = L_->rows_;
     double* ws = amd::alloc_doubles(2 * size_t(n) * n);
-    amd::check(smg_chol_tangent_rev(amd::ctx(), L_->val_, n, W_, Y_, P_, n, Ld_->adj_, n, n, L_->adj_, n,
+    amd::check(smg_chol_tangent_rev(amd::ctx(), L_->val_, n, W_, Wt_, Y_, P_, n, Ld_->adj_, n, n, L_->adj_, n,
                                     Ad_->adj_, n, ws),
                "cholesky_decompose");
   }

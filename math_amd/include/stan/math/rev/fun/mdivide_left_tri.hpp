@@ -27,15 +27,18 @@ class mdivide_left_tri_dev_vari : public device_vari {
   dev_matrix_vari* C_;
   mdivide_left_tri_dev_vari(int lower, const dev_operand& A, const dev_operand& B)
       : device_vari(0.0), lower_(lower), A_(A), B_(B), C_(new dev_matrix_vari(B.rows, B.cols)) {
-    amd::check(smg_mdivide_left_tri_fwd(amd::ctx(), lower_, A_.val(), A_.rows, B_.val(), B_.rows,
-                                        B_.rows, B_.cols, C_->val_, C_->rows_),
+    amd::check(smg_mdivide_left_tri_aux_fwd(amd::ctx(), lower_, A_.val(), A_.rows, aux(), B_.val(), B_.rows,
+                                            B_.rows, B_.cols, C_->val_, C_->rows_),
                "mdivide_left_tri");
   }
+  // A Cholesky factor carries its diagonal-block inverses (aux_): the
+  // solves reuse them
+  const double* aux() const { return lower_ && A_.vi ? A_.vi->aux_ : nullptr; }
   void chain() override {
     const int m = B_.rows, n = B_.cols;
     double* ws = amd::alloc_doubles(size_t(m) * n);
-    amd::check(smg_mdivide_left_tri_rev(amd::ctx(), lower_, A_.val(), A_.rows, C_->val_, m,
-                                        C_->adj_, m, m, n, A_.adj(), A_.rows, B_.adj(), m, ws),
+    amd::check(smg_mdivide_left_tri_aux_rev(amd::ctx(), lower_, A_.val(), A_.rows, aux(), C_->val_, m,
+                                            C_->adj_, m, m, n, A_.adj(), A_.rows, B_.adj(), m, ws),
                "mdivide_left_tri");
   }
 };
