@@ -171,6 +171,16 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
   __shared__ double pool[POOL];
 
   int bi, bj, tile, split;
+  // A triangular operand gives every tile a K range set by its row (op(A))
+  // or column (op(B)) block.  The workgroups a CU holds at once are assigned
+  // by index, so an order in which that block index varied fastest gave each
+  // CU tiles of ONE block: the CUs of the long-K blocks carried ~2x the mean
+  // work (N^3 products with a triangular op(A) took 0.88x the full product's
+  // time instead of 0.5x).  Such grids run in the linear order (the launch
+  // sets px = 0) with that block index varying slowest, longest K first
+  // (N = 4096, op(A) upper: 2120 -> 1143 us; op(B) upper 1136 us).
+  const bool tri_a_only = !TRIC && (tri & 3) && !(tri & 12);
+  const bool tri_b_only = !TRIC && (tri & 12) && !(tri & 3);
   if (px > 0) {
     // XCD-aware placement (full / trapezoidal grids): workgroups b and b + 8
     // share an XCD (round-robin dispatch), so XCD slot x = b % 8 takes one
@@ -200,6 +210,14 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
     tri_decode(tile, bi, bj);
   } else if (UPT && tri_sq) {
     tri_decode(tile, bj, bi);
+  } else if (tri_a_only) {  // rows slowest, longest K first
+    const int r = tile / (ntiles / tiles_m);
+    bi = (tri & 1) ? tiles_m - 1 - r : r;
+    bj = tile % (ntiles / tiles_m);
+  } else if (tri_b_only) {  // columns slowest, longest K first
+    const int tn = ntiles / tiles_m, c = tile / tiles_m;
+    bi = tile % tiles_m;
+    bj = (tri & 8) ? tn - 1 - c : c;
   } else {
     bi = tile % tiles_m;
     bj = tile / tiles_m;
@@ -468,8 +486,11 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   // XCD partition px x (8 / px) of a full tile grid minimising the per-XCD
   // operand footprint (rows of A + columns of B, in tiles); triangle grids
   // (tri_decode order) and grids too small to split keep the linear order
+  // (a triangular operand alone: the linear, longest-K-first order of the
+  // kernel's tile decode instead)
+  const bool tri_one = !TRIC && tri && (!(tri & 3) || !(tri & 12));
   int px = 0, ntp = ntiles;
-  if (!(TRIC && m == n && BM == BN) && ntiles >= 64) {
+  if (!(TRIC && m == n && BM == BN) && ntiles >= 64 && !tri_one) {
     long long best = -1;
     for (int p = 1; p <= 8; p *= 2) {
       const int q = 8 / p;
