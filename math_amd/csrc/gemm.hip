@@ -207,7 +207,30 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
   // Cholesky) -> the full grid, tiles wholly outside the triangle exit
   const bool tri_sq = TRIC && m == n && BM == BN;
   if (LOWT && tri_sq) {
-    tri_decode(tile, bi, bj);
+    // lower-triangle grids in the order of decreasing K range under the
+    // triangular operands (see tri_a_only below): by column (op(B) lower:
+    // K in [j0, k)), by column from the right (op(B) upper: K below j0 + BN),
+    // by diagonal from the corner (both lower: K in [j0, i0 + BM)), by row
+    // from the bottom (op(A) lower alone), else by row from the top
+    const int T = tiles_m;
+    int r, q;
+    if (tri == SMG_TRI_B_LOWER) {
+      tri_decode(ntiles - 1 - tile, r, q);
+      bj = T - 1 - r;
+      bi = bj + q;
+    } else if (tri == SMG_TRI_B_UPPER || tri == (SMG_TRI_A_LOWER | SMG_TRI_B_UPPER)) {
+      tri_decode(tile, r, q);
+      bj = T - 1 - r;
+      bi = bj + q;
+    } else if (tri == (SMG_TRI_A_LOWER | SMG_TRI_B_LOWER)) {
+      tri_decode(tile, r, q);
+      bj = q;
+      bi = q + (T - 1 - r);
+    } else if (tri == SMG_TRI_A_LOWER) {
+      tri_decode(ntiles - 1 - tile, bi, bj);
+    } else {
+      tri_decode(tile, bi, bj);
+    }
   } else if (UPT && tri_sq) {
     tri_decode(tile, bj, bi);
   } else if (tri_a_only) {  // rows slowest, longest K first
