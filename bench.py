@@ -76,7 +76,7 @@ def pmc_traffic(workload):
     summary (tools/pmc_traffic.sh + tools/pmc_traffic.py: separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes, calibrated on a known 8 B/lane
     stream), or None when absent."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
