@@ -15,7 +15,10 @@
 constexpr int SMG_NB = 64;           // diagonal block size of every blocked kernel
 constexpr int SMG_NB2 = 256;         // outer block of the blocked triangular solves
 constexpr int SMG_NBR = 512;         // outer block of the two-level Cholesky reverse
-constexpr int SMG_NBF = 512;         // panel width of the two-level Cholesky forward
+#ifndef SMG_NBF_COLS
+#define SMG_NBF_COLS 512
+#endif
+constexpr int SMG_NBF = SMG_NBF_COLS;  // panel width of the two-level Cholesky forward
 // cholesky aux layout (n rows each, ld n): inverses of the 64-, 128-, 256-
 // and 512-row diagonal blocks of L
 constexpr int SMG_AUX_W128 = SMG_NB;
