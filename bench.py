@@ -209,10 +209,23 @@ class GPEigen(GP):
         return c
 
     def extra(self, timed, steps):
+        ph = np.zeros(4)
+        self.bl.smg_bench_gp_eigen_phases.argtypes = [D, D]
+        best = None
+        for _ in range(3):
+            if self.bl.smg_bench_gp_eigen_phases(ptr(self.theta), ptr(ph)) != 0:
+                raise SystemExit(f"gp_eigen phases failed: {self.bl.smg_bench_error().decode()}")
+            if best is None or ph[3] < best[3]:
+                best = ph.copy()
         out = np.zeros(5)
         if self.bl.smg_bench_bridge_cost(self.N, 3, ptr(out)) != 0:
             raise SystemExit(f"bridge cost failed: {self.bl.smg_bench_error().decode()}")
-        return {"bridge_cost_ms": {"to_host_matrix": out[0] * 1e3, "to_dev_recognised": out[1] * 1e3,
+        return {"eval_phases_ms": {"forward": best[0] * 1e3, "reverse": best[1] * 1e3, "recover": best[2] * 1e3,
+                                   "gradient_call": best[3] * 1e3,
+                                   "note": "one evaluation split by hand (functor forward incl. three crossings; "
+                                           "grad() to a device sync; recover_memory), best of 3; gradient_call: "
+                                           "the same evaluation through stan::math::gradient"},
+                "bridge_cost_ms": {"to_host_matrix": out[0] * 1e3, "to_dev_recognised": out[1] * 1e3,
                                    "to_dev_gathered_copy": out[2] * 1e3, "reverse_gather_touched": out[3] * 1e3,
                                    "reverse_untouched_sweep": out[4] * 1e3,
                                    "note": f"one crossing of an N={self.N} matrix, best of 3 "

@@ -130,6 +130,40 @@ int smg_bench_gp_eigen_step(const double* theta, double* fx, double* grad) {
     return fail(e);
   }
 }
+/* Where one gp_eigen evaluation's host time goes (seconds): out[0] the
+ * functor's forward pass (three crossings), out[1] the reverse sweep, out[2]
+ * recover_memory, out[3] the whole evaluation (gradient()). */
+int smg_bench_gp_eigen_phases(const double* theta, double* out) {
+  try {
+    using namespace stan::math;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto sec = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
+    Eigen::VectorXd th = Eigen::Map<const Eigen::VectorXd>(theta, 3);
+    auto t0 = now();
+    Eigen::Matrix<var, -1, 1> tv(3);
+    for (int i = 0; i < 3; ++i) tv(i) = th(i);
+    var f = gp_eigen_functor{g_xh, g_yh}(tv);
+    auto t1 = now();
+    grad(f.vi_);
+    amd::check(smg_sync(amd::ctx()), "phases");
+    auto t2 = now();
+    recover_memory();
+    auto t3 = now();
+    double fx;
+    Eigen::VectorXd g;
+    auto t4 = now();
+    gradient(gp_eigen_functor{g_xh, g_yh}, th, fx, g);
+    auto t5 = now();
+    out[0] = sec(t0, t1);
+    out[1] = sec(t1, t2);
+    out[2] = sec(t2, t3);
+    out[3] = sec(t4, t5);
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
 void smg_bench_malloc_tuning(int on) {
   if (on) {
     mallopt(M_MMAP_MAX, 0);
