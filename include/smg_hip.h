@@ -402,6 +402,17 @@ int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
                          const double* aux, int n, const double* ws, double adj,
                          int lower_only, double* yadj, double* muadj,
                          double* Ladj, int ldla);
+/* cholesky_decompose's reverse (rev/mat/fun/cholesky_decompose.hpp:118-166)
+ * for the one adjoint multi_normal_cholesky_lpdf gives a lower-structured
+ * factor (the Ladj above with lower_only = 1: adj (tril(s w^T) - diag(1/L_ii)),
+ * s = ws + n of smg_mvn_cholesky_fwd), in closed form:
+ *   Aadj (lower) += adj Phi(s s^T - K^{-1}),  K^{-1} = L^{-T} L^{-1}
+ * (Phi: strict lower + half diagonal).  aux: the factor's smg_cholesky_fwd
+ * block inverses (NULL: a blocked solve forms L^{-1}).  ws: at least
+ * smg_cholesky_mvn_rev_ws_doubles(n) doubles. */
+size_t smg_cholesky_mvn_rev_ws_doubles(int n);
+int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
+                         const double* s, double adj, double* Aadj, int ldaa, double* ws);
 
 /* log_sum_exp(vector<var>) (rev/mat/fun/log_sum_exp.hpp:20-53):
  *   fwd: out = max + log(sum exp(x - max)); empty -> -inf; non-finite max -> max

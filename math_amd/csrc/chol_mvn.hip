@@ -1,0 +1,185 @@
+// The reverse of cholesky_decompose when the factor's whole adjoint comes from
+// multi_normal_cholesky_lpdf(y | mu, L) (the GP marginal, config 3).
+//
+// The MVN's partials for a lower-structured L are
+//   Lbar = adj (tril(s w^T) - diag(1/L_ii)),  w = L^{-1}(y - mu),  s = L^{-T} w
+// (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:139-155, upper half on the
+// dummy vari), and pushing exactly that Lbar through the Cholesky adjoint
+// (rev/mat/fun/cholesky_decompose.hpp:118-166, Murray's blocked algorithm,
+// 2 N^3 / 3 in ~N/64 dependent GEMM rounds) has the closed form
+//   Abar (lower) += adj Phi(s s^T - K^{-1}),  K = L L^T,
+// Phi = strict lower triangle + half the diagonal (the reference's lower-entry
+// convention: an off-diagonal A_ij stands for both K_ij and K_ji).  K^{-1} =
+// V V^T with V = L^{-T}: V by recursive doubling from the factorisation's
+// 512-row block inverses (N^3 / 3), V V^T lower (N^3 / 3) -- the same
+// 2 N^3 / 3 as Murray's, in 16 large triangular-operand GEMMs instead of
+// ~40 dependent rounds of small ones.  The host layer takes this path only
+// when it can prove no other node wrote the factor's adjoint
+// (stan/math/rev/fun/cholesky_decompose.hpp).
+#include "smg_internal.h"
+#include "tri_small.h"
+
+namespace {
+
+// V[lo:hi, lo:hi] = L[lo:hi, lo:hi]^{-T} (upper) from the 512-row block
+// inverses W_b (aux level SMG_AUX_W512, ld n; lower with stored zeros above):
+//   leaves V_bb = W_b^T;  V12 = -V11 (L21^T V22)  -- as T = V11 L21^T (NT),
+//   V12 = -T V22 (NN), T a workspace of ld n.
+// Only the upper triangle and the strict-lower zeros inside the 512 leaves
+// are written: every later product reads V through triangular K-range cuts
+// whose tiles never leave a leaf below the diagonal.
+// (the leaves and, with `pairs`, the 1024-row nodes are formed beforehand in
+// batched launches: inv_t_leaves)
+int inv_t_rec(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n, double* V, int ldv, double* T,
+              int lo, int hi, bool pairs) {
+  if (hi - lo == SMG_NBR || (pairs && hi - lo == 2 * SMG_NBR)) return SMG_OK;
+  const int mid = lo + ((hi - lo) / SMG_NBR / 2) * SMG_NBR;
+  int rc = inv_t_rec(ctx, L, ldl, w512, n, V, ldv, T, lo, mid, pairs);
+  if (!rc) rc = inv_t_rec(ctx, L, ldl, w512, n, V, ldv, T, mid, hi, pairs);
+  if (rc) return rc;
+  const int b = mid - lo, a = hi - mid;
+  // T (b x a) = V11 L21^T: op(A) = V11 upper
+  rc = smg_gemm_impl(ctx, 0, 1, 0, b, a, b, 1.0, V + lo + (size_t)lo * ldv, ldv, L + mid + (size_t)lo * ldl, ldl, 0.0,
+                     T, n, SMG_TRI_A_UPPER);
+  if (rc) return rc;
+  // V12 (b x a) = -T V22: op(B) = V22 upper
+  return smg_gemm_impl(ctx, 0, 0, 0, b, a, a, -1.0, T, n, V + mid + (size_t)mid * ldv, ldv, 0.0,
+                       V + lo + (size_t)mid * ldv, ldv, SMG_TRI_B_UPPER);
+}
+
+// V_bb = W_b^T for every 512-row leaf b (one launch: blockIdx.z = leaf,
+// 64 x 64 tiles through LDS)
+__global__ __launch_bounds__(256) void k_leaf_transpose(const double* __restrict__ w512, int n,
+                                                       double* __restrict__ V, int ldv) {
+  __shared__ double t[64][65];
+  const int b0 = blockIdx.z * SMG_NBR;
+  const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;  // tile of W_b (rows i, cols j)
+  const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int c = c4; c < 64; c += 4) t[c][r] = w512[b0 + i0 + r + (size_t)(j0 + c) * n];
+  __syncthreads();
+#pragma unroll 4
+  for (int c = c4; c < 64; c += 4)  // V(b0 + j0 + r, b0 + i0 + c) = W_b(i0 + c, j0 + r)
+    V[b0 + j0 + r + (size_t)(b0 + i0 + c) * ldv] = t[r][c];
+}
+
+// the leaves, and (n / 512 a power of two: the recursion's 1024-row nodes are
+// then the aligned leaf pairs) every pair's V12 = -V11 L21^T V22 as two
+// strided-batched products; returns whether the pairs were formed
+int inv_t_leaves(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n, double* V, int ldv, double* T,
+                 bool* pairs) {
+  const int nl = n / SMG_NBR;
+  hipLaunchKernelGGL(k_leaf_transpose, dim3(SMG_NBR / 64, SMG_NBR / 64, nl), dim3(256), 0, ctx->stream, w512, n, V,
+                     ldv);
+  SMG_LAUNCH_CHECK();
+  *pairs = (nl & (nl - 1)) == 0 && nl >= 2;
+  if (!*pairs) return SMG_OK;
+  const int np = nl / 2, b = SMG_NBR;
+  const long long sv = 2LL * b * (1 + (long long)ldv), sl = 2LL * b * (1 + (long long)ldl);
+  // T_p (b x b, rows p b of T, ld n) = V11_p L21_p^T
+  int rc = smg_gemm_batched_impl(ctx, 0, 1, b, b, b, 1.0, V, ldv, sv, L + b, ldl, sl, 0.0, T, n, b, np);
+  if (rc) return rc;
+  // V12_p = -T_p V22_p
+  return smg_gemm_batched_impl(ctx, 0, 0, b, b, b, -1.0, T, n, b, V + b + (size_t)b * ldv, ldv, sv, 0.0,
+                               V + (size_t)b * ldv, ldv, sv, np);
+}
+
+// Abar(i, j) += adj ((s_i s_j - C_ij) * (i == j ? 1/2 : 1)), i >= j, C lower;
+// the column form of k_add_lower_col2 (16-byte accesses, whole columns per
+// workgroup, only the row pairs at or below the diagonal touched)
+__global__ __launch_bounds__(256) void k_chol_mvn_adj_col2(const double* __restrict__ C, int ldc, int n,
+                                                          const double* __restrict__ s, double adj,
+                                                          double* __restrict__ A, int lda) {
+  const int np = n >> 1;
+  const double2* s2 = reinterpret_cast<const double2*>(s);
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double2* c = reinterpret_cast<const double2*>(C + (size_t)j * ldc);
+    double2* a = reinterpret_cast<double2*>(A + (size_t)j * lda);
+    const double sj = adj * s[j];
+    const int p1 = j >> 1;  // first pair holding a row >= j
+    for (int p0 = p1 + threadIdx.x; p0 < np; p0 += 4 * 256) {
+      double2 cv[4], av[4], sv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          cv[k] = c[p];
+          av[k] = a[p];
+          sv[k] = s2[p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 256 * k;
+        if (p < np) {
+          const int r = 2 * p;
+          const double gx = sv[k].x * sj - adj * cv[k].x;
+          const double gy = sv[k].y * sj - adj * cv[k].y;
+          if (r > j) av[k].x += gx;
+          else if (r == j) av[k].x += 0.5 * gx;
+          if (r + 1 > j) av[k].y += gy;  // row 2p + 1 >= j for every p >= j / 2
+          else av[k].y += 0.5 * gy;
+          a[p] = av[k];
+        }
+      }
+    }
+  }
+}
+
+__global__ void k_chol_mvn_adj(const double* __restrict__ C, int ldc, int n, const double* __restrict__ s,
+                               double adj, double* __restrict__ A, int lda) {
+  for (smg_mn it(n, n); it.ok(); it.next()) {
+    const int i = it.i, j = it.j;
+    if (i < j) continue;
+    const double g = adj * (s[i] * s[j] - C[i + (size_t)j * ldc]);
+    A[i + (size_t)j * lda] += (i == j) ? 0.5 * g : g;
+  }
+}
+
+inline int grid_for(long long tot) {
+  long long g = (tot + 255) / 256;
+  return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t smg_cholesky_mvn_rev_ws_doubles(int n) { return n > 0 ? 2 * (size_t)n * n : 0; }
+
+int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s,
+                         double adj, double* Aadj, int ldaa, double* ws) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!L || !s || !Aadj || !ws || ldl < n || ldaa < n) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
+  const size_t nn = (size_t)n * n;
+  double* V = ws;       // L^{-T} (upper), or W = L^{-1} on the general path
+  double* C = ws + nn;  // K^{-1} (lower); the doubling's T before that
+  int rc;
+  if (n % SMG_NBR == 0 && n >= 2 * SMG_NBR && aux) {
+    const double* w512 = aux + (size_t)n * SMG_AUX_W512;
+    bool pairs = false;
+    if ((rc = inv_t_leaves(ctx, L, ldl, w512, n, V, n, C, &pairs))) return rc;
+    if ((rc = inv_t_rec(ctx, L, ldl, w512, n, V, n, C, 0, n, pairs))) return rc;
+    // C = V V^T, lower: op(A) = V upper, op(B) = V^T lower
+    rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+  } else {  // any n: W = L^{-1} by the blocked solve, C = W^T W
+    if ((rc = smg_memset(ctx, V, 0, sizeof(double) * nn))) return rc;
+    if ((rc = smg_add_diag_fwd(ctx, V, n, n, 1.0, nullptr, V, n))) return rc;  // W = I
+    if ((rc = smg_trsm_impl(ctx, 1, 0, L, ldl, nullptr, 0, V, n, n, n, nullptr, 0, aux))) return rc;
+    rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+  }
+  if (rc) return rc;
+  if (n % 2 == 0 && ldaa % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(Aadj) | reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(C)) & 15) ==
+          0)
+    hipLaunchKernelGGL(k_chol_mvn_adj_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, C, n, n, s, adj,
+                       Aadj, ldaa);
+  else
+    hipLaunchKernelGGL(k_chol_mvn_adj, dim3(grid_for(nn)), dim3(256), 0, ctx->stream, C, n, n, s, adj, Aadj, ldaa);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+}  // extern "C"

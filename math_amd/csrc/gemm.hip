@@ -21,6 +21,9 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef SMG_GEMM_TRI128_MIN
+#define SMG_GEMM_TRI128_MIN 1024  // fewest 128 x 128 tiles a product with a triangular operand takes them at
+#endif
 #ifndef SMG_GEMM_KS2_MAX
 #define SMG_GEMM_KS2_MAX 1536  // largest 64 x 64 tile count that takes the 8-wave variant
 #endif
@@ -626,7 +629,11 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   // the diagonal, and the split-K those few tiles need costs a reduction; at
   // N = K = 4096 the 528-tile 128 triangle -- 2.06 waves over the CUs -- ran
   // 1692 vs 1416 us for the 64 grid)
-  if (FULLC && big_tiles >= 256 && k > 128)
+  // (a triangular operand gives the tiles K ranges from 128 to k: with one
+  // 128 tile per CU the longest sets the time -- the 2048^3 products of the
+  // inverse doubling ran at 27 TF/s -- so those need 4 per CU to balance,
+  // else the 64 x 64 grid's longest-K-first order takes them)
+  if (FULLC && big_tiles >= (tri ? SMG_GEMM_TRI128_MIN : 256) && k > 128)
     return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
   // long-K transposed-A products with a small output (the Murray reverse's
   // [R_adj | D_adj] -= C_adj^T [B | C]: 512 x K x m, m >= 1536): 128 x 64

@@ -38,6 +38,18 @@ enum class dev_structure : int {
   lower = 1  // strict upper triangle is constant zero (cholesky_decompose output)
 };
 
+/** A node that can take a consumer's adjoint contribution in structured
+ * (unexpanded) form instead of as a dense device adjoint: cholesky_decompose
+ * takes multi_normal_cholesky_lpdf's partials for its factor and applies
+ * them in closed form (rev/fun/cholesky_decompose.hpp). */
+class structured_adjoint_sink {
+ public:
+  /** owner: the consumer node; ws: its device [w, s] (smg_mvn_cholesky_fwd);
+   * adj: its adjoint.  True when taken (the consumer then writes no dense
+   * adjoint for the factor); false: the consumer writes it densely. */
+  virtual bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) = 0;
+};
+
 class dev_matrix_vari {
  public:
   const int rows_;
@@ -49,6 +61,8 @@ class dev_matrix_vari {
   // set on transpose(A)'s output: multiply(A, transpose(A)) recognises the
   // Gram product (one lower GEMM forward, one GEMM reverse)
   dev_matrix_vari* transpose_of_ = nullptr;
+  // the producing node when it accepts structured adjoints (a Cholesky factor)
+  structured_adjoint_sink* sink_ = nullptr;
 
   dev_matrix_vari(int rows, int cols, dev_structure s = dev_structure::general)
       : rows_(rows),
@@ -196,12 +210,20 @@ class dev_to_host_vari : public vari {
  public:
   size_t blk_;  // index in host_blocks_
   size_t pos_;  // this node's index in var_stack_
+  size_t ran_ = 0;     // the sweep (ChainableStack::sweep_) of the last chain()
+  bool wrote_ = false;  // whether that chain() added into the node's adjoint
   explicit dev_to_host_vari(size_t blk)
       : vari(0.0), blk_(blk), pos_(ChainableStack::instance_->var_stack_.size() - 1) {}
   bool reads_other_adjoints() const override { return true; }
   bool touches_adjoints_in(const vari*, const vari*) const override { return false; }
+  bool may_write_device_adjoint(const void* node) const override {
+    auto* st = ChainableStack::instance_;
+    return node == st->host_blocks_[blk_].node && (ran_ != st->sweep_ || wrote_);
+  }
   void chain() override {
     auto* st = ChainableStack::instance_;
+    ran_ = st->sweep_;
+    wrote_ = false;
     const host_block b = st->host_blocks_[blk_];
     const vari* lo = b.first;
     const vari* hi = b.first + b.n;
@@ -209,6 +231,7 @@ class dev_to_host_vari : public vari {
     for (size_t i = pos_ + 1; !touched && i < st->var_stack_.size(); ++i)
       touched = st->var_stack_[i]->touches_adjoints_in(lo, hi);
     if (!touched) return;
+    wrote_ = true;
     smg_ctx* c = amd::ctx();
     double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
     if (!stage) throw std::bad_alloc();
@@ -274,11 +297,11 @@ inline const host_block& materialise(dev_matrix_vari* m,
 }
 
 // host varis -> device (reverse: device adjoint -> host adjoints)
-class host_to_dev_vari : public local_adjoint_vari {
+class host_to_dev_vari : public host_local_vari {
  public:
   dev_matrix_vari* dst_;
   vari** elems_;
-  host_to_dev_vari(dev_matrix_vari* dst, vari** elems) : local_adjoint_vari(0.0), dst_(dst), elems_(elems) {}
+  host_to_dev_vari(dev_matrix_vari* dst, vari** elems) : host_local_vari(0.0), dst_(dst), elems_(elems) {}
   bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
     const size_t n = dst_->size();
     return !host_parallel_all(n, [&](size_t s, size_t e) {

@@ -75,6 +75,9 @@ struct AutodiffStackSingleton {
     std::vector<pending_adjoint> pending_;
     std::vector<host_block> host_blocks_;
     std::vector<size_t> nested_host_block_sizes_;
+    // reverse sweeps started on this tape (grad()): a structured adjoint a
+    // node deposits is valid for the sweep that deposited it only
+    size_t sweep_ = 0;
   };
 
   AutodiffStackSingleton() : own_instance_(init()) {}

@@ -94,6 +94,7 @@ static void grad(vari* vi) {
   using it_t = std::vector<vari*>::reverse_iterator;
   auto* st = ChainableStack::instance_;
   join_device_adjoints();
+  ++st->sweep_;
   vi->init_dependent();
   for (auto& b : st->host_blocks_)  // the root itself may be an element of a host block
     if (vi >= b.first && vi < b.first + b.n) b.dirty = true;

@@ -19,21 +19,21 @@ namespace math {
 namespace internal {
 constexpr double NaN = std::numeric_limits<double>::quiet_NaN();
 
-class op_v_vari : public local_adjoint_vari {
+class op_v_vari : public host_local_vari {
  protected:
   vari* avi_;
 
  public:
-  op_v_vari(double f, vari* a) : local_adjoint_vari(f), avi_(a) {}
+  op_v_vari(double f, vari* a) : host_local_vari(f), avi_(a) {}
   bool touches_adjoints_in(const vari* lo, const vari* hi) const override { return avi_ >= lo && avi_ < hi; }
 };
-class op_vv_vari : public local_adjoint_vari {
+class op_vv_vari : public host_local_vari {
  protected:
   vari* avi_;
   vari* bvi_;
 
  public:
-  op_vv_vari(double f, vari* a, vari* b) : local_adjoint_vari(f), avi_(a), bvi_(b) {}
+  op_vv_vari(double f, vari* a, vari* b) : host_local_vari(f), avi_(a), bvi_(b) {}
   bool touches_adjoints_in(const vari* lo, const vari* hi) const override {
     return (avi_ >= lo && avi_ < hi) || (bvi_ >= lo && bvi_ < hi);
   }

@@ -13,7 +13,7 @@
 namespace stan {
 namespace math {
 
-class precomputed_gradients_vari : public local_adjoint_vari {
+class precomputed_gradients_vari : public host_local_vari {
  protected:
   const size_t size_;
   vari** varis_;
@@ -21,11 +21,11 @@ class precomputed_gradients_vari : public local_adjoint_vari {
 
  public:
   precomputed_gradients_vari(double val, size_t size, vari** varis, double* gradients)
-      : local_adjoint_vari(val), size_(size), varis_(varis), gradients_(gradients) {}
+      : host_local_vari(val), size_(size), varis_(varis), gradients_(gradients) {}
 
   precomputed_gradients_vari(double val, const std::vector<var>& vars,
                              const std::vector<double>& gradients)
-      : local_adjoint_vari(val),
+      : host_local_vari(val),
         size_(vars.size()),
         varis_(ChainableStack::instance_->memalloc_.alloc_array<vari*>(vars.size())),
         gradients_(ChainableStack::instance_->memalloc_.alloc_array<double>(vars.size())) {

@@ -63,6 +63,18 @@ class vari {
     return true;
   }
 
+  /** True when chain() may add into the DEVICE adjoint of the matrix node
+   * `node` (a dev_matrix_vari; stan/math/amd/matrix.hpp), asked of the nodes
+   * chained after a cholesky_decompose node once they have run: its factor's
+   * adjoint may skip the dense form only when no node but the consuming
+   * multi_normal_cholesky_lpdf wrote it (rev/fun/cholesky_decompose.hpp).  A
+   * vari written in the reference's style sees host adjoints only: false.
+   * The library's own nodes (local_adjoint_vari) answer true unless audited. */
+  virtual bool may_write_device_adjoint(const void* node) const {
+    (void)node;
+    return false;
+  }
+
   void init_dependent() { adj_ = 1.0; }
 
   void set_zero_adjoint() { adj_ = 0.0; }
@@ -84,6 +96,14 @@ class local_adjoint_vari : public vari {
  public:
   using vari::vari;
   bool reads_other_adjoints() const override { return false; }
+  bool may_write_device_adjoint(const void*) const override { return true; }
+};
+
+/** A library node whose chain() writes host adjoints only. */
+class host_local_vari : public local_adjoint_vari {
+ public:
+  using local_adjoint_vari::local_adjoint_vari;
+  bool may_write_device_adjoint(const void*) const override { return false; }
 };
 
 /** Base of the library's device nodes: chain() reads only this->adj_ and

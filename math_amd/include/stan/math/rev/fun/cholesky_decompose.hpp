@@ -19,6 +19,7 @@
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/core.hpp>
 
+#include <cstdlib>
 #include <sstream>
 #include <stdexcept>
 
@@ -69,17 +70,75 @@ class add_diag_dev_vari : public device_vari {
   }
 };
 
-class cholesky_dev_vari : public device_vari {
+/**
+ * The factor's adjoint reaches this node in one of two forms:
+ *  - dense (L_->adj_): Murray's blocked reverse, like the reference's chain()
+ *    (rev/mat/fun/cholesky_decompose.hpp:118-166);
+ *  - structured: a multi_normal_cholesky_lpdf consuming the factor deposits
+ *    its partials unexpanded (take_mvn_adjoint) instead of writing the dense
+ *    adj (tril(s w^T) - diag(1/L_ii)).  When no other node chained after this
+ *    one wrote the factor's adjoint (may_write_device_adjoint), the reverse is
+ *    the closed form Abar += adj Phi(s s^T - K^{-1}) (smg_cholesky_mvn_rev:
+ *    the same 2N^3/3 in a few large GEMMs); otherwise the deposit is expanded
+ *    into L_->adj_ first and Murray's reverse runs on the sum.
+ */
+class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
  public:
   dev_matrix_vari* A_;
   dev_matrix_vari* L_;
   int n_;
+  size_t pos_;  // this node's index in var_stack_
+  // the deposited multi_normal_cholesky_lpdf partials
+  const vari* dep_owner_ = nullptr;
+  const double* dep_ws_ = nullptr;
+  double dep_adj_ = 0.0;
+  size_t dep_sweep_ = 0;
 
-  cholesky_dev_vari(dev_matrix_vari* A, dev_matrix_vari* L) : device_vari(0.0), A_(A), L_(L), n_(A->rows_) {}
+  cholesky_dev_vari(dev_matrix_vari* A, dev_matrix_vari* L)
+      : device_vari(0.0), A_(A), L_(L), n_(A->rows_), pos_(ChainableStack::instance_->var_stack_.size() - 1) {
+    L->sink_ = this;
+  }
+
+  bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) override {
+    // SMG_CHOL_MVN_CLOSED_FORM=0: always the dense adjoint + Murray (A/B, tests)
+    static const bool on = [] {
+      const char* e = std::getenv("SMG_CHOL_MVN_CLOSED_FORM");
+      return !(e && e[0] == '0');
+    }();
+    if (!on) return false;
+    auto* st = ChainableStack::instance_;
+    if (dep_owner_ && dep_sweep_ == st->sweep_ && dep_owner_ != owner) return false;  // one consumer only
+    dep_owner_ = owner;
+    dep_ws_ = ws;
+    dep_adj_ = adj;
+    dep_sweep_ = st->sweep_;
+    return true;
+  }
 
   void chain() override {
     smg_ctx* c = amd::ctx();
+    auto* st = ChainableStack::instance_;
     const size_t nn = size_t(n_) * n_;
+    const bool deposit = dep_owner_ && dep_sweep_ == st->sweep_;
+    if (deposit) {
+      const vari* owner = dep_owner_;
+      dep_owner_ = nullptr;
+      bool dense = false;  // did any other node write L's adjoint?
+      for (size_t i = pos_ + 1; !dense && i < st->var_stack_.size(); ++i) {
+        const vari* v = st->var_stack_[i];
+        dense = v != owner && v->may_write_device_adjoint(L_);
+      }
+      if (!dense) {
+        double* ws = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
+        amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws),
+                   "cholesky_decompose");
+        return;
+      }
+      // expand the deposit: the MVN's own lower-only partials, added densely
+      amd::check(smg_mvn_cholesky_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_, dep_adj_, 1, nullptr, nullptr,
+                                      L_->adj_, n_),
+                 "cholesky_decompose");
+    }
     // Murray's algorithm overwrites its input and reads only its lower triangle
     double* work = amd::alloc_doubles(nn);
     amd::check(smg_copy_tril(c, n_, n_, L_->adj_, n_, work, n_), "cholesky_decompose");

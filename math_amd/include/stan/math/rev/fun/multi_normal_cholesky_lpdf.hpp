@@ -35,15 +35,24 @@ class mvn_cholesky_dev_vari : public device_vari {
   dev_matrix_vari* y_;   // null when y is data
   dev_matrix_vari* mu_;  // null when mu is data
 
+  bool deposited_ = false;  // the last chain() handed L's partials to its producer
+
   mvn_cholesky_dev_vari(double lp, dev_matrix_vari* L, const double* ws,
                         dev_matrix_vari* y = nullptr, dev_matrix_vari* mu = nullptr)
       : device_vari(lp), L_(L), ws_(ws), n_(L->rows_), y_(y), mu_(mu) {}
 
+  bool may_write_device_adjoint(const void* node) const override {
+    return (node == L_ && !deposited_) || (y_ && node == y_) || (mu_ && node == mu_);
+  }
+
   void chain() override {
     const int lower_only = L_->structure_ == dev_structure::lower ? 1 : 0;
+    // a cholesky_decompose factor takes the lower-only partials unexpanded
+    // (rev/fun/cholesky_decompose.hpp: its reverse then has a closed form)
+    deposited_ = lower_only && L_->sink_ && L_->sink_->take_mvn_adjoint(this, ws_, adj_);
     amd::check(smg_mvn_cholesky_rev(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, adj_, lower_only,
-                                    y_ ? y_->adj_ : nullptr, mu_ ? mu_->adj_ : nullptr, L_->adj_,
-                                    n_),
+                                    y_ ? y_->adj_ : nullptr, mu_ ? mu_->adj_ : nullptr,
+                                    deposited_ ? nullptr : L_->adj_, n_),
                "multi_normal_cholesky_lpdf");
   }
 };
@@ -131,14 +140,24 @@ class mvn_multi_dev_vari : public device_vari {
   int n_, k_, lower_only_;
   const double* ws_;  // k blocks of 2n doubles: [w_i, sd_i]
   mvn_obs* obs_;
+  bool deposited_ = false;  // the last chain() handed L's partials to its producer
   mvn_multi_dev_vari(double lp, const dev_operand& L, const double* aux, int lower_only, const double* ws,
                      mvn_obs* obs, int k)
       : device_vari(lp), L_(L), aux_(aux), n_(L.rows), k_(k), lower_only_(lower_only), ws_(ws), obs_(obs) {}
+  bool may_write_device_adjoint(const void* node) const override {
+    if (L_.vi && node == L_.vi) return !deposited_;
+    for (int i = 0; i < k_; ++i)  // (an observation's y / mu nodes)
+      if (node && (obs_[i].yadj || obs_[i].muadj)) return true;
+    return false;
+  }
   void chain() override {
     smg_ctx* c = amd::ctx();
+    // one observation and a cholesky_decompose factor: the lower-only
+    // partials go to the factor's node unexpanded (rev/fun/cholesky_decompose.hpp)
+    deposited_ = k_ == 1 && lower_only_ && L_.vi && L_.vi->sink_ && L_.vi->sink_->take_mvn_adjoint(this, ws_, adj_);
     for (int i = 0; i < k_; ++i)
       amd::check(smg_mvn_cholesky_rev(c, L_.val(), n_, aux_, n_, ws_ + 2 * size_t(n_) * i, adj_, lower_only_,
-                                      obs_[i].yadj, obs_[i].muadj, L_.adj(), n_),
+                                      obs_[i].yadj, obs_[i].muadj, deposited_ ? nullptr : L_.adj(), n_),
                  "multi_normal_cholesky_lpdf");
   }
 };

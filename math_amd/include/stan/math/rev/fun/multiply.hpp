@@ -138,11 +138,11 @@ class sum_dev_vari : public device_vari {
 
 // sum(std::vector<var>) (rev/arr/fun/sum.hpp:14-57): a host node, the
 // values summed in order on the host like the reference's sum_of_val
-class sum_v_vari : public local_adjoint_vari {
+class sum_v_vari : public host_local_vari {
  public:
   vari** v_;
   size_t n_;
-  sum_v_vari(double s, vari** v, size_t n) : local_adjoint_vari(s), v_(v), n_(n) {}
+  sum_v_vari(double s, vari** v, size_t n) : host_local_vari(s), v_(v), n_(n) {}
   void chain() override {
     for (size_t i = 0; i < n_; ++i) v_[i]->adj_ += adj_;
   }

@@ -43,21 +43,61 @@ def test_cpp_programs_built():
         assert os.path.exists(os.path.join(BIN, name)), f"{name} not built (run __graft_entry__.build())"
 
 
-def _run(name, stdin):
-    p = subprocess.run([os.path.join(BIN, name)], input=stdin, capture_output=True, text=True, timeout=300)
+def _run(name, stdin, args=(), env=None):
+    e = None if env is None else {**os.environ, **env}
+    p = subprocess.run([os.path.join(BIN, name), *args], input=stdin, capture_output=True, text=True, timeout=300,
+                       env=e)
     assert p.returncode == 0, p.stderr[-2000:]
     return p.stdout
 
 
+def _gp_stdin(d):
+    N = len(d["x"])
+    stdin = f"{N} " + " ".join(repr(float(v)) for v in d["theta"]) + "\n"
+    return stdin + " ".join(repr(float(v)) for v in d["x"]) + "\n" + " ".join(repr(float(v)) for v in d["y"]) + "\n"
+
+
+def _gp_rows(out):
+    return np.array([[float(v) for v in l.split()] for l in out.strip().splitlines()[:3]])
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [16, 256, 4096])
+@pytest.mark.parametrize("N", [16, 256, 1024, 4096])
 def test_gp_gradient_through_tape(N):
     d = golden(f"gp_N{N}")
-    stdin = f"{N} " + " ".join(repr(float(v)) for v in d["theta"]) + "\n"
-    stdin += " ".join(repr(float(v)) for v in d["x"]) + "\n" + " ".join(repr(float(v)) for v in d["y"]) + "\n"
-    lines = [l.split() for l in _run("test_gp_tape", stdin).strip().splitlines()]
+    lines = [l.split() for l in _run("test_gp_tape", _gp_stdin(d)).strip().splitlines()]
     for row in lines[:3]:  # std::vector twice (re-use of recovered arenas) + Eigen::VectorXd
         vals = np.array([float(v) for v in row])
         near_rel(vals[0], d["fx"], 1e-12, what="fx")
         near_rel(vals[1:], d["grad"], 1e-10, what="grad")
     assert lines[3] == ["stack", "0", "0"]  # nested tape fully recovered
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [64, 1024])
+def test_gp_cholesky_reverse_closed_form_vs_murray(N):
+    """The GP's factor has one consumer, the MVN: cholesky_decompose's reverse
+    takes the closed form adj Phi(s s^T - K^{-1}) (smg_cholesky_mvn_rev; N = 64
+    the blocked-solve inverse, N = 1024 the doubling from the 512-row block
+    inverses); SMG_CHOL_MVN_CLOSED_FORM=0 forces the dense adjoint + Murray's
+    reverse.  Both match the reference's golden gradient at 1e-10 and each
+    other at 1e-11."""
+    d = golden(f"gp_N{N}")
+    a = _gp_rows(_run("test_gp_tape", _gp_stdin(d)))
+    b = _gp_rows(_run("test_gp_tape", _gp_stdin(d), env={"SMG_CHOL_MVN_CLOSED_FORM": "0"}))
+    for r in (a, b):
+        near_rel(r[:, 1:], np.tile(d["grad"], (3, 1)), 1e-10, what="grad")
+    near_rel(a, b, 1e-11, what="closed form vs Murray")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [64, 1024])
+def test_gp_cholesky_second_consumer_takes_dense_path(N):
+    """lp + 1e-3 sum(L): the factor's adjoint is no longer the MVN's alone, so
+    the deposited MVN partials are expanded into the dense adjoint and Murray's
+    reverse runs on the sum -- equal to the run that never deposits."""
+    d = golden(f"gp_N{N}")
+    a = _gp_rows(_run("test_gp_tape", _gp_stdin(d), args=("mixed",)))
+    b = _gp_rows(_run("test_gp_tape", _gp_stdin(d), args=("mixed",), env={"SMG_CHOL_MVN_CLOSED_FORM": "0"}))
+    near_rel(a, b, 1e-12, what="mixed consumers")
+    assert abs(a[0, 0] - d["fx"]) > 1e-9  # the extra term is really there

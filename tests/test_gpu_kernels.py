@@ -292,6 +292,40 @@ def test_cholesky_vs_oracle(ctx, N):
     near_rel(g, Aref, 1e-10, atol=1e-10 * np.abs(Aref).max(), what="grad_A")
 
 
+@pytest.mark.parametrize("N", [65, 300, 1024, 2048])
+def test_cholesky_mvn_closed_form_vs_oracle(ctx, N):
+    """smg_cholesky_mvn_rev: cholesky_decompose's reverse for the MVN's
+    lower-only partials Lbar = adj (tril(s w^T) - diag(1/L_ii)), in closed form
+    adj Phi(s s^T - K^{-1}), against the oracle's Murray reverse of that Lbar
+    (N = 65, 300: L^{-1} by the blocked solve; 1024, 2048: the doubling from
+    the 512-row block inverses, with and without the factorisation's aux)."""
+    rng = np.random.default_rng(N + 11)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + 0.2 * np.eye(N)
+    A = 0.5 * (A + A.T)
+    y = rng.uniform(-1, 1, N)
+    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(N))
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
+    ws, dlp = ctx.zeros(2 * N), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd", ctx.put(y), None, dL, N, dD, N, ws, dlp)
+    L = ctx.get(dL, N * N).reshape(N, N).T
+    w, s = np.split(ctx.get(ws, 2 * N), 2)
+    adj = 0.75
+    Lbar = adj * (np.tril(np.outer(s, w)) - np.diag(1.0 / np.diag(L)))
+    Aref = np.zeros(N * N)
+    oracle().oracle_cholesky_rev(ptr(F(L)), ptr(F(Lbar)), N, ptr(Aref))
+    Aref = Aref.reshape(N, N).T
+    wsz = ctx.lib.smg_cholesky_mvn_rev_ws_doubles(N)
+    for aux in (dD, None):
+        G0 = rng.uniform(-1, 1, (N, N))  # accumulates into the lower triangle only
+        dG = ctx.put(F(G0))
+        ctx.call("smg_cholesky_mvn_rev", dL, N, aux, N, ws + 8 * N, adj, dG, N, ctx.zeros(wsz))
+        G = ctx.get(dG, N * N).reshape(N, N).T
+        low = np.tril(np.ones((N, N), bool))
+        near_rel(G[low] - G0[low], Aref[low], 1e-10, atol=1e-10 * np.abs(Aref).max(), what="grad_A")
+        assert np.array_equal(G[~low], G0[~low])
+
+
 def test_cholesky_not_pd_and_not_symmetric(ctx):
     N = 70
     A = np.eye(N)
