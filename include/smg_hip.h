@@ -413,6 +413,16 @@ int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
 size_t smg_cholesky_mvn_rev_ws_doubles(int n);
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                          const double* s, double adj, double* Aadj, int ldaa, double* ws);
+/* The same in two parts, the first overlapping the MVN's forward solves:
+ * smg_cholesky_inv_t_async forms V = L^{-T} in ws (with aux, n % 512 == 0,
+ * n >= 1024; else *started = 0 and nothing is queued) on the context's side
+ * stream after the work queued so far; smg_cholesky_mvn_rev_v (the same ws)
+ * joins it and applies the closed form.  smg_join_async and arena rewinds
+ * also join it. */
+int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
+                             double* ws, int* started);
+int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa,
+                           double* ws);
 
 /* log_sum_exp(vector<var>) (rev/mat/fun/log_sum_exp.hpp:20-53):
  *   fwd: out = max + log(sum exp(x - max)); empty -> -inf; non-finite max -> max

@@ -141,6 +141,31 @@ inline int grid_for(long long tot) {
   return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
 }
 
+// V = L^{-T} (n % 512 == 0, n >= 1024, with the factorisation's aux)
+int form_v(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* V, double* T) {
+  const double* w512 = aux + (size_t)n * SMG_AUX_W512;
+  bool pairs = false;
+  int rc = inv_t_leaves(ctx, L, ldl, w512, n, V, n, T, &pairs);
+  if (!rc) rc = inv_t_rec(ctx, L, ldl, w512, n, V, n, T, 0, n, pairs);
+  return rc;
+}
+
+bool v_by_doubling(int n, const double* aux) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR && aux; }
+
+// Abar (lower) += adj Phi(s s^T - C), C = K^{-1} lower
+int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, double adj, double* Aadj, int ldaa) {
+  if (n % 2 == 0 && ldaa % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(Aadj) | reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(C)) & 15) ==
+          0)
+    hipLaunchKernelGGL(k_chol_mvn_adj_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, C, n, n, s, adj,
+                       Aadj, ldaa);
+  else
+    hipLaunchKernelGGL(k_chol_mvn_adj, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, C, n, n, s, adj,
+                       Aadj, ldaa);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -157,11 +182,8 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
   double* V = ws;       // L^{-T} (upper), or W = L^{-1} on the general path
   double* C = ws + nn;  // K^{-1} (lower); the doubling's T before that
   int rc;
-  if (n % SMG_NBR == 0 && n >= 2 * SMG_NBR && aux) {
-    const double* w512 = aux + (size_t)n * SMG_AUX_W512;
-    bool pairs = false;
-    if ((rc = inv_t_leaves(ctx, L, ldl, w512, n, V, n, C, &pairs))) return rc;
-    if ((rc = inv_t_rec(ctx, L, ldl, w512, n, V, n, C, 0, n, pairs))) return rc;
+  if (v_by_doubling(n, aux)) {
+    if ((rc = form_v(ctx, L, ldl, aux, n, V, C))) return rc;
     // C = V V^T, lower: op(A) = V upper, op(B) = V^T lower
     rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
   } else {  // any n: W = L^{-1} by the blocked solve, C = W^T W
@@ -171,15 +193,49 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
     rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
   }
   if (rc) return rc;
-  if (n % 2 == 0 && ldaa % 2 == 0 &&
-      ((reinterpret_cast<uintptr_t>(Aadj) | reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(C)) & 15) ==
-          0)
-    hipLaunchKernelGGL(k_chol_mvn_adj_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, C, n, n, s, adj,
-                       Aadj, ldaa);
-  else
-    hipLaunchKernelGGL(k_chol_mvn_adj, dim3(grid_for(nn)), dim3(256), 0, ctx->stream, C, n, n, s, adj, Aadj, ldaa);
-  SMG_LAUNCH_CHECK();
+  return mvn_adj_epilogue(ctx, C, n, s, adj, Aadj, ldaa);
+}
+
+int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws,
+                             int* started) {
+  if (!ctx || n < 0 || !started) return SMG_ERR_ARG;
+  *started = 0;
+  if (n == 0 || !v_by_doubling(n, aux)) return SMG_OK;
+  if (!L || !ws || ldl < n) return SMG_ERR_ARG;
+  if (int rc = smg_side_begin(ctx)) return rc;
+  if (!ctx->inv_ev) {
+    SMG_HIP_TRY(hipEventCreateWithFlags(&ctx->inv_ev, hipEventDisableTiming));
+    SMG_HIP_TRY(hipEventCreateWithFlags(&ctx->inv_ev_main, hipEventDisableTiming));
+  }
+  // L and its block inverses are complete once the main stream's queued work is
+  SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
+  SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
+  int rc;
+  {
+    smg_on_side on(ctx);
+    rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);
+  }
+  if (rc) return rc;
+  SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
+  ctx->inv_pending = 1;
+  *started = 1;
   return SMG_OK;
+}
+
+int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa, double* ws) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!s || !Aadj || !ws || ldaa < n) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
+  if (ctx->inv_pending) {
+    SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev, 0));
+    ctx->inv_pending = 0;
+  }
+  const size_t nn = (size_t)n * n;
+  double* C = ws + nn;
+  int rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, ws, n, ws, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+  if (rc) return rc;
+  return mvn_adj_epilogue(ctx, C, n, s, adj, Aadj, ldaa);
 }
 
 }  // extern "C"

@@ -154,6 +154,8 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->zero_stream = nullptr;
   ctx->zero_ev_main = ctx->zero_ev_done = nullptr;
   ctx->zero_pending = 0;
+  ctx->inv_ev = ctx->inv_ev_main = nullptr;
+  ctx->inv_pending = 0;
   ctx->side = nullptr;
   ctx->main_stream = nullptr;
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
@@ -220,6 +222,8 @@ int smg_ctx_destroy(smg_ctx* ctx) {
     hipStreamSynchronize(ctx->side);
     hipStreamDestroy(ctx->side);
   }
+  if (ctx->inv_ev) hipEventDestroy(ctx->inv_ev);
+  if (ctx->inv_ev_main) hipEventDestroy(ctx->inv_ev_main);
   for (int i = 0; i < SMG_WS_COUNT; ++i)
     if (ctx->ws[i]) hipFree(ctx->ws[i]);
   hipFree(ctx->status_d);
@@ -420,6 +424,10 @@ int smg_zero_flush(smg_ctx* ctx) {
 
 int smg_join_async(smg_ctx* ctx) {
   if (!ctx) return SMG_ERR_ARG;
+  if (ctx->inv_pending) {  // an smg_cholesky_inv_t_async still on the side stream
+    SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev, 0));
+    ctx->inv_pending = 0;
+  }
   if (int e = smg_zero_flush(ctx)) return e;
   if (!ctx->zero_pending) return SMG_OK;
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->zero_ev_done, 0));

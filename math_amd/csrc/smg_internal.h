@@ -62,6 +62,11 @@ struct smg_ctx {
   // overlap those rather than the HBM-bound element-wise kernels before them,
   // and at the latest by smg_join_async / an arena rewind (smg_zero_flush)
   std::vector<std::pair<void*, size_t>> zero_queue;
+  // smg_cholesky_inv_t_async: L^{-T} formed on `side` while the main stream
+  // runs the (latency-bound) MVN solves; `inv_ev` is recorded after it and
+  // joined into `stream` by smg_cholesky_mvn_rev_v or smg_join_async
+  hipEvent_t inv_ev, inv_ev_main;
+  int inv_pending;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;

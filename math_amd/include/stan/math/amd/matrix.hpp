@@ -48,6 +48,9 @@ class structured_adjoint_sink {
    * adj: its adjoint.  True when taken (the consumer then writes no dense
    * adjoint for the factor); false: the consumer writes it densely. */
   virtual bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) = 0;
+  /** Called by such a consumer's forward pass before its own device work:
+   * the node may start, on a side stream, what that reverse will need. */
+  virtual void prepare_mvn_adjoint() {}
 };
 
 class dev_matrix_vari {

@@ -93,19 +93,40 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   const double* dep_ws_ = nullptr;
   double dep_adj_ = 0.0;
   size_t dep_sweep_ = 0;
+  double* ws_ = nullptr;  // smg_cholesky_mvn_rev's workspace [V = L^{-T}, K^{-1}]
+  bool v_ready_ = false;  // V formed (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
+
+  static bool closed_form_enabled() {
+    // SMG_CHOL_MVN_CLOSED_FORM=0: always the dense adjoint + Murray (A/B, tests)
+    static const bool on = [] {
+      const char* e = std::getenv("SMG_CHOL_MVN_CLOSED_FORM");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
 
   cholesky_dev_vari(dev_matrix_vari* A, dev_matrix_vari* L)
       : device_vari(0.0), A_(A), L_(L), n_(A->rows_), pos_(ChainableStack::instance_->var_stack_.size() - 1) {
     L->sink_ = this;
   }
 
-  bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) override {
-    // SMG_CHOL_MVN_CLOSED_FORM=0: always the dense adjoint + Murray (A/B, tests)
-    static const bool on = [] {
-      const char* e = std::getenv("SMG_CHOL_MVN_CLOSED_FORM");
+  // L^{-T} is formed while the MVN's forward solves run (they are
+  // latency-bound: most CUs idle); unused if the reverse takes the dense path
+  void prepare_mvn_adjoint() override {
+    static const bool async = [] {  // SMG_CHOL_MVN_ASYNC=0: V formed in the reverse (A/B)
+      const char* e = std::getenv("SMG_CHOL_MVN_ASYNC");
       return !(e && e[0] == '0');
     }();
-    if (!on) return false;
+    if (!closed_form_enabled() || !async || ws_) return;
+    ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
+    int started = 0;
+    amd::check(smg_cholesky_inv_t_async(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, &started),
+               "multi_normal_cholesky_lpdf");
+    v_ready_ = started != 0;
+  }
+
+  bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) override {
+    if (!closed_form_enabled()) return false;
     auto* st = ChainableStack::instance_;
     if (dep_owner_ && dep_sweep_ == st->sweep_ && dep_owner_ != owner) return false;  // one consumer only
     dep_owner_ = owner;
@@ -129,9 +150,13 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
         dense = v != owner && v->may_write_device_adjoint(L_);
       }
       if (!dense) {
-        double* ws = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
-        amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws),
-                   "cholesky_decompose");
+        if (v_ready_) {
+          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_), "cholesky_decompose");
+        } else {
+          if (!ws_) ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
+          amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_),
+                     "cholesky_decompose");
+        }
         return;
       }
       // expand the deposit: the MVN's own lower-only partials, added densely
