@@ -416,13 +416,23 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
 /* The same in two parts, the first overlapping the MVN's forward solves:
  * smg_cholesky_inv_t_async forms V = L^{-T} in ws (with aux, n % 512 == 0,
  * n >= 1024; else *started = 0 and nothing is queued) on the context's side
- * stream after the work queued so far; smg_cholesky_mvn_rev_v (the same ws)
- * joins it and applies the closed form.  smg_join_async and arena rewinds
+ * stream after the work queued so far; smg_cholesky_mvn_rev_v (the same ws,
+ * c_formed = 0) joins it, forms K^{-1} and applies the closed form.  smg_join_async and arena rewinds
  * also join it. */
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                              double* ws, int* started);
 int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa,
-                           double* ws);
+                           double* ws, int c_formed);
+/* smg_cholesky_fwd_checked_mark that also forms V = L^{-T} and K^{-1} = V V^T
+ * (lower) in ws (smg_cholesky_mvn_rev_ws_doubles(n)) on a second side stream:
+ * the top half's part as soon as the first n/2 columns are factored
+ * (overlapping the remaining panels), the rest after the last; *started = 1
+ * when queued (n / 512 a power of two >= 2), then smg_cholesky_mvn_rev_v(...,
+ * c_formed = 1) applies the closed form.  For a factor whose reverse is
+ * predicted to take the closed form (the host layer's history per tape
+ * position). */
+int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                      double* aux, double* ws, int* started);
 
 /* log_sum_exp(vector<var>) (rev/mat/fun/log_sum_exp.hpp:20-53):
  *   fwd: out = max + log(sum exp(x - max)); empty -> -inf; non-finite max -> max

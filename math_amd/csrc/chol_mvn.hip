@@ -47,12 +47,12 @@ int inv_t_rec(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n,
                        V + lo + (size_t)mid * ldv, ldv, SMG_TRI_B_UPPER);
 }
 
-// V_bb = W_b^T for every 512-row leaf b (one launch: blockIdx.z = leaf,
-// 64 x 64 tiles through LDS)
-__global__ __launch_bounds__(256) void k_leaf_transpose(const double* __restrict__ w512, int n,
+// V_bb = W_b^T for every 512-row leaf b from b0 (one launch: blockIdx.z =
+// leaf, 64 x 64 tiles through LDS)
+__global__ __launch_bounds__(256) void k_leaf_transpose(const double* __restrict__ w512, int n, int lo,
                                                        double* __restrict__ V, int ldv) {
   __shared__ double t[64][65];
-  const int b0 = blockIdx.z * SMG_NBR;
+  const int b0 = lo + blockIdx.z * SMG_NBR;
   const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;  // tile of W_b (rows i, cols j)
   const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
 #pragma unroll 4
@@ -63,25 +63,28 @@ __global__ __launch_bounds__(256) void k_leaf_transpose(const double* __restrict
     V[b0 + j0 + r + (size_t)(b0 + i0 + c) * ldv] = t[r][c];
 }
 
-// the leaves, and (n / 512 a power of two: the recursion's 1024-row nodes are
-// then the aligned leaf pairs) every pair's V12 = -V11 L21^T V22 as two
-// strided-batched products; returns whether the pairs were formed
-int inv_t_leaves(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n, double* V, int ldv, double* T,
-                 bool* pairs) {
-  const int nl = n / SMG_NBR;
-  hipLaunchKernelGGL(k_leaf_transpose, dim3(SMG_NBR / 64, SMG_NBR / 64, nl), dim3(256), 0, ctx->stream, w512, n, V,
-                     ldv);
+// the leaves of V[lo:hi, lo:hi] and, when (hi - lo) / 512 is a power of two
+// (the recursion's 1024-row nodes are then the aligned leaf pairs), every
+// pair's V12 = -V11 L21^T V22 as two strided-batched products (T: ld n);
+// returns whether the pairs were formed
+int inv_t_leaves(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n, int lo, int hi, double* V,
+                 int ldv, double* T, bool* pairs) {
+  const int nl = (hi - lo) / SMG_NBR;
+  hipLaunchKernelGGL(k_leaf_transpose, dim3(SMG_NBR / 64, SMG_NBR / 64, nl), dim3(256), 0, ctx->stream, w512, n, lo,
+                     V, ldv);
   SMG_LAUNCH_CHECK();
   *pairs = (nl & (nl - 1)) == 0 && nl >= 2;
   if (!*pairs) return SMG_OK;
   const int np = nl / 2, b = SMG_NBR;
   const long long sv = 2LL * b * (1 + (long long)ldv), sl = 2LL * b * (1 + (long long)ldl);
+  const double* V0 = V + lo + (size_t)lo * ldv;
+  const double* L0 = L + lo + (size_t)lo * ldl;
   // T_p (b x b, rows p b of T, ld n) = V11_p L21_p^T
-  int rc = smg_gemm_batched_impl(ctx, 0, 1, b, b, b, 1.0, V, ldv, sv, L + b, ldl, sl, 0.0, T, n, b, np);
+  int rc = smg_gemm_batched_impl(ctx, 0, 1, b, b, b, 1.0, V0, ldv, sv, L0 + b, ldl, sl, 0.0, T, n, b, np);
   if (rc) return rc;
   // V12_p = -T_p V22_p
-  return smg_gemm_batched_impl(ctx, 0, 0, b, b, b, -1.0, T, n, b, V + b + (size_t)b * ldv, ldv, sv, 0.0,
-                               V + (size_t)b * ldv, ldv, sv, np);
+  return smg_gemm_batched_impl(ctx, 0, 0, b, b, b, -1.0, T, n, b, V0 + b + (size_t)b * ldv, ldv, sv, 0.0,
+                               V + lo + (size_t)(lo + b) * ldv, ldv, sv, np);
 }
 
 // Abar(i, j) += adj ((s_i s_j - C_ij) * (i == j ? 1/2 : 1)), i >= j, C lower;
@@ -142,11 +145,14 @@ inline int grid_for(long long tot) {
 }
 
 // V = L^{-T} (n % 512 == 0, n >= 1024, with the factorisation's aux)
-int form_v(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* V, double* T) {
+// (V[lo:hi, lo:hi] only: the diagonal block of rows lo..hi)
+int form_v(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* V, double* T, int lo = 0,
+           int hi = -1) {
+  if (hi < 0) hi = n;
   const double* w512 = aux + (size_t)n * SMG_AUX_W512;
   bool pairs = false;
-  int rc = inv_t_leaves(ctx, L, ldl, w512, n, V, n, T, &pairs);
-  if (!rc) rc = inv_t_rec(ctx, L, ldl, w512, n, V, n, T, 0, n, pairs);
+  int rc = inv_t_leaves(ctx, L, ldl, w512, n, lo, hi, V, n, T, &pairs);
+  if (!rc) rc = inv_t_rec(ctx, L, ldl, w512, n, V, n, T, lo, hi, pairs);
   return rc;
 }
 
@@ -167,6 +173,43 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, doub
 }
 
 }  // namespace
+
+// K^{-1} formed during the factorisation (cholesky.hip chol_fwd, on side2):
+// with h = n / 2, V = [[V11, V12], [0, V22]], V12 = -(V11 L21^T) V22.
+bool smg_inv_split_ok(int n) {
+  const int nl = n / SMG_NBR;
+  return n % SMG_NBR == 0 && nl >= 2 && (nl & (nl - 1)) == 0;
+}
+
+// early (the first h columns of L and their block inverses final): V11, and
+// T = V11 L21^T into the C half of ws (ld n, rows 0..h)
+int smg_inv_early(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws) {
+  const int h = n / 2;
+  double* V = ws;
+  double* T = ws + (size_t)n * n;
+  int rc = form_v(ctx, L, ldl, aux, n, V, T + h, 0, h);  // (its own T below row h)
+  if (rc) return rc;
+  return smg_gemm_impl(ctx, 0, 1, 0, h, h, h, 1.0, V, n, L + h, ldl, 0.0, T, n, SMG_TRI_A_UPPER);
+}
+
+// late (all of L and its block inverses): V22, V12 = -T V22 (or all of V when
+// the early part did not run), then C = V V^T (lower)
+int smg_inv_late(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws, bool early) {
+  const int h = n / 2;
+  const size_t nn = (size_t)n * n;
+  double* V = ws;
+  double* C = ws + nn;
+  int rc;
+  if (early) {
+    if ((rc = form_v(ctx, L, ldl, aux, n, V, C + h, h, n))) return rc;
+    rc = smg_gemm_impl(ctx, 0, 0, 0, h, h, h, -1.0, C, n, V + h + (size_t)h * n, n, 0.0, V + (size_t)h * n, n,
+                       SMG_TRI_B_UPPER);
+  } else {
+    rc = form_v(ctx, L, ldl, aux, n, V, C);
+  }
+  if (rc) return rc;
+  return smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+}
 
 extern "C" {
 
@@ -203,17 +246,14 @@ int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const doubl
   if (n == 0 || !v_by_doubling(n, aux)) return SMG_OK;
   if (!L || !ws || ldl < n) return SMG_ERR_ARG;
   if (int rc = smg_side_begin(ctx)) return rc;
-  if (!ctx->inv_ev) {
-    SMG_HIP_TRY(hipEventCreateWithFlags(&ctx->inv_ev, hipEventDisableTiming));
-    SMG_HIP_TRY(hipEventCreateWithFlags(&ctx->inv_ev_main, hipEventDisableTiming));
-  }
+  if (int rc = smg_inv_events(ctx)) return rc;
   // L and its block inverses are complete once the main stream's queued work is
   SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
   int rc;
   {
     smg_on_side on(ctx);
-    rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);
+    rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);  // (V only: C in the reverse)
   }
   if (rc) return rc;
   SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
@@ -222,7 +262,8 @@ int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const doubl
   return SMG_OK;
 }
 
-int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa, double* ws) {
+int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa, double* ws,
+                           int c_formed) {
   if (!ctx || n < 0) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   if (!s || !Aadj || !ws || ldaa < n) return SMG_ERR_ARG;
@@ -233,8 +274,10 @@ int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, dou
   }
   const size_t nn = (size_t)n * n;
   double* C = ws + nn;
-  int rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, ws, n, ws, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
-  if (rc) return rc;
+  if (!c_formed) {
+    int rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, ws, n, ws, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+    if (rc) return rc;
+  }
   return mvn_adj_epilogue(ctx, C, n, s, adj, Aadj, ldaa);
 }
 

@@ -685,18 +685,23 @@ int chol_rev_blocks(smg_ctx* ctx, const double* L, int ldl, const double* Dv, in
 // Inverses of the full 128-, 256- and 512-row diagonal blocks of L by
 // recursive doubling from the SMG_NB-block inverses: aux (ld n) holds the
 // levels at the SMG_AUX_W* column offsets (smg_cholesky_aux_doubles).
-int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int n) {
-  const double* Wi = aux;
+// (rows [row0, row0 + nrows) only, nrows < 0: all; T: workspace of
+// nrows / 2 x 256 doubles, NULL: SMG_WS_TMP)
+int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0 = 0,
+                        int nrows = -1, double* Tbuf = nullptr) {
+  if (nrows < 0) nrows = n;
+  L += (size_t)row0 * (ldl + 1);
+  const double* Wi = aux + row0;
   int ldi = n;
   for (int s2 = 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
-    const int s = s2 / 2, nb = n / s2;
+    const int s = s2 / 2, nb = nrows / s2;
     if (nb == 0) return SMG_OK;
     const int off = s2 == 128 ? SMG_AUX_W128 : (s2 == 256 ? SMG_AUX_W256 : SMG_AUX_W512);
-    double* Wo = aux + (size_t)n * off;
+    double* Wo = aux + (size_t)n * off + row0;
     const int ldw = n;
     hipLaunchKernelGGL(k_inv_double_diag, dim3(grid_for((long long)nb * s2 * s2)), dim3(256), 0,
                        ctx->stream, nb, s2, Wi, ldi, Wo, ldw);
-    double* T = smg_ws(ctx, SMG_WS_TMP, (size_t)nb * s * s);
+    double* T = Tbuf ? Tbuf : smg_ws(ctx, SMG_WS_TMP, (size_t)nb * s * s);
     if (!T) return SMG_ERR_OOM;
     // T_q = L21_q X11_q ;  X21_q = -X22_q T_q
     int rc = smg_gemm_batched_impl(ctx, 0, 0, s, s, s, 1.0, L + s, ldl, (long long)s2 * (ldl + 1),
@@ -850,7 +855,7 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
 }
 
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym, bool mark = false);
+             bool check_sym, bool mark = false, double* inv_ws = nullptr, int* inv_started = nullptr);
 
 }  // namespace
 
@@ -858,6 +863,10 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
 // 64-row ones (aux: n x SMG_AUX_COLS, ld n, 64-row level filled)
 int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux, int n) {
   return chol_block_inverses(ctx, L, ldl, aux, n);
+}
+int smg_block_inverses_rows(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0, int nrows,
+                            double* T) {
+  return chol_block_inverses(ctx, L, ldl, aux, n, row0, nrows, T);
 }
 
 extern "C" {
@@ -894,12 +903,20 @@ int smg_cholesky_fwd_checked_mark(smg_ctx* ctx, const double* A, int lda, int n,
   return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true);
 }
 
+int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                      double* Dinv, double* ws, int* started) {
+  if (!started) return SMG_ERR_ARG;
+  *started = 0;
+  if (ws && !Dinv) return SMG_ERR_ARG;
+  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started);
+}
+
 }  // extern "C"
 
 namespace {
 
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym, bool mark) {
+             bool check_sym, bool mark, double* inv_ws, int* inv_started) {
   if (!ctx || n < 0 || (n > 0 && (!A || !L || lda < n || ldl < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_FWD);
@@ -947,6 +964,10 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   static_assert(SMG_NBF <= PANEL_MAX_STEPS * SMG_NB, "panel width");
   const int NB2 = n > SMG_NBF ? SMG_NBF : n;
   const bool look = NB2 < n && smg_side_begin(ctx) == SMG_OK;
+  // K^{-1} on `side2` (the closed-form reverse under an MVN): the top half's
+  // part once its columns are final, overlapping the remaining panels
+  const bool inv = inv_ws && look && smg_inv_split_ok(n) && smg_side2_begin(ctx) == SMG_OK;
+  const bool early = inv && n / 2 % NB2 == 0;
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
   for (int J = 0; J < n; J += NB2) {
@@ -967,6 +988,16 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if (grid + nh > PANEL_MAX_GRID || nbp > T) nh = 0;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
+    }
+    if (early && K == n / 2) {  // L's first n/2 columns are final after this panel
+      SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->inv_ev_main, 0));
+      smg_on_side2 on(ctx);
+      const size_t nn = (size_t)n * n;
+      int rc = chol_block_inverses(ctx, L, ldl, aux, n, 0, n / 2, inv_ws + nn);
+      if (rc) return rc;
+      SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->side2));
+      if ((rc = smg_inv_early(ctx, L, ldl, aux, n, inv_ws))) return rc;
     }
     if (K >= n) break;
     const int m = n - K;
@@ -1010,9 +1041,22 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     if (rc) return rc;
   }
   if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
-  // the 128- and 256-block inverses (reverse pass, triangular solves)
-  int rc = chol_block_inverses(ctx, L, ldl, aux, n);
+  // the 128- and 256-block inverses (reverse pass, triangular solves); the
+  // top half's came from side2
+  int rc = early ? chol_block_inverses(ctx, L, ldl, aux, n, n / 2, n - n / 2) : chol_block_inverses(ctx, L, ldl, aux, n);
   if (rc) return rc;
+  if (early) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
+  if (inv) {
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main2, ctx->stream));
+    SMG_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->inv_ev_main2, 0));
+    {
+      smg_on_side2 on(ctx);
+      if ((rc = smg_inv_late(ctx, L, ldl, aux, n, inv_ws, early))) return rc;
+    }
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side2));
+    ctx->inv_pending = 1;
+    *inv_started = 1;
+  }
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

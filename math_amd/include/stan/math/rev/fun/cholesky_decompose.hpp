@@ -14,7 +14,9 @@
 // output's strict upper triangle is structurally zero (the reference points
 // those entries at a dummy vari, :34-48), which downstream nodes exploit.
 // chain() runs Murray's blocked adjoint on the device (smg_cholesky_rev) and
-// adds into the LOWER triangle of A's adjoint only, like :159-164.
+// adds into the LOWER triangle of A's adjoint only, like :159-164 -- or, when
+// the factor's only adjoint is a multi_normal_cholesky_lpdf's, the closed
+// form of that composition (cholesky_dev_vari below).
 
 #include <stan/math/amd/matrix.hpp>
 #include <stan/math/rev/core.hpp>
@@ -22,6 +24,8 @@
 #include <cstdlib>
 #include <sstream>
 #include <stdexcept>
+#include <utility>
+#include <vector>
 
 namespace stan {
 namespace math {
@@ -95,6 +99,36 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   size_t dep_sweep_ = 0;
   double* ws_ = nullptr;  // smg_cholesky_mvn_rev's workspace [V = L^{-T}, K^{-1}]
   bool v_ready_ = false;  // V formed (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
+  bool c_ready_ = false;  // and K^{-1} (formed during the factorisation)
+
+  /** Which factorisations took the closed-form reverse last time, by tape
+   * position and size: a sampler re-runs the same program every gradient, so
+   * the next factorisation at that position forms K^{-1} alongside its panels
+   * (smg_cholesky_fwd_checked_mark_inv) instead of after them. */
+  static std::vector<std::pair<std::pair<size_t, int>, bool>>& history() {
+    static thread_local std::vector<std::pair<std::pair<size_t, int>, bool>> h;
+    return h;
+  }
+  static bool predicted(size_t pos, int n) {
+    static const bool on = [] {  // SMG_CHOL_INV_FWD=0: K^{-1} never formed with the panels (A/B)
+      const char* e = std::getenv("SMG_CHOL_INV_FWD");
+      return !(e && e[0] == '0');
+    }();
+    if (!on) return false;
+    for (const auto& e : history())
+      if (e.first.first == pos && e.first.second == n) return e.second;
+    return false;
+  }
+  void record(bool closed) const {
+    auto& h = history();
+    for (auto& e : h)
+      if (e.first.first == pos_ && e.first.second == n_) {
+        e.second = closed;
+        return;
+      }
+    if (h.size() >= 64) h.erase(h.begin());
+    h.push_back({{pos_, n_}, closed});
+  }
 
   static bool closed_form_enabled() {
     // SMG_CHOL_MVN_CLOSED_FORM=0: always the dense adjoint + Murray (A/B, tests)
@@ -149,9 +183,11 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
         const vari* v = st->var_stack_[i];
         dense = v != owner && v->may_write_device_adjoint(L_);
       }
+      record(!dense);
       if (!dense) {
         if (v_ready_) {
-          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_), "cholesky_decompose");
+          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_, c_ready_ ? 1 : 0),
+                     "cholesky_decompose");
         } else {
           if (!ws_) ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
           amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_),
@@ -164,6 +200,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
                                       L_->adj_, n_),
                  "cholesky_decompose");
     }
+    if (!deposit) record(false);
     // Murray's algorithm overwrites its input and reads only its lower triangle
     double* work = amd::alloc_doubles(nn);
     amd::check(smg_copy_tril(c, n_, n_, L_->adj_, n_, work, n_), "cholesky_decompose");
@@ -236,15 +273,28 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   if (n == 0) return dev_var_matrix(new dev_matrix_vari(0, 0, dev_structure::lower));
   auto* L = new dev_matrix_vari(n, n, dev_structure::lower);
   L->aux_ = amd::alloc_doubles(size_t(smg_cholesky_aux_doubles(n)));
+  // the node's tape position once pushed (cholesky_dev_vari::pos_)
+  const size_t pos = ChainableStack::instance_->var_stack_.size();
+  double* inv_ws = nullptr;
+  if (internal::cholesky_dev_vari::closed_form_enabled() && internal::cholesky_dev_vari::predicted(pos, n))
+    inv_ws = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n));
   // check_symmetric fused with the factorisation's copy of A (one pass); the
   // status is read at the mark after the panels, so the block inverses that
   // follow run while the host builds the next node
-  amd::check(smg_cholesky_fwd_checked_mark(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
+  int inv_started = 0;
+  if (inv_ws)
+    amd::check(smg_cholesky_fwd_checked_mark_inv(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started), fn);
+  else
+    amd::check(smg_cholesky_fwd_checked_mark(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
   int st = 0;
   amd::check(smg_status_mark_wait(c, &st), fn);
   if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
   if (st) amd::throw_status(st, fn, "m");
-  new internal::cholesky_dev_vari(A.vi_, L);
+  auto* node = new internal::cholesky_dev_vari(A.vi_, L);
+  if (inv_started) {
+    node->ws_ = inv_ws;
+    node->v_ready_ = node->c_ready_ = true;
+  }
   return dev_var_matrix(L);
 }
 
