@@ -417,20 +417,23 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
  * smg_cholesky_inv_t_async forms V = L^{-T} in ws (with aux, n % 512 == 0,
  * n >= 1024; else *started = 0 and nothing is queued) on the context's side
  * stream after the work queued so far; smg_cholesky_mvn_rev_v (the same ws,
- * c_formed = 0) joins it, forms K^{-1} and applies the closed form.  smg_join_async and arena rewinds
+ * c_formed = 0) joins it, forms K^{-1} and applies the closed form.  With
+ * early_done (after smg_cholesky_fwd_checked_mark_inv) it forms the rest of V
+ * and K^{-1} itself (then c_formed = 1).  smg_join_async and arena rewinds
  * also join it. */
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
-                             double* ws, int* started);
+                             double* ws, int early_done, int* started);
 int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa,
                            double* ws, int c_formed);
-/* smg_cholesky_fwd_checked_mark that also forms V = L^{-T} and K^{-1} = V V^T
- * (lower) in ws (smg_cholesky_mvn_rev_ws_doubles(n)) on a second side stream:
- * the top half's part as soon as the first n/2 columns are factored
- * (overlapping the remaining panels), the rest after the last; *started = 1
- * when queued (n / 512 a power of two >= 2), then smg_cholesky_mvn_rev_v(...,
- * c_formed = 1) applies the closed form.  For a factor whose reverse is
- * predicted to take the closed form (the host layer's history per tape
- * position). */
+/* smg_cholesky_fwd_checked_mark that also queues the top half's part of
+ * V = L^{-T} (V11, V11 L21^T, with the top half's block inverses) into ws
+ * (smg_cholesky_mvn_rev_ws_doubles(n)) on the side stream as soon as the
+ * first n/2 columns are factored, in steps behind the remaining trailing
+ * updates; *started = 1 when queued (n / 512 a power of two >= 2).  Then
+ * smg_cholesky_inv_t_async(..., early_done = 1) queues the rest of V and
+ * K^{-1} = V V^T, and smg_cholesky_mvn_rev_v(..., c_formed = 1) applies the
+ * closed form.  For a factor whose reverse is predicted to take the closed
+ * form (the host layer's history per tape position). */
 int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                                       double* aux, double* ws, int* started);
 

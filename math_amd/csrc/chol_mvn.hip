@@ -19,6 +19,8 @@
 #include "smg_internal.h"
 #include "tri_small.h"
 
+#include <vector>
+
 namespace {
 
 // V[lo:hi, lo:hi] = L[lo:hi, lo:hi]^{-T} (upper) from the 512-row block
@@ -174,22 +176,68 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, doub
 
 }  // namespace
 
-// K^{-1} formed during the factorisation (cholesky.hip chol_fwd, on side2):
-// with h = n / 2, V = [[V11, V12], [0, V22]], V12 = -(V11 L21^T) V22.
+// K^{-1} formed partly during the factorisation (cholesky.hip chol_fwd): with
+// h = n / 2, V = [[V11, V12], [0, V22]], V12 = -(V11 L21^T) V22.
 bool smg_inv_split_ok(int n) {
   const int nl = n / SMG_NBR;
   return n % SMG_NBR == 0 && nl >= 2 && (nl & (nl - 1)) == 0;
 }
 
-// early (the first h columns of L and their block inverses final): V11, and
-// T = V11 L21^T into the C half of ws (ld n, rows 0..h)
-int smg_inv_early(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws) {
+// The early part as steps queued by chol_fwd behind the trailing updates on
+// `side`, a few per panel (cholesky.hip): the top half's block inverses, V11
+// (leaves and pairs, then every higher recursion node's two products), and
+// T = V11 L21^T in column slices.  T lives in the C half of ws (rows 0..h,
+// ld n); V11's own recursion workspace below row h.
+static void inv_nodes(int lo, int hi, bool pairs, std::vector<smg_inv_step>& out) {
+  if (hi - lo == SMG_NBR || (pairs && hi - lo == 2 * SMG_NBR)) return;
+  const int mid = lo + ((hi - lo) / SMG_NBR / 2) * SMG_NBR;
+  inv_nodes(lo, mid, pairs, out);
+  inv_nodes(mid, hi, pairs, out);
+  const double b = mid - lo, a = hi - mid;
+  out.push_back({2, lo, mid, hi, a * b * b});
+  out.push_back({3, lo, mid, hi, a * a * b});
+}
+
+std::vector<smg_inv_step> smg_inv_early_steps(int n) {
+  const int h = n / 2, nl = h / SMG_NBR;
+  const bool pairs = nl >= 2 && (nl & (nl - 1)) == 0;
+  std::vector<smg_inv_step> st;
+  st.push_back({0, 0, 0, 0, 2.0 * h * SMG_NBR * SMG_NBR});  // block inverses (latency-bound: weighted up)
+  st.push_back({1, 0, 0, 0, pairs ? 2.0 * (nl / 2) * 2.0 * SMG_NBR * SMG_NBR * SMG_NBR : 1e6});
+  inv_nodes(0, h, pairs, st);
+  const int slices = h >= 2048 ? 2 : 1;
+  for (int k = 0; k < slices; ++k) st.push_back({4, k * h / slices, (k + 1) * h / slices, 0, (double)h * h * h / slices});
+  return st;
+}
+
+int smg_inv_early_run(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, const smg_inv_step& s) {
   const int h = n / 2;
+  const size_t nn = (size_t)n * n;
   double* V = ws;
-  double* T = ws + (size_t)n * n;
-  int rc = form_v(ctx, L, ldl, aux, n, V, T + h, 0, h);  // (its own T below row h)
-  if (rc) return rc;
-  return smg_gemm_impl(ctx, 0, 1, 0, h, h, h, 1.0, V, n, L + h, ldl, 0.0, T, n, SMG_TRI_A_UPPER);
+  double* T = ws + nn;  // T (rows 0..h) | V11's recursion workspace (rows h..)
+  const double* w512 = aux + (size_t)n * SMG_AUX_W512;
+  switch (s.kind) {
+    case 0:
+      return smg_block_inverses_rows(ctx, L, ldl, aux, n, 0, h, T);
+    case 1: {
+      bool pairs = false;
+      return inv_t_leaves(ctx, L, ldl, w512, n, 0, h, V, n, T + h, &pairs);
+    }
+    case 2: {  // node (lo, mid, hi): T' = V11' L21'^T
+      const int lo = s.lo, mid = s.mid, hi = s.hi, b = mid - lo, a = hi - mid;
+      return smg_gemm_impl(ctx, 0, 1, 0, b, a, b, 1.0, V + lo + (size_t)lo * n, n, L + mid + (size_t)lo * ldl, ldl,
+                           0.0, T + h, n, SMG_TRI_A_UPPER);
+    }
+    case 3: {  // V12' = -T' V22'
+      const int lo = s.lo, mid = s.mid, hi = s.hi, b = mid - lo, a = hi - mid;
+      return smg_gemm_impl(ctx, 0, 0, 0, b, a, a, -1.0, T + h, n, V + mid + (size_t)mid * n, n, 0.0,
+                           V + lo + (size_t)mid * n, n, SMG_TRI_B_UPPER);
+    }
+    case 4:  // T[:, c0:c1] = V11 L21[c0:c1, :]^T
+      return smg_gemm_impl(ctx, 0, 1, 0, h, s.mid - s.lo, h, 1.0, V, n, L + h + s.lo, ldl, 0.0, T + (size_t)s.lo * n, n,
+                           SMG_TRI_A_UPPER);
+  }
+  return SMG_ERR_ARG;
 }
 
 // late (all of L and its block inverses): V22, V12 = -T V22 (or all of V when
@@ -240,10 +288,11 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
 }
 
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws,
-                             int* started) {
+                             int early_done, int* started) {
   if (!ctx || n < 0 || !started) return SMG_ERR_ARG;
   *started = 0;
   if (n == 0 || !v_by_doubling(n, aux)) return SMG_OK;
+  if (early_done && !smg_inv_split_ok(n)) return SMG_ERR_ARG;
   if (!L || !ws || ldl < n) return SMG_ERR_ARG;
   if (int rc = smg_side_begin(ctx)) return rc;
   if (int rc = smg_inv_events(ctx)) return rc;
@@ -253,7 +302,10 @@ int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const doubl
   int rc;
   {
     smg_on_side on(ctx);
-    rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);  // (V only: C in the reverse)
+    if (early_done)  // the rest of V and K^{-1} = V V^T
+      rc = smg_inv_late(ctx, L, ldl, aux, n, ws, true);
+    else  // V only: K^{-1} in the reverse (formed here it measured no faster)
+      rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);
   }
   if (rc) return rc;
   SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));

@@ -964,10 +964,37 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   static_assert(SMG_NBF <= PANEL_MAX_STEPS * SMG_NB, "panel width");
   const int NB2 = n > SMG_NBF ? SMG_NBF : n;
   const bool look = NB2 < n && smg_side_begin(ctx) == SMG_OK;
-  // K^{-1} on `side2` (the closed-form reverse under an MVN): the top half's
-  // part once its columns are final, overlapping the remaining panels
-  const bool inv = inv_ws && look && smg_inv_split_ok(n) && smg_side2_begin(ctx) == SMG_OK;
-  const bool early = inv && n / 2 % NB2 == 0;
+  // K^{-1} for the closed-form reverse under an MVN (chol_mvn.hip): once the
+  // first n/2 columns are final, the top half's part runs on `side` in steps
+  // behind each remaining trailing update (b), sized so each panel's side
+  // work still fits in the panel (one long stretch there delayed the next
+  // (b) and, through F, the main stream's next panel by ~0.4 ms)
+  const bool early = inv_ws && look && smg_inv_split_ok(n) && n / 2 % NB2 == 0 && smg_inv_events(ctx) == SMG_OK;
+  std::vector<smg_inv_step> steps;
+  size_t next_step = 0;
+  double steps_left = 0.0;
+  if (early) {
+    steps = smg_inv_early_steps(n);
+    for (const auto& st : steps) steps_left += st.flops;
+  }
+  // slots: the (b) launches from the one after panel n/2 on
+  auto slots_left = [&](int K) {
+    int c = 0;
+    for (int k = K; k + NB2 < n; k += NB2) ++c;
+    return c;
+  };
+  auto queue_steps = [&](double budget) -> int {  // on `side`, after what is queued there
+    smg_on_side on(ctx);
+    double done = 0.0;
+    while (next_step < steps.size() && (done == 0.0 || done + steps[next_step].flops <= budget * 1.25)) {
+      const smg_inv_step& st = steps[next_step++];
+      if (int rc = smg_inv_early_run(ctx, L, ldl, aux, n, inv_ws, st)) return rc;
+      if (st.kind == 0) SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->side));
+      done += st.flops;
+      steps_left -= st.flops;
+    }
+    return SMG_OK;
+  };
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
   for (int J = 0; J < n; J += NB2) {
@@ -991,13 +1018,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     }
     if (early && K == n / 2) {  // L's first n/2 columns are final after this panel
       SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
-      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->inv_ev_main, 0));
-      smg_on_side2 on(ctx);
-      const size_t nn = (size_t)n * n;
-      int rc = chol_block_inverses(ctx, L, ldl, aux, n, 0, n / 2, inv_ws + nn);
-      if (rc) return rc;
-      SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->side2));
-      if ((rc = smg_inv_early(ctx, L, ldl, aux, n, inv_ws))) return rc;
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
     }
     if (K >= n) break;
     const int m = n - K;
@@ -1031,7 +1052,19 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       F = smg_event(ctx, nev++);
       if (!F) return SMG_ERR_HIP;
       SMG_HIP_TRY(hipEventRecord(F, ctx->side));
+      if (early && K >= n / 2 && next_step < steps.size()) {  // this panel's share of the K^{-1} steps
+        const int slots = slots_left(K);
+        if ((rc = queue_steps(steps_left / (slots > 0 ? slots : 1)))) return rc;
+      }
     }
+  }
+  if (early) {  // (steps no slot took)
+    if (int rc = queue_steps(1e300)) return rc;
+    // their writes to ws are joined before anything on the main stream may
+    // touch ws (smg_join_async; the late part re-records it)
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
+    ctx->inv_pending = 1;
+    *inv_started = 1;
   }
   // every launch that can latch the status (the symmetric check, the panels'
   // not-PD and hand-off bits) is enqueued: the status mark goes here, so a
@@ -1042,21 +1075,10 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   }
   if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
   // the 128- and 256-block inverses (reverse pass, triangular solves); the
-  // top half's came from side2
+  // top half's are the first K^{-1} step on `side`
   int rc = early ? chol_block_inverses(ctx, L, ldl, aux, n, n / 2, n - n / 2) : chol_block_inverses(ctx, L, ldl, aux, n);
   if (rc) return rc;
   if (early) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
-  if (inv) {
-    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main2, ctx->stream));
-    SMG_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->inv_ev_main2, 0));
-    {
-      smg_on_side2 on(ctx);
-      if ((rc = smg_inv_late(ctx, L, ldl, aux, n, inv_ws, early))) return rc;
-    }
-    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side2));
-    ctx->inv_pending = 1;
-    *inv_started = 1;
-  }
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -101,17 +101,8 @@ int smg_side_begin(smg_ctx* ctx) {
   return SMG_OK;
 }
 
-int smg_side2_begin(smg_ctx* ctx) {
-  if (!ctx->side2 && hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking) != hipSuccess) {
-    ctx->side2 = nullptr;
-    ctx->host_status |= SMG_ERR_HIP;
-    return SMG_ERR_HIP;
-  }
-  return smg_inv_events(ctx);
-}
-
 int smg_inv_events(smg_ctx* ctx) {
-  for (hipEvent_t* e : {&ctx->inv_ev, &ctx->inv_ev_main, &ctx->inv_ev_main2, &ctx->inv_ev_aux})
+  for (hipEvent_t* e : {&ctx->inv_ev, &ctx->inv_ev_main, &ctx->inv_ev_aux})
     if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
       *e = nullptr;
       ctx->host_status |= SMG_ERR_HIP;
@@ -173,8 +164,7 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->zero_stream = nullptr;
   ctx->zero_ev_main = ctx->zero_ev_done = nullptr;
   ctx->zero_pending = 0;
-  ctx->inv_ev = ctx->inv_ev_main = ctx->inv_ev_main2 = ctx->inv_ev_aux = nullptr;
-  ctx->side2 = nullptr;
+  ctx->inv_ev = ctx->inv_ev_main = ctx->inv_ev_aux = nullptr;
   ctx->inv_pending = 0;
   ctx->side = nullptr;
   ctx->main_stream = nullptr;
@@ -242,11 +232,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
     hipStreamSynchronize(ctx->side);
     hipStreamDestroy(ctx->side);
   }
-  if (ctx->side2) {
-    hipStreamSynchronize(ctx->side2);
-    hipStreamDestroy(ctx->side2);
-  }
-  for (hipEvent_t e : {ctx->inv_ev, ctx->inv_ev_main, ctx->inv_ev_main2, ctx->inv_ev_aux})
+  for (hipEvent_t e : {ctx->inv_ev, ctx->inv_ev_main, ctx->inv_ev_aux})
     if (e) hipEventDestroy(e);
   for (int i = 0; i < SMG_WS_COUNT; ++i)
     if (ctx->ws[i]) hipFree(ctx->ws[i]);

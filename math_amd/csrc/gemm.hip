@@ -505,7 +505,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   double* slab = nullptr;
   if (splits > 1) {
     // the side stream has its own slab so concurrent split-K GEMMs never share one
-    slab = smg_ws(ctx, ctx->stream == ctx->side ? SMG_WS_GEMM_SIDE : (ctx->stream == ctx->side2 ? SMG_WS_GEMM_SIDE2 : SMG_WS_GEMM),
+    slab = smg_ws(ctx, ctx->stream == ctx->side ? SMG_WS_GEMM_SIDE : SMG_WS_GEMM,
                   (size_t)splits * m * n);
     if (!slab) return SMG_ERR_OOM;
   }

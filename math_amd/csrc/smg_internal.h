@@ -65,11 +65,8 @@ struct smg_ctx {
   // smg_cholesky_inv_t_async: L^{-T} formed on `side` while the main stream
   // runs the (latency-bound) MVN solves; `inv_ev` is recorded after it and
   // joined into `stream` by smg_cholesky_mvn_rev_v or smg_join_async
-  hipEvent_t inv_ev, inv_ev_main, inv_ev_main2, inv_ev_aux;
+  hipEvent_t inv_ev, inv_ev_main, inv_ev_aux;
   int inv_pending;
-  // second side stream (created lazily): K^{-1} formed during the factorisation
-  // (smg_cholesky_fwd_checked_mark_inv) without queueing behind the trailing updates on `side`
-  hipStream_t side2;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;
@@ -86,7 +83,7 @@ struct smg_ctx {
   long long done_seq;
   unsigned int* red_counter_d;  // last-block-done counter of the fused reductions (device, self-resetting)
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[11];  // SMG_WS_COUNT
+  double* ws[10];  // SMG_WS_COUNT
   size_t ws_doubles[10];
   // profiling
   int prof_on;
@@ -133,8 +130,7 @@ struct smg_prof_scope {
 enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_ALIAS = 4,
        SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_RHS = 8,
        SMG_WS_GLM = 9,  // the GLM parameters [alpha, beta] (not the Cholesky aux's TMP2)
-       SMG_WS_GEMM_SIDE2 = 10,  // split-K slabs of products issued on `side2`
-       SMG_WS_COUNT = 11 };
+       SMG_WS_COUNT = 10 };
 static_assert(SMG_WS_COUNT == sizeof(((smg_ctx*)nullptr)->ws) / sizeof(double*), "workspace slots");
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 // spin on the host-coherent completion word until it reaches seq (then the
@@ -143,7 +139,6 @@ extern "C" int smg_wait_done(smg_ctx* ctx, long long seq);
 
 // side-stream helpers (ctx.hip): events come from a per-context pool
 int smg_side_begin(smg_ctx* ctx);          // ensure `side` exists
-int smg_side2_begin(smg_ctx* ctx);         // ensure `side2` exists (and the inv_ev* events)
 int smg_inv_events(smg_ctx* ctx);          // ensure the inv_ev* events exist
 hipEvent_t smg_event(smg_ctx* ctx, int i); // i-th pooled event (grown on demand)
 // RAII: issue the enclosed launches on the side stream
@@ -155,18 +150,19 @@ struct smg_on_side {
   }
   ~smg_on_side() { ctx->stream = ctx->main_stream; }
 };
-struct smg_on_side2 {
-  smg_ctx* ctx;
-  hipStream_t saved;
-  explicit smg_on_side2(smg_ctx* c) : ctx(c), saved(c->stream) { ctx->stream = ctx->side2; }
-  ~smg_on_side2() { ctx->stream = saved; }
+// chol_mvn.hip: K^{-1} for the closed-form reverse, the top half's part
+// formed during the factorisation; ws = [V | C] (2 n^2 doubles).  Early
+// steps (kind 0: the top half's block inverses, 1: V11's leaves and pairs,
+// 2 / 3: a recursion node's two products, 4: a column slice of V11 L21^T)
+// are queued by chol_fwd behind the trailing updates on `side`; late: V22,
+// V12 and C = V V^T (smg_cholesky_inv_t_async with early_done)
+struct smg_inv_step {
+  int kind, lo, mid, hi;
+  double flops;
 };
-// chol_mvn.hip: K^{-1} for the closed-form reverse, formed during the
-// factorisation; ws = [V | C] (2 n^2 doubles).  early: V11 (the top half's
-// inverse) and V11 L21^T, once the top half's columns are final; late: V22,
-// V12 and C = V V^T (after the factorisation and its block inverses)
 bool smg_inv_split_ok(int n);
-int smg_inv_early(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws);
+std::vector<smg_inv_step> smg_inv_early_steps(int n);
+int smg_inv_early_run(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, const smg_inv_step& s);
 int smg_inv_late(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws, bool early);
 // block inverses of the rows [row0, row0 + nrows) (multiples of 512), T: a
 // workspace (NULL: SMG_WS_TMP)

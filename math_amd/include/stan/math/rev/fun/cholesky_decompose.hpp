@@ -98,8 +98,9 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   double dep_adj_ = 0.0;
   size_t dep_sweep_ = 0;
   double* ws_ = nullptr;  // smg_cholesky_mvn_rev's workspace [V = L^{-T}, K^{-1}]
-  bool v_ready_ = false;  // V formed (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
-  bool c_ready_ = false;  // and K^{-1} (formed during the factorisation)
+  bool early_ = false;    // the factorisation queued K^{-1}'s top-half steps into ws_
+  bool v_ready_ = false;  // V queued (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
+  bool c_ready_ = false;  // and K^{-1} (after early_)
 
   /** Which factorisations took the closed-form reverse last time, by tape
    * position and size: a sampler re-runs the same program every gradient, so
@@ -144,19 +145,22 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     L->sink_ = this;
   }
 
-  // L^{-T} is formed while the MVN's forward solves run (they are
-  // latency-bound: most CUs idle); unused if the reverse takes the dense path
+  // L^{-T} (and K^{-1} when the factorisation queued its top half) is formed
+  // on the side stream from the MVN's forward on, queued behind the MVN's
+  // latency-bound solves so that they are not starved of CUs; unused if the
+  // reverse takes the dense path
   void prepare_mvn_adjoint() override {
     static const bool async = [] {  // SMG_CHOL_MVN_ASYNC=0: V formed in the reverse (A/B)
       const char* e = std::getenv("SMG_CHOL_MVN_ASYNC");
       return !(e && e[0] == '0');
     }();
-    if (!closed_form_enabled() || !async || ws_) return;
-    ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
+    if (!closed_form_enabled() || !async || v_ready_) return;
+    if (!ws_) ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
     int started = 0;
-    amd::check(smg_cholesky_inv_t_async(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, &started),
+    amd::check(smg_cholesky_inv_t_async(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, early_ ? 1 : 0, &started),
                "multi_normal_cholesky_lpdf");
     v_ready_ = started != 0;
+    c_ready_ = v_ready_ && early_;
   }
 
   bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) override {
@@ -293,7 +297,7 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   auto* node = new internal::cholesky_dev_vari(A.vi_, L);
   if (inv_started) {
     node->ws_ = inv_ws;
-    node->v_ready_ = node->c_ready_ = true;
+    node->early_ = true;
   }
   return dev_var_matrix(L);
 }

@@ -102,8 +102,8 @@ inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const 
   amd::check(smg_memset(c, lp_d + 1, 0, 2 * sizeof(double)), fn);
   if (mu_d) amd::check(smg_check_domain(c, mu_d, n, 1, lp_d + 1), fn);
   amd::check(smg_check_domain(c, y_d, n, 0, lp_d + 2), fn);
-  if (L.vi_->sink_) L.vi_->sink_->prepare_mvn_adjoint();  // (overlaps the solves below)
   amd::check(smg_mvn_cholesky_fwd(c, y_d, mu_d, L.val_ptr(), n, L.vi_->aux_, n, ws, lp_d), fn);
+  if (L.vi_->sink_) L.vi_->sink_->prepare_mvn_adjoint();  // (behind the solves: overlaps their tail and the host)
   double out[3] = {0, 0, 0};
   amd::to_host(out, lp_d, 3);
   if (out[1] != 0.0 || out[2] != 0.0) {  // error path: the values on the host, the reference's message
@@ -178,10 +178,10 @@ inline vari* mvn_cholesky_multi(const dev_operand& L, const double* aux, bool lo
   smg_ctx* c = amd::ctx();
   double* ws = amd::alloc_doubles(2 * size_t(n) * size_t(k) + size_t(k));
   double* lp_d = ws + 2 * size_t(n) * size_t(k);
-  if (k == 1 && lower_only && L.vi && L.vi->sink_) L.vi->sink_->prepare_mvn_adjoint();  // (overlaps the solves)
   for (int i = 0; i < k; ++i)
     amd::check(smg_mvn_cholesky_fwd(c, obs[i].y, obs[i].mu, L.val(), n, aux, n, ws + 2 * size_t(n) * i, lp_d + i),
                fn);
+  if (k == 1 && lower_only && L.vi && L.vi->sink_) L.vi->sink_->prepare_mvn_adjoint();  // (behind the solves)
   std::vector<double> lps(static_cast<size_t>(k));
   amd::to_host(lps.data(), lp_d, lps.size());
   double lp = 0.0;
