@@ -162,7 +162,8 @@ class GP(Workload):
 
     data = "synthetic (reference harness config-3 inputs: x~U(-10,10), y=sin(x)+0.3eps; theta=(1,1.5,0.3))"
 
-    eval_flops_expr = "N^3 (chol fwd N^3/3 + Murray adjoint 2N^3/3), SURVEY.md §8(d)"
+    eval_flops_expr = ("N^3 (chol fwd N^3/3 + its adjoint 2N^3/3: Murray's, or under the MVN its closed form "
+                       "V = L^-T N^3/3 + V V^T N^3/3), SURVEY.md §8(d)")
 
     def eval_flops(self):
         return float(self.N) ** 3
@@ -642,6 +643,9 @@ def main():
     t = timed(args.steps)
     value = args.steps * wl.units_per_step() / t
     ms_per_step = 1e3 * t / args.steps
+    ok, msg = wl.guard()  # and on the last timed step
+    if not ok:
+        raise SystemExit(f"parity failure after the timed steps: {msg}")
 
     # profiled copy of the timed region: HIP events on the context stream
     lib.smg_profile_enable(ctx, 1)
