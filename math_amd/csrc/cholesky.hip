@@ -1079,6 +1079,25 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   int rc = early ? chol_block_inverses(ctx, L, ldl, aux, n, n / 2, n - n / 2) : chol_block_inverses(ctx, L, ldl, aux, n);
   if (rc) return rc;
   if (early) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
+  // the rest of K^{-1} queued here, overlapping the MVN's forward solves and
+  // the host's work up to the reverse (*inv_started = 2); same-box A/B
+  // against queueing it behind the solves: 3.00 vs 3.18 ms per GP gradient
+  // (SMG_LATE_AT_FWD=0 restores that)
+  static const bool late_here = [] {
+    const char* e = getenv("SMG_LATE_AT_FWD");
+    return !(e && e[0] == '0');
+  }();
+  if (early && late_here) {
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
+    SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
+    {
+      smg_on_side on(ctx);
+      if ((rc = smg_inv_late(ctx, L, ldl, aux, n, inv_ws, true))) return rc;
+    }
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
+    ctx->inv_pending = 1;
+    *inv_started = 2;
+  }
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -110,15 +110,18 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     static thread_local std::vector<std::pair<std::pair<size_t, int>, bool>> h;
     return h;
   }
+  // 1: took the closed form last time, 0: did not, -1: no record
+  static int history_of(size_t pos, int n) {
+    for (const auto& e : history())
+      if (e.first.first == pos && e.first.second == n) return e.second ? 1 : 0;
+    return -1;
+  }
   static bool predicted(size_t pos, int n) {
     static const bool on = [] {  // SMG_CHOL_INV_FWD=0: K^{-1} never formed with the panels (A/B)
       const char* e = std::getenv("SMG_CHOL_INV_FWD");
       return !(e && e[0] == '0');
     }();
-    if (!on) return false;
-    for (const auto& e : history())
-      if (e.first.first == pos && e.first.second == n) return e.second;
-    return false;
+    return on && history_of(pos, n) == 1;
   }
   void record(bool closed) const {
     auto& h = history();
@@ -155,6 +158,9 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       return !(e && e[0] == '0');
     }();
     if (!closed_form_enabled() || !async || v_ready_) return;
+    // (a factor whose adjoint had other writers last time -- the HVP's value
+    // factor feeds the tangent nodes too -- would form V for nothing)
+    if (history_of(pos_, n_) == 0) return;
     if (!ws_) ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
     int started = 0;
     amd::check(smg_cholesky_inv_t_async(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws_, early_ ? 1 : 0, &started),
@@ -298,6 +304,7 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   if (inv_started) {
     node->ws_ = inv_ws;
     node->early_ = true;
+    node->v_ready_ = node->c_ready_ = inv_started == 2;  // (all of K^{-1} queued already)
   }
   return dev_var_matrix(L);
 }
