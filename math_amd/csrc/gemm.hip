@@ -718,9 +718,13 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
     static const bool log = getenv("SMG_GEMM_LOG") != nullptr;
     if (log) fprintf(stderr, "gemm ta=%d tb=%d uplo=%d m=%d n=%d k=%d tri=%d\n", ta, tb, uplo, m, n, k, tri);
   }
-  if (ctx->prof_on)
+  if (ctx->prof_on) {
+    // the K cuts of triangular operands execute about half (one) or a third
+    // (two, as in V V^T with a triangle output) of the dense count
+    const double cut = (tri & 3) && (tri & 12) ? 1.0 / 3.0 : (tri ? 0.5 : 1.0);
     ctx->prof_flops[SMG_FAM_GEMM] +=
-        uplo ? 2.0 * k * ((double)m * n - (double)n * (n - 1) / 2) : 2.0 * m * n * k;
+        cut * (uplo ? 2.0 * k * ((double)m * n - (double)n * (n - 1) / 2) : 2.0 * m * n * k);
+  }
   if (uplo == 1) {
     if (!ta && tb) return dispatch_tile<false, true, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
     if (ta && !tb) return dispatch_tile<true, false, 1>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);

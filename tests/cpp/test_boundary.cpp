@@ -11,6 +11,7 @@
 //                                                        device <-> Eigen round trip
 //   chol_nan_arena N                                     cholesky gradient after NaN-poisoned arena
 #include <stan/math.hpp>
+#include <algorithm>
 
 #include <chrono>
 #include <cmath>
@@ -195,6 +196,49 @@ static void cmd_chol_nan_arena() {
   std::printf("diff_entries %zu\n", diff);
 }
 
+// The closed-form Cholesky reverse under an MVN across evaluations at one
+// tape position (rev/fun/cholesky_decompose.hpp): evaluation 1 takes it
+// unpredicted, 2 with K^{-1} formed alongside the factorisation (history),
+// 3 fails in the factorisation (not positive definite) with that work queued,
+// 4 must again equal 1.  Prints the max relative difference of 2 and 4 from 1
+// and whether 3 threw the reference's domain_error.
+static void cmd_chol_mvn_predicted() {
+  int N;
+  std::cin >> N;
+  std::vector<double> a(size_t(N) * N), bad, y(N);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) a[size_t(j) * N + i] = (i == j ? 2.0 : 0.0) + std::cos(0.37 * (i - j)) * 0.5;
+  for (int i = 0; i < N; ++i) y[i] = std::sin(0.1 * i);
+  bad = a;
+  bad[size_t(N / 2) * N + N / 2] = -1.0;  // a negative pivot in the second half
+  auto run = [&](const std::vector<double>& m) {
+    start_nested();
+    std::vector<double> g;
+    try {
+      dev_var_matrix A = to_dev_var_matrix(m.data(), N, N);
+      var f = multi_normal_cholesky_lpdf(to_dev_data(y), cholesky_decompose(A));
+      f.grad();
+      g = A.adj();
+      g.push_back(f.val());
+    } catch (const std::domain_error&) {
+      g.clear();
+    }
+    recover_memory_nested();
+    return g;
+  };
+  std::vector<double> g1 = run(a), g2 = run(a), g3 = run(bad), g4 = run(a);
+  auto rel = [&](const std::vector<double>& u) {
+    double m = 0.0, s = 0.0;
+    for (double v : g1) s = std::max(s, std::fabs(v));
+    for (size_t i = 0; i < u.size(); ++i) m = std::max(m, std::fabs(u[i] - g1[i]) / s);
+    return m;
+  };
+  std::printf("rel2 %.3e\n", rel(g2));
+  std::printf("threw3 %d\n", g3.empty() ? 1 : 0);
+  std::printf("rel4 %.3e\n", rel(g4));
+  std::printf("finite %d\n", std::all_of(g4.begin(), g4.end(), [](double v) { return std::isfinite(v); }) ? 1 : 0);
+}
+
 int main() {
   std::string cmd;
   while (std::cin >> cmd) {
@@ -203,6 +247,7 @@ int main() {
     else if (cmd == "gp_nd") cmd_gp_nd();
     else if (cmd == "bridge") cmd_bridge();
     else if (cmd == "chol_nan_arena") cmd_chol_nan_arena();
+    else if (cmd == "chol_mvn_predicted") cmd_chol_mvn_predicted();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;

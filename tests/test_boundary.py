@@ -130,3 +130,16 @@ def test_cholesky_gradient_after_nan_poisoned_arena():
     r = _parse(_run("chol_nan_arena 1100\n"))
     assert r["nan_entries"][0] == 0
     assert r["diff_entries"][0] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1024, 2048])
+def test_cholesky_mvn_closed_form_predicted_across_failure(N):
+    """The closed-form Cholesky reverse under an MVN at one tape position:
+    evaluation 2 forms K^{-1} alongside the factorisation (the history says
+    the closed form), 3 fails with a not-positive-definite input while that
+    work is queued, 4 runs normally again -- 2 and 4 equal the unpredicted 1."""
+    r = _parse(_run(f"chol_mvn_predicted {N}\n"))
+    assert r["threw3"][0] == 1
+    assert r["finite"][0] == 1
+    assert r["rel2"][0] < 1e-12 and r["rel4"][0] < 1e-12
