@@ -51,6 +51,11 @@ class structured_adjoint_sink {
   /** Called by such a consumer's forward pass before its own device work:
    * the node may start, on a side stream, what that reverse will need. */
   virtual void prepare_mvn_adjoint() {}
+  /** Before the node's own device adjoint is read (dev_var_matrix::adj()):
+   * write the structured contribution of the last sweep into it densely, so
+   * that it holds what the reference's varis would (the closed form never
+   * formed it). */
+  virtual void expand_adjoint() {}
 };
 
 class dev_matrix_vari {
@@ -106,6 +111,7 @@ class dev_var_matrix {
   }
   /** Column-major host copy of the adjoints (synchronising). */
   std::vector<double> adj() const {
+    if (vi_->sink_) vi_->sink_->expand_adjoint();
     join_device_adjoints();
     std::vector<double> h(size());
     amd::to_host(h.data(), vi_->adj_, size());

@@ -101,6 +101,11 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   bool early_ = false;    // the factorisation queued K^{-1}'s top-half steps into ws_
   bool v_ready_ = false;  // V queued (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
   bool c_ready_ = false;  // and K^{-1} (after early_)
+  // the closed form applied these MVN partials without writing L's dense
+  // adjoint (expand_adjoint writes them if L's adjoint is read)
+  const double* exp_ws_ = nullptr;
+  double exp_adj_ = 0.0;
+  size_t exp_sweep_ = 0;
 
   /** Which factorisations took the closed-form reverse last time, by tape
    * position and size: a sampler re-runs the same program every gradient, so
@@ -180,6 +185,24 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     return true;
   }
 
+  void expand_adjoint() override {
+    auto* st = ChainableStack::instance_;
+    const double* ws = nullptr;
+    double adj = 0.0;
+    if (dep_owner_ && dep_sweep_ == st->sweep_) {  // deposited, and this node was not chained
+      ws = dep_ws_;
+      adj = dep_adj_;
+      dep_owner_ = nullptr;
+    } else if (exp_ws_ && exp_sweep_ == st->sweep_) {  // consumed by the closed form
+      ws = exp_ws_;
+      adj = exp_adj_;
+      exp_ws_ = nullptr;
+    }
+    if (ws)
+      amd::check(smg_mvn_cholesky_rev(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws, adj, 1, nullptr, nullptr, L_->adj_, n_),
+                 "cholesky_decompose");
+  }
+
   void chain() override {
     smg_ctx* c = amd::ctx();
     auto* st = ChainableStack::instance_;
@@ -195,6 +218,9 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       }
       record(!dense);
       if (!dense) {
+        exp_ws_ = dep_ws_;
+        exp_adj_ = dep_adj_;
+        exp_sweep_ = st->sweep_;
         if (v_ready_) {
           amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_, c_ready_ ? 1 : 0),
                      "cholesky_decompose");

@@ -239,6 +239,33 @@ static void cmd_chol_mvn_predicted() {
   std::printf("finite %d\n", std::all_of(g4.begin(), g4.end(), [](double v) { return std::isfinite(v); }) ? 1 : 0);
 }
 
+// The factor's own adjoint after a sweep whose Cholesky reverse took the
+// closed form (never forming it): read through dev_var_matrix::adj() it must
+// still hold the MVN's partials, as the reference's varis would.  Prints
+// [sum, sum of squares] of L's and A's adjoints.
+static void cmd_chol_mvn_ladj() {
+  int N;
+  std::cin >> N;
+  std::vector<double> a(size_t(N) * N), y(N);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) a[size_t(j) * N + i] = (i == j ? 2.0 : 0.0) + std::cos(0.37 * (i - j)) * 0.5;
+  for (int i = 0; i < N; ++i) y[i] = std::sin(0.1 * i);
+  start_nested();
+  dev_var_matrix A = to_dev_var_matrix(a.data(), N, N);
+  dev_var_matrix L = cholesky_decompose(A);
+  var f = multi_normal_cholesky_lpdf(to_dev_data(y), L);
+  f.grad();
+  for (const auto& v : {L.adj(), A.adj()}) {
+    double s = 0.0, q = 0.0;
+    for (double x : v) {
+      s += x;
+      q += x * x;
+    }
+    std::printf("adj %.17g %.17g\n", s, q);
+  }
+  recover_memory_nested();
+}
+
 int main() {
   std::string cmd;
   while (std::cin >> cmd) {
@@ -248,6 +275,7 @@ int main() {
     else if (cmd == "bridge") cmd_bridge();
     else if (cmd == "chol_nan_arena") cmd_chol_nan_arena();
     else if (cmd == "chol_mvn_predicted") cmd_chol_mvn_predicted();
+    else if (cmd == "chol_mvn_ladj") cmd_chol_mvn_ladj();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;

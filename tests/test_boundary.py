@@ -20,8 +20,9 @@ BIN = os.path.join(ROOT, "tests", "cpp", "_bin", "test_boundary")
 RTOL = 1e-10
 
 
-def _run(stdin, timeout=600):
-    p = subprocess.run([BIN], input=stdin, capture_output=True, text=True, timeout=timeout)
+def _run(stdin, timeout=600, env=None):
+    e = None if env is None else {**os.environ, **env}
+    p = subprocess.run([BIN], input=stdin, capture_output=True, text=True, timeout=timeout, env=e)
     assert p.returncode == 0, p.stderr[-3000:]
     return p.stdout
 
@@ -143,3 +144,17 @@ def test_cholesky_mvn_closed_form_predicted_across_failure(N):
     assert r["threw3"][0] == 1
     assert r["finite"][0] == 1
     assert r["rel2"][0] < 1e-12 and r["rel4"][0] < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [300, 1024])
+def test_cholesky_factor_adjoint_readable_after_closed_form(N):
+    """After a sweep whose Cholesky reverse took the closed form (L's dense
+    adjoint never formed), L.adj() still returns the MVN's partials, and A's
+    adjoint is unchanged: equal to the dense path's (SMG_CHOL_MVN_CLOSED_FORM=0)."""
+    def rows(env):
+        out = _run(f"chol_mvn_ladj {N}\n", env=env)
+        return np.array([[float(v) for v in l.split()[1:]] for l in out.strip().splitlines()])
+    a, b = rows(None), rows({"SMG_CHOL_MVN_CLOSED_FORM": "0"})
+    near_rel(a, b, 1e-11, what="L / A adjoint sums")
+    assert abs(a[0, 0]) > 0
