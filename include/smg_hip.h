@@ -407,12 +407,15 @@ int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
  * factor (the Ladj above with lower_only = 1: adj (tril(s w^T) - diag(1/L_ii)),
  * s = ws + n of smg_mvn_cholesky_fwd), in closed form:
  *   Aadj (lower) += adj Phi(s s^T - K^{-1}),  K^{-1} = L^{-T} L^{-1}
- * (Phi: strict lower + half diagonal).  aux: the factor's smg_cholesky_fwd
+ * (Phi: strict lower + half diagonal); k observations sharing L (the array
+ * form, s_o = s + o s_stride): adj Phi(sum_o s_o s_o^T - k K^{-1}).  aux: the
+ * factor's smg_cholesky_fwd
  * block inverses (NULL: a blocked solve forms L^{-1}).  ws: at least
  * smg_cholesky_mvn_rev_ws_doubles(n) doubles. */
 size_t smg_cholesky_mvn_rev_ws_doubles(int n);
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
-                         const double* s, double adj, double* Aadj, int ldaa, double* ws);
+                         const double* s, int k, long long s_stride, double adj, double* Aadj, int ldaa,
+                         double* ws);
 /* The same in two parts, the first overlapping the MVN's forward solves:
  * smg_cholesky_inv_t_async forms V = L^{-T} in ws (with aux, n % 512 == 0,
  * n >= 1024; else *started = 0 and nothing is queued) on the context's side
@@ -423,8 +426,8 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
  * also join it. */
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                              double* ws, int early_done, int* started);
-int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa,
-                           double* ws, int c_formed);
+int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long long s_stride, double adj,
+                           double* Aadj, int ldaa, double* ws, int c_formed);
 /* smg_cholesky_fwd_checked_mark that also queues the top half's part of
  * V = L^{-T} (V11, V11 L21^T, with the top half's block inverses) into ws
  * (smg_cholesky_mvn_rev_ws_doubles(n)) on the side stream as soon as the
