@@ -72,6 +72,12 @@ void* smg_host_scratch(smg_ctx* ctx, size_t bytes);
  * of the *_fused entries; coarse-grained: the kernels publish it with one
  * system-scope release); grown on demand, reused by the next call */
 void* smg_pinned_io(smg_ctx* ctx, size_t bytes);
+/* pinned host memory mapped into the device, fine-grained (coherent): every
+ * kernel store reaches the host without relying on a cache write-back, so
+ * the host may read it as soon as the completion word moves.  For small
+ * results published by the zero-copy reducer steps (the GLM's M + 3 sums);
+ * grown on demand, reused by the next call. */
+void* smg_pinned_result(smg_ctx* ctx, size_t bytes);
 /* dst (pinned host memory from smg_pinned_io) <- n device doubles of src, in
  * stream order, written by a one-workgroup kernel that then publishes a
  * completion word; returns once they have landed (no copy-engine transfer,
@@ -407,12 +413,15 @@ int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
  * factor (the Ladj above with lower_only = 1: adj (tril(s w^T) - diag(1/L_ii)),
  * s = ws + n of smg_mvn_cholesky_fwd), in closed form:
  *   Aadj (lower) += adj Phi(s s^T - K^{-1}),  K^{-1} = L^{-T} L^{-1}
- * (Phi: strict lower + half diagonal).  aux: the factor's smg_cholesky_fwd
+ * (Phi: strict lower + half diagonal); k observations sharing L (the array
+ * form, s_o = s + o s_stride): adj Phi(sum_o s_o s_o^T - k K^{-1}).  aux: the
+ * factor's smg_cholesky_fwd
  * block inverses (NULL: a blocked solve forms L^{-1}).  ws: at least
  * smg_cholesky_mvn_rev_ws_doubles(n) doubles. */
 size_t smg_cholesky_mvn_rev_ws_doubles(int n);
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
-                         const double* s, double adj, double* Aadj, int ldaa, double* ws);
+                         const double* s, int k, long long s_stride, double adj, double* Aadj, int ldaa,
+                         double* ws);
 /* The same in two parts, the first overlapping the MVN's forward solves:
  * smg_cholesky_inv_t_async forms V = L^{-T} in ws (with aux, n % 512 == 0,
  * n >= 1024; else *started = 0 and nothing is queued) on the context's side
@@ -423,8 +432,8 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
  * also join it. */
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                              double* ws, int early_done, int* started);
-int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa,
-                           double* ws, int c_formed);
+int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long long s_stride, double adj,
+                           double* Aadj, int ldaa, double* ws, int c_formed);
 /* smg_cholesky_fwd_checked_mark that also queues the top half's part of
  * V = L^{-T} (V11, V11 L21^T, with the top half's block inverses) into ws
  * (smg_cholesky_mvn_rev_ws_doubles(n)) on the side stream as soon as the
@@ -555,6 +564,18 @@ int smg_copy_matrix(smg_ctx* ctx, int m, int n, const double* A, int lda,
  * lower one (multiply(A, transpose(A)) forms the lower half of the Gram
  * product on the GEMM, then mirrors it). */
 int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda);
+/* The Eigen boundary's packed lower triangle (column-major: column j's rows
+ * j..n-1 at offset j n - j (j - 1) / 2; n (n + 1) / 2 doubles), the layout of
+ * the host varis of a cholesky_decompose factor (its strict upper triangle is
+ * one dummy vari, rev/mat/fun/cholesky_decompose.hpp:34-48) and of a
+ * gp_exp_quad_cov matrix (K(i, j) and K(j, i) share one vari,
+ * rev/mat/fun/gp_exp_quad_cov.hpp:235).  pack: mode 0 dst <- tril(A);
+ * mode 1 dst <- tril(A) + strict tril(A^T) (the shared vari's adjoint);
+ * mode 2 dst[i] <- A_ii (n doubles: add_diag's own varis,
+ * prim/mat/fun/add_diag.hpp:25-27).  unpack_tril_add: modes 0 / 1
+ * tril(A) += unpack(src), mode 2 A_ii += src[i]. */
+int smg_pack_tril(smg_ctx* ctx, int mode, int n, const double* A, int lda, double* dst);
+int smg_unpack_tril_add(smg_ctx* ctx, int mode, int n, const double* src, double* A, int lda);
 /* B (n x m) = A^T + beta B, A m x n (transpose(Matrix<var>): forward copy and
  * the reverse Aadj += Badj^T) */
 int smg_transpose(smg_ctx* ctx, int m, int n, const double* A, int lda,

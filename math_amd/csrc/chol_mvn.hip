@@ -89,54 +89,70 @@ int inv_t_leaves(smg_ctx* ctx, const double* L, int ldl, const double* w512, int
                                V + lo + (size_t)(lo + b) * ldv, ldv, sv, np);
 }
 
-// Abar(i, j) += adj ((s_i s_j - C_ij) * (i == j ? 1/2 : 1)), i >= j, C lower;
-// the column form of k_add_lower_col2 (16-byte accesses, whole columns per
-// workgroup, only the row pairs at or below the diagonal touched)
+// Abar(i, j) += adj ((sum_o s_oi s_oj - k C_ij) * (i == j ? 1/2 : 1)), i >= j,
+// C lower; s_o = s + o * ss (k observations); the column form of
+// k_add_lower_col2 (16-byte accesses, whole columns per workgroup, only the
+// row pairs at or below the diagonal touched)
 __global__ __launch_bounds__(256) void k_chol_mvn_adj_col2(const double* __restrict__ C, int ldc, int n,
-                                                          const double* __restrict__ s, double adj,
-                                                          double* __restrict__ A, int lda) {
+                                                          const double* __restrict__ s, int k, long long ss,
+                                                          double adj, double* __restrict__ A, int lda) {
   const int np = n >> 1;
-  const double2* s2 = reinterpret_cast<const double2*>(s);
+  const double kc = adj * k;
   for (int j = blockIdx.x; j < n; j += gridDim.x) {
     const double2* c = reinterpret_cast<const double2*>(C + (size_t)j * ldc);
     double2* a = reinterpret_cast<double2*>(A + (size_t)j * lda);
-    const double sj = adj * s[j];
     const int p1 = j >> 1;  // first pair holding a row >= j
     for (int p0 = p1 + threadIdx.x; p0 < np; p0 += 4 * 256) {
-      double2 cv[4], av[4], sv[4];
+      double2 cv[4], av[4], gv[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int p = p0 + 256 * k;
+      for (int q = 0; q < 4; ++q) {
+        const int p = p0 + 256 * q;
+        gv[q] = double2{0.0, 0.0};
         if (p < np) {
-          cv[k] = c[p];
-          av[k] = a[p];
-          sv[k] = s2[p];
+          cv[q] = c[p];
+          av[q] = a[p];
+        }
+      }
+      for (int o = 0; o < k; ++o) {
+        const double* so = s + o * ss;
+        const double2* s2 = reinterpret_cast<const double2*>(so);
+        const double sj = adj * so[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int p = p0 + 256 * q;
+          if (p < np) {
+            const double2 sv = s2[p];
+            gv[q].x += sv.x * sj;
+            gv[q].y += sv.y * sj;
+          }
         }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int p = p0 + 256 * k;
+      for (int q = 0; q < 4; ++q) {
+        const int p = p0 + 256 * q;
         if (p < np) {
           const int r = 2 * p;
-          const double gx = sv[k].x * sj - adj * cv[k].x;
-          const double gy = sv[k].y * sj - adj * cv[k].y;
-          if (r > j) av[k].x += gx;
-          else if (r == j) av[k].x += 0.5 * gx;
-          if (r + 1 > j) av[k].y += gy;  // row 2p + 1 >= j for every p >= j / 2
-          else av[k].y += 0.5 * gy;
-          a[p] = av[k];
+          const double gx = gv[q].x - kc * cv[q].x;
+          const double gy = gv[q].y - kc * cv[q].y;
+          if (r > j) av[q].x += gx;
+          else if (r == j) av[q].x += 0.5 * gx;
+          if (r + 1 > j) av[q].y += gy;  // row 2p + 1 >= j for every p >= j / 2
+          else av[q].y += 0.5 * gy;
+          a[p] = av[q];
         }
       }
     }
   }
 }
 
-__global__ void k_chol_mvn_adj(const double* __restrict__ C, int ldc, int n, const double* __restrict__ s,
-                               double adj, double* __restrict__ A, int lda) {
+__global__ void k_chol_mvn_adj(const double* __restrict__ C, int ldc, int n, const double* __restrict__ s, int k,
+                               long long ss, double adj, double* __restrict__ A, int lda) {
   for (smg_mn it(n, n); it.ok(); it.next()) {
     const int i = it.i, j = it.j;
     if (i < j) continue;
-    const double g = adj * (s[i] * s[j] - C[i + (size_t)j * ldc]);
+    double g = 0.0;
+    for (int o = 0; o < k; ++o) g += s[o * ss + i] * s[o * ss + j];
+    g = adj * (g - k * C[i + (size_t)j * ldc]);
     A[i + (size_t)j * lda] += (i == j) ? 0.5 * g : g;
   }
 }
@@ -160,16 +176,17 @@ int form_v(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, dou
 
 bool v_by_doubling(int n, const double* aux) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR && aux; }
 
-// Abar (lower) += adj Phi(s s^T - C), C = K^{-1} lower
-int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, double adj, double* Aadj, int ldaa) {
-  if (n % 2 == 0 && ldaa % 2 == 0 &&
+// Abar (lower) += adj Phi(sum_o s_o s_o^T - k C), C = K^{-1} lower
+int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int k, long long ss, double adj,
+                     double* Aadj, int ldaa) {
+  if (n % 2 == 0 && ldaa % 2 == 0 && ss % 2 == 0 &&
       ((reinterpret_cast<uintptr_t>(Aadj) | reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(C)) & 15) ==
           0)
-    hipLaunchKernelGGL(k_chol_mvn_adj_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, C, n, n, s, adj,
-                       Aadj, ldaa);
+    hipLaunchKernelGGL(k_chol_mvn_adj_col2, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, C, n, n, s, k, ss,
+                       adj, Aadj, ldaa);
   else
-    hipLaunchKernelGGL(k_chol_mvn_adj, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, C, n, n, s, adj,
-                       Aadj, ldaa);
+    hipLaunchKernelGGL(k_chol_mvn_adj, dim3(grid_for((long long)n * n)), dim3(256), 0, ctx->stream, C, n, n, s, k, ss,
+                       adj, Aadj, ldaa);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
@@ -263,9 +280,9 @@ extern "C" {
 
 size_t smg_cholesky_mvn_rev_ws_doubles(int n) { return n > 0 ? 2 * (size_t)n * n : 0; }
 
-int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s,
-                         double adj, double* Aadj, int ldaa, double* ws) {
-  if (!ctx || n < 0) return SMG_ERR_ARG;
+int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s, int k,
+                         long long s_stride, double adj, double* Aadj, int ldaa, double* ws) {
+  if (!ctx || n < 0 || k < 1 || (k > 1 && s_stride < n)) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   if (!L || !s || !Aadj || !ws || ldl < n || ldaa < n) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
@@ -284,7 +301,7 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
     rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
   }
   if (rc) return rc;
-  return mvn_adj_epilogue(ctx, C, n, s, adj, Aadj, ldaa);
+  return mvn_adj_epilogue(ctx, C, n, s, k, s_stride, adj, Aadj, ldaa);
 }
 
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws,
@@ -314,9 +331,9 @@ int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const doubl
   return SMG_OK;
 }
 
-int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, double* Aadj, int ldaa, double* ws,
-                           int c_formed) {
-  if (!ctx || n < 0) return SMG_ERR_ARG;
+int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long long s_stride, double adj, double* Aadj,
+                           int ldaa, double* ws, int c_formed) {
+  if (!ctx || n < 0 || k < 1 || (k > 1 && s_stride < n)) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   if (!s || !Aadj || !ws || ldaa < n) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
@@ -330,7 +347,7 @@ int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, double adj, dou
     int rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, ws, n, ws, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
     if (rc) return rc;
   }
-  return mvn_adj_epilogue(ctx, C, n, s, adj, Aadj, ldaa);
+  return mvn_adj_epilogue(ctx, C, n, s, k, s_stride, adj, Aadj, ldaa);
 }
 
 }  // extern "C"

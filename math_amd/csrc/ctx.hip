@@ -150,6 +150,8 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->status_armed = 0;
   ctx->pin_io = nullptr;
   ctx->pin_io_size = 0;
+  ctx->res_h = nullptr;
+  ctx->res_h_size = 0;
   ctx->done_h = nullptr;
   ctx->done_seq = 0;
   ctx->red_counter_d = nullptr;
@@ -240,6 +242,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   hipHostFree(ctx->status_h);
   hipHostFree(ctx->host_scratch);
   if (ctx->pin_io) hipHostFree(ctx->pin_io);
+  if (ctx->res_h) hipHostFree(ctx->res_h);
   hipHostFree(ctx->done_h);
   hipFree(ctx->red_counter_d);
   hipStreamDestroy(ctx->stream);
@@ -353,6 +356,24 @@ void* smg_pinned_io(smg_ctx* ctx, size_t bytes) {
     ctx->pin_io_size = n;
   }
   return ctx->pin_io;
+}
+
+void* smg_pinned_result(smg_ctx* ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  if (bytes > ctx->res_h_size) {
+    hipStreamSynchronize(ctx->stream);
+    if (ctx->res_h) hipHostFree(ctx->res_h);
+    size_t n = ctx->res_h_size ? ctx->res_h_size : (size_t)1 << 12;
+    while (n < bytes) n *= 2;
+    if (hipHostMalloc(&ctx->res_h, n, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      hipGetLastError();
+      ctx->res_h = nullptr;
+      ctx->res_h_size = 0;
+      return nullptr;
+    }
+    ctx->res_h_size = n;
+  }
+  return ctx->res_h;
 }
 
 int smg_wait_done(smg_ctx* ctx, long long seq) {

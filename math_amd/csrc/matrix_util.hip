@@ -5,6 +5,11 @@
 //               rev/mat/fun/sum.hpp:18-60)
 //   dot        (dot_product / the scalar side of multiply(var, Matrix<var>),
 //               rev/mat/fun/multiply.hpp:562-600)
+//   pack_tril / unpack_tril_add  (the Eigen boundary: a cholesky_decompose
+//               factor's or a gp_exp_quad_cov matrix's host varis cover the
+//               lower triangle only, packed column by column --
+//               rev/mat/fun/cholesky_decompose.hpp:34-48,
+//               rev/mat/fun/gp_exp_quad_cov.hpp:235 -- so only it crosses PCIe)
 // All deterministic (fixed-order reductions).
 #include "smg_internal.h"
 
@@ -139,6 +144,58 @@ __global__ void k_diag_ratio_rev(int n, const double* __restrict__ A, int lda,
   }
 }
 
+// packed lower triangle, column-major: column j's rows j..n-1 start at
+// j n - j (j - 1) / 2
+__device__ __forceinline__ long long tril_off(long long n, long long j) { return j * n - j * (j - 1) / 2; }
+
+// mode 0: dst <- tril(A); mode 1: dst <- tril(A) + strict tril(A^T).  One
+// 64 x 64 tile of the lower triangle per workgroup; mode 1 reads the mirror
+// tile through LDS so both reads are column-coalesced.
+__global__ __launch_bounds__(256) void k_pack_tril(int mode, int n, const double* __restrict__ A, int lda,
+                                                   double* __restrict__ dst) {
+  const int bx = blockIdx.x, by = blockIdx.y;  // tile rows bx, cols by
+  if (bx < by) return;
+  __shared__ double t[TT][TT + 1];
+  const int i0 = bx * TT, j0 = by * TT;
+  const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
+  if (mode == 1) {
+#pragma unroll 4
+    for (int c = c4; c < TT; c += 4) {  // mirror tile: A(j0 + r, i0 + c) -> t[r][c] = A^T(i0 + c, j0 + r)
+      const int i = j0 + r, j = i0 + c;
+      t[r][c] = (i < n && j < n) ? A[i + (size_t)j * lda] : 0.0;
+    }
+    __syncthreads();
+  }
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    const int i = i0 + r, j = j0 + c;
+    if (i < n && j < n && i >= j) {
+      double v = A[i + (size_t)j * lda];
+      if (mode == 1 && i != j) v += t[c][r];  // A(j, i)
+      dst[tril_off(n, j) + (i - j)] = v;
+    }
+  }
+}
+
+// tril(A) += unpack(src) (modes 0 / 1); A_ii += src[i] (mode 2)
+__global__ __launch_bounds__(256) void k_unpack_tril_add(int mode, int n, const double* __restrict__ src,
+                                                         double* __restrict__ A, int lda) {
+  if (mode == 2) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) A[i + (size_t)i * lda] += src[i];
+    return;
+  }
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double* s = src + tril_off(n, j) - j;
+    double* a = A + (size_t)j * lda;
+    for (int i = j + threadIdx.x; i < n; i += 256) a[i] += s[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack_diag(int n, const double* __restrict__ A, int lda,
+                                                   double* __restrict__ dst) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) dst[i] = A[i + (size_t)i * lda];
+}
+
 inline int grid_for(long long tot, int cap = 4096) {
   long long g = (tot + 255) / 256;
   if (g > cap) g = cap;
@@ -167,6 +224,31 @@ int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda) {
   if (!A || lda < n) return SMG_ERR_ARG;
   const int t = smg_ceil_div(n, TT);
   hipLaunchKernelGGL(k_sym_from_lower, dim3(t, t), dim3(256), 0, ctx->stream, n, A, lda);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_pack_tril(smg_ctx* ctx, int mode, int n, const double* A, int lda, double* dst) {
+  if (!ctx || n < 0 || mode < 0 || mode > 2) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!A || !dst || lda < n) return SMG_ERR_ARG;
+  if (mode == 2) {
+    hipLaunchKernelGGL(k_pack_diag, dim3(smg_ceil_div(n, 256) < 1024 ? smg_ceil_div(n, 256) : 1024), dim3(256), 0,
+                       ctx->stream, n, A, lda, dst);
+  } else {
+    const int t = smg_ceil_div(n, TT);
+    hipLaunchKernelGGL(k_pack_tril, dim3(t, t), dim3(256), 0, ctx->stream, mode, n, A, lda, dst);
+  }
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_unpack_tril_add(smg_ctx* ctx, int mode, int n, const double* src, double* A, int lda) {
+  if (!ctx || n < 0 || mode < 0 || mode > 2) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!A || !src || lda < n) return SMG_ERR_ARG;
+  const int g = mode == 2 ? (smg_ceil_div(n, 256) < 1024 ? smg_ceil_div(n, 256) : 1024) : (n < 4096 ? n : 4096);
+  hipLaunchKernelGGL(k_unpack_tril_add, dim3(g), dim3(256), 0, ctx->stream, mode, n, src, A, lda);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -79,6 +79,8 @@ struct smg_ctx {
   // completion word they publish (host spins on it instead of a stream sync)
   void* pin_io;
   size_t pin_io_size;
+  void* res_h;           // fine-grained pinned results (smg_pinned_result)
+  size_t res_h_size;
   long long* done_h;     // host-coherent completion word
   long long done_seq;
   unsigned int* red_counter_d;  // last-block-done counter of the fused reductions (device, self-resetting)

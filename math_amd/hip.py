@@ -47,6 +47,9 @@ _SIGS = {
     "smg_status_enqueue": (_I, [_P, _P]),
     "smg_status_inject": (_I, [_P, _I]),
     "smg_pinned_io": (_P, [_P, _S]),
+    "smg_pinned_result": (_P, [_P, _S]),
+    "smg_pack_tril": (_I, [_P, _I, _I, _P, _I, _P]),
+    "smg_unpack_tril_add": (_I, [_P, _I, _I, _P, _P, _I]),
     "smg_publish_to_host": (_I, [_P, _P, _L, _P]),
     "smg_profile_enable": (_I, [_P, _I]),
     "smg_profile_read": (_I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
@@ -85,9 +88,9 @@ _SIGS = {
     "smg_mvn_cholesky_fwd": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
     "smg_mvn_cholesky_rev": (_I, [_P, _P, _I, _P, _I, _P, _D, _I, _P, _P, _P, _I]),
     "smg_cholesky_mvn_rev_ws_doubles": (ctypes.c_size_t, [_I]),
-    "smg_cholesky_mvn_rev": (_I, [_P, _P, _I, _P, _I, _P, _D, _P, _I, _P]),
+    "smg_cholesky_mvn_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _L, _D, _P, _I, _P]),
     "smg_cholesky_inv_t_async": (_I, [_P, _P, _I, _P, _I, _P, _I, _P]),
-    "smg_cholesky_mvn_rev_v": (_I, [_P, _I, _P, _D, _P, _I, _P, _I]),
+    "smg_cholesky_mvn_rev_v": (_I, [_P, _I, _P, _I, _L, _D, _P, _I, _P, _I]),
     "smg_cholesky_fwd_checked_mark_inv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
     "smg_log_sum_exp_fwd": (_I, [_P, _P, _L, _P]),
     "smg_log_sum_exp_rev": (_I, [_P, _P, _L, _D, _D, _P]),

@@ -44,10 +44,11 @@ enum class dev_structure : int {
  * them in closed form (rev/fun/cholesky_decompose.hpp). */
 class structured_adjoint_sink {
  public:
-  /** owner: the consumer node; ws: its device [w, s] (smg_mvn_cholesky_fwd);
-   * adj: its adjoint.  True when taken (the consumer then writes no dense
-   * adjoint for the factor); false: the consumer writes it densely. */
-  virtual bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) = 0;
+  /** owner: the consumer node; ws: its device [w, s] (smg_mvn_cholesky_fwd),
+   * k of them 2n doubles apart (the array form's observations); adj: its
+   * adjoint.  True when taken (the consumer then writes no dense adjoint for
+   * the factor); false: the consumer writes it densely. */
+  virtual bool take_mvn_adjoint(const vari* owner, const double* ws, double adj, int k = 1) = 0;
   /** Called by such a consumer's forward pass before its own device work:
    * the node may start, on a side stream, what that reverse will need. */
   virtual void prepare_mvn_adjoint() {}

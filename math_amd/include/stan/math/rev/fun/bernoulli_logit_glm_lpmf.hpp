@@ -172,7 +172,7 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
   amd::check(smg_status_armed(c, &armed), fn);
   const double* h;
   if (!s.distributed && !armed) {
-    double* o = static_cast<double*>(smg_pinned_io(c, size_t(M + 3) * sizeof(double)));
+    double* o = static_cast<double*>(smg_pinned_result(c, size_t(M + 3) * sizeof(double)));
     if (!o) throw std::bad_alloc();
     amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out, o), fn);
     h = o;
@@ -183,7 +183,7 @@ inline glm_result glm_eval(const glm_shard& s, const glm_params& p) {
     amd::check(smg_bernoulli_logit_glm_io(c, s.y, s.x, s.rows, M, s.ldx, p.alpha, p.beta.data(), ws, out,
                                           nullptr), fn);
     amd::allreduce_sum(out, M + 3, fn);
-    double* o = static_cast<double*>(smg_pinned_io(c, size_t(M + 3) * sizeof(double)));
+    double* o = static_cast<double*>(smg_pinned_result(c, size_t(M + 3) * sizeof(double)));
     if (!o) throw std::bad_alloc();
     amd::check(smg_publish_to_host(c, out, M + 3, o), fn);
     h = o;

@@ -96,6 +96,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   const vari* dep_owner_ = nullptr;
   const double* dep_ws_ = nullptr;
   double dep_adj_ = 0.0;
+  int dep_k_ = 1;  // observations (the array form), [w, s] 2n doubles apart
   size_t dep_sweep_ = 0;
   double* ws_ = nullptr;  // smg_cholesky_mvn_rev's workspace [V = L^{-T}, K^{-1}]
   bool early_ = false;    // the factorisation queued K^{-1}'s top-half steps into ws_
@@ -105,7 +106,17 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   // adjoint (expand_adjoint writes them if L's adjoint is read)
   const double* exp_ws_ = nullptr;
   double exp_adj_ = 0.0;
+  int exp_k_ = 1;
   size_t exp_sweep_ = 0;
+
+  // the deposited partials written densely into L's adjoint (what the MVN
+  // would have written: one smg_mvn_cholesky_rev per observation)
+  void expand(const double* ws, double adj, int k) const {
+    for (int o = 0; o < k; ++o)
+      amd::check(smg_mvn_cholesky_rev(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws + 2 * size_t(n_) * o, adj, 1, nullptr,
+                                      nullptr, L_->adj_, n_),
+                 "cholesky_decompose");
+  }
 
   /** Which factorisations took the closed-form reverse last time, by tape
    * position and size: a sampler re-runs the same program every gradient, so
@@ -174,33 +185,28 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     c_ready_ = v_ready_ && early_;
   }
 
-  bool take_mvn_adjoint(const vari* owner, const double* ws, double adj) override {
+  bool take_mvn_adjoint(const vari* owner, const double* ws, double adj, int k) override {
     if (!closed_form_enabled()) return false;
     auto* st = ChainableStack::instance_;
     if (dep_owner_ && dep_sweep_ == st->sweep_ && dep_owner_ != owner) return false;  // one consumer only
     dep_owner_ = owner;
     dep_ws_ = ws;
     dep_adj_ = adj;
+    dep_k_ = k;
     dep_sweep_ = st->sweep_;
     return true;
   }
 
   void expand_adjoint() override {
     auto* st = ChainableStack::instance_;
-    const double* ws = nullptr;
-    double adj = 0.0;
     if (dep_owner_ && dep_sweep_ == st->sweep_) {  // deposited, and this node was not chained
-      ws = dep_ws_;
-      adj = dep_adj_;
       dep_owner_ = nullptr;
+      expand(dep_ws_, dep_adj_, dep_k_);
     } else if (exp_ws_ && exp_sweep_ == st->sweep_) {  // consumed by the closed form
-      ws = exp_ws_;
-      adj = exp_adj_;
+      const double* ws = exp_ws_;
       exp_ws_ = nullptr;
+      expand(ws, exp_adj_, exp_k_);
     }
-    if (ws)
-      amd::check(smg_mvn_cholesky_rev(amd::ctx(), L_->val_, n_, L_->aux_, n_, ws, adj, 1, nullptr, nullptr, L_->adj_, n_),
-                 "cholesky_decompose");
   }
 
   void chain() override {
@@ -220,21 +226,22 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       if (!dense) {
         exp_ws_ = dep_ws_;
         exp_adj_ = dep_adj_;
+        exp_k_ = dep_k_;
         exp_sweep_ = st->sweep_;
         if (v_ready_) {
-          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_, c_ready_ ? 1 : 0),
+          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_k_, 2LL * n_, dep_adj_, A_->adj_, n_, ws_,
+                                            c_ready_ ? 1 : 0),
                      "cholesky_decompose");
         } else {
           if (!ws_) ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
-          amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_adj_, A_->adj_, n_, ws_),
+          amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_k_, 2LL * n_, dep_adj_,
+                                          A_->adj_, n_, ws_),
                      "cholesky_decompose");
         }
         return;
       }
       // expand the deposit: the MVN's own lower-only partials, added densely
-      amd::check(smg_mvn_cholesky_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_, dep_adj_, 1, nullptr, nullptr,
-                                      L_->adj_, n_),
-                 "cholesky_decompose");
+      expand(dep_ws_, dep_adj_, dep_k_);
     }
     if (!deposit) record(false);
     // Murray's algorithm overwrites its input and reads only its lower triangle

@@ -153,9 +153,9 @@ class mvn_multi_dev_vari : public device_vari {
   }
   void chain() override {
     smg_ctx* c = amd::ctx();
-    // one observation and a cholesky_decompose factor: the lower-only
-    // partials go to the factor's node unexpanded (rev/fun/cholesky_decompose.hpp)
-    deposited_ = k_ == 1 && lower_only_ && L_.vi && L_.vi->sink_ && L_.vi->sink_->take_mvn_adjoint(this, ws_, adj_);
+    // a cholesky_decompose factor: the lower-only partials of all the
+    // observations go to the factor's node unexpanded (rev/fun/cholesky_decompose.hpp)
+    deposited_ = lower_only_ && L_.vi && L_.vi->sink_ && L_.vi->sink_->take_mvn_adjoint(this, ws_, adj_, k_);
     for (int i = 0; i < k_; ++i)
       amd::check(smg_mvn_cholesky_rev(c, L_.val(), n_, aux_, n_, ws_ + 2 * size_t(n_) * i, adj_, lower_only_,
                                       obs_[i].yadj, obs_[i].muadj, deposited_ ? nullptr : L_.adj(), n_),
@@ -181,7 +181,7 @@ inline vari* mvn_cholesky_multi(const dev_operand& L, const double* aux, bool lo
   for (int i = 0; i < k; ++i)
     amd::check(smg_mvn_cholesky_fwd(c, obs[i].y, obs[i].mu, L.val(), n, aux, n, ws + 2 * size_t(n) * i, lp_d + i),
                fn);
-  if (k == 1 && lower_only && L.vi && L.vi->sink_) L.vi->sink_->prepare_mvn_adjoint();  // (behind the solves)
+  if (lower_only && L.vi && L.vi->sink_) L.vi->sink_->prepare_mvn_adjoint();  // (behind the solves)
   std::vector<double> lps(static_cast<size_t>(k));
   amd::to_host(lps.data(), lp_d, lps.size());
   double lp = 0.0;

@@ -335,7 +335,7 @@ inline typename internal::ops_return<T_y, T_loc, T_scale>::type normal_lpdf(cons
     g_off[i] = off;
     if (want_g[i] && ops[i].vec && ops[i].host) off += ops[i].n;
   }
-  double* st = static_cast<double*>(smg_pinned_io(c, off * sizeof(double)));
+  double* st = static_cast<double*>(smg_pinned_result(c, off * sizeof(double)));
   if (!st) throw std::bad_alloc();
   for (int i = 0; i < 8; ++i) st[i] = 0.0;
   internal::fused_stage(y, st + val_off[0]);

@@ -67,6 +67,56 @@ inline void map_rect_size_match(const char* what1, size_t a, const char* what2, 
   }
 }
 
+/** The outcome of map_rect's argument checks (prim/mat/functor/map_rect.hpp:
+ * 133-167, in that order): code 0 = passed, else which check failed and the
+ * two sizes it compared.  On a distributed job it travels in the first
+ * exchange of the call, so every rank throws the same invalid_argument
+ * together (the reference's root checks before it dispatches to its workers;
+ * a rank throwing alone would leave the others waiting in a collective). */
+struct map_rect_check {
+  int code = 0;
+  size_t a = 0, b = 0;
+};
+
+inline void map_rect_throw(const map_rect_check& c) {
+  static const char* const what[6][2] = {
+      {"", ""},
+      {"job parameters", "real data"},
+      {"job parameters", "int data"},
+      {"Size of one of the vectors of the job specific parameters",
+       "size of another vector of the job specifc parameters"},
+      {"Size of one of the arrays of the job specific real data", "size of another array of the job specifc real data"},
+      {"Size of one of the arrays of the job specific int data", "size of another array of the job specifc int data"}};
+  if (c.code > 0 && c.code < 6) map_rect_size_match(what[c.code][0], c.a, what[c.code][1], c.b);
+}
+
+/** The checks; data_elsewhere: this rank left the job data to the root. */
+template <typename T_job>
+map_rect_check map_rect_checks(const std::vector<Eigen::Matrix<T_job, Eigen::Dynamic, 1>>& job_params,
+                               const std::vector<std::vector<double>>& x_r, const std::vector<std::vector<int>>& x_i,
+                               bool data_elsewhere) {
+  const size_t J = job_params.size();
+  if (!data_elsewhere && J != x_r.size()) return {1, J, x_r.size()};
+  if (!data_elsewhere && J != x_i.size()) return {2, J, x_i.size()};
+  for (size_t i = 1; i < J; ++i) {
+    if (job_params[i].size() != job_params[0].size())
+      return {3, size_t(job_params[i].size()), size_t(job_params[0].size())};
+    if (data_elsewhere) continue;
+    if (x_r[i].size() != x_r[0].size()) return {4, x_r[i].size(), x_r[0].size()};
+    if (x_i[i].size() != x_i[0].size()) return {5, x_i[i].size(), x_i[0].size()};
+  }
+  return {};
+}
+
+/** After an exchange that carried every rank's check outcome at `all + r *
+ * stride + off` (code, a, b): throw the first failing rank's (root first). */
+inline void map_rect_throw_gathered(const double* all, int W, size_t stride, size_t off) {
+  for (int r = 0; r < W; ++r) {
+    const double* h = all + size_t(r) * stride + off;
+    if (h[0] != 0.0) map_rect_throw({int(h[0]), size_t(h[1]), size_t(h[2])});
+  }
+}
+
 template <typename T>
 inline Eigen::Matrix<double, Eigen::Dynamic, 1> map_rect_values(
     const Eigen::Matrix<T, Eigen::Dynamic, 1>& v) {
@@ -150,20 +200,22 @@ inline std::vector<int> map_rect_chunks(size_t J, int W) {
  * (every rank holds the data) or two scatters from rank 0 (x_r, then x_i as
  * doubles: exact for every int).  The root's sizes are the job's. */
 inline void map_rect_fill_cache(map_rect_data& c, size_t J, const std::vector<std::vector<double>>& x_r,
-                                const std::vector<std::vector<int>>& x_i) {
+                                const std::vector<std::vector<int>>& x_i, const map_rect_check& chk) {
   const int W = amd::world_size(), rank = amd::world_rank();
   const bool have = x_r.size() == J && x_i.size() == J;
-  double hdr[4] = {double(J), have && J ? double(x_r[0].size()) : 0.0, have && J ? double(x_i[0].size()) : 0.0,
-                   have ? 1.0 : 0.0};
-  std::vector<double> all(size_t(4) * W);
-  amd::allgather(hdr, 4, all.data());
-  if (all[3] != 1.0)  // (every rank sees the root's flag: all of them throw)
+  // [J, x_r length, x_i length, holds data, check code, its two sizes]
+  double hdr[7] = {double(J), have && J ? double(x_r[0].size()) : 0.0, have && J ? double(x_i[0].size()) : 0.0,
+                   have ? 1.0 : 0.0, double(chk.code), double(chk.a), double(chk.b)};
+  std::vector<double> all(size_t(7) * W);
+  amd::allgather(hdr, 7, all.data());
+  map_rect_throw_gathered(all.data(), W, 7, 4);  // (every rank sees every rank's checks: all of them throw)
+  if (all[3] != 1.0)
     throw std::invalid_argument("map_rect: the root (rank 0) must hold the job data");
   const size_t nr = size_t(all[1]), ni = size_t(all[2]);
   bool everyone = true;
   for (int r = 0; r < W; ++r) {
-    everyone = everyone && all[size_t(4 * r + 3)] == 1.0;
-    if (size_t(all[size_t(4 * r)]) != J)
+    everyone = everyone && all[size_t(7 * r + 3)] == 1.0;
+    if (size_t(all[size_t(7 * r)]) != J)
       throw std::invalid_argument("map_rect: every rank must pass the same number of jobs");
   }
   const std::vector<int> chunks = map_rect_chunks(J, W);
@@ -213,7 +265,8 @@ inline void map_rect_fill_cache(map_rect_data& c, size_t J, const std::vector<st
 template <typename F, bool SV, bool JV, typename T_job>
 std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_d,
                                                   const std::vector<Eigen::Matrix<T_job, Eigen::Dynamic, 1>>& job_params,
-                                                  const map_rect_data& data, std::ostream* msgs, Eigen::Index rows) {
+                                                  const map_rect_data& data, std::ostream* msgs, Eigen::Index rows,
+                                                  const map_rect_check& chk) {
   const int W = amd::world_size(), rank = amd::world_rank();
   const size_t J = job_params.size();
   const std::vector<int> chunks = map_rect_chunks(J, W);
@@ -224,9 +277,9 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
   }
   const int mine = chunks[size_t(rank)];
   std::vector<Eigen::MatrixXd> local(static_cast<size_t>(mine));
-  double ok = 1.0;
+  double ok = chk.code ? 0.0 : 1.0;  // (a failed check: nothing evaluated)
   try {
-    for (int i = 0; i < mine; ++i) {
+    for (int i = 0; ok != 0.0 && i < mine; ++i) {
       const size_t j = size_t(first + i);
       const Eigen::VectorXd job_d = map_rect_values(job_params[j]);
       if constexpr (SV || JV) {
@@ -240,19 +293,23 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
   } catch (const std::exception&) {
     ok = 0.0;  // flagged, not rethrown: every rank must reach the exchange
   }
-  // (1) status and the number of outputs of each local job
-  const long long hn = 1 + maxc;
+  // (1) status, the argument checks (code, a, b) and the number of outputs of each local job
+  const long long hn = 4 + maxc;
   std::vector<double> hdr(size_t(hn), 0.0), all_hdr(size_t(hn) * W);
   hdr[0] = ok;
+  hdr[1] = double(chk.code);
+  hdr[2] = double(chk.a);
+  hdr[3] = double(chk.b);
   if (ok != 0.0)
-    for (int i = 0; i < mine; ++i) hdr[size_t(1 + i)] = double(local[size_t(i)].cols());
+    for (int i = 0; i < mine; ++i) hdr[size_t(4 + i)] = double(local[size_t(i)].cols());
   amd::allgather(hdr.data(), hn, all_hdr.data());
+  map_rect_throw_gathered(all_hdr.data(), W, size_t(hn), 1);
   for (int r = 0; r < W; ++r)
     if (all_hdr[size_t(r) * hn] != 1.0) throw std::domain_error("Error during MPI evaluation.");
   long long max_pay = 0;
   for (int r = 0; r < W; ++r) {
     long long p = 0;
-    for (int i = 0; i < chunks[size_t(r)]; ++i) p += rows * (long long)all_hdr[size_t(r) * hn + 1 + i];
+    for (int i = 0; i < chunks[size_t(r)]; ++i) p += rows * (long long)all_hdr[size_t(r) * hn + 4 + i];
     max_pay = std::max(max_pay, p);
   }
   // (2) every job's columns, rank r's block at r * max_pay
@@ -269,7 +326,7 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
   for (int r = 0; r < W; ++r) {
     const double* base = all.data() + size_t(r) * max_pay;
     for (int i = 0; i < chunks[size_t(r)]; ++i, ++j) {
-      const Eigen::Index cols = Eigen::Index(all_hdr[size_t(r) * hn + 1 + i]);
+      const Eigen::Index cols = Eigen::Index(all_hdr[size_t(r) * hn + 4 + i]);
       outs[j] = Eigen::Map<const Eigen::MatrixXd>(base, rows, cols);
       base += rows * cols;
     }
@@ -301,36 +358,21 @@ map_rect(const Eigen::Matrix<T_shared, Eigen::Dynamic, 1>& shared_params,
   const size_t J = job_params.size();
   // a non-root rank of a distributed job may leave the job data to the root
   // (empty x_r and x_i; its block then comes from the cache / the scatter)
-  const bool data_elsewhere = amd::distributed() && amd::world_rank() != 0 && x_r.empty() && x_i.empty();
-  if (!data_elsewhere) {
-    internal::map_rect_size_match("job parameters", job_params.size(), "real data", x_r.size());
-    internal::map_rect_size_match("job parameters", job_params.size(), "int data", x_i.size());
-  }
-  for (size_t i = 1; i < J; ++i) {
-    internal::map_rect_size_match("Size of one of the vectors of the job specific parameters",
-                                  job_params[i].size(),
-                                  "size of another vector of the job specifc parameters",
-                                  job_params[0].size());
-    if (data_elsewhere) continue;
-    internal::map_rect_size_match("Size of one of the arrays of the job specific real data",
-                                  x_r[i].size(),
-                                  "size of another array of the job specifc real data",
-                                  x_r[0].size());
-    internal::map_rect_size_match("Size of one of the arrays of the job specific int data",
-                                  x_i[i].size(), "size of another array of the job specifc int data",
-                                  x_i[0].size());
-  }
+  const bool dist = amd::distributed();
+  const bool data_elsewhere = dist && amd::world_rank() != 0 && x_r.empty() && x_i.empty();
+  const internal::map_rect_check chk = internal::map_rect_checks(job_params, x_r, x_i, data_elsewhere);
+  if (!dist || J == 0) internal::map_rect_throw(chk);  // (no exchange follows: throw here)
   if (J == 0) return result_t();
 
   const Eigen::VectorXd shared_d = internal::map_rect_values(shared_params);
   std::vector<Eigen::MatrixXd> outs(J);
-  if (amd::distributed()) {
+  if (dist) {
     const Eigen::Index rows = 1 + (SV ? shared_params.size() : 0) + (JV ? job_params[0].size() : 0);
     internal::map_rect_data& data = internal::map_rect_cache<call_id>();
-    if (!data.valid) internal::map_rect_fill_cache(data, J, x_r, x_i);
+    if (!data.valid) internal::map_rect_fill_cache(data, J, x_r, x_i, chk);
     if (data.J != J || data.world != amd::world_size())
       throw std::invalid_argument("map_rect: the number of jobs of a call_id must not change between calls");
-    outs = internal::map_rect_distributed<F, SV, JV>(shared_d, job_params, data, msgs, rows);
+    outs = internal::map_rect_distributed<F, SV, JV>(shared_d, job_params, data, msgs, rows, chk);
   } else {
     for (size_t j = 0; j < J; ++j) {
       const Eigen::VectorXd job_d = internal::map_rect_values(job_params[j]);

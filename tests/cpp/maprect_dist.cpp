@@ -46,9 +46,15 @@ struct hier_job {
   }
 };
 
+int g_ragged = 0;  // rank 0's last job gets one real datum fewer (maprect_set_ragged)
+
 }  // namespace
 
 extern "C" {
+
+/* Make rank 0's x_r ragged in the following calls (the argument-check
+ * agreement test: every rank must throw rank 0's invalid_argument). */
+void maprect_set_ragged(int on) { g_ragged = on; }
 
 /* mode 0: phi and theta var; 1: phi var, theta data; 2: phi data, theta var;
  * 3: all data.  f = sum_i (1 + 0.1 i) out_i.  grad: (phi(2), theta(J)) (zeros
@@ -69,6 +75,7 @@ int maprect_hier_ex(int nranks, int rank, amd::allgather_fn fn, amd::scatterv_fn
     xr[size_t(j)].assign(xr_flat + size_t(j) * nr, xr_flat + size_t(j + 1) * nr);
     xi[size_t(j)].assign(xi_flat + 2 * j, xi_flat + 2 * j + 2);
   }
+  if (g_ragged && rank == 0 && J > 1) xr[size_t(J - 1)].pop_back();
   int rc = 0;
   start_nested();
   try {

@@ -319,7 +319,7 @@ def test_cholesky_mvn_closed_form_vs_oracle(ctx, N):
     for aux in (dD, None):
         G0 = rng.uniform(-1, 1, (N, N))  # accumulates into the lower triangle only
         dG = ctx.put(F(G0))
-        ctx.call("smg_cholesky_mvn_rev", dL, N, aux, N, ws + 8 * N, adj, dG, N, ctx.zeros(wsz))
+        ctx.call("smg_cholesky_mvn_rev", dL, N, aux, N, ws + 8 * N, 1, 0, adj, dG, N, ctx.zeros(wsz))
         G = ctx.get(dG, N * N).reshape(N, N).T
         low = np.tril(np.ones((N, N), bool))
         near_rel(G[low] - G0[low], Aref[low], 1e-10, atol=1e-10 * np.abs(Aref).max(), what="grad_A")

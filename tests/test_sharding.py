@@ -335,6 +335,58 @@ def test_map_rect_job_data_cache_gloo(tmp_path, world, use_hook):
                         assert kinds == ["ag"] * 5, (J, mode, r, got["log"])
 
 
+def _maprect_ragged_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(send, count, recv, _user):
+        t = torch.from_numpy(np.ctypeslib.as_array(send, shape=(count,)).copy())
+        parts = [torch.empty(count, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, t)
+        np.ctypeslib.as_array(recv, shape=(count * world,))[:] = torch.cat(parts).numpy()
+
+    cb = _AG(allgather)
+    lib = _maprect_lib()
+    xr, xi, th = gen.maprect_inputs(7)
+    res = {}
+    # (a) the first call of a call_id: the checks travel in the cache's size exchange
+    lib.maprect_set_ragged(1)
+    res["fill"] = _maprect_ex(lib, world, rank, cb, _SC(), xr, xi, th, 0, 1, 1)
+    # (b) a cached call_id: they travel in the status exchange
+    lib.maprect_set_ragged(0)
+    res["good"] = _maprect_ex(lib, world, rank, cb, _SC(), xr, xi, th, 0, 1, 1)
+    lib.maprect_set_ragged(1)
+    res["cached"] = _maprect_ex(lib, world, rank, cb, _SC(), xr, xi, th, 0, 0, 1)
+    # (c) a later good call still agrees (no rank left behind in a collective)
+    lib.maprect_set_ragged(0)
+    res["after"] = _maprect_ex(lib, world, rank, cb, _SC(), xr, xi, th, 0, 0, 1)
+    np.save(out + f".{rank}.npy", np.array(res, dtype=object), allow_pickle=True)
+    dist.destroy_process_group()
+
+
+def test_map_rect_argument_checks_agree_gloo(tmp_path):
+    """Rank 0 passes a ragged x_r, rank 1 leaves the job data to the root
+    (empty x_r / x_i): both ranks throw rank 0's invalid_argument -- on the
+    first call of the call_id (the job data cache's size exchange carries the
+    checks) and on a cached one (the status exchange carries them) -- instead
+    of rank 1 waiting in a collective rank 0 never reaches; the reference's
+    root checks before it dispatches (prim/mat/functor/map_rect.hpp:133-167)."""
+    out = str(tmp_path / "rg")
+    _spawn(_maprect_ragged_rank, 2, out)
+    ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(2)]
+    xr, _, _ = gen.maprect_inputs(7)
+    n = xr.shape[1]
+    msg = (f"map_rect: Size of one of the arrays of the job specific real data ({n - 1}) and size of another "
+           f"array of the job specifc real data ({n}) must match in size")
+    for r in range(2):
+        for key in ("fill", "cached"):
+            rc, _, _, _, err = ranks[r][key]
+            assert rc == 2 and err == msg, (r, key, rc, err)
+        for key in ("good", "after"):
+            assert ranks[r][key][0] == 0, (r, key, ranks[r][key][4])
+        assert ranks[r]["good"][1] == ranks[r]["after"][1]
+
+
 # ---------------------------------------------------------------- product GLM reducers, W = 2
 GLMDIST_LIB = os.path.join(ROOT, "tests", "cpp", "_bin", "libglm_dist.so")
 _AR = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.c_longlong, ctypes.c_void_p)
