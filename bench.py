@@ -251,7 +251,8 @@ class GLM(Workload):
         # SMG_BENCH_GLM_RCCL1=1 at one GPU: a one-rank RCCL communicator, so the
         # step is the sharded path one rank of W runs (the per-rank proxy of
         # an 8-GPU run at --rows R/8)
-        self.rccl1 = self.world == 1 and os.environ.get("SMG_BENCH_GLM_RCCL1") == "1"
+        self.rccl1 = self.world == 1 and (getattr(self, "force_rccl1", False)
+                                          or os.environ.get("SMG_BENCH_GLM_RCCL1") == "1")
         if self.rccl1:
             from math_amd import hip
             buf = ctypes.create_string_buffer(128)
@@ -440,14 +441,17 @@ class HVP(GP):
 
     def roofline(self, fams, steps, t_prof, ms_per_step):
         r = eval_roofline(self, fams, steps, ms_per_step, (None, None))
-        # the same step time priced on the flops this build executes: the Gram
-        # product lower-only 2N^3 -> N^3 ... (A A^T: N^3, reverse GEMM 2N^3,
-        # chol fwd N^3/3 + Murray adjoint N^3)
-        ex = (1.0 + 2.0 + 1.0 / 3.0 + 1.0) * float(self.N) ** 3
+        # the same step time priced on the flops the GEMM family executes per
+        # product (each launch's flops, triangular K cuts counted, summed over
+        # the profiled steps): measured, not a formula
+        gms, gn, gfl = fams["gemm"]
+        ex = gfl / steps
         ach = ex / (ms_per_step * 1e-3) / 1e12
         r["executed_flops_per_eval"] = ex
-        r["executed_flops_expr"] = ("4.33N^3: forward Gram A A^T lower-only N^3 + reverse (A' = (S + S^T) A) "
-                                    "2N^3 + Cholesky forward N^3/3 + Murray adjoint N^3")
+        r["executed_flops_expr"] = ("the GEMM family's executed flops per product (per-launch counts with the "
+                                    "triangular K cuts, summed over the profiled steps): the value factor's forward "
+                                    "and Murray adjoint, the Cholesky tangent node (W = L^-1, W A' W^T, L P and their "
+                                    "reverse) and the MVN / solve products")
         r["executed_achieved"] = ach
         r["frac_on_executed"] = ach / PEAK_FP64_TFLOPS
         return r
@@ -574,6 +578,51 @@ def spawn_ranks(n):
     return 0
 
 
+def glm_strong(bl, args, rank, world, local, dist, timed, lib, ctx):
+    """The north star's strong-scaling config in the default run: the config-4
+    GLM (1e7 rows x 256, bernoulli_logit_glm_lpmf) on the same N GPUs, rows
+    sharded (stan::math::row_partition), ONE ncclAllReduce of [logp, alpha',
+    beta'] per gradient -- at N = 1 through a one-rank RCCL communicator, so
+    every N runs the same sharded path.  The driver's 1..8-GPU runs of
+    `bench.py --gpus N` thereby record the GLM's strong-scaling curve
+    (value = gradient evals/s of the whole 1e7-row model) beside the GP
+    replicas."""
+    a = argparse.Namespace(**vars(args))
+    a.rows = 1e7
+    g = GLM(bl, a, rank, world, local, dist)
+    g.force_rccl1 = True
+    if g.init() != 0:
+        raise SystemExit(f"glm_strong init failed: {bl.smg_bench_error().decode()}")
+    for _ in range(3):
+        if g.step() != 0:
+            raise SystemExit(f"glm_strong step failed: {bl.smg_bench_error().decode()}")
+    ok, msg = g.guard()
+    if not ok:
+        raise SystemExit(f"glm_strong parity failure: {msg}")
+    steps = max(args.steps, 20)
+    t = _timed_glm(g, steps, timed)
+    lib.smg_profile_enable(ctx, 1)
+    tp = _timed_glm(g, steps, timed)
+    fams = {f: hip_profile_read(lib, ctx, f) for f in ("glm",)}
+    lib.smg_profile_enable(ctx, 0)
+    roof = g.roofline(fams, steps, tp, 1e3 * t / steps)
+    return {"metric": g.metric, "value": steps / t, "unit": g.unit, "n_gpus": world, "steps": steps,
+            "ms_per_step": 1e3 * t / steps, "scaling": "strong", "rows": int(a.rows), "covariates": g.M,
+            "rows_per_rank": int(g.rows), "config": g.config(),
+            "roofline": {k: roof[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
+                                              "bytes_per_launch", "avg_launch_ms", "step_minus_glm_kernels_us")}}
+
+
+def _timed_glm(g, steps, timed):
+    """timed() over the GLM's step (the GP workload's timed() calls its own step)."""
+    return timed(steps, g.step)
+
+
+def hip_profile_read(lib, ctx, fam):
+    from math_amd import hip
+    return hip.profile_read(lib, ctx, fam)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -582,6 +631,8 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="gp")
     ap.add_argument("--rows", type=float, default=1e7, help="GLM rows (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-glm-strong", action="store_true",
+                    help="gp workload: skip the config-4 GLM strong-scaling line (glm_strong)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -614,11 +665,15 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def timed(k):
+    def timed(k, fn=None):
         barrier()
         lib.smg_sync(ctx)
         t0 = time.perf_counter()
-        if hasattr(wl, "run"):
+        if fn is not None:
+            for _ in range(k):
+                if fn() != 0:
+                    raise SystemExit(f"step failed: {bl.smg_bench_error().decode()}")
+        elif hasattr(wl, "run"):
             if wl.run(k) != 0:
                 raise SystemExit(f"step failed: {bl.smg_bench_error().decode()}")
         else:
@@ -678,9 +733,12 @@ def main():
             line["cpu_baseline"] = wl.cpu_baseline()
         except Exception as e:  # noqa: BLE001
             line["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
+    strong = args.workload == "gp" and not args.no_glm_strong
+    if strong:
+        line["glm_strong"] = glm_strong(bl, args, rank, world, local, dist, timed, lib, ctx)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1 and args.workload == "glm":
+    if (world > 1 and args.workload == "glm") or strong:
         lib.smg_comm_destroy(ctx)
     if dist is not None:
         dist.destroy_process_group()

@@ -35,7 +35,9 @@ namespace math {
 /** Structural information carried by a matrix node. */
 enum class dev_structure : int {
   general = 0,
-  lower = 1  // strict upper triangle is constant zero (cholesky_decompose output)
+  lower = 1,     // strict upper triangle is constant zero (cholesky_decompose output)
+  symmetric = 2  // values symmetric, and the reference's matrix holds one vari per
+                 // (i, j), (j, i) pair (gp_exp_quad_cov output)
 };
 
 /** A node that can take a consumer's adjoint contribution in structured
@@ -179,43 +181,134 @@ inline dev_var_matrix to_dev_var_matrix(const double* host_colmajor, int rows, i
 
 namespace internal {
 
-/** The host block (if any) that vari pointer range d[0..n) mirrors exactly:
- * element i is block.first + i (a lower-structured node: the block's dummy
- * above the diagonal).  The full pointer check runs on every call (a caller
- * may have replaced single elements); it is one parallel read of n pointers. */
-inline dev_matrix_vari* recognise_block(const var* d, size_t n, int rows, int cols) {
-  if (n == 0) return nullptr;
+enum block_layout : int { layout_dense = 0, layout_lower = 1, layout_sym = 2, layout_diag = 3 };
+
+/** packed lower triangle, column-major: column j's rows j..n-1 start at
+ * j n - j (j - 1) / 2 (smg_pack_tril) */
+inline size_t tril_off(size_t n, size_t j) { return j * n - j * (j - 1) / 2; }
+inline size_t tril_count(size_t n) { return n * (n + 1) / 2; }
+
+inline void block_column_ptrs(const host_block& b, size_t j, vari** out);
+
+/** f(i, v) for every row i of column j of host block b, in order: v is the
+ * vari the reference's matrix holds at (i, j) (host_block's layouts). */
+template <typename F>
+inline void block_column(const host_block& b, size_t j, F&& f) {
+  const size_t r = size_t(b.rows);
+  switch (b.layout) {
+    case layout_lower: {
+      for (size_t i = 0; i < j && i < r; ++i) f(i, b.dummy);
+      vari* c = b.first + tril_off(r, j) - j;
+      for (size_t i = j; i < r; ++i) f(i, c + i);
+      break;
+    }
+    case layout_sym: {
+      for (size_t i = 0; i < j && i < r; ++i) f(i, b.first + tril_off(r, i) + (j - i));
+      vari* c = b.first + tril_off(r, j) - j;
+      for (size_t i = j; i < r; ++i) f(i, c + i);
+      break;
+    }
+    case layout_diag: {
+      vari* own = j < b.n ? b.first + j : nullptr;
+      if (b.base >= 0) {  // (the base's column through a buffer: no recursive instantiation)
+        thread_local std::vector<vari*> col;
+        col.resize(r);
+        block_column_ptrs(ChainableStack::instance_->host_blocks_[size_t(b.base)], j, col.data());
+        for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : col[i]);
+      } else {
+        vari* const* e = b.base_elems + j * r;
+        for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : e[i]);
+      }
+      break;
+    }
+    default: {
+      vari* c = b.first + j * r;
+      for (size_t i = 0; i < r; ++i) f(i, c + i);
+    }
+  }
+}
+
+inline void block_column_ptrs(const host_block& b, size_t j, vari** out) {
+  block_column(b, j, [out](size_t i, vari* v) { out[i] = v; });
+}
+
+/** the vari at element (i, j) of host block b */
+inline vari* block_elem(const host_block& b, size_t i, size_t j) {
+  const size_t r = size_t(b.rows);
+  switch (b.layout) {
+    case layout_lower: return i >= j ? b.first + tril_off(r, j) + (i - j) : b.dummy;
+    case layout_sym: return i >= j ? b.first + tril_off(r, j) + (i - j) : b.first + tril_off(r, i) + (j - i);
+    case layout_diag:
+      if (i == j && j < b.n) return b.first + j;
+      return b.base >= 0 ? block_elem(ChainableStack::instance_->host_blocks_[size_t(b.base)], i, j)
+                         : b.base_elems[i + j * r];
+    default: return b.first + i + j * r;
+  }
+}
+
+/** smg_pack_tril's mode for a layout's owned varis (-1: dense, no packing) */
+inline int block_pack_mode(int layout) {
+  return layout == layout_lower ? 0 : layout == layout_sym ? 1 : layout == layout_diag ? 2 : -1;
+}
+
+/** column grain for the host pool: about 2^18 elements per task */
+inline size_t col_grain(int rows) { return std::max<size_t>(1, (size_t(1) << 18) / size_t(rows > 0 ? rows : 1)); }
+
+/** Index in host_blocks_ of the block whose elements are exactly d[0..n)
+ * (column-major rows x cols) by the block's layout, or -1.  The full pointer
+ * check runs on every call (a caller may have replaced single elements); it
+ * is one parallel read of n pointers. */
+inline long recognise_block_index(const var* d, size_t n, int rows, int cols) {
+  if (n == 0) return -1;
   auto& blocks = ChainableStack::instance_->host_blocks_;
   const vari* v0 = d[0].vi_;
   for (size_t k = blocks.size(); k-- > 0;) {
     const host_block& b = blocks[k];
     if (b.first != v0) continue;
-    if (b.n != n || b.rows != rows || b.cols != cols) return nullptr;
-    const vari* first = b.first;
-    const vari* dummy = b.dummy;
+    if (b.rows != rows || b.cols != cols || size_t(rows) * size_t(cols) != n) return -1;
     const size_t r = size_t(rows);
-    const bool ok = host_parallel_all(n, [&](size_t lo, size_t hi) {
-      if (!dummy) {
-        for (size_t i = lo; i < hi; ++i)
-          if (d[i].vi_ != first + i) return false;
-        return true;
-      }
-      for (size_t i = lo; i < hi; ++i) {
-        const size_t row = i % r, col = i / r;
-        if (d[i].vi_ != (row >= col ? first + i : dummy)) return false;
-      }
-      return true;
-    });
-    return ok ? static_cast<dev_matrix_vari*>(b.node) : nullptr;
+    const bool ok = host_parallel_all(
+        size_t(cols),
+        [&](size_t j0, size_t j1) {
+          bool good = true;
+          for (size_t j = j0; good && j < j1; ++j) {
+            const var* col = d + j * r;
+            block_column(b, j, [&](size_t i, vari* v) { good &= col[i].vi_ == v; });
+          }
+          return good;
+        },
+        col_grain(rows));
+    return ok ? long(k) : -1;
   }
-  return nullptr;
+  return -1;
+}
+inline dev_matrix_vari* recognise_block(const var* d, size_t n, int rows, int cols) {
+  const long k = recognise_block_index(d, n, rows, cols);
+  return k < 0 ? nullptr : static_cast<dev_matrix_vari*>(ChainableStack::instance_->host_blocks_[size_t(k)].node);
+}
+
+/** Write block b's element varis into d (column-major rows x cols). */
+inline void fill_block_pointers(const host_block& b, var* d) {
+  const size_t r = size_t(b.rows);
+  host_parallel_for(
+      size_t(b.cols),
+      [&](size_t j0, size_t j1) {
+        for (size_t j = j0; j < j1; ++j) {
+          var* col = d + j * r;
+          block_column(b, j, [&](size_t i, vari* v) { col[i].vi_ = v; });
+        }
+      },
+      col_grain(b.rows));
 }
 
 // The bridge of a host block: in the reverse sweep, the host adjoints of the
-// block's varis are gathered into the device node's adjoint -- unless no node
-// chained after the block touched them (device consumers of the recognised
-// node add into its device adjoint directly) and no device->host pending
-// adjoint landed in it, in which case they are all still zero.
+// varis the block owns are gathered into the device node's adjoint (packed
+// layouts into the lower triangle / the diagonal) -- unless no node chained
+// after the block touched them (device consumers of the recognised node add
+// into its device adjoint directly) and no device->host pending adjoint
+// landed in it, in which case they are all still zero.  A shared vari (a
+// symmetric block's (i, j) = (j, i), add_diag's off-diagonal elements) is
+// gathered once, by the block that owns it.
 class dev_to_host_vari : public vari {
  public:
   size_t blk_;  // index in host_blocks_
@@ -235,6 +328,7 @@ class dev_to_host_vari : public vari {
     ran_ = st->sweep_;
     wrote_ = false;
     const host_block b = st->host_blocks_[blk_];
+    if (!b.n) return;
     const vari* lo = b.first;
     const vari* hi = b.first + b.n;
     bool touched = b.dirty;
@@ -245,65 +339,160 @@ class dev_to_host_vari : public vari {
     smg_ctx* c = amd::ctx();
     double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
     if (!stage) throw std::bad_alloc();
-    const size_t r = size_t(b.rows);
-    const bool lower = b.dummy != nullptr;
     host_parallel_for(b.n, [&](size_t s, size_t e) {
-      for (size_t i = s; i < e; ++i) stage[i] = (!lower || i % r >= i / r) ? b.first[i].adj_ : 0.0;
+      for (size_t i = s; i < e; ++i) stage[i] = b.first[i].adj_;
     });
     double* dst = amd::alloc_doubles(b.n);
     auto* node = static_cast<dev_matrix_vari*>(b.node);
     amd::check(smg_memcpy_h2d(c, dst, stage, b.n * sizeof(double)), "to_host");
-    amd::check(smg_axpy(c, (long long)b.n, 1.0, dst, 1, node->adj_, 1), "to_host");
+    const int mode = block_pack_mode(b.layout);
+    if (mode < 0)
+      amd::check(smg_axpy(c, (long long)b.n, 1.0, dst, 1, node->adj_, 1), "to_host");
+    else
+      amd::check(smg_unpack_tril_add(c, mode, mode == 2 ? int(b.n) : b.rows, dst, node->adj_, b.rows), "to_host");
     amd::check(smg_sync(c), "to_host");  // the staging buffer is reused by the next host copy
   }
 };
 
-/**
- * Materialise device node m as n contiguous host varis (off every stack; the
- * tape's host_blocks_ owns them) plus one bridge vari on var_stack_.  The
- * values come down in chunks (one marker each); the host constructs chunk k's
- * varis in parallel while chunk k+1 is in flight, after running `overlap`
- * (work that needs the block's addresses but not its values: the caller's
- * pointer array) while the first chunk transfers.  Returns the block
- * (element i = first + i; a lower-structured node's strict upper triangle is
- * the one dummy vari, like cholesky_decompose.hpp:34-48).
- */
-inline const host_block& materialise(dev_matrix_vari* m,
-                                     const std::function<void(vari* first, vari* dummy)>& overlap = nullptr) {
+/** After a sweep (grad.hpp): every host block from index `from` on gets its
+ * device node's adjoint written into the varis it owns -- what the
+ * reference's varis hold after grad(): a symmetric block's shared vari the
+ * sum of both elements' adjoints, a Cholesky factor's varis the partials its
+ * consumers wrote (a closed-form reverse never formed them: expand_adjoint). */
+inline void publish_block_adjoints(size_t from) {
   auto* st = ChainableStack::instance_;
-  const size_t n = m->size();
-  vari* first = static_cast<vari*>(st->memalloc_.alloc((n ? n : 1) * sizeof(vari)));
-  const bool lower = m->structure_ == dev_structure::lower;
-  vari* dummy = lower ? new vari(0.0, vari::unstacked_tag{}) : nullptr;
-  if (n) {
-    smg_ctx* c = amd::ctx();
-    int armed = 0;
-    amd::check(smg_status_armed(c, &armed), "to_host");
-    double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
+  if (from >= st->host_blocks_.size() || !amd::has_ctx()) return;
+  smg_ctx* c = amd::ctx();
+  join_device_adjoints();
+  for (size_t k = from; k < st->host_blocks_.size(); ++k) {
+    const host_block b = st->host_blocks_[k];
+    if (!b.n) continue;
+    auto* node = static_cast<dev_matrix_vari*>(b.node);
+    if (node->sink_) node->sink_->expand_adjoint();
+    const double* src = node->adj_;
+    const int mode = block_pack_mode(b.layout);
+    if (mode >= 0) {
+      double* t = amd::alloc_doubles(b.n);
+      amd::check(smg_pack_tril(c, mode, mode == 2 ? int(b.n) : b.rows, node->adj_, b.rows, t), "grad");
+      src = t;
+    }
+    double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
     if (!stage) throw std::bad_alloc();
-    const int nch = n >= (size_t(1) << 21) ? 8 : 1;
-    const size_t chunk = (n + size_t(nch) - 1) / size_t(nch);
-    if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(stage + n)), "to_host");
-    for (int k = 0; k < nch; ++k) {
-      const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
-      amd::check(smg_memcpy_d2h(c, stage + b, m->val_ + b, (e - b) * sizeof(double)), "to_host");
-      amd::check(smg_marker_record(c, k), "to_host");
-    }
-    if (overlap) overlap(first, dummy);
-    for (int k = 0; k < nch; ++k) {
-      const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
-      amd::check(smg_marker_wait(c, k), "to_host");
-      if (k == 0 && armed) amd::throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
-      host_parallel_for(e - b, [&](size_t s0, size_t s1) {
-        for (size_t i = b + s0; i < b + s1; ++i) ::new (static_cast<void*>(first + i)) vari(stage[i], vari::unstacked_tag{});
-      });
-    }
-  } else if (overlap) {
-    overlap(first, dummy);
+    amd::check(smg_memcpy_d2h(c, stage, src, b.n * sizeof(double)), "grad");
+    amd::check(smg_sync(c), "grad");
+    host_parallel_for(b.n, [&](size_t s, size_t e) {
+      for (size_t i = s; i < e; ++i) b.first[i].adj_ = stage[i];
+    });
   }
-  st->host_blocks_.push_back(host_block{first, n, m, dummy, m->rows_, m->cols_, false});
+}
+
+/** n varis constructed in place at first from values streamed device->host:
+ * `src` (device, n doubles) comes down in chunks (one marker each) and the
+ * host constructs chunk k's varis in parallel while chunk k+1 is in flight,
+ * after running `overlap` while the first chunk transfers. */
+inline void stream_varis(vari* first, const double* src, size_t n, const std::function<void()>& overlap) {
+  if (!n) {
+    if (overlap) overlap();
+    return;
+  }
+  smg_ctx* c = amd::ctx();
+  int armed = 0;
+  amd::check(smg_status_armed(c, &armed), "to_host");
+  double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
+  if (!stage) throw std::bad_alloc();
+  const int nch = n >= (size_t(1) << 21) ? 8 : 1;
+  const size_t chunk = (n + size_t(nch) - 1) / size_t(nch);
+  if (armed) amd::check(smg_status_enqueue(c, reinterpret_cast<int*>(stage + n)), "to_host");
+  for (int k = 0; k < nch; ++k) {
+    const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
+    amd::check(smg_memcpy_d2h(c, stage + b, src + b, (e - b) * sizeof(double)), "to_host");
+    amd::check(smg_marker_record(c, k), "to_host");
+  }
+  if (overlap) overlap();
+  for (int k = 0; k < nch; ++k) {
+    const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
+    amd::check(smg_marker_wait(c, k), "to_host");
+    if (k == 0 && armed) amd::throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
+    host_parallel_for(e - b, [&](size_t s0, size_t s1) {
+      for (size_t i = b + s0; i < b + s1; ++i) ::new (static_cast<void*>(first + i)) vari(stage[i], vari::unstacked_tag{});
+    });
+  }
+}
+
+/** Register block b (its bridge vari on var_stack_) and return its index. */
+inline size_t push_block(const host_block& b) {
+  auto* st = ChainableStack::instance_;
+  st->host_blocks_.push_back(b);
+  st->publish_ = &publish_block_adjoints;
   new dev_to_host_vari(st->host_blocks_.size() - 1);
-  return st->host_blocks_.back();
+  return st->host_blocks_.size() - 1;
+}
+
+/**
+ * Materialise device node m as host varis (off every stack; the tape's
+ * host_blocks_ owns them) plus one bridge vari on var_stack_, with the
+ * reference's vari identity for m's structure: a lower-structured node (a
+ * Cholesky factor) owns its lower triangle's varis, the strict upper being
+ * one dummy (cholesky_decompose.hpp:34-48); a symmetric one (gp_exp_quad_cov)
+ * one vari per (i, j), (j, i) pair (gp_exp_quad_cov.hpp:235); any other node
+ * one vari per element.  Only the owned values cross PCIe (packed on the
+ * device first).  `overlap` runs while the first chunk of values transfers
+ * (work that needs the block's addresses but not its values: the caller's
+ * pointer array).  Returns the block's index.
+ */
+inline size_t materialise(dev_matrix_vari* m, const std::function<void(const host_block&)>& overlap = nullptr) {
+  auto* st = ChainableStack::instance_;
+  host_block b{};
+  b.node = m;
+  b.rows = m->rows_;
+  b.cols = m->cols_;
+  b.dirty = false;
+  const bool square = m->rows_ == m->cols_;
+  b.layout = square && m->structure_ == dev_structure::lower       ? layout_lower
+             : square && m->structure_ == dev_structure::symmetric ? layout_sym
+                                                                   : layout_dense;
+  b.n = b.layout == layout_dense ? m->size() : tril_count(size_t(m->rows_));
+  b.first = static_cast<vari*>(st->memalloc_.alloc((b.n ? b.n : 1) * sizeof(vari)));
+  b.dummy = b.layout == layout_lower ? new vari(0.0, vari::unstacked_tag{}) : nullptr;
+  const double* src = m->val_;
+  if (b.layout != layout_dense && b.n) {
+    double* t = amd::alloc_doubles(b.n);
+    amd::check(smg_pack_tril(amd::ctx(), 0, b.rows, m->val_, b.rows, t), "to_host");
+    src = t;
+  }
+  stream_varis(b.first, src, b.n, [&] {
+    if (overlap) overlap(b);
+  });
+  return push_block(b);
+}
+
+/**
+ * add_diag's output at the Eigen boundary (prim/mat/fun/add_diag.hpp:25-27:
+ * a copy of mat whose diagonal gets new varis): device node B = mat +
+ * diag(d), whose elements off the diagonal are mat's own varis -- host block
+ * `base`'s, or base_elems (mat's pointers, column-major) when mat is no
+ * block -- and whose min(rows, cols) diagonal varis are new.  Returns the
+ * block's index.
+ */
+inline size_t materialise_diag(dev_matrix_vari* B, long base, vari* const* base_elems) {
+  auto* st = ChainableStack::instance_;
+  host_block b{};
+  b.node = B;
+  b.rows = B->rows_;
+  b.cols = B->cols_;
+  b.dirty = false;
+  b.layout = layout_diag;
+  b.base = base;
+  b.base_elems = base_elems;
+  b.n = size_t(std::min(B->rows_, B->cols_));
+  b.first = static_cast<vari*>(st->memalloc_.alloc((b.n ? b.n : 1) * sizeof(vari)));
+  b.dummy = nullptr;
+  if (b.n) {
+    double* t = amd::alloc_doubles(b.n);
+    amd::check(smg_pack_tril(amd::ctx(), 2, int(b.n), B->val_, b.rows, t), "add_diag");
+    stream_varis(b.first, t, b.n, nullptr);
+  }
+  return push_block(b);
 }
 
 // host varis -> device (reverse: device adjoint -> host adjoints)
@@ -357,10 +546,8 @@ inline dev_var_matrix to_dev(const std::vector<var>& v, int rows = -1, int cols 
 
 /** Device node -> host vars, column-major (bridged in the reverse sweep). */
 inline std::vector<var> to_var_vector(const dev_var_matrix& m) {
-  const host_block& b = internal::materialise(m.vi_);
-  std::vector<var> out(b.n);
-  const size_t r = size_t(b.rows);
-  for (size_t i = 0; i < b.n; ++i) out[i] = var((b.dummy && i % r < i / r) ? b.dummy : b.first + i);
+  std::vector<var> out(m.size());
+  internal::materialise(m.vi_, [&](const host_block& b) { internal::fill_block_pointers(b, out.data()); });
   return out;
 }
 

@@ -119,6 +119,7 @@ struct eig_in {
   size_t n = 0;
   int rows = 0, cols = 0;
   dev_matrix_vari* node = nullptr;
+  long block = -1;  // its host block's index
 };
 template <int R, int C, int O, int MR, int MC>
 inline eig_in prepare(const Eigen::Matrix<var, R, C, O, MR, MC>& m, const char* nan_fn = nullptr,
@@ -128,7 +129,8 @@ inline eig_in prepare(const Eigen::Matrix<var, R, C, O, MR, MC>& m, const char* 
   e.n = size_t(m.size());
   e.rows = int(m.rows());
   e.cols = int(m.cols());
-  e.node = recognise_block(e.vd, e.n, e.rows, e.cols);
+  e.block = recognise_block_index(e.vd, e.n, e.rows, e.cols);
+  if (e.block >= 0) e.node = static_cast<dev_matrix_vari*>(ChainableStack::instance_->host_blocks_[size_t(e.block)].node);
   if (nan_fn) {
     if (e.node) {
       smg_ctx* c = amd::ctx();
@@ -170,17 +172,9 @@ template <int R = Eigen::Dynamic, int C = Eigen::Dynamic>
 inline Eigen::Matrix<var, R, C> to_host_matrix(const dev_var_matrix& m) {
   Eigen::Matrix<var, R, C> out(m.rows(), m.cols());
   var* d = out.data();
-  const size_t n = m.size(), r = size_t(m.rows());
   // the pointer array needs only the block's addresses: filled while the
   // values are in flight
-  internal::materialise(m.vi_, [&](vari* first, vari* dummy) {
-    internal::host_parallel_for(n, [&](size_t s, size_t e) {
-      if (!dummy)
-        for (size_t i = s; i < e; ++i) d[i].vi_ = first + i;
-      else
-        for (size_t i = s; i < e; ++i) d[i].vi_ = i % r >= i / r ? first + i : dummy;
-    });
-  });
+  internal::materialise(m.vi_, [&](const host_block& b) { internal::fill_block_pointers(b, d); });
   return out;
 }
 
@@ -302,15 +296,43 @@ inline var sum(const Eigen::Matrix<var, R, C>& m) {
  * (:20-29) or a vector of min(rows, cols) entries (:42-55), mat and to_add
  * var or double in any combination, mat rectangular or square.
  */
+namespace internal {
+/** add_diag's Eigen output: mat's own varis off the diagonal, new ones on it
+ * (prim/mat/fun/add_diag.hpp:25-27: mat_out(mat), then diagonal() +=);
+ * B is the device node of mat + diag(to_add).  A double mat has no varis to
+ * share: every element is new, as the reference's var(double) conversions. */
+template <typename T_m>
+inline matrix_v add_diag_output(const Eigen::Matrix<T_m, Eigen::Dynamic, Eigen::Dynamic>& mat, const eig_in& em,
+                                const dev_var_matrix& B) {
+  if constexpr (!is_var<T_m>::value) {
+    return to_host_matrix(B);
+  } else {
+    matrix_v out(mat.rows(), mat.cols());
+    const long base = em.block;
+    vari** elems = nullptr;
+    if (base < 0 && em.n) {  // mat is no block: its pointers, for recognising the output later
+      elems = ChainableStack::instance_->memalloc_.alloc_array<vari*>(em.n);
+      host_parallel_for(em.n, [&](size_t s, size_t e) {
+        for (size_t i = s; i < e; ++i) elems[i] = em.vd[i].vi_;
+      });
+    }
+    const size_t k = materialise_diag(B.vi_, base, elems);
+    fill_block_pointers(ChainableStack::instance_->host_blocks_[k], out.data());
+    return out;
+  }
+}
+}  // namespace internal
+
 template <typename T_m, typename T_a,
           typename = std::enable_if_t<internal::is_ad_scalar<T_m>::value && internal::is_ad_scalar<T_a>::value &&
                                       internal::any_var<T_m, T_a>::value>>
 inline matrix_v add_diag(const Eigen::Matrix<T_m, Eigen::Dynamic, Eigen::Dynamic>& mat, const T_a& to_add) {
-  const internal::dev_operand a = internal::commit(internal::prepare(mat));
+  const internal::eig_in em = internal::prepare(mat);
+  const internal::dev_operand a = internal::commit(em);
   if constexpr (internal::is_var<T_a>::value)
-    return to_host_matrix(internal::add_diag_dev(a, to_add.val(), to_add.vi_, {}));
+    return internal::add_diag_output(mat, em, internal::add_diag_dev(a, to_add.val(), to_add.vi_, {}));
   else
-    return to_host_matrix(internal::add_diag_dev(a, double(to_add), nullptr, {}));
+    return internal::add_diag_output(mat, em, internal::add_diag_dev(a, double(to_add), nullptr, {}));
 }
 template <typename T_m, typename T_a, int R, int C,
           typename = std::enable_if_t<internal::is_ad_scalar<T_m>::value && internal::is_ad_scalar<T_a>::value &&
@@ -331,7 +353,7 @@ inline matrix_v add_diag(const Eigen::Matrix<T_m, Eigen::Dynamic, Eigen::Dynamic
   internal::dev_operand d = internal::commit(ed);
   d.rows = int(d.size());
   d.cols = 1;
-  return to_host_matrix(internal::add_diag_dev(a, 0.0, nullptr, d));
+  return internal::add_diag_output(mat, em, internal::add_diag_dev(a, 0.0, nullptr, d));
 }
 
 template <int R, int C>
@@ -355,7 +377,8 @@ template <int TriView, typename T1, int R1, int C1, typename T2, int R2, int C2,
 inline Eigen::Matrix<var, R1, C2> mdivide_left_tri(const Eigen::Matrix<T1, R1, C1>& A,
                                                    const Eigen::Matrix<T2, R2, C2>& b) {
   internal::check_square("mdivide_left_tri", "A", int(A.rows()), int(A.cols()));
-  internal::check_multiplicable("mdivide_left_tri", int(A.rows()), int(A.cols()), int(b.rows()), int(b.cols()));
+  internal::check_multiplicable("mdivide_left_tri", int(A.rows()), int(A.cols()), int(b.rows()), int(b.cols()), "A",
+                                "b");
   const internal::dev_operand a = internal::commit(internal::prepare(A));
   const internal::dev_operand bb = internal::commit(internal::prepare(b));
   return to_host_matrix<R1, C2>(internal::mdivide_left_tri_dev<TriView>(a, bb));
@@ -363,6 +386,56 @@ inline Eigen::Matrix<var, R1, C2> mdivide_left_tri(const Eigen::Matrix<T1, R1, C
 template <int TriView, int R, int C>
 inline Eigen::Matrix<var, R, C> mdivide_left_tri(const Eigen::Matrix<var, R, C>& A) {
   return to_host_matrix<R, C>(mdivide_left_tri<TriView>(to_dev(A)));
+}
+/** prim/mat/fun/mdivide_left_tri.hpp:25-44 on data (host, Eigen's triangular solve) */
+template <int TriView, int R1, int C1, int R2, int C2>
+inline Eigen::Matrix<double, R1, C2> mdivide_left_tri(const Eigen::Matrix<double, R1, C1>& A,
+                                                      const Eigen::Matrix<double, R2, C2>& b) {
+  internal::check_square("mdivide_left_tri", "A", int(A.rows()), int(A.cols()));
+  internal::check_multiplicable("mdivide_left_tri", int(A.rows()), int(A.cols()), int(b.rows()), int(b.cols()), "A",
+                                "b");
+  return A.template triangularView<Eigen::UpLoType(TriView)>().solve(b);
+}
+
+/** mdivide_left_tri_low(A, b) = mdivide_left_tri<Lower>(A, b) after the
+ * reference's own checks (prim/mat/fun/mdivide_left_tri_low.hpp:33-47), and
+ * the one-argument form tril(A)^{-1} -- the name Stan-generated code emits. */
+template <typename T1, int R1, int C1, typename T2, int R2, int C2,
+          typename = std::enable_if_t<internal::is_ad_scalar<T1>::value && internal::is_ad_scalar<T2>::value>>
+inline auto mdivide_left_tri_low(const Eigen::Matrix<T1, R1, C1>& A, const Eigen::Matrix<T2, R2, C2>& b) {
+  internal::check_square("mdivide_left_tri_low", "A", int(A.rows()), int(A.cols()));
+  internal::check_multiplicable("mdivide_left_tri_low", int(A.rows()), int(A.cols()), int(b.rows()), int(b.cols()),
+                                "A", "b");
+  return mdivide_left_tri<Eigen::Lower>(A, b);
+}
+template <typename T, int R1, int C1, typename = std::enable_if_t<internal::is_ad_scalar<T>::value>>
+inline Eigen::Matrix<T, R1, C1> mdivide_left_tri_low(const Eigen::Matrix<T, R1, C1>& A) {
+  internal::check_square("mdivide_left_tri_low", "A", int(A.rows()), int(A.cols()));
+  if constexpr (internal::is_var<T>::value) {
+    return mdivide_left_tri<Eigen::Lower>(A);
+  } else {
+    const Eigen::Matrix<double, R1, C1> I = Eigen::Matrix<double, R1, C1>::Identity(A.rows(), A.cols());
+    return A.template triangularView<Eigen::Lower>().solve(I);
+  }
+}
+
+/** mdivide_right_tri_low(b, A) = b tril(A)^{-1} (prim/mat/fun/
+ * mdivide_right_tri_low.hpp:25-31 -> mdivide_right_tri<Lower>,
+ * prim/mat/fun/mdivide_right_tri.hpp:28-48: check_square, then
+ * check_multiplicable(b, A)).  On the device as (tril(A)^{-T} b^T)^T: the
+ * transposes are Eigen pointer copies (they share the varis, as the
+ * reference's transpose does), the solve is mdivide_left_tri<Upper>. */
+template <typename T1, int R1, int C1, typename T2, int R2, int C2,
+          typename = std::enable_if_t<internal::is_ad_scalar<T1>::value && internal::is_ad_scalar<T2>::value>>
+inline auto mdivide_right_tri_low(const Eigen::Matrix<T1, R1, C1>& b, const Eigen::Matrix<T2, R2, C2>& A) {
+  internal::check_square("mdivide_right_tri", "A", int(A.rows()), int(A.cols()));
+  internal::check_multiplicable("mdivide_right_tri", int(b.rows()), int(b.cols()), int(A.rows()), int(A.cols()), "b",
+                                "A");
+  using R = std::conditional_t<internal::any_var<T1, T2>::value, var, double>;
+  const Eigen::Matrix<T2, C2, R2> At = A.transpose();
+  const Eigen::Matrix<T1, C1, R1> bt = b.transpose();
+  const Eigen::Matrix<R, C2, R1> xt = mdivide_left_tri<Eigen::Upper>(At, bt);
+  return Eigen::Matrix<R, R1, C2>(xt.transpose());
 }
 
 // ------------------------------------------------ §8(f) row 3 (spd_functors.hpp)

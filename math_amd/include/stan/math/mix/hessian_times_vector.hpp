@@ -30,6 +30,7 @@ template <typename F>
 void hessian_times_vector(const F& f, const std::vector<double>& x, const std::vector<double>& v,
                           double& fx, std::vector<double>& Hv) {
   start_nested();
+  no_publish_scope quiet;
   try {
     std::vector<var> x_var(x.begin(), x.end());
     std::vector<fvar<var>> x_fvar(x.size());
@@ -53,6 +54,7 @@ void hessian_times_vector(const F& f, const Eigen::Matrix<double, Eigen::Dynamic
                           const Eigen::Matrix<double, Eigen::Dynamic, 1>& v, double& fx,
                           Eigen::Matrix<double, Eigen::Dynamic, 1>& Hv) {
   start_nested();
+  no_publish_scope quiet;
   try {
     const Eigen::Index n = x.size();
     Eigen::Matrix<var, Eigen::Dynamic, 1> x_var(n);
@@ -91,6 +93,7 @@ void hessian(const F& f, const Eigen::Matrix<double, Eigen::Dynamic, 1>& x, doub
   if (n == 0) {  // (:45-48): the value at the empty input (evaluated at fvar<var>,
                  // so functors need not instantiate at double)
     start_nested();
+    no_publish_scope quiet;
     try {
       fx = f(Eigen::Matrix<fvar<var>, Eigen::Dynamic, 1>(0)).val_.val();
     } catch (const std::exception&) {
@@ -102,6 +105,7 @@ void hessian(const F& f, const Eigen::Matrix<double, Eigen::Dynamic, 1>& x, doub
   }
   for (Eigen::Index i = 0; i < n; ++i) {
     start_nested();
+    no_publish_scope quiet;
     try {
       Eigen::Matrix<var, Eigen::Dynamic, 1> x_var(n);
       Eigen::Matrix<fvar<var>, Eigen::Dynamic, 1> x_fvar(n);

@@ -40,16 +40,31 @@ struct pending_adjoint {
   vari* target;       // host vari whose adj_ receives the value
   const double* src;  // device scalar
 };
-/** A device matrix node materialised as host varis (stan/math/eigen/bridge.hpp):
- * n contiguous nochain varis in the arena, column-major, registered here
- * instead of on var_nochain_stack_ (zeroed by set_zero_all_adjoints). */
+/** A device matrix node materialised as host varis (stan/math/amd/matrix.hpp):
+ * the n varis the block owns, contiguous in the arena, registered here
+ * instead of on var_nochain_stack_ (zeroed by set_zero_all_adjoints).  Which
+ * vari stands at element (i, j) follows the reference's vari identity for the
+ * producing function (layout; stan/math/amd/matrix.hpp block_elem):
+ *   0 dense  every element its own vari, column-major (n = rows cols);
+ *   1 lower  a cholesky_decompose factor: the lower triangle packed column by
+ *            column (n = rows (rows + 1) / 2), the strict upper one dummy vari
+ *            (rev/mat/fun/cholesky_decompose.hpp:34-48);
+ *   2 sym    a gp_exp_quad_cov matrix: the lower triangle packed, (i, j) and
+ *            (j, i) one vari (rev/mat/fun/gp_exp_quad_cov.hpp:235);
+ *   3 diag   add_diag's output: n = min(rows, cols) new diagonal varis, every
+ *            other element the input's own vari (prim/mat/fun/add_diag.hpp:25-27)
+ *            -- block `base`'s, or base_elems[i + j rows] when the input was
+ *            no block. */
 struct host_block {
-  vari* first;   // element i is first + i (a lower-structured node: i on or below the diagonal)
+  vari* first;   // the owned varis
   size_t n;
   void* node;    // the dev_matrix_vari it mirrors
-  vari* dummy;   // the shared vari of a lower-structured node's upper triangle, else null
+  vari* dummy;   // layout 1: the strict upper triangle's one vari, else null
   int rows, cols;
   bool dirty;    // a landed device->host pending adjoint targeted one of its varis
+  int layout = 0;
+  long base = -1;
+  vari* const* base_elems = nullptr;
 };
 
 template <typename ChainableT, typename ChainableAllocT>
@@ -78,6 +93,13 @@ struct AutodiffStackSingleton {
     // reverse sweeps started on this tape (grad()): a structured adjoint a
     // node deposits is valid for the sweep that deposited it only
     size_t sweep_ = 0;
+    // after a sweep, publish_ (set once a host block exists: stan/math/amd/
+    // matrix.hpp) writes every host block's device adjoint into its varis, so
+    // they read what the reference's would; no_publish_ > 0 while a functional
+    // that reads only its independent variables runs its sweeps (gradient(),
+    // hessian(), hessian_times_vector(), map_rect's jobs, var::grad(x, g))
+    void (*publish_)(size_t from) = nullptr;
+    int no_publish_ = 0;
   };
 
   AutodiffStackSingleton() : own_instance_(init()) {}

@@ -113,7 +113,18 @@ static void grad(vari* vi) {
     (*it)->chain();
   }
   flush_pending(true);
+  if (st->publish_ && st->no_publish_ == 0) st->publish_(empty_nested() ? 0 : st->nested_host_block_sizes_.back());
 }
+
+/** While alive, sweeps leave the host blocks' varis unpublished (their
+ * device adjoints stay on the device): for callers that read only their
+ * independent variables' adjoints and then recover the tape. */
+struct no_publish_scope {
+  no_publish_scope() { ++ChainableStack::instance_->no_publish_; }
+  ~no_publish_scope() { --ChainableStack::instance_->no_publish_; }
+  no_publish_scope(const no_publish_scope&) = delete;
+  no_publish_scope& operator=(const no_publish_scope&) = delete;
+};
 
 static inline void start_nested() {
   auto* st = ChainableStack::instance_;

@@ -30,8 +30,12 @@ class var {
   inline double adj() const { return vi_->adj_; }
 
   /** Reverse sweep from this variable; fills g with the adjoints of x
-   * (var.hpp:318-329): recovers memory afterwards, like the reference. */
+   * (var.hpp:318-324; does not recover memory).  This is the reference's
+   * log_prob_grad path, which reads only x and recovers the tape next: the
+   * host blocks of an Eigen boundary are not published (grad() publishes
+   * them, grad.hpp). */
   void grad(std::vector<var>& x, std::vector<double>& g) {
+    no_publish_scope quiet;
     stan::math::grad(vi_);
     g.resize(x.size());
     for (size_t i = 0; i < x.size(); ++i) g[i] = x[i].vi_->adj_;

@@ -50,7 +50,7 @@ class gp_exp_quad_cov_dev_vari : public device_vari {
         l_d_(l),
         sigma_vi_(sigma_vi),
         l_vi_(l_vi),
-        K_(new dev_matrix_vari(n, n)),
+        K_(new dev_matrix_vari(n, n, dev_structure::symmetric)),
         out2_(amd::alloc_doubles(2)) {
     amd::check(smg_gp_exp_quad_cov_nd_fwd(amd::ctx(), x_, D_, n_, sigma_d_, l_d_, K_->val_, n_), "gp_exp_quad_cov");
   }

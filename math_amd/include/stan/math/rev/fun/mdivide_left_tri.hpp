@@ -47,7 +47,7 @@ template <int TriView>
 inline dev_var_matrix mdivide_left_tri_dev(const dev_operand& A, const dev_operand& B) {
   static_assert(TriView == 1 || TriView == 2, "TriView must be Eigen::Lower or Eigen::Upper");
   check_square("mdivide_left_tri", "A", A.rows, A.cols);
-  check_multiplicable("mdivide_left_tri", A.rows, A.cols, B.rows, B.cols);
+  check_multiplicable("mdivide_left_tri", A.rows, A.cols, B.rows, B.cols, "A", "b");
   auto* node = new mdivide_left_tri_dev_vari(TriView == 1 ? 1 : 0, A, B);
   return dev_var_matrix(node->C_);
 }

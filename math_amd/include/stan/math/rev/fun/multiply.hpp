@@ -27,15 +27,30 @@ namespace math {
 
 namespace internal {
 
-inline void check_multiplicable(const char* fn, int a_rows, int a_cols, int b_rows, int b_cols) {
-  (void)a_rows;
-  (void)b_cols;
+/** check_positive(function, name, expr, size) (prim/scal/err/check_positive.hpp:68-77) */
+inline void check_positive_size(const char* fn, const char* name, const char* expr, int size) {
+  if (size <= 0) {
+    std::ostringstream m;
+    m << fn << ": " << name << " must have a positive size, but is " << size << "; dimension size expression = "
+      << expr;
+    throw std::invalid_argument(m.str());
+  }
+}
+
+/** check_multiplicable(function, name1, y1, name2, y2)
+ * (prim/mat/err/check_multiplicable.hpp:30-38), in its order: positive
+ * rows of y1 and columns of y2, the size match, positive columns of y1. */
+inline void check_multiplicable(const char* fn, int a_rows, int a_cols, int b_rows, int b_cols,
+                                const char* na = "A", const char* nb = "B") {
+  check_positive_size(fn, na, "rows()", a_rows);
+  check_positive_size(fn, nb, "cols()", b_cols);
   if (a_cols != b_rows) {
     std::ostringstream m;
-    m << fn << ": Columns of A (" << a_cols << ") and Rows of B (" << b_rows
+    m << fn << ": Columns of " << na << " (" << a_cols << ") and Rows of " << nb << " (" << b_rows
       << ") must match in size";
     throw std::invalid_argument(m.str());
   }
+  check_positive_size(fn, na, "cols()", a_cols);
 }
 
 class multiply_dev_vari : public device_vari {

@@ -32,6 +32,7 @@ template <typename F, typename Vec>
 void gradient(const F& f, const Vec& x, double& fx, Vec& grad_fx) {
   using VarVec = typename internal::var_vector_of<Vec>::type;
   start_nested();
+  no_publish_scope quiet;  // (the tape is recovered before anyone could read a block)
   try {
     // the independent variables are leaves (their chain() is a no-op): they
     // go on the no-chain stack, so the reverse sweep makes no call for them;
@@ -61,6 +62,7 @@ void gradient(const F& f, const Vec& x, double& fx, Vec& grad_fx) {
 template <typename F>
 void gradient(const F& f, const dev_data<double>& x, double& fx, double* grad_dev) {
   start_nested();
+  no_publish_scope quiet;  // (the tape is recovered before anyone could read a block)
   try {
     smg_ctx* c = amd::ctx();
     auto* leaf = new dev_matrix_vari(x.rows(), x.cols());

@@ -134,6 +134,7 @@ Eigen::MatrixXd map_rect_reduce_job(const Eigen::VectorXd& shared, const Eigen::
   const Eigen::Index ns = SV ? shared.size() : 0, nj = JV ? job.size() : 0;
   Eigen::MatrixXd out(1 + ns + nj, 0);
   start_nested();
+  no_publish_scope quiet;  // (the job reads only its leaves' adjoints)
   try {
     vector_var s_v(shared.size()), j_v(job.size());
     for (Eigen::Index i = 0; i < shared.size(); ++i) s_v(i) = shared(i);

@@ -1511,6 +1511,27 @@ static void fix_boundary() {
     }
     write_fixture("gp_nd_D3_N" + std::to_string(N), j);
   }
+  // intermediate adjoints and vari identity after a top-level lp.grad()
+  // (bnd::run_gp_intermediate): the config-3 inputs at N = 64 (variants 0-2)
+  // and N = 256 (variants 0, 1)
+  for (int N : {64, 256}) {
+    std::vector<double> x;
+    VectorXd y;
+    gp_inputs(N, x, y);
+    const double th[3] = {1.0, 1.5, 0.3};
+    Json j;
+    j.put_str("what", "after lp.grad() of the Stan-codegen GP marginal (K = gp_exp_quad_cov(x, th0, th1), Kd = add_diag(K, th2^2), L = cholesky_decompose(Kd), lp = multi_normal_cholesky_lpdf(y | 0, L); variant 1 + host uses of L, variant 2 + host uses of K and Kd's diagonal): v<k> = [grad th | K adj lower packed | Kd diag adj | L adj lower packed | L val lower packed | K sym-shared, Kd shares K, Kd diag new, L upper dummy, #varis K, #varis K+Kd, #varis L]");
+    j.put_int("N", N);
+    j.put_vec("x", x);
+    j.put_vec("y", y);
+    j.put_vec("theta", std::vector<double>(th, th + 3));
+    for (int v = 0; v < (N == 64 ? 3 : 2); ++v)
+      bnd::run_gp_intermediate(x, y, th, v, [&](const std::string&, double f, const std::vector<double>& out) {
+        j.put("fx_v" + std::to_string(v), f);
+        j.put_vec("v" + std::to_string(v), out);
+      });
+    write_fixture("gp_intermediate_N" + std::to_string(N), j);
+  }
 }
 
 // ------------------------------------------------------------------ bench

@@ -23,6 +23,7 @@
 
 #include <functional>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 namespace bnd {
@@ -340,6 +341,76 @@ inline void run_form_cases(const form_inputs& in, const emit_fn& emit) {
     f.grad();
     finish(emit, "mvn_arr_chol", f, grads().add(S));
   }
+  // ---- mdivide_left_tri_low / mdivide_right_tri_low, the names Stan-generated
+  // code emits (prim/mat/fun/mdivide_left_tri_low.hpp:33-47,
+  // mdivide_right_tri_low.hpp:25-31): L s x s (its strict upper is ignored),
+  // b s x 2 / 2 x s
+  {
+    using stan::math::mdivide_left_tri_low;
+    using stan::math::mdivide_right_tri_low;
+    MV L = mat<var, -1, -1>(in.S, s, s);  // a full matrix: only its lower triangle is read
+    MV b = mat<var, -1, -1>(in.ys, s, 2);
+    MV out = mdivide_left_tri_low(L, b);
+    var f = wsum(out, in.W);
+    f.grad();
+    finish(emit, "mdl_tri_low_vv", f, grads().add(L).add(b));
+  }
+  {
+    using stan::math::mdivide_left_tri_low;
+    MD L = mat<double, -1, -1>(in.S, s, s);
+    VV b = mat<var, -1, 1>(in.ys, s, 1);
+    VV out = mdivide_left_tri_low(L, b);
+    var f = wsum(out, in.W);
+    f.grad();
+    finish(emit, "mdl_tri_low_dv", f, grads().add(b));
+  }
+  {
+    using stan::math::mdivide_left_tri_low;
+    MV L = mat<var, -1, -1>(in.S, s, s);
+    MD b = mat<double, -1, -1>(in.ys, s, 2);
+    MV out = mdivide_left_tri_low(L, b);
+    var f = wsum(out, in.W);
+    f.grad();
+    finish(emit, "mdl_tri_low_vd", f, grads().add(L));
+  }
+  {
+    using stan::math::mdivide_left_tri_low;
+    MV L = mat<var, -1, -1>(in.S, s, s);
+    MV out = mdivide_left_tri_low(L);
+    var f = wsum(out, in.W);
+    f.grad();
+    finish(emit, "mdl_tri_low_inv", f, grads().add(L));
+  }
+  {
+    using stan::math::mdivide_right_tri_low;
+    MV b = mat<var, -1, -1>(in.ys, 2, s);
+    MV L = mat<var, -1, -1>(in.S, s, s);
+    MV out = mdivide_right_tri_low(b, L);
+    var f = wsum(out, in.W);
+    f.grad();
+    finish(emit, "mdr_tri_low_vv", f, grads().add(b).add(L));
+  }
+  {
+    using stan::math::mdivide_right_tri_low;
+    RV b = mat<var, 1, -1>(in.ys, 1, s);
+    MD L = mat<double, -1, -1>(in.S, s, s);
+    RV out = mdivide_right_tri_low(b, L);
+    var f = wsum(out, in.W);
+    f.grad();
+    finish(emit, "mdr_tri_low_rv_d", f, grads().add(b));
+  }
+  {
+    using stan::math::mdivide_left_tri_low;
+    using stan::math::mdivide_right_tri_low;
+    MD L = mat<double, -1, -1>(in.S, s, s);
+    MD b = mat<double, -1, -1>(in.ys, s, 2);
+    MD o1 = mdivide_left_tri_low(L, b);
+    MD o2 = mdivide_right_tri_low(MD(b.transpose()), L);
+    double f = 0.0;
+    for (int i = 0; i < o1.size(); ++i) f += in.W[size_t(i)] * o1(i) + 0.5 * in.W[size_t(i)] * o2(i);
+    emit("mdl_mdr_tri_low_dd", f, {});
+    stan::math::recover_memory();
+  }
 }
 
 // The Stan-codegen-shaped GP marginal: `matrix[N,N] K = ...` is an
@@ -379,6 +450,76 @@ struct gp_marginal {
     return multi_normal_cholesky_lpdf(ys[0], mu, L);
   }
 };
+
+/**
+ * What the varis of a Stan-codegen GP hold after a top-level lp.grad()
+ * (intermediate adjoints and vari identity at the Eigen boundary):
+ *   K = gp_exp_quad_cov(x, th0, th1)  (1-D x; rev/mat/fun/gp_exp_quad_cov.hpp:211-244:
+ *                                      K(i, j) and K(j, i) one vari)
+ *   Kd = add_diag(K, square(th2))      (prim/mat/fun/add_diag.hpp:25-27: K's varis
+ *                                      off the diagonal, new ones on it)
+ *   L = cholesky_decompose(Kd)         (rev/mat/fun/cholesky_decompose.hpp:378-427:
+ *                                      new lower varis, one dummy above)
+ *   lp = multi_normal_cholesky_lpdf(y | 0, L)
+ * variant 1 adds a host consumer of L (0.25 L(n-1, 0) + 0.5 L(n/2, n/4): the
+ * factor's adjoint then has a second writer), variant 2 host consumers of K's
+ * shared varis and of add_diag's own (0.5 K(1, 0) + 0.25 K(0, 1) + 0.125 Kd(2, 2)).
+ * emit("gpi", lp, [grad th (3) | K(i, j).adj() lower packed | Kd(i, i).adj() |
+ *                 L(i, j).adj() lower packed | L(i, j).val() lower packed |
+ *                 identity: K symmetric-shared, Kd shares K off the diagonal,
+ *                 Kd's diagonal new and distinct, L's strict upper one dummy,
+ *                 distinct varis in K, in K and Kd, in L]).
+ */
+inline void run_gp_intermediate(const std::vector<double>& x, const VD& y, const double* th3, int variant,
+                                const emit_fn& emit) {
+  using stan::math::add_diag;
+  using stan::math::cholesky_decompose;
+  using stan::math::gp_exp_quad_cov;
+  using stan::math::multi_normal_cholesky_lpdf;
+  using stan::math::square;
+  const int N = int(x.size());
+  VV th(3);
+  for (int i = 0; i < 3; ++i) th(i) = th3[i];
+  MV K = gp_exp_quad_cov(x, th(0), th(1));
+  MV Kd = add_diag(K, square(th(2)));
+  MV L = cholesky_decompose(Kd);
+  VD mu = VD::Zero(N);
+  var lp = multi_normal_cholesky_lpdf(y, mu, L);
+  if (variant == 1) lp = lp + 0.25 * L(N - 1, 0) + 0.5 * L(N / 2, N / 4);
+  if (variant == 2) lp = lp + 0.5 * K(1, 0) + 0.25 * K(0, 1) + 0.125 * Kd(2, 2);
+  lp.grad();
+  std::vector<double> out;
+  for (int i = 0; i < 3; ++i) out.push_back(th(i).adj());
+  for (int j = 0; j < N; ++j)
+    for (int i = j; i < N; ++i) out.push_back(K(i, j).adj());
+  for (int i = 0; i < N; ++i) out.push_back(Kd(i, i).adj());
+  for (int j = 0; j < N; ++j)
+    for (int i = j; i < N; ++i) out.push_back(L(i, j).adj());
+  for (int j = 0; j < N; ++j)
+    for (int i = j; i < N; ++i) out.push_back(L(i, j).val());
+  bool k_sym = true, kd_shares = true, kd_new = true, l_dummy = true;
+  std::unordered_set<const void*> sk, skd, sl;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) {
+      k_sym &= K(i, j).vi_ == K(j, i).vi_;
+      if (i != j) kd_shares &= Kd(i, j).vi_ == K(i, j).vi_;
+      if (i < j) l_dummy &= L(i, j).vi_ == L(0, 1).vi_ && L(i, j).val() == 0.0;
+      sk.insert(K(i, j).vi_);
+      skd.insert(K(i, j).vi_);
+      skd.insert(Kd(i, j).vi_);
+      sl.insert(L(i, j).vi_);
+    }
+  for (int i = 0; i < N; ++i) kd_new &= Kd(i, i).vi_ != K(i, i).vi_;
+  out.push_back(k_sym);
+  out.push_back(kd_shares);
+  out.push_back(kd_new && skd.size() == sk.size() + size_t(N));
+  out.push_back(l_dummy);
+  out.push_back(double(sk.size()));
+  out.push_back(double(skd.size()));
+  out.push_back(double(sl.size()));
+  emit("gpi", lp.val(), out);
+  stan::math::recover_memory();
+}
 
 /** Error cases of the new forms: name -> "<kind> <what()>". */
 inline void run_error_cases(const std::function<void(const std::string&, const std::function<void()>&)>& expect) {
@@ -449,6 +590,39 @@ inline void run_error_cases(const std::function<void(const std::string&, const s
   expect("gp_nd_sigma_data", [] {
     std::vector<Eigen::VectorXd> x(2, Eigen::VectorXd::Zero(3));
     gp_exp_quad_cov(x, -1.0, var(1.0));
+  });
+  expect("mdl_tri_low_not_square", [] {
+    MV L(3, 2);
+    MV b(3, 1);
+    for (int i = 0; i < L.size(); ++i) L(i) = 1.0;
+    for (int i = 0; i < b.size(); ++i) b(i) = 1.0;
+    stan::math::mdivide_left_tri_low(L, b);
+  });
+  expect("mdl_tri_low_sizes", [] {
+    MV L(3, 3);
+    MV b(2, 1);
+    for (int i = 0; i < L.size(); ++i) L(i) = 1.0;
+    for (int i = 0; i < b.size(); ++i) b(i) = 1.0;
+    stan::math::mdivide_left_tri_low(L, b);
+  });
+  expect("mdl_tri_low_empty_b", [] {
+    MV L(3, 3);
+    MV b(3, 0);
+    for (int i = 0; i < L.size(); ++i) L(i) = 1.0;
+    stan::math::mdivide_left_tri_low(L, b);
+  });
+  expect("mdr_tri_low_sizes", [] {
+    MV L(3, 3);
+    MV b(1, 2);
+    for (int i = 0; i < L.size(); ++i) L(i) = 1.0;
+    for (int i = 0; i < b.size(); ++i) b(i) = 1.0;
+    stan::math::mdivide_right_tri_low(b, L);
+  });
+  expect("mul_empty", [] {
+    MV A(0, 2);
+    MV B(2, 3);
+    for (int i = 0; i < B.size(); ++i) B(i) = 1.0;
+    multiply(A, B);
   });
 }
 

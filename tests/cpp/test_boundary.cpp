@@ -266,6 +266,36 @@ static void cmd_chol_mvn_ladj() {
   recover_memory_nested();
 }
 
+// bnd::run_gp_intermediate on the fixture's inputs: "gpi lp out..."
+static void cmd_gp_inter() {
+  int N, variant;
+  std::cin >> N >> variant;
+  std::vector<double> x = read_vec(size_t(N)), yv = read_vec(size_t(N)), th = read_vec(3);
+  Eigen::VectorXd y = Eigen::Map<Eigen::VectorXd>(yv.data(), N);
+  bnd::run_gp_intermediate(x, y, th.data(), variant,
+                           [](const std::string& name, double f, const std::vector<double>& g) { print(name, f, g); });
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->host_blocks_.size());
+}
+
+// The Stan-codegen GP with 1-D x (bnd::gp_marginal<double>, form 0) through
+// gradient(), `reps` times (the second and later evaluations take the
+// predicted closed form): "gp1d_<r> fx g..." per evaluation
+static void cmd_gp_1d() {
+  int N, reps;
+  std::cin >> N >> reps;
+  std::vector<double> x = read_vec(size_t(N)), yv = read_vec(size_t(N)), th = read_vec(3);
+  std::vector<Eigen::VectorXd> ys(1, Eigen::Map<Eigen::VectorXd>(yv.data(), N));
+  Eigen::VectorXd t = Eigen::Map<Eigen::VectorXd>(th.data(), 3), g;
+  for (int r = 0; r < reps; ++r) {
+    double fx = 0;
+    gradient(bnd::gp_marginal<double>{x, ys, 0}, t, fx, g);
+    print("gp1d_" + std::to_string(r), fx, std::vector<double>(g.data(), g.data() + g.size()));
+  }
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->host_blocks_.size());
+}
+
 int main() {
   std::string cmd;
   while (std::cin >> cmd) {
@@ -276,6 +306,8 @@ int main() {
     else if (cmd == "chol_nan_arena") cmd_chol_nan_arena();
     else if (cmd == "chol_mvn_predicted") cmd_chol_mvn_predicted();
     else if (cmd == "chol_mvn_ladj") cmd_chol_mvn_ladj();
+    else if (cmd == "gp_inter") cmd_gp_inter();
+    else if (cmd == "gp_1d") cmd_gp_1d();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;

@@ -158,3 +158,62 @@ def test_cholesky_factor_adjoint_readable_after_closed_form(N):
     a, b = rows(None), rows({"SMG_CHOL_MVN_CLOSED_FORM": "0"})
     near_rel(a, b, 1e-11, what="L / A adjoint sums")
     assert abs(a[0, 0]) > 0
+
+
+def _gpi_split(v, N):
+    t = N * (N + 1) // 2
+    o = [3, t, N, t, t, 7]
+    parts, k = [], 0
+    for n in o:
+        parts.append(np.asarray(v[k:k + n]))
+        k += n
+    assert k == len(v)
+    return parts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("closed", ["1", "0"])
+@pytest.mark.parametrize("N,variant", [(64, 0), (64, 1), (64, 2), (256, 0), (256, 1)])
+def test_gp_intermediate_adjoints(N, variant, closed):
+    """After a top-level lp.grad() of the Stan-codegen GP (Eigen::Matrix<var>
+    K, Kd, L), the intermediate varis hold what the reference's do
+    (tests/golden/gp_intermediate_N*.json, written by the real Stan Math from
+    the same bnd::run_gp_intermediate): K(i, j).adj() (K(i, j) and K(j, i)
+    one vari, rev/mat/fun/gp_exp_quad_cov.hpp:235), Kd's own diagonal varis
+    (add_diag shares K's off-diagonal varis, prim/mat/fun/add_diag.hpp:25-27),
+    L's lower adjoints (the MVN's partials; one dummy above the diagonal,
+    cholesky_decompose.hpp:34-48) and the same number of distinct varis.
+    Variant 1 adds host consumers of L (the factor's adjoint has a second
+    writer: the dense reverse), variant 2 of K's shared varis and Kd's
+    diagonal (the bridges gather them); closed = "0" forces the dense
+    Cholesky reverse throughout.  1e-10 relative (matrix entries with a
+    1e-10 * max-norm absolute floor: they carry cancellation)."""
+    d = golden(f"gp_intermediate_N{N}")
+    th = d["theta"]
+    env = None if closed == "1" else {"SMG_CHOL_MVN_CLOSED_FORM": "0"}
+    res = _parse(_run(f"gp_inter {N} {variant} {_num(d['x'])} {_num(d['y'])} {_num(th)}\n", env=env))
+    got, want = res["gpi"], np.concatenate([[d[f"fx_v{variant}"]], d[f"v{variant}"]])
+    near_rel(got[0], want[0], 1e-12, what="lp")
+    g, w = _gpi_split(got[1:], N), _gpi_split(want[1:], N)
+    near_rel(g[0], w[0], RTOL, what="grad theta")
+    for name, a, b in zip(("K adj", "Kd diag adj", "L adj", "L val"), g[1:5], w[1:5]):
+        near_rel(a, b, RTOL, atol=RTOL * float(np.abs(b).max()), what=name)
+    assert list(g[5]) == list(w[5]), ("identity", list(g[5]), list(w[5]))
+    assert list(res["stack"]) == [0.0, 0.0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1024, 4096])
+def test_gp_codegen_1d_golden(N):
+    """The Stan-codegen GP marginal (1-D x, Eigen::Matrix<var> K, Kd, L, the
+    path Stan models take) through gradient() at N = 1024 and the north-star
+    N = 4096, twice (the second evaluation forms K^{-1} alongside the
+    factorisation: the predicted closed form), against the reference's
+    gradient (gp_N*.json) at 1e-10."""
+    d = golden(f"gp_N{N}")
+    res = _parse(_run(f"gp_1d {N} 2 {_num(d['x'])} {_num(d['y'])} {_num(d['theta'])}\n", timeout=600))
+    for r in range(2):
+        got = res[f"gp1d_{r}"]
+        near_rel(got[0], d["fx"], 1e-12, what=f"fx {r}")
+        near_rel(got[1:], d["grad"], RTOL, what=f"grad {r}")
+    assert list(res["stack"]) == [0.0, 0.0]

@@ -1,0 +1,20 @@
+#!/bin/bash
+# one GPU call (round 4): selected GPU tests (TESTS, default the boundary suite),
+# then the bench workloads in WLS (default gp gp_eigen), each time-limited;
+# the first failure ends it.
+set -o pipefail
+TAG=${1:-r04q}
+O=$GRAFT_REPO_ROOT/gpurun_out
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+TESTS=${TESTS:-tests/test_boundary.py}
+if [ "$TESTS" != none ]; then
+  timeout -k 10 900 python -u -m pytest $TESTS -q -m gpu -x --timeout 300 --timeout-method thread > $O/${TAG}_pytest.log 2>&1 || { tail -40 $O/${TAG}_pytest.log; exit 1; }
+  tail -3 $O/${TAG}_pytest.log
+fi
+for w in ${WLS:-gp gp_eigen}; do
+  [ $w = none ] && continue
+  ST=20; [ $w = normal ] && ST=20000
+  timeout -k 10 400 python bench.py --workload $w --steps $ST --no-cpu-baseline > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err || { tail $O/${TAG}_bench_$w.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/${TAG}_bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('eval_phases_ms', ''))"
+done
