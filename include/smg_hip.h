@@ -84,6 +84,14 @@ void* smg_pinned_result(smg_ctx* ctx, size_t bytes);
  * no stream synchronisation).  For small results read right after the work
  * that produced them (the row-sharded reducers after their all-reduce). */
 int smg_publish_to_host(smg_ctx* ctx, const double* src, long long n, double* dst);
+/* dst[i] <- *src[i] for n device scalars (src a host array of device
+ * pointers), in stream order, written to fine-grained pinned memory (dst from
+ * smg_pinned_result) by one kernel that then publishes the completion word;
+ * returns once they have landed -- the reverse sweep's device->host scalar
+ * adjoints (the reference's vari::adj_ of scalar operands) in one launch and
+ * one host wait instead of a copy and a stream synchronisation each.
+ * status_out != NULL: the device status word as well (smg_status_enqueue). */
+int smg_gather_scalars(smg_ctx* ctx, const double* const* src, int n, double* dst, int* status_out);
 
 int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src_host, size_t bytes);
 int smg_memcpy_d2h(smg_ctx* ctx, void* dst_host, const void* src, size_t bytes);

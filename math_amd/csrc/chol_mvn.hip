@@ -193,92 +193,59 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int 
 
 }  // namespace
 
-// K^{-1} formed partly during the factorisation (cholesky.hip chol_fwd): with
-// h = n / 2, V = [[V11, V12], [0, V22]], V12 = -(V11 L21^T) V22.
-bool smg_inv_split_ok(int n) {
-  const int nl = n / SMG_NBR;
-  return n % SMG_NBR == 0 && nl >= 2 && (nl & (nl - 1)) == 0;
-}
+// K^{-1} formed progressively during the factorisation (cholesky.hip
+// chol_fwd), one 512-row block row k of W = L^{-1} at a time, on the side
+// stream once panel k is final:
+//   W_kk = L_kk^{-1}                       (the block inverses of rows k P.., P = 512)
+//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}   (Y_k formed one panel earlier)
+//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k     (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
+//   Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}  (needs only panels <= k)
+// so that after the last panel only its own block row remains (its inverse,
+// -W_77 Y_7 and one rank-512 update) instead of V22, V12 and all of V V^T.
+// ws: [W (n x n, ld n) | C (n x n, lower) | Y (P x n, ld P) | T (P/2 x 256)];
+// W's strict upper is never read outside its diagonal blocks (the triangular
+// K cuts stay inside a tile band), whose copies from aux carry stored zeros.
+bool smg_inv_prog_ok(int n) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR; }
 
-// The early part as steps queued by chol_fwd behind the trailing updates on
-// `side`, a few per panel (cholesky.hip): the top half's block inverses, V11
-// (leaves and pairs, then every higher recursion node's two products), and
-// T = V11 L21^T in column slices.  T lives in the C half of ws (rows 0..h,
-// ld n); V11's own recursion workspace below row h.
-static void inv_nodes(int lo, int hi, bool pairs, std::vector<smg_inv_step>& out) {
-  if (hi - lo == SMG_NBR || (pairs && hi - lo == 2 * SMG_NBR)) return;
-  const int mid = lo + ((hi - lo) / SMG_NBR / 2) * SMG_NBR;
-  inv_nodes(lo, mid, pairs, out);
-  inv_nodes(mid, hi, pairs, out);
-  const double b = mid - lo, a = hi - mid;
-  out.push_back({2, lo, mid, hi, a * b * b});
-  out.push_back({3, lo, mid, hi, a * a * b});
-}
-
-std::vector<smg_inv_step> smg_inv_early_steps(int n) {
-  const int h = n / 2, nl = h / SMG_NBR;
-  const bool pairs = nl >= 2 && (nl & (nl - 1)) == 0;
-  std::vector<smg_inv_step> st;
-  st.push_back({0, 0, 0, 0, 2.0 * h * SMG_NBR * SMG_NBR});  // block inverses (latency-bound: weighted up)
-  st.push_back({1, 0, 0, 0, pairs ? 2.0 * (nl / 2) * 2.0 * SMG_NBR * SMG_NBR * SMG_NBR : 1e6});
-  inv_nodes(0, h, pairs, st);
-  const int slices = h >= 2048 ? 2 : 1;
-  for (int k = 0; k < slices; ++k) st.push_back({4, k * h / slices, (k + 1) * h / slices, 0, (double)h * h * h / slices});
-  return st;
-}
-
-int smg_inv_early_run(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, const smg_inv_step& s) {
-  const int h = n / 2;
+int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
   const size_t nn = (size_t)n * n;
-  double* V = ws;
-  double* T = ws + nn;  // T (rows 0..h) | V11's recursion workspace (rows h..)
-  const double* w512 = aux + (size_t)n * SMG_AUX_W512;
-  switch (s.kind) {
-    case 0:
-      return smg_block_inverses_rows(ctx, L, ldl, aux, n, 0, h, T);
-    case 1: {
-      bool pairs = false;
-      return inv_t_leaves(ctx, L, ldl, w512, n, 0, h, V, n, T + h, &pairs);
-    }
-    case 2: {  // node (lo, mid, hi): T' = V11' L21'^T
-      const int lo = s.lo, mid = s.mid, hi = s.hi, b = mid - lo, a = hi - mid;
-      return smg_gemm_impl(ctx, 0, 1, 0, b, a, b, 1.0, V + lo + (size_t)lo * n, n, L + mid + (size_t)lo * ldl, ldl,
-                           0.0, T + h, n, SMG_TRI_A_UPPER);
-    }
-    case 3: {  // V12' = -T' V22'
-      const int lo = s.lo, mid = s.mid, hi = s.hi, b = mid - lo, a = hi - mid;
-      return smg_gemm_impl(ctx, 0, 0, 0, b, a, a, -1.0, T + h, n, V + mid + (size_t)mid * n, n, 0.0,
-                           V + lo + (size_t)mid * n, n, SMG_TRI_B_UPPER);
-    }
-    case 4:  // T[:, c0:c1] = V11 L21[c0:c1, :]^T
-      return smg_gemm_impl(ctx, 0, 1, 0, h, s.mid - s.lo, h, 1.0, V, n, L + h + s.lo, ldl, 0.0, T + (size_t)s.lo * n, n,
-                           SMG_TRI_A_UPPER);
-  }
-  return SMG_ERR_ARG;
+  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, nn * sizeof(double), ctx->stream));  // C accumulates
+  return SMG_OK;
 }
 
-// late (all of L and its block inverses): V22, V12 = -T V22 (or all of V when
-// the early part did not run), then C = V V^T (lower)
-int smg_inv_late(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws, bool early) {
-  const int h = n / 2;
+int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k,
+                     bool inverses_here) {
+  constexpr int P = SMG_NBR;
   const size_t nn = (size_t)n * n;
-  double* V = ws;
+  double* W = ws;
   double* C = ws + nn;
+  double* Y = C + nn;
+  double* T = Y + (size_t)P * n;
+  const int r0 = k * P, r1 = r0 + P;
   int rc;
-  if (early) {
-    if ((rc = form_v(ctx, L, ldl, aux, n, V, C + h, h, n))) return rc;
-    rc = smg_gemm_impl(ctx, 0, 0, 0, h, h, h, -1.0, C, n, V + h + (size_t)h * n, n, 0.0, V + (size_t)h * n, n,
-                       SMG_TRI_B_UPPER);
-  } else {
-    rc = form_v(ctx, L, ldl, aux, n, V, C);
+  if (inverses_here) {  // (the solves after the factorisation wait for them: inv_ev_aux)
+    if ((rc = smg_block_inverses_rows(ctx, L, ldl, aux, n, r0, P, T))) return rc;
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->stream));
   }
-  if (rc) return rc;
-  return smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
+  const double* Wkk = aux + (size_t)n * SMG_AUX_W512 + r0;  // ld n, stored zeros above
+  SMG_HIP_TRY(hipMemcpy2DAsync(W + r0 + (size_t)r0 * n, n * sizeof(double), Wkk, n * sizeof(double),
+                               P * sizeof(double), P, hipMemcpyDeviceToDevice, ctx->stream));
+  if (k > 0) {  // W_{k,0:k} = -W_kk Y_k
+    if ((rc = smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y, P, 0.0, W + r0, n, SMG_TRI_A_LOWER))) return rc;
+  }
+  // C (lower, leading r1 x r1) += W_k^T W_k
+  if ((rc = smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n))) return rc;
+  if (r1 < n) {  // Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}
+    if ((rc = smg_gemm_impl(ctx, 0, 0, 0, P, r1, r1, 1.0, L + r1, ldl, W, n, 0.0, Y, P, SMG_TRI_B_LOWER))) return rc;
+  }
+  return SMG_OK;
 }
 
 extern "C" {
 
-size_t smg_cholesky_mvn_rev_ws_doubles(int n) { return n > 0 ? 2 * (size_t)n * n : 0; }
+size_t smg_cholesky_mvn_rev_ws_doubles(int n) {
+  return n > 0 ? 2 * (size_t)n * n + (size_t)SMG_NBR * n + SMG_NBR / 2 * 256 : 0;
+}
 
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s, int k,
                          long long s_stride, double adj, double* Aadj, int ldaa, double* ws) {
@@ -309,7 +276,10 @@ int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const doubl
   if (!ctx || n < 0 || !started) return SMG_ERR_ARG;
   *started = 0;
   if (n == 0 || !v_by_doubling(n, aux)) return SMG_OK;
-  if (early_done && !smg_inv_split_ok(n)) return SMG_ERR_ARG;
+  if (early_done) {  // K^{-1} already queued by the factorisation (its inv_ev joins it)
+    *started = 1;
+    return SMG_OK;
+  }
   if (!L || !ws || ldl < n) return SMG_ERR_ARG;
   if (int rc = smg_side_begin(ctx)) return rc;
   if (int rc = smg_inv_events(ctx)) return rc;
@@ -318,11 +288,8 @@ int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const doubl
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
   int rc;
   {
-    smg_on_side on(ctx);
-    if (early_done)  // the rest of V and K^{-1} = V V^T
-      rc = smg_inv_late(ctx, L, ldl, aux, n, ws, true);
-    else  // V only: K^{-1} in the reverse (formed here it measured no faster)
-      rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);
+    smg_on_side on(ctx);  // V only: K^{-1} in the reverse (formed here it measured no faster)
+    rc = form_v(ctx, L, ldl, aux, n, ws, ws + (size_t)n * n);
   }
   if (rc) return rc;
   SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));

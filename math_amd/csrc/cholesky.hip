@@ -964,37 +964,15 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   static_assert(SMG_NBF <= PANEL_MAX_STEPS * SMG_NB, "panel width");
   const int NB2 = n > SMG_NBF ? SMG_NBF : n;
   const bool look = NB2 < n && smg_side_begin(ctx) == SMG_OK;
-  // K^{-1} for the closed-form reverse under an MVN (chol_mvn.hip): once the
-  // first n/2 columns are final, the top half's part runs on `side` in steps
-  // behind each remaining trailing update (b), sized so each panel's side
-  // work still fits in the panel (one long stretch there delayed the next
-  // (b) and, through F, the main stream's next panel by ~0.4 ms)
-  const bool early = inv_ws && look && smg_inv_split_ok(n) && n / 2 % NB2 == 0 && smg_inv_events(ctx) == SMG_OK;
-  std::vector<smg_inv_step> steps;
-  size_t next_step = 0;
-  double steps_left = 0.0;
-  if (early) {
-    steps = smg_inv_early_steps(n);
-    for (const auto& st : steps) steps_left += st.flops;
-  }
-  // slots: the (b) launches from the one after panel n/2 on
-  auto slots_left = [&](int K) {
-    int c = 0;
-    for (int k = K; k + NB2 < n; k += NB2) ++c;
-    return c;
-  };
-  auto queue_steps = [&](double budget) -> int {  // on `side`, after what is queued there
+  // K^{-1} for the closed-form reverse under an MVN (chol_mvn.hip), formed
+  // progressively: block row k of W = L^{-1} and its rank-512 share of
+  // K^{-1} on `side` behind each panel's trailing update (b), so that after
+  // the last panel only that panel's own block row remains
+  const bool prog = inv_ws && look && NB2 == SMG_NBR && smg_inv_prog_ok(n) && smg_inv_events(ctx) == SMG_OK;
+  if (prog) {
     smg_on_side on(ctx);
-    double done = 0.0;
-    while (next_step < steps.size() && (done == 0.0 || done + steps[next_step].flops <= budget * 1.25)) {
-      const smg_inv_step& st = steps[next_step++];
-      if (int rc = smg_inv_early_run(ctx, L, ldl, aux, n, inv_ws, st)) return rc;
-      if (st.kind == 0) SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->side));
-      done += st.flops;
-      steps_left -= st.flops;
-    }
-    return SMG_OK;
-  };
+    if (int rc = smg_inv_prog_init(ctx, n, inv_ws)) return rc;
+  }
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
   for (int J = 0; J < n; J += NB2) {
@@ -1015,10 +993,6 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if (grid + nh > PANEL_MAX_GRID || nbp > T) nh = 0;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
-    }
-    if (early && K == n / 2) {  // L's first n/2 columns are final after this panel
-      SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
-      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
     }
     if (K >= n) break;
     const int m = n - K;
@@ -1052,19 +1026,13 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       F = smg_event(ctx, nev++);
       if (!F) return SMG_ERR_HIP;
       SMG_HIP_TRY(hipEventRecord(F, ctx->side));
-      if (early && K >= n / 2 && next_step < steps.size()) {  // this panel's share of the K^{-1} steps
-        const int slots = slots_left(K);
-        if ((rc = queue_steps(steps_left / (slots > 0 ? slots : 1)))) return rc;
-      }
+    } else if (prog) {  // no (b): the side stream still follows this panel
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
     }
-  }
-  if (early) {  // (steps no slot took)
-    if (int rc = queue_steps(1e300)) return rc;
-    // their writes to ws are joined before anything on the main stream may
-    // touch ws (smg_join_async; the late part re-records it)
-    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
-    ctx->inv_pending = 1;
-    *inv_started = 1;
+    if (prog) {  // block row J / P of W and K^{-1} (F is recorded before it: the next (a) does not wait for it)
+      smg_on_side on(ctx);
+      if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, J / NB2, true))) return rc;
+    }
   }
   // every launch that can latch the status (the symmetric check, the panels'
   // not-PD and hand-off bits) is enqueued: the status mark goes here, so a
@@ -1074,29 +1042,29 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     if (rc) return rc;
   }
   if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
-  // the 128- and 256-block inverses (reverse pass, triangular solves); the
-  // top half's are the first K^{-1} step on `side`
-  int rc = early ? chol_block_inverses(ctx, L, ldl, aux, n, n / 2, n - n / 2) : chol_block_inverses(ctx, L, ldl, aux, n);
-  if (rc) return rc;
-  if (early) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
-  // the rest of K^{-1} queued here, overlapping the MVN's forward solves and
-  // the host's work up to the reverse (*inv_started = 2); same-box A/B
-  // against queueing it behind the solves: 3.00 vs 3.18 ms per GP gradient
-  // (SMG_LATE_AT_FWD=0 restores that)
-  static const bool late_here = [] {
-    const char* e = getenv("SMG_LATE_AT_FWD");
-    return !(e && e[0] == '0');
-  }();
-  if (early && late_here) {
+  // the 128-, 256- and 512-block inverses (reverse pass, triangular solves);
+  // progressive: every block row's but the last were formed on `side`, the
+  // last one's here on the main stream (idle after the last panel), then the
+  // last block row of W and its K^{-1} update go to `side`, overlapping the
+  // MVN's forward solves and the host's work up to the reverse
+  int rc;
+  if (prog) {
+    const int r0 = n - SMG_NBR;
+    SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
+    if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, r0, SMG_NBR))) return rc;
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
     {
       smg_on_side on(ctx);
-      if ((rc = smg_inv_late(ctx, L, ldl, aux, n, inv_ws, true))) return rc;
+      if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, n / SMG_NBR - 1, false))) return rc;
     }
+    // its writes to ws are joined before anything on the main stream may
+    // touch ws (smg_cholesky_mvn_rev_v / smg_join_async)
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
     ctx->inv_pending = 1;
     *inv_started = 2;
+  } else if ((rc = chol_block_inverses(ctx, L, ldl, aux, n))) {
+    return rc;
   }
   SMG_LAUNCH_CHECK();
   return SMG_OK;

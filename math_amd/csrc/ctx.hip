@@ -33,6 +33,20 @@ __global__ __launch_bounds__(256) void k_publish(const double* __restrict__ src,
   if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+constexpr int GATHER_MAX = 64;  // scalars per launch (kernel-argument array)
+struct gather_args {
+  const double* p[GATHER_MAX];
+};
+__global__ __launch_bounds__(64) void k_gather_scalars(gather_args a, int n, double* dst, const int* status,
+                                                       int* status_out, long long* done, long long seq) {
+  const int i = threadIdx.x;
+  if (i < n) __hip_atomic_store(dst + i, *a.p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (i == 0 && status_out) __hip_atomic_store(status_out, *status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (i == 0 && done) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 smg_prof_scope::smg_prof_scope(smg_ctx* c, int f) : ctx(c), fam(f), on(c && c->prof_on) {
@@ -392,6 +406,26 @@ int smg_publish_to_host(smg_ctx* ctx, const double* src, long long n, double* ds
   const long long seq = ++ctx->done_seq;
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, src, n, dst, ctx->done_h, seq);
   SMG_LAUNCH_CHECK();
+  return smg_wait_done(ctx, seq);
+}
+
+int smg_gather_scalars(smg_ctx* ctx, const double* const* src, int n, double* dst, int* status_out) {
+  if (!ctx || n < 0 || (n > 0 && (!src || !dst))) return SMG_ERR_ARG;
+  if (n == 0 && !status_out) return SMG_OK;
+  long long seq = 0;
+  for (int b = 0; b < n || (b == 0 && status_out); b += GATHER_MAX) {
+    const int m = n - b < GATHER_MAX ? n - b : GATHER_MAX;
+    gather_args a;
+    for (int i = 0; i < m; ++i) a.p[i] = src[b + i];
+    const bool last = b + GATHER_MAX >= n;
+    int* so = last ? status_out : nullptr;
+    if (last) seq = ++ctx->done_seq;
+    hipLaunchKernelGGL(k_gather_scalars, dim3(1), dim3(64), 0, ctx->stream, a, m, dst + b, ctx->status_d, so,
+                       last ? ctx->done_h : nullptr, seq);
+    SMG_LAUNCH_CHECK();
+    if (last) break;
+  }
+  if (status_out) ctx->status_armed = 0;
   return smg_wait_done(ctx, seq);
 }
 

@@ -152,20 +152,14 @@ struct smg_on_side {
   }
   ~smg_on_side() { ctx->stream = ctx->main_stream; }
 };
-// chol_mvn.hip: K^{-1} for the closed-form reverse, the top half's part
-// formed during the factorisation; ws = [V | C] (2 n^2 doubles).  Early
-// steps (kind 0: the top half's block inverses, 1: V11's leaves and pairs,
-// 2 / 3: a recursion node's two products, 4: a column slice of V11 L21^T)
-// are queued by chol_fwd behind the trailing updates on `side`; late: V22,
-// V12 and C = V V^T (smg_cholesky_inv_t_async with early_done)
-struct smg_inv_step {
-  int kind, lo, mid, hi;
-  double flops;
-};
-bool smg_inv_split_ok(int n);
-std::vector<smg_inv_step> smg_inv_early_steps(int n);
-int smg_inv_early_run(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, const smg_inv_step& s);
-int smg_inv_late(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws, bool early);
+// chol_mvn.hip: K^{-1} for the closed-form reverse formed progressively
+// during the factorisation, block row k of W = L^{-1} once panel k is final
+// (queued by chol_fwd on `side`); ws: smg_cholesky_mvn_rev_ws_doubles(n)
+bool smg_inv_prog_ok(int n);
+int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws);
+// (inverses_here: the block row's 128/256/512 inverses first, then inv_ev_aux recorded)
+int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k,
+                     bool inverses_here);
 // block inverses of the rows [row0, row0 + nrows) (multiples of 512), T: a
 // workspace (NULL: SMG_WS_TMP)
 int smg_block_inverses_rows(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0, int nrows,

@@ -48,6 +48,7 @@ _SIGS = {
     "smg_status_inject": (_I, [_P, _I]),
     "smg_pinned_io": (_P, [_P, _S]),
     "smg_pinned_result": (_P, [_P, _S]),
+    "smg_gather_scalars": (_I, [_P, _P, _I, _P, _P]),
     "smg_pack_tril": (_I, [_P, _I, _I, _P, _I, _P]),
     "smg_unpack_tril_add": (_I, [_P, _I, _I, _P, _P, _I]),
     "smg_publish_to_host": (_I, [_P, _P, _L, _P]),

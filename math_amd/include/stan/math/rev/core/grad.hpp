@@ -58,13 +58,14 @@ inline void flush_pending(bool status = false) {
   if (pend.empty() && !armed) return;
   smg_ctx* c = amd::ctx();
   const size_t n = pend.size();
-  double* stage = static_cast<double*>(smg_host_scratch(c, (n + 1) * sizeof(double)));
+  // one gather kernel into fine-grained pinned memory and one host wait
+  // (smg_gather_scalars), not a copy per scalar and a stream sync
+  double* stage = static_cast<double*>(smg_pinned_result(c, (n + 1) * sizeof(double)));
   if (!stage) throw std::bad_alloc();
-  for (size_t i = 0; i < n; ++i)
-    amd::check(smg_memcpy_d2h(c, stage + i, pend[i].src, sizeof(double)), "flush_pending");
+  std::vector<const double*> src(n);
+  for (size_t i = 0; i < n; ++i) src[i] = pend[i].src;
   int* st = reinterpret_cast<int*>(stage + n);
-  if (armed) amd::check(smg_status_enqueue(c, st), "grad");
-  amd::check(smg_sync(c), "flush_pending");
+  amd::check(smg_gather_scalars(c, src.data(), int(n), stage, armed ? st : nullptr), "flush_pending");
   auto& blocks = ChainableStack::instance_->host_blocks_;
   for (size_t i = 0; i < n; ++i) {
     vari* t = pend[i].target;

@@ -99,7 +99,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   int dep_k_ = 1;  // observations (the array form), [w, s] 2n doubles apart
   size_t dep_sweep_ = 0;
   double* ws_ = nullptr;  // smg_cholesky_mvn_rev's workspace [V = L^{-T}, K^{-1}]
-  bool early_ = false;    // the factorisation queued K^{-1}'s top-half steps into ws_
+  bool early_ = false;    // the factorisation queued all of K^{-1} into ws_ (progressively, with its panels)
   bool v_ready_ = false;  // V queued (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
   bool c_ready_ = false;  // and K^{-1} (after early_)
   // the closed form applied these MVN partials without writing L's dense
@@ -132,13 +132,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       if (e.first.first == pos && e.first.second == n) return e.second ? 1 : 0;
     return -1;
   }
-  static bool predicted(size_t pos, int n) {
-    static const bool on = [] {  // SMG_CHOL_INV_FWD=0: K^{-1} never formed with the panels (A/B)
-      const char* e = std::getenv("SMG_CHOL_INV_FWD");
-      return !(e && e[0] == '0');
-    }();
-    return on && history_of(pos, n) == 1;
-  }
+  static bool predicted(size_t pos, int n) { return history_of(pos, n) == 1; }
   void record(bool closed) const {
     auto& h = history();
     for (auto& e : h)
@@ -164,16 +158,13 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     L->sink_ = this;
   }
 
-  // L^{-T} (and K^{-1} when the factorisation queued its top half) is formed
-  // on the side stream from the MVN's forward on, queued behind the MVN's
-  // latency-bound solves so that they are not starved of CUs; unused if the
-  // reverse takes the dense path
+  // When the factorisation did not already queue K^{-1} (no prediction yet,
+  // or a size it cannot form progressively), L^{-T} is formed on the side
+  // stream from the MVN's forward on, queued behind the MVN's latency-bound
+  // solves so that they are not starved of CUs; unused if the reverse takes
+  // the dense path
   void prepare_mvn_adjoint() override {
-    static const bool async = [] {  // SMG_CHOL_MVN_ASYNC=0: V formed in the reverse (A/B)
-      const char* e = std::getenv("SMG_CHOL_MVN_ASYNC");
-      return !(e && e[0] == '0');
-    }();
-    if (!closed_form_enabled() || !async || v_ready_) return;
+    if (!closed_form_enabled() || v_ready_) return;
     // (a factor whose adjoint had other writers last time -- the HVP's value
     // factor feeds the tangent nodes too -- would form V for nothing)
     if (history_of(pos_, n_) == 0) return;
@@ -334,10 +325,10 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
   if (st) amd::throw_status(st, fn, "m");
   auto* node = new internal::cholesky_dev_vari(A.vi_, L);
+  node->ws_ = inv_ws;  // (reused by prepare_mvn_adjoint when the factorisation could not form K^{-1})
   if (inv_started) {
-    node->ws_ = inv_ws;
     node->early_ = true;
-    node->v_ready_ = node->c_ready_ = inv_started == 2;  // (all of K^{-1} queued already)
+    node->v_ready_ = node->c_ready_ = true;  // all of K^{-1} queued already
   }
   return dev_var_matrix(L);
 }
