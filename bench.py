@@ -62,13 +62,23 @@ def ptr(a):
     return a.ctypes.data_as(D)
 
 
-def ref_bench(cfg, n, reps=1, timeout=300):
-    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+def ref_bench(cfg, n, reps=1, timeout=300, threads=None):
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness" + ("_mt" if threads else ""))
     if not os.path.exists(exe):
         return None
-    out = subprocess.run([exe, "bench", cfg, str(n), str(reps)], capture_output=True, text=True,
-                         timeout=timeout, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    cmd = [exe, "bench", cfg, str(n), str(reps)] + ([str(threads)] if threads else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=dict(os.environ, OMP_NUM_THREADS="1"))
     return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def host_cores():
+    """The host cores this process may use (the GPU box grants a 16-CPU share;
+    os.cpu_count() shows the whole machine there)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def pmc_traffic(workload):
@@ -171,6 +181,29 @@ class GP(Workload):
     def roofline(self, fams, steps, t_prof, ms_per_step):
         return eval_roofline(self, fams, steps, ms_per_step, pmc_traffic("gp"))
 
+    def extra(self, timed, steps):
+        if type(self) is not GP:
+            return {}
+        # the headline functor takes x / y / mu device-resident (dev_data);
+        # the reference's gp_functor passes std::vector x and Eigen y, mu:
+        # the same evaluation with those argument types (uploaded per call)
+        bl = self.bl
+        bl.smg_bench_gp_step_reftypes.argtypes = [D, D, D]
+        fx, g = np.zeros(1), np.zeros(3)
+        step = lambda: bl.smg_bench_gp_step_reftypes(ptr(self.theta), ptr(fx), ptr(g))  # noqa: E731
+        for _ in range(2):
+            if step() != 0:
+                raise SystemExit(f"reftypes step failed: {bl.smg_bench_error().decode()}")
+        want = np.array(self.gold["grad"])
+        if np.abs(g - want).max() > 1e-10 * np.abs(want).max():
+            raise SystemExit(f"reftypes parity failure: {g} vs {want}")
+        t = timed(steps, step)
+        return {"reference_input_types": {
+            "value": steps / t, "ms_per_step": 1e3 * t / steps,
+            "note": "the same gradient with the reference harness's argument types (std::vector<double> x, "
+                    "Eigen::VectorXd y and mu, uploaded each evaluation; intermediates auto = device nodes); "
+                    "the headline line passes x / y / mu as dev_data"}}
+
     def cpu_baseline(self):
         r = ref_bench("gp", self.N, 1)
         if r is None:
@@ -210,7 +243,7 @@ class GPEigen(GP):
         return c
 
     def extra(self, timed, steps):
-        ph = np.zeros(4)
+        ph = np.zeros(8)
         self.bl.smg_bench_gp_eigen_phases.argtypes = [D, D]
         best = None
         for _ in range(3):
@@ -221,11 +254,15 @@ class GPEigen(GP):
         out = np.zeros(5)
         if self.bl.smg_bench_bridge_cost(self.N, 3, ptr(out)) != 0:
             raise SystemExit(f"bridge cost failed: {self.bl.smg_bench_error().decode()}")
-        return {"eval_phases_ms": {"forward": best[0] * 1e3, "reverse": best[1] * 1e3, "recover": best[2] * 1e3,
-                                   "gradient_call": best[3] * 1e3,
+        return {"eval_phases_ms": {"forward": best[0] * 1e3, "reverse_published": best[1] * 1e3,
+                                   "recover": best[2] * 1e3, "gradient_call": best[3] * 1e3,
+                                   "forward_K": best[4] * 1e3, "forward_Kd": best[5] * 1e3,
+                                   "forward_L": best[6] * 1e3, "forward_mvn": best[7] * 1e3,
                                    "note": "one evaluation split by hand (functor forward incl. three crossings; "
-                                           "grad() to a device sync; recover_memory), best of 3; gradient_call: "
-                                           "the same evaluation through stan::math::gradient"},
+                                           "a top-level grad() to a device sync, which also publishes the "
+                                           "intermediate blocks' adjoints into their varis; recover_memory), best "
+                                           "of 3; gradient_call: the same evaluation through stan::math::gradient "
+                                           "(nothing published); forward_*: the forward's four statements"},
                 "bridge_cost_ms": {"to_host_matrix": out[0] * 1e3, "to_dev_recognised": out[1] * 1e3,
                                    "to_dev_gathered_copy": out[2] * 1e3, "reverse_gather_touched": out[3] * 1e3,
                                    "reverse_untouched_sweep": out[4] * 1e3,
@@ -324,14 +361,19 @@ class GLM(Workload):
                                  "partials reduction + launch gaps"}
 
     def cpu_baseline(self):
-        rs = 1000000
-        r = ref_bench("glm", rs, 1)
+        # every host core, the reference's threaded map_rect
+        # shape (32 row-shard jobs, their nested gradients in parallel on
+        # thread-local tapes: oracle/_ref/ref_harness_mt, STAN_THREADS build)
+        rs, cores = 2000000, host_cores()
+        r = ref_bench("glm_mt", rs, 2, threads=cores)
         if r is None:
             return None
-        per = r["seconds_per_eval"] * self.R / rs  # linear in rows (one pass over x)
-        return {"value": 1.0 / per, "unit": "gradient evals/s", "cores": 1, "kind": "reference",
-                "sample": f"1 gradient eval at {rs} rows x {self.M} (Stan Math 3.0.0, {r['seconds_per_eval']:.2f} s)"
-                          f", scaled x{self.R // rs} to {self.R} rows (linear in rows)"}
+        per = r["seconds_per_eval"] * self.R / rs  # linear in rows (passes over x)
+        return {"value": 1.0 / per, "unit": "gradient evals/s", "cores": r["threads"], "kind": "reference",
+                "sample": f"2 gradient evals at {rs} rows x {self.M} as 32 map_rect-style row-shard jobs on "
+                          f"{r['threads']} threads (Stan Math 3.0.0 with STAN_THREADS, "
+                          f"{r['seconds_per_eval']:.3f} s each), scaled x{self.R // rs} to {self.R} rows "
+                          "(linear in rows)"}
 
 
 class MulChol(Workload):

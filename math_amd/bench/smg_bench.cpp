@@ -35,6 +35,23 @@ struct gp_functor {
   const dev_data<double>& mu0;
 };
 
+// the same with the reference's input types (the harness's gp_functor
+// arguments: std::vector<double> x, Eigen y and mu -- uploaded per
+// evaluation) and device-typed intermediates (`auto`)
+struct gp_reftypes_functor {
+  const std::vector<double>& x;
+  const Eigen::VectorXd& y;
+  template <typename T>
+  T operator()(const std::vector<T>& th) const {
+    using namespace stan::math;
+    auto K = gp_exp_quad_cov(x, th[0], th[1]);
+    auto Kd = add_diag(K, square(th[2]));
+    auto L = cholesky_decompose(Kd);
+    const Eigen::VectorXd mu = Eigen::VectorXd::Zero(y.size());
+    return multi_normal_cholesky_lpdf(y, mu, L);
+  }
+};
+
 // config 3 exactly as Stan-generated code declares it (and as the reference
 // harness times it, oracle/ref_harness.cpp gp_functor): host std::vector x,
 // Eigen y / mu, and `matrix[N,N] K = ...` as Eigen::Matrix<var,-1,-1>, so
@@ -116,6 +133,18 @@ int smg_bench_gp_step(const double* theta, double* fx, double* grad) {
   }
 }
 
+/* config 3 with the reference's argument types (gp_reftypes_functor). */
+int smg_bench_gp_step_reftypes(const double* theta, double* fx, double* grad) {
+  try {
+    std::vector<double> th(theta, theta + 3), g;
+    stan::math::gradient(gp_reftypes_functor{g_xh, g_yh}, th, *fx, g);
+    for (int i = 0; i < 3; ++i) grad[i] = g[i];
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
 /* config 3 through the Eigen-typed boundary (gp_eigen_functor); data from
  * smg_bench_gp_init.  malloc_tuning != 0 keeps Eigen's N^2 heap buffers in
  * the brk heap (M_MMAP_MAX = 0, no trimming) so they are reused without page
@@ -131,8 +160,11 @@ int smg_bench_gp_eigen_step(const double* theta, double* fx, double* grad) {
   }
 }
 /* Where one gp_eigen evaluation's host time goes (seconds): out[0] the
- * functor's forward pass (three crossings), out[1] the reverse sweep, out[2]
- * recover_memory, out[3] the whole evaluation (gradient()). */
+ * functor's forward pass (three crossings), out[1] the reverse sweep of a
+ * top-level grad() (with the host blocks' adjoints published), out[2]
+ * recover_memory, out[3] the whole evaluation (gradient()), out[4..7] the
+ * forward's statements: K = gp_exp_quad_cov, Kd = add_diag, L =
+ * cholesky_decompose, the MVN. */
 int smg_bench_gp_eigen_phases(const double* theta, double* out) {
   try {
     using namespace stan::math;
@@ -158,6 +190,27 @@ int smg_bench_gp_eigen_phases(const double* theta, double* out) {
     out[1] = sec(t1, t2);
     out[2] = sec(t2, t3);
     out[3] = sec(t4, t5);
+    {  // the forward statement by statement (each ends where the host has its result)
+      start_nested();
+      Eigen::Matrix<var, -1, 1> tv2(3);
+      for (int i = 0; i < 3; ++i) tv2(i) = th(i);
+      auto s0 = now();
+      Eigen::Matrix<var, -1, -1> K = gp_exp_quad_cov(g_xh, tv2(0), tv2(1));
+      auto s1 = now();
+      Eigen::Matrix<var, -1, -1> Kd = add_diag(K, square(tv2(2)));
+      auto s2 = now();
+      Eigen::Matrix<var, -1, -1> L = cholesky_decompose(Kd);
+      auto s3 = now();
+      Eigen::VectorXd mu = Eigen::VectorXd::Zero(g_n);
+      var lp = multi_normal_cholesky_lpdf(g_yh, mu, L);
+      auto s4 = now();
+      out[4] = sec(s0, s1);
+      out[5] = sec(s1, s2);
+      out[6] = sec(s2, s3);
+      out[7] = sec(s3, s4);
+      (void)lp;
+      recover_memory_nested();
+    }
     return 0;
   } catch (const std::exception& e) {
     return fail(e);
@@ -205,7 +258,10 @@ int smg_bench_bridge_cost(int n, int reps, double* out) {
         if (touch) f += 2.0 * M(1, 1);
         amd::check(smg_sync(amd::ctx()), "bridge");
         auto t4 = now();
-        f.grad();  // the block's bridge runs inside: gathers when touched, skips otherwise
+        {
+          no_publish_scope quiet;  // (the bridge's own cost: the blocks' adjoints are not published)
+          f.grad();  // the block's bridge runs inside: gathers when touched, skips otherwise
+        }
         auto t5 = now();
         out[0] = std::min(out[0], sec(t0, t1));
         out[1] = std::min(out[1], sec(t1, t2));

@@ -221,7 +221,7 @@ __global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int 
 // (64 rows from J + 64 t) belongs to workgroup 1 + (t - 1) mod (gridDim.x - 1),
 // which applies every step's update to it, so the only cross-workgroup
 // dependencies are
-//   * the factored diagonal block j (Dinv_j): flag diag[j];
+//   * the factored diagonal block j (L_jj, which every tile solves against): flag diag[j];
 //   * the panel-region rows L_cj (c < nb) that update tile t's column block c:
 //     flag row[j][c];
 //   * tile j + 2's step-j updates, which the chain's step j + 1 reads:
@@ -264,7 +264,10 @@ __device__ int g_panel_trace_n[PANEL_MAX_GRID];
 #ifndef SMG_CHAIN_INLINE
 typedef __attribute__((address_space(3))) double lds_dbl;
 __device__ __noinline__ void chain_factor(lds_dbl* D, int* status) { lds_potrf64_lookahead(D, status); }
-__device__ __noinline__ void chain_inverse(const lds_dbl* D, lds_dbl* X, lds_dbl* T) { lds_trtri64_mfma(D, X, T); }
+__device__ __noinline__ void chain_leaves(const lds_dbl* D, lds_dbl* X) {
+  if ((threadIdx.x >> 6) < 4) trtri_leaf16(D, X, threadIdx.x >> 6);
+}
+__device__ __noinline__ void chain_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) { lds_trsm64_rt(Y, D, X); }
 __device__ __noinline__ void chain_ltj(lds_dbl* Y, const lds_dbl* X) {
   lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Y, Y, X);
 }
@@ -273,13 +276,16 @@ __device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const ld
   lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
 }
 #define CHAIN_FACTOR(D, st) chain_factor((lds_dbl*)(D), (st))
-#define CHAIN_INVERSE(D, X, T) chain_inverse((const lds_dbl*)(D), (lds_dbl*)(X), (lds_dbl*)(T))
+#define CHAIN_LEAVES(D, X) chain_leaves((const lds_dbl*)(D), (lds_dbl*)(X))
+#define CHAIN_TRSM(Y, D, X) chain_trsm((lds_dbl*)(Y), (const lds_dbl*)(D), (const lds_dbl*)(X))
 #define CHAIN_LTJ(Y, X) chain_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
 #define CHAIN_SYRK(Zn, Y, b) chain_syrk((lds_dbl*)(Zn), (const lds_dbl*)(Y), (b))
 #define OWNER_UPDATE(Z, D, B) owner_update((lds_dbl*)(Z), (const lds_dbl*)(D), (const lds_dbl*)(B))
 #else
 #define CHAIN_FACTOR(D, st) lds_potrf64_lookahead((D), (st))
-#define CHAIN_INVERSE(D, X, T) lds_trtri64_mfma((D), (X), (T))
+#define CHAIN_LEAVES(D, X) \
+  if ((threadIdx.x >> 6) < 4) trtri_leaf16((D), (X), threadIdx.x >> 6)
+#define CHAIN_TRSM(Y, D, X) lds_trsm64_rt((Y), (D), (X))
 #define CHAIN_LTJ(Y, X) lds_mma64_8w<false, true>((Y), (Y), (X))
 #define CHAIN_SYRK(Zn, Y, b) lds_syrk64_8w_next((Zn), (Y), (b))
 #define OWNER_UPDATE(Z, D, B) lds_mma64_8w<false, true>((Z), (D), (B), -1.0, 1.0)
@@ -319,6 +325,16 @@ __device__ inline void panel_gstore(const double* D, double* A, int ld, int rows
     if (r < rows && c < cols && (!lower || r >= c)) st_dev(&A[r + (size_t)c * ld], D[r * SMG_NBP + c]);
   }
 }
+// a b x b lower triangle (loaded with lower = true) into LDS with identity
+// padding beyond b: the factor's leaf inverses stay finite
+__device__ inline void panel_lstore_id(double* D, const panel_regs& R, int b) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    const int r = e & 63, c = e >> 6;
+    D[r * SMG_NBP + c] = ((R.ok >> q) & 1u) ? R.v[q] : (r == c && r >= b ? 1.0 : 0.0);
+  }
+}
 // b x b lower triangle of D with zeros above (the factored block / inverse)
 __device__ inline void panel_gstore_tri(const double* D, double* A, int ld, int b) {
 #pragma unroll
@@ -342,7 +358,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   __shared__ double Y[SMG_NB * SMG_NBP];
   __shared__ double Z[SMG_NB * SMG_NBP];
   constexpr int S = PANEL_MAX_STEPS;
-  int* diag = flags;           // diag[j]: L_jj, Dinv_j stored
+  int* diag = flags;           // diag[j]: L_jj stored
   int* row = flags + S;        // row[j S + t]: L_tj stored (panel tiles t < nb)
   int* done = flags + S + S * S;  // done[j S + t]: tile t's step-j updates stored
   int* hflag = flags + S + 2 * S * S;  // hflag[j S + t]: tile t's helper finished step j
@@ -402,7 +418,6 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     // it with L_{j+1,j} only after seeing diag[j].
     double* Dc = D;  // current diagonal block (LDS)
     double* Zn = Z;  // next one
-    __shared__ double Tch[3 * 256];  // lds_trtri64_mfma scratch
     lds_load_block(Dc, L + J + (size_t)J * ldl, ldl, min(SMG_NB, K - J), true);
     __syncthreads();
     for (int j = 0; j < nb; ++j) {
@@ -419,28 +434,28 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
         panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
       };
-      // the next tile's operands are loaded between the factorisation and
-      // the inverse: their latency hides behind the inverse instead of
-      // sitting between the publish and the next products
+      // L_jj is what the other tiles wait for (they solve against it): its
+      // stores are issued right after the factorisation and published after
+      // the leaf inverses, so their latency hides behind them; the next
+      // tile's operands are loaded there too.  No 64 x 64 inverse on the
+      // chain: L_{t,j} = A_{t,j} L_jj^{-T} by the leaf inverses and one
+      // row-tile solve (the block inverses for later use come from
+      // k_trtri_blocks after the panel)
       CHAIN_FACTOR(Dc, status);
       __syncthreads();
+      panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
       if (more) load_next();
-      CHAIN_INVERSE(Dc, X, Tch);
-      __syncthreads();
+      CHAIN_LEAVES(Dc, X);
       PANEL_EV((j << 16) | (j << 8) | 10);
-      // Dinv_j is what the other tiles wait for; L_jj is read by no one in
-      // the launch, so it is stored after the publish (off the chain)
-      panel_gstore_tri(X, Dinv + cj, ldd, bj);
-      PANEL_EV((j << 16) | (j << 8) | 3);
       panel_publish(&diag[j], epoch);
       PANEL_EV((j << 16) | (j << 8) | 4);
-      panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
       if (!more) break;
       panel_lstore(Y, Ra);
       panel_lstore(Zn, Rz);
       __syncthreads();
       PANEL_EV((j << 16) | (t << 8) | 12);
-      CHAIN_LTJ(Y, X);  // L_{t,j} = A_{t,j} Dinv_j^T (private)
+      CHAIN_TRSM(Y, Dc, X);  // L_{t,j} = A_{t,j} L_jj^{-T} (private)
+      __syncthreads();
       PANEL_EV((j << 16) | (t << 8) | 13);
       // A_tt -= L_tj L_tj^T, written as the factorisation's input: lower
       // triangle, zero strict upper, identity padding beyond bt
@@ -473,11 +488,14 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);  // own data, final
       panel_wait(&diag[j], epoch, status);
       PANEL_EV((j << 16) | (t << 8) | 6);
-      panel_gload(Rd, Dinv + cj, ldd, bj, bj, true);
+      panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
       panel_lstore(D, Ra);
-      panel_lstore(X, Rd);
+      panel_lstore_id(X, Rd, bj);
       __syncthreads();
-      CHAIN_LTJ(D, X);  // L_tj = A_tj Dinv_j^T (the chain's own product: the same bits)
+      CHAIN_LEAVES(X, Y);
+      __syncthreads();
+      CHAIN_TRSM(D, X, Y);  // L_tj = A_tj L_jj^{-T} (the chain's own solve: the same bits)
+      __syncthreads();
       panel_gstore(D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
       PANEL_EV((j << 16) | (t << 8) | 7);
       if (t < nb) panel_publish(&row[j * S + t], epoch);
@@ -529,6 +547,21 @@ __global__ __launch_bounds__(512) void k_trtri_diag(const double* __restrict__ L
   lds_load_block(D, L, ldl, b, true);
   __syncthreads();
   lds_potrf_inv64_blk(D, X, b, nullptr, 0, Dinv, ldd, nullptr, false);
+}
+
+// The 64-row block inverses (the aux level SMG_NB, lower with zeros above) of
+// the diagonal blocks [j0, j1) of L, one workgroup per block: the panel
+// kernel solves against L_jj itself, so the inverses the later blocked
+// solves and the doubling start from are formed here, off the panel chain
+__global__ __launch_bounds__(512) void k_trtri_blocks(const double* __restrict__ L, int ldl, int j0, int j1,
+                                                      double* __restrict__ Dinv, int ldd) {
+  __shared__ double D[SMG_NB * SMG_NBP];
+  __shared__ double X[SMG_NB * SMG_NBP];
+  const int j = j0 + SMG_NB * blockIdx.x;
+  const int b = min(SMG_NB, j1 - j);
+  lds_load_block(D, L + j + (size_t)j * ldl, ldl, b, true);
+  __syncthreads();
+  lds_potrf_inv64_blk(D, X, b, nullptr, 0, Dinv + j, ldd, nullptr, false);
 }
 
 // symbolic_rev (cholesky_decompose.hpp:101-111) on one diagonal block:
@@ -975,6 +1008,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   }
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
+  hipEvent_t Tinv = nullptr;  // the side stream's last k_trtri_blocks
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
@@ -998,6 +1032,9 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     const int m = n - K;
     const double* P = L + K + (size_t)J * ldl;
     if (!look) {  // trailing A[K:, K:] -= L[K:, J:K] L[K:, J:K]^T (lower)
+      hipLaunchKernelGGL(k_trtri_blocks, dim3(smg_ceil_div(K - J, SMG_NB)), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
+                         ldl, J, K, Dinv, n);
+      SMG_LAUNCH_CHECK();
       int rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, K - J, -1.0, P, ldl, P, ldl, 1.0,
                              L + K + (size_t)K * ldl, ldl);
       if (rc) return rc;
@@ -1026,8 +1063,17 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       F = smg_event(ctx, nev++);
       if (!F) return SMG_ERR_HIP;
       SMG_HIP_TRY(hipEventRecord(F, ctx->side));
-    } else if (prog) {  // no (b): the side stream still follows this panel
+    } else {  // no (b): the side stream still follows this panel
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
+    }
+    {  // this panel's 64-row block inverses, behind (b) on the side stream (off the chain)
+      smg_on_side on(ctx);
+      hipLaunchKernelGGL(k_trtri_blocks, dim3(smg_ceil_div(K - J, SMG_NB)), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
+                         ldl, J, K, Dinv, n);
+      SMG_LAUNCH_CHECK();
+      Tinv = smg_event(ctx, nev++);
+      if (!Tinv) return SMG_ERR_HIP;
+      SMG_HIP_TRY(hipEventRecord(Tinv, ctx->side));
     }
     if (prog) {  // block row J / P of W and K^{-1} (F is recorded before it: the next (a) does not wait for it)
       smg_on_side on(ctx);
@@ -1042,6 +1088,13 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     if (rc) return rc;
   }
   if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
+  if (Tinv) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, Tinv, 0));
+  {  // the last panel's 64-row block inverses (the others': behind each panel)
+    const int Jl = ((n - 1) / NB2) * NB2;
+    hipLaunchKernelGGL(k_trtri_blocks, dim3(smg_ceil_div(n - Jl, SMG_NB)), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
+                       ldl, Jl, n, Dinv, n);
+    SMG_LAUNCH_CHECK();
+  }
   // the 128-, 256- and 512-block inverses (reverse pass, triangular solves);
   // progressive: every block row's but the last were formed on `side`, the
   // last one's here on the main stream (idle after the last panel), then the

@@ -846,6 +846,47 @@ __device__ inline void lds_trtri64_mfma(CP D, P X, P T) {
   }
 }
 
+// Y <- Y L^{-T} in place (Y: 64 x 64, L: 64 x 64 lower, both LDS [r][c]
+// stride SMG_NBP), given the 16 x 16 leaf inverses Li_pp = L_pp^{-1} on the
+// diagonal blocks of Li (trtri_leaf16).  Wave w < 4 solves row tile w alone,
+// column blocks p = 0..3 in order:
+//   Z = Y[w, p] - sum_{q < p} X[w, q] L[p, q]^T,   X[w, p] = Z Li_pp^T
+// (40 MFMAs on one dependency chain per wave; no barrier inside: a wave's
+// LDS accesses complete in order).  Waves >= 4 return at once.
+template <typename P, typename CP>
+__device__ inline void lds_trsm64_rt(P Y, CP L, CP Li) {
+  const int w = threadIdx.x >> 6;
+  if (w >= 4) return;
+  const int l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
+  const int r0 = 16 * w;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < p; ++q)
+#pragma unroll
+      for (int k0 = 0; k0 < 16; k0 += 4) {
+        const double a = Y[(r0 + fr) * SMG_NBP + 16 * q + k0 + fk];  // X[w, q](fr, k)
+        const double b = L[(16 * p + fr) * SMG_NBP + 16 * q + k0 + fk];  // L[p, q]^T(k, fr)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      auto y = &Y[(r0 + fk + 4 * r) * SMG_NBP + 16 * p + fr];
+      *y = *y - acc[r];
+    }
+    d4 x = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += 4) {
+      const double a = Y[(r0 + fr) * SMG_NBP + 16 * p + k0 + fk];        // Z(fr, k)
+      const double b = Li[(16 * p + fr) * SMG_NBP + 16 * p + k0 + fk];   // Li_pp^T(k, fr)
+      x = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, x, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Y[(r0 + fk + 4 * r) * SMG_NBP + 16 * p + fr] = x[r];
+  }
+}
+
 // Drop-in for lds_potrf_inv64_v2 built from the blocked pieces: factor (if
 // asked) then invert, then one coalesced write of L (lower) and X = L^{-1}.
 __device__ __forceinline__ void lds_potrf_inv64_blk(double* D, double* X, int b, double* Lout, int ldl,

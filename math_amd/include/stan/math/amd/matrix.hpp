@@ -188,12 +188,14 @@ enum block_layout : int { layout_dense = 0, layout_lower = 1, layout_sym = 2, la
 inline size_t tril_off(size_t n, size_t j) { return j * n - j * (j - 1) / 2; }
 inline size_t tril_count(size_t n) { return n * (n + 1) / 2; }
 
-inline void block_column_ptrs(const host_block& b, size_t j, vari** out);
+inline void block_column_ptrs(const std::vector<host_block>& blocks, const host_block& b, size_t j, vari** out);
 
 /** f(i, v) for every row i of column j of host block b, in order: v is the
- * vari the reference's matrix holds at (i, j) (host_block's layouts). */
+ * vari the reference's matrix holds at (i, j) (host_block's layouts).
+ * blocks: the tape's host_blocks_ (passed in: the host pool's workers have
+ * no tape of their own). */
 template <typename F>
-inline void block_column(const host_block& b, size_t j, F&& f) {
+inline void block_column(const std::vector<host_block>& blocks, const host_block& b, size_t j, F&& f) {
   const size_t r = size_t(b.rows);
   switch (b.layout) {
     case layout_lower: {
@@ -213,7 +215,7 @@ inline void block_column(const host_block& b, size_t j, F&& f) {
       if (b.base >= 0) {  // (the base's column through a buffer: no recursive instantiation)
         thread_local std::vector<vari*> col;
         col.resize(r);
-        block_column_ptrs(ChainableStack::instance_->host_blocks_[size_t(b.base)], j, col.data());
+        block_column_ptrs(blocks, blocks[size_t(b.base)], j, col.data());
         for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : col[i]);
       } else {
         vari* const* e = b.base_elems + j * r;
@@ -228,22 +230,8 @@ inline void block_column(const host_block& b, size_t j, F&& f) {
   }
 }
 
-inline void block_column_ptrs(const host_block& b, size_t j, vari** out) {
-  block_column(b, j, [out](size_t i, vari* v) { out[i] = v; });
-}
-
-/** the vari at element (i, j) of host block b */
-inline vari* block_elem(const host_block& b, size_t i, size_t j) {
-  const size_t r = size_t(b.rows);
-  switch (b.layout) {
-    case layout_lower: return i >= j ? b.first + tril_off(r, j) + (i - j) : b.dummy;
-    case layout_sym: return i >= j ? b.first + tril_off(r, j) + (i - j) : b.first + tril_off(r, i) + (j - i);
-    case layout_diag:
-      if (i == j && j < b.n) return b.first + j;
-      return b.base >= 0 ? block_elem(ChainableStack::instance_->host_blocks_[size_t(b.base)], i, j)
-                         : b.base_elems[i + j * r];
-    default: return b.first + i + j * r;
-  }
+inline void block_column_ptrs(const std::vector<host_block>& blocks, const host_block& b, size_t j, vari** out) {
+  block_column(blocks, b, j, [out](size_t i, vari* v) { out[i] = v; });
 }
 
 /** smg_pack_tril's mode for a layout's owned varis (-1: dense, no packing) */
@@ -273,7 +261,7 @@ inline long recognise_block_index(const var* d, size_t n, int rows, int cols) {
           bool good = true;
           for (size_t j = j0; good && j < j1; ++j) {
             const var* col = d + j * r;
-            block_column(b, j, [&](size_t i, vari* v) { good &= col[i].vi_ == v; });
+            block_column(blocks, b, j, [&](size_t i, vari* v) { good &= col[i].vi_ == v; });
           }
           return good;
         },
@@ -289,13 +277,14 @@ inline dev_matrix_vari* recognise_block(const var* d, size_t n, int rows, int co
 
 /** Write block b's element varis into d (column-major rows x cols). */
 inline void fill_block_pointers(const host_block& b, var* d) {
+  const std::vector<host_block>& blocks = ChainableStack::instance_->host_blocks_;
   const size_t r = size_t(b.rows);
   host_parallel_for(
       size_t(b.cols),
       [&](size_t j0, size_t j1) {
         for (size_t j = j0; j < j1; ++j) {
           var* col = d + j * r;
-          block_column(b, j, [&](size_t i, vari* v) { col[i].vi_ = v; });
+          block_column(blocks, b, j, [&](size_t i, vari* v) { col[i].vi_ = v; });
         }
       },
       col_grain(b.rows));

@@ -44,7 +44,7 @@ struct pending_adjoint {
  * the n varis the block owns, contiguous in the arena, registered here
  * instead of on var_nochain_stack_ (zeroed by set_zero_all_adjoints).  Which
  * vari stands at element (i, j) follows the reference's vari identity for the
- * producing function (layout; stan/math/amd/matrix.hpp block_elem):
+ * producing function (layout; stan/math/amd/matrix.hpp block_column):
  *   0 dense  every element its own vari, column-major (n = rows cols);
  *   1 lower  a cholesky_decompose factor: the lower triangle packed column by
  *            column (n = rows (rows + 1) / 2), the strict upper one dummy vari

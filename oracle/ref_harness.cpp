@@ -46,6 +46,7 @@
 #define STAN_MATH_REV_CORE_INIT_CHAINABLESTACK_HPP
 #include <stan/math/mix/mat.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -55,6 +56,7 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gen.h"
@@ -709,6 +711,7 @@ static void fix_glm() {
     j.put_int("M", c.M);
     j.put("fx", fx);
     j.put_vec("grad", g);
+#ifndef STAN_THREADS  // (the threaded map_rect needs libtbb: the STAN_THREADS build only benches)
     if (c.R == 100000) {
       std::vector<std::vector<double>> xr;
       std::vector<std::vector<int>> xi;
@@ -719,6 +722,7 @@ static void fix_glm() {
       j.put("fx_map_rect32", fx2);
       j.put_vec("grad_map_rect32", g2);
     }
+#endif
     write_fixture("glm_R" + std::to_string(c.R) + "_M" + std::to_string(c.M), j);
   }
   {  // extreme linear predictors exercise the +-20 cutoff branches
@@ -998,6 +1002,7 @@ struct hier_maprect_functor {
   }
 };
 static void fix_maprect() {
+#ifndef STAN_THREADS
   for (int J : {7, 1, 16}) {
     std::vector<std::vector<double>> xr;
     std::vector<std::vector<int>> xi;
@@ -1016,6 +1021,7 @@ static void fix_maprect() {
     j.put_vec("values", vals);
     write_fixture("map_rect_hier_J" + std::to_string(J), j);
   }
+#endif
 }
 
 // ---- mdivide_left_spd, log_determinant_spd,
@@ -1540,6 +1546,61 @@ static double now() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+#ifdef STAN_THREADS
+// config 4 on every host core the way the reference's threaded map_rect
+// runs it (rev/mat/functor/map_rect_concurrent.hpp:39-57: the jobs' nested
+// gradients -- map_rect_reduce -- in parallel, here on std::threads instead
+// of TBB, each with its own thread-local tape; STAN_THREADS build
+// oracle/_ref/ref_harness_mt): 32 row-shard jobs of bernoulli_logit_glm_lpmf,
+// their values and gradients summed in job order.
+struct glm_rows_functor {
+  const MatrixXd& x;
+  const std::vector<int>& y;
+  template <typename T>
+  T operator()(const Matrix<T, Dynamic, 1>& th) const {
+    Matrix<T, Dynamic, 1> beta = th.tail(x.cols());
+    return stan::math::bernoulli_logit_glm_lpmf(y, x, th(0), beta);
+  }
+};
+static int bench_glm_mt(int R, int reps, int threads) {
+  const int shards = 32, M = 256;
+  glm_data d = glm_inputs(R, M);
+  std::vector<MatrixXd> xs(shards);
+  std::vector<std::vector<int>> ys(shards);
+  for (int s = 0; s < shards; ++s) {
+    const int r0 = (int)((long long)R * s / shards), r1 = (int)((long long)R * (s + 1) / shards);
+    xs[s] = d.x.middleRows(r0, r1 - r0);
+    ys[s].assign(d.y.begin() + r0, d.y.begin() + r1);
+  }
+  std::vector<double> fxs(shards);
+  std::vector<VectorXd> gs(shards);
+  double fx = 0.0;
+  VectorXd g = VectorXd::Zero(M + 1);
+  const double t0 = now();
+  for (int rep = 0; rep < reps; ++rep) {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+      pool.emplace_back([&, t] {
+        stan::math::ChainableStack tape;  // this thread's tape (the reference's STAN_THREADS contract)
+        for (int s = t; s < shards; s += threads)
+          stan::math::gradient(glm_rows_functor{xs[s], ys[s]}, d.theta, fxs[s], gs[s]);
+      });
+    for (auto& th : pool) th.join();
+    fx = 0.0;
+    g.setZero();
+    for (int s = 0; s < shards; ++s) {
+      fx += fxs[s];
+      g += gs[s];
+    }
+  }
+  const double per = (now() - t0) / reps;
+  std::printf("{\"config\": \"glm_mt\", \"N\": %d, \"reps\": %d, \"seconds_per_eval\": %.9g, "
+              "\"evals_per_sec\": %.9g, \"fx\": %.17g, \"threads\": %d, \"shards\": %d, \"grad0\": %.17g}\n",
+              R, reps, per, 1.0 / per, fx, threads, shards, g(0));
+  return 0;
+}
+#endif
+
 static int bench(const std::string& cfg, int N, int reps) {
   double t0 = 0, t1 = 0, fx = 0;
   VectorXd g;
@@ -1624,6 +1685,13 @@ int main(int argc, char** argv) {
     if (want("boundary")) fix_boundary();
     return 0;
   }
+#ifdef STAN_THREADS
+  if (argc >= 5 && std::string(argv[1]) == "bench" && std::string(argv[2]) == "glm_mt") {
+    int threads = argc >= 6 ? std::atoi(argv[5]) : 0;
+    if (threads <= 0) threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    return bench_glm_mt(std::atoi(argv[3]), std::atoi(argv[4]), threads);
+  }
+#endif
   if (argc >= 5 && std::string(argv[1]) == "bench")
     return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
   std::fprintf(stderr,

@@ -9,7 +9,7 @@ for line in txt.splitlines():
     if not line.startswith("WG 0:"):
         continue
     ev = [(int(j), int(t), int(p), float(us)) for j, t, p, us in re.findall(r"\[j(\d+) t(\d+) p(\d+) ([\d.]+)us\]", line)]
-    names = {2: "start", 10: "factor+inv", 3: "Dinv st", 4: "publish", 11: "wait+load", 12: "lstore", 13: "LTJ", 9: "SYRK"}
+    names = {2: "start", 10: "factor+leaves", 3: "Dinv st", 4: "publish", 11: "wait+load", 12: "lstore", 13: "TRSM", 9: "SYRK"}
     prev = None
     for j, t, p, us in ev:
         if prev is not None:

@@ -18,3 +18,12 @@ for w in ${WLS:-gp gp_eigen}; do
   timeout -k 10 400 python bench.py --workload $w --steps $ST --no-cpu-baseline > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err || { tail $O/${TAG}_bench_$w.err; exit 1; }
   python -c "import json;d=json.load(open('$O/${TAG}_bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('eval_phases_ms', ''))"
 done
+if [ "${UBP:-0}" = 1 ]; then  # the panel kernel's chain trace (tools/ubench_panel.hip) + its accuracy vs a host Cholesky
+  timeout -k 10 120 ./tools/ubench_panel > $O/${TAG}_ubp.txt 2>&1 || { tail $O/${TAG}_ubp.txt; exit 1; }
+  grep -E "panel kernel|potrf_diag" $O/${TAG}_ubp.txt
+fi
+if [ "${PROF:-0}" = 1 ]; then  # kernel trace of the GP bench (rocprofv3; the program itself after --)
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-glm-strong > $O/${TAG}_prof.log 2>&1 || { tail $O/${TAG}_prof.log; exit 1; }
+  echo prof ok
+fi
