@@ -218,7 +218,9 @@ __global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int 
 // PANEL_MAX_STEPS diagonal blocks (columns [J, K), all rows below), where the
 // blocked loop above would issue potrf / TRSM / trapezoid-update launches
 // per 64-column step.  Workgroup 0 is the diagonal chain; row tile t >= 1
-// (64 rows from J + 64 t) belongs to workgroup 1 + (t - 1) mod (gridDim.x - 1),
+// (64 rows from J + 64 t in the panel, 32-row tiles below it: panel_tiles)
+// belongs to workgroup 2 + (t - 1) mod (gown - 2)
+// (workgroup 1 inverts the factored diagonal blocks),
 // which applies every step's update to it, so the only cross-workgroup
 // dependencies are
 //   * the factored diagonal block j (L_jj, which every tile solves against): flag diag[j];
@@ -235,6 +237,7 @@ __global__ __launch_bounds__(512) void k_potrf_diag(double* __restrict__ L, int 
 // hang the device.
 constexpr int PANEL_MAX_STEPS = 8;
 constexpr int PANEL_MAX_GRID = 256;
+constexpr int PANEL_BELOW_ROWS = 32;  // row tiles below the panel (panel_tiles)
 
 // dev instrumentation (tools/ubench_panel.hip): per-workgroup event log of
 // (s_memrealtime, code); compiled out of the library
@@ -253,6 +256,36 @@ __device__ int g_panel_trace_n[PANEL_MAX_GRID];
 #define PANEL_EV(code)
 #endif
 
+// dev instrumentation (tools/ubench_timeline.cpp): device-clock start / end
+// of every panel launch (slot = epoch mod 64) and host-placed stamps, to see
+// the panels' gaps inside a whole evaluation without a profiler (which
+// serialises dispatches); compiled out of the library
+#ifdef SMG_PANEL_TIMELINE
+__device__ unsigned long long g_panel_tl[3 * 64];
+struct panel_tl_end {
+  int e;
+  __device__ ~panel_tl_end() {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&g_panel_tl[2 * (e & 63) + 1], __builtin_amdgcn_s_memrealtime());
+  }
+};
+#define PANEL_TL()                                                                               \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_panel_tl[2 * (epoch & 63)] = __builtin_amdgcn_s_memrealtime(); \
+  panel_tl_end tl_end_{epoch};
+__global__ void k_tl_stamp(int slot) {
+  if (threadIdx.x == 0) g_panel_tl[128 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+extern "C" int smg_dev_timeline(smg_ctx* ctx, int stamp_slot, unsigned long long* out) {
+  if (stamp_slot >= 0) {
+    hipLaunchKernelGGL(k_tl_stamp, dim3(1), dim3(64), 0, ctx->stream, stamp_slot & 63);
+    return 0;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_panel_tl), sizeof(g_panel_tl)) == hipSuccess ? 0 : SMG_ERR_HIP;
+}
+#else
+#define PANEL_TL()
+#endif
+
 // hand-off primitives (st_dev / panel_publish / panel_wait): smg_sync.h
 
 // The chain's LDS phases out of line: each compiles with its own register
@@ -268,9 +301,6 @@ __device__ __noinline__ void chain_leaves(const lds_dbl* D, lds_dbl* X) {
   if ((threadIdx.x >> 6) < 4) trtri_leaf16(D, X, threadIdx.x >> 6);
 }
 __device__ __noinline__ void chain_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) { lds_trsm64_rt(Y, D, X); }
-__device__ __noinline__ void chain_ltj(lds_dbl* Y, const lds_dbl* X) {
-  lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Y, Y, X);
-}
 __device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }
 __device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const lds_dbl* B) {
   lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
@@ -278,15 +308,28 @@ __device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const ld
 #define CHAIN_FACTOR(D, st) chain_factor((lds_dbl*)(D), (st))
 #define CHAIN_LEAVES(D, X) chain_leaves((const lds_dbl*)(D), (lds_dbl*)(X))
 #define CHAIN_TRSM(Y, D, X) chain_trsm((lds_dbl*)(Y), (const lds_dbl*)(D), (const lds_dbl*)(X))
-#define CHAIN_LTJ(Y, X) chain_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
+__device__ __noinline__ void below_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) {
+  lds_trsm64_rt(Y, D, X, PANEL_BELOW_ROWS / 16);
+}
+__device__ __noinline__ void below_ltj(lds_dbl* Y, const lds_dbl* X) {
+  lds_mma32_8w<lds_dbl*, const lds_dbl*>(Y, Y, X);
+}
+__device__ __noinline__ void below_update(lds_dbl* Z, const lds_dbl* D, const lds_dbl* B) {
+  lds_mma32_8w<lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
+}
 #define CHAIN_SYRK(Zn, Y, b) chain_syrk((lds_dbl*)(Zn), (const lds_dbl*)(Y), (b))
 #define OWNER_UPDATE(Z, D, B) owner_update((lds_dbl*)(Z), (const lds_dbl*)(D), (const lds_dbl*)(B))
+#define BELOW_LTJ(Y, X) below_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
+#define BELOW_TRSM(Y, D, X) below_trsm((lds_dbl*)(Y), (const lds_dbl*)(D), (const lds_dbl*)(X))
+#define BELOW_UPDATE(Z, D, B) below_update((lds_dbl*)(Z), (const lds_dbl*)(D), (const lds_dbl*)(B))
 #else
+#define BELOW_LTJ(Y, X) lds_mma32_8w<double*, const double*>((Y), (Y), (X))
+#define BELOW_TRSM(Y, D, X) lds_trsm64_rt((Y), (D), (X), PANEL_BELOW_ROWS / 16)
+#define BELOW_UPDATE(Z, D, B) lds_mma32_8w<double*, const double*>((Z), (D), (B), -1.0, 1.0)
 #define CHAIN_FACTOR(D, st) lds_potrf64_lookahead((D), (st))
 #define CHAIN_LEAVES(D, X) \
   if ((threadIdx.x >> 6) < 4) trtri_leaf16((D), (X), threadIdx.x >> 6)
 #define CHAIN_TRSM(Y, D, X) lds_trsm64_rt((Y), (D), (X))
-#define CHAIN_LTJ(Y, X) lds_mma64_8w<false, true>((Y), (Y), (X))
 #define CHAIN_SYRK(Zn, Y, b) lds_syrk64_8w_next((Zn), (Y), (b))
 #define OWNER_UPDATE(Z, D, B) lds_mma64_8w<false, true>((Z), (D), (B), -1.0, 1.0)
 #endif
@@ -298,30 +341,35 @@ struct panel_regs {
   double v[8];
   unsigned ok;
 };
-__device__ inline void panel_gload(panel_regs& R, const double* A, int ld, int rows, int cols,
+// R = 64: a 64-row tile (8 elements per thread); R = 32: the 32-row tiles
+// below the panel (4 per thread), rows 0 .. 31 of the same LDS layout
+template <int R = 64>
+__device__ inline void panel_gload(panel_regs& Rg, const double* A, int ld, int rows, int cols,
                                    bool lower) {
-  R.ok = 0;
+  Rg.ok = 0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < R / 8; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
-    const int c = e >> 6, r = e & 63;
-    R.v[q] = ld_dev(&A[min(r, rows - 1) + (size_t)min(c, cols - 1) * ld]);  // handed-off data: sc1
-    R.ok |= (r < rows && c < cols && (!lower || r >= c)) ? (1u << q) : 0u;
+    const int c = e / R, r = e % R;
+    Rg.v[q] = ld_dev(&A[min(r, rows - 1) + (size_t)min(c, cols - 1) * ld]);  // handed-off data: sc1
+    Rg.ok |= (r < rows && c < cols && (!lower || r >= c)) ? (1u << q) : 0u;
   }
 }
-__device__ inline void panel_lstore(double* D, const panel_regs& R) {
+template <int R = 64>
+__device__ inline void panel_lstore(double* D, const panel_regs& Rg) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < R / 8; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
-    D[(e & 63) * SMG_NBP + (e >> 6)] = ((R.ok >> q) & 1u) ? R.v[q] : 0.0;
+    D[(e % R) * SMG_NBP + e / R] = ((Rg.ok >> q) & 1u) ? Rg.v[q] : 0.0;
   }
 }
+template <int R = 64>
 __device__ inline void panel_gstore(const double* D, double* A, int ld, int rows, int cols,
                                     bool lower) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < R / 8; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
-    const int c = e >> 6, r = e & 63;
+    const int c = e / R, r = e % R;
     if (r < rows && c < cols && (!lower || r >= c)) st_dev(&A[r + (size_t)c * ld], D[r * SMG_NBP + c]);
   }
 }
@@ -345,6 +393,15 @@ __device__ inline void panel_gstore_tri(const double* D, double* A, int ld, int 
   }
 }
 
+// Row tiles of a panel: t < nb are the panel's 64-row tiles (rows J + 64 t),
+// the rows below the panel come in 32-row tiles (rows J + 64 nb + 32 (t - nb)):
+// their owners' seven column updates per step, not the chain, bounded the
+// panel's end at 64 rows, and their rows are independent (no extra hand-off)
+__host__ __device__ inline int panel_tiles(int n, int J, int nb) {
+  const int below0 = J + SMG_NB * nb;
+  return nb + (n > below0 ? (n - below0 + PANEL_BELOW_ROWS - 1) / PANEL_BELOW_ROWS : 0);
+}
+
 // column block c of panel tile t is updated by t's helper workgroup
 __device__ __forceinline__ bool panel_helped(int t, int c, int nb, int nh) {
   return t < nb && t >= 3 && t - 3 < nh && (c & 1) && c <= t - 2;
@@ -357,19 +414,44 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
   __shared__ double Z[SMG_NB * SMG_NBP];
+  PANEL_TL();
   constexpr int S = PANEL_MAX_STEPS;
   int* diag = flags;           // diag[j]: L_jj stored
   int* row = flags + S;        // row[j S + t]: L_tj stored (panel tiles t < nb)
   int* done = flags + S + S * S;  // done[j S + t]: tile t's step-j updates stored
   int* hflag = flags + S + 2 * S * S;  // hflag[j S + t]: tile t's helper finished step j
+  int* dinvf = flags + S + 3 * S * S;  // dinvf[j]: Dinv_j stored (the inverter workgroup)
   const int nb = (K - J + SMG_NB - 1) / SMG_NB;
-  const int T = (n - J + SMG_NB - 1) / SMG_NB;
+  const int T = panel_tiles(n, J, nb);
   // Column helpers: panel tile t >= 3 (t < nb) gets workgroup gown + t - 3,
   // which applies the updates of its odd column blocks c <= t - 2 (panel_helped);
   // the owner of t does the rest, its L_tj, and waits hflag[(j-1) S + t]
   // before reading a helped column j.  The owners of the last panel tiles
   // were the chain's bottleneck (their seven column updates per step).
+  // workgroup 1 is the inverter: Dinv_j = L_jj^{-1} (the aux level SMG_NB)
+  // once the chain publishes L_jj; the tiles below the panel multiply by it
+  // (their column updates, not the chain, bound the panel's end, so their
+  // cheaper product beats the solve), the panel tiles solve against L_jj
+  // (the chain needs their updates sooner).  Owners are workgroups
+  // 2 .. gown - 1, column helpers gown ...
   const int nh = gridDim.x - gown;
+  if (blockIdx.x == 1) {
+    __shared__ double Tin[3 * 256];
+    for (int j = 0; j < nb; ++j) {
+      const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
+      panel_wait(&diag[j], epoch, status);
+      panel_regs Rl;
+      panel_gload(Rl, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);
+      __syncthreads();
+      panel_lstore_id(D, Rl, bj);
+      __syncthreads();
+      lds_trtri64_mfma(D, X, Tin);
+      __syncthreads();
+      panel_gstore_tri(X, Dinv + cj, ldd, bj);
+      panel_publish(&dinvf[j], epoch);
+    }
+    return;
+  }
 
   if (blockIdx.x >= gown) {
     const int t = 3 + (blockIdx.x - gown);
@@ -439,11 +521,12 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       // the leaf inverses, so their latency hides behind them; the next
       // tile's operands are loaded there too.  No 64 x 64 inverse on the
       // chain: L_{t,j} = A_{t,j} L_jj^{-T} by the leaf inverses and one
-      // row-tile solve (the block inverses for later use come from
-      // k_trtri_blocks after the panel)
+      // row-tile solve (the inverter workgroup forms Dinv_j beside it)
       CHAIN_FACTOR(Dc, status);
       __syncthreads();
+      PANEL_EV((j << 16) | (j << 8) | 14);
       panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
+      PANEL_EV((j << 16) | (j << 8) | 15);
       if (more) load_next();
       CHAIN_LEAVES(Dc, X);
       PANEL_EV((j << 16) | (j << 8) | 10);
@@ -468,16 +551,67 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     return;
   }
 
-  // the other workgroups: tiles t >= 1, owner(t) = 1 + (t - 1) mod (grid - 1);
+  // the other workgroups: tiles t >= 1, owner(t) = 2 + (t - 1) mod (gown - 2);
   // every step of tile t.  At step t - 1 of a panel tile (t < nb) the owner
   // only computes, stores and publishes L_{t,t-1}: the chain applies the
   // A_tt update privately
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
-    for (int t = 1 + (blockIdx.x - 1); t < T; t += gown - 1) {
+    for (int t = 1 + (blockIdx.x - 2); t < T; t += gown - 2) {
       if (t <= j) continue;  // done
-      const bool next = t == j + 1 && t < nb;  // the chain's next diagonal tile
+      if (t >= nb) {  // a 32-row tile below the panel: L_tj = A_tj Dinv_j^T, then A_tc -= L_tj L_cj^T (c < nb)
+        constexpr int R = PANEL_BELOW_ROWS;
+        const int rt0 = J + SMG_NB * nb + R * (t - nb), rt = min(R, n - rt0);
+        __syncthreads();  // LDS of the previous item fully consumed
+        PANEL_EV((j << 16) | (t << 8) | 5);
+        panel_regs Ra, Rd;
+        panel_gload<R>(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);  // own data, final
+        if (j + 1 < nb) {
+          panel_wait(&dinvf[j], epoch, status);
+          PANEL_EV((j << 16) | (t << 8) | 6);
+          panel_gload(Rd, Dinv + cj, ldd, bj, bj, true);
+          panel_lstore<R>(D, Ra);
+          panel_lstore(X, Rd);
+          __syncthreads();
+          BELOW_LTJ(D, X);
+        } else {  // the last step: solve against L_jj (the chain's end, not the inverter's, bounds it)
+          panel_wait(&diag[j], epoch, status);
+          PANEL_EV((j << 16) | (t << 8) | 6);
+          panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
+          panel_lstore<R>(D, Ra);
+          panel_lstore_id(X, Rd, bj);
+          __syncthreads();
+          CHAIN_LEAVES(X, Y);
+          __syncthreads();
+          BELOW_TRSM(D, X, Y);
+          __syncthreads();
+        }
+        panel_gstore<R>(D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+        PANEL_EV((j << 16) | (t << 8) | 7);
+        if (j + 1 >= nb) continue;
+        panel_wait_all(row + j * S, j + 1, nb - 1, 1, epoch, status);
+        panel_regs Ryn, Rzn;
+        auto issue = [&](int c) {
+          const int cc = J + SMG_NB * c;
+          panel_gload<R>(Rzn, L + rt0 + (size_t)cc * ldl, ldl, rt, min(SMG_NB, K - cc), false);
+          panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
+        };
+        issue(j + 1);
+        for (int c = j + 1; c < nb; ++c) {
+          const int cc = J + SMG_NB * c;
+          __syncthreads();  // previous product's Y / Z consumed
+          panel_lstore(Y, Ryn);
+          panel_lstore<R>(Z, Rzn);
+          __syncthreads();
+          if (c + 1 < nb) issue(c + 1);  // in flight during this product
+          BELOW_UPDATE(Z, D, Y);
+          panel_gstore<R>(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, min(SMG_NB, K - cc), false);
+          PANEL_EV((j << 16) | (t << 8) | (16 + c));
+        }
+        continue;
+      }
+      const bool next = t == j + 1;  // the chain's next diagonal tile
       const int rt0 = J + SMG_NB * t;
       const int rt = min(SMG_NB, n - rt0);
       __syncthreads();  // LDS of the previous item fully consumed
@@ -486,6 +620,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       // a helped column is final once the helper has finished step j - 1
       if (panel_helped(t, j, nb, nh)) panel_wait(&hflag[(j - 1) * S + t], epoch, status);
       panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);  // own data, final
+      // a panel tile: solve against L_jj (the chain's own solve for tile j + 1: the same bits)
       panel_wait(&diag[j], epoch, status);
       PANEL_EV((j << 16) | (t << 8) | 6);
       panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
@@ -494,18 +629,18 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       __syncthreads();
       CHAIN_LEAVES(X, Y);
       __syncthreads();
-      CHAIN_TRSM(D, X, Y);  // L_tj = A_tj L_jj^{-T} (the chain's own solve: the same bits)
+      CHAIN_TRSM(D, X, Y);
       __syncthreads();
       panel_gstore(D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
       PANEL_EV((j << 16) | (t << 8) | 7);
-      if (t < nb) panel_publish(&row[j * S + t], epoch);
+      panel_publish(&row[j * S + t], epoch);
       if (next) continue;
       // A_tc -= L_tj L_cj^T for the panel's later column blocks c <= t.  The
       // rows L_cj (c < t) are published by their owners at about the same
       // time, so ONE wait covers all of them; the operands of update c + 1
       // are then loaded while update c's product runs.
-      const int clast = min(t, nb - 1);
-      const int cwait = min(clast, t - 1);  // L_tt's row is this tile's own
+      const int clast = t;
+      const int cwait = t - 1;  // L_tt's row is this tile's own
       if (j + 1 <= cwait) panel_wait_all(row + j * S, j + 1, cwait, 1, epoch, status);
       panel_regs Ryn, Rzn;
       auto issue = [&](int c) {
@@ -534,7 +669,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, own);
         PANEL_EV((j << 16) | (t << 8) | (16 + c));
       }
-      if (t == j + 2 && t < nb) panel_publish(&done[j * S + t], epoch);
+      if (t == j + 2) panel_publish(&done[j * S + t], epoch);
     }
   }
 }
@@ -547,21 +682,6 @@ __global__ __launch_bounds__(512) void k_trtri_diag(const double* __restrict__ L
   lds_load_block(D, L, ldl, b, true);
   __syncthreads();
   lds_potrf_inv64_blk(D, X, b, nullptr, 0, Dinv, ldd, nullptr, false);
-}
-
-// The 64-row block inverses (the aux level SMG_NB, lower with zeros above) of
-// the diagonal blocks [j0, j1) of L, one workgroup per block: the panel
-// kernel solves against L_jj itself, so the inverses the later blocked
-// solves and the doubling start from are formed here, off the panel chain
-__global__ __launch_bounds__(512) void k_trtri_blocks(const double* __restrict__ L, int ldl, int j0, int j1,
-                                                      double* __restrict__ Dinv, int ldd) {
-  __shared__ double D[SMG_NB * SMG_NBP];
-  __shared__ double X[SMG_NB * SMG_NBP];
-  const int j = j0 + SMG_NB * blockIdx.x;
-  const int b = min(SMG_NB, j1 - j);
-  lds_load_block(D, L + j + (size_t)j * ldl, ldl, b, true);
-  __syncthreads();
-  lds_potrf_inv64_blk(D, X, b, nullptr, 0, Dinv + j, ldd, nullptr, false);
 }
 
 // symbolic_rev (cholesky_decompose.hpp:101-111) on one diagonal block:
@@ -1008,13 +1128,13 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   }
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
-  hipEvent_t Tinv = nullptr;  // the side stream's last k_trtri_blocks
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
       // workgroup 0 = diagonal chain; tiles 1 .. T-1 over the others
-      const int T = smg_ceil_div(n - J, SMG_NB);
-      const int grid = T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID;  // chain + owners of tiles 1..T-1
+      const int T = panel_tiles(n, J, smg_ceil_div(K - J, SMG_NB));
+      // chain, inverter, owners of tiles 1..T-1
+      const int grid = (T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID) + 1;
       const int epoch = ++ctx->flag_epoch;
       ctx->status_armed = 1;
       // column helpers for panel tiles 3 .. nb-1 (SMG_PANEL_HELPERS=0: none)
@@ -1024,7 +1144,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       }();
       const int nbp = smg_ceil_div(K - J, SMG_NB);
       int nh = use_helpers && nbp > 3 ? nbp - 3 : 0;
-      if (grid + nh > PANEL_MAX_GRID || nbp > T) nh = 0;
+      if (grid + nh > PANEL_MAX_GRID + 1 || nbp > T) nh = 0;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
     }
@@ -1032,9 +1152,6 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     const int m = n - K;
     const double* P = L + K + (size_t)J * ldl;
     if (!look) {  // trailing A[K:, K:] -= L[K:, J:K] L[K:, J:K]^T (lower)
-      hipLaunchKernelGGL(k_trtri_blocks, dim3(smg_ceil_div(K - J, SMG_NB)), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
-                         ldl, J, K, Dinv, n);
-      SMG_LAUNCH_CHECK();
       int rc = smg_gemm_impl(ctx, 0, 1, 1, m, m, K - J, -1.0, P, ldl, P, ldl, 1.0,
                              L + K + (size_t)K * ldl, ldl);
       if (rc) return rc;
@@ -1063,17 +1180,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       F = smg_event(ctx, nev++);
       if (!F) return SMG_ERR_HIP;
       SMG_HIP_TRY(hipEventRecord(F, ctx->side));
-    } else {  // no (b): the side stream still follows this panel
+    } else if (prog) {  // no (b): the side stream still follows this panel
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
-    }
-    {  // this panel's 64-row block inverses, behind (b) on the side stream (off the chain)
-      smg_on_side on(ctx);
-      hipLaunchKernelGGL(k_trtri_blocks, dim3(smg_ceil_div(K - J, SMG_NB)), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
-                         ldl, J, K, Dinv, n);
-      SMG_LAUNCH_CHECK();
-      Tinv = smg_event(ctx, nev++);
-      if (!Tinv) return SMG_ERR_HIP;
-      SMG_HIP_TRY(hipEventRecord(Tinv, ctx->side));
     }
     if (prog) {  // block row J / P of W and K^{-1} (F is recorded before it: the next (a) does not wait for it)
       smg_on_side on(ctx);
@@ -1088,13 +1196,6 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     if (rc) return rc;
   }
   if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
-  if (Tinv) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, Tinv, 0));
-  {  // the last panel's 64-row block inverses (the others': behind each panel)
-    const int Jl = ((n - 1) / NB2) * NB2;
-    hipLaunchKernelGGL(k_trtri_blocks, dim3(smg_ceil_div(n - Jl, SMG_NB)), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L,
-                       ldl, Jl, n, Dinv, n);
-    SMG_LAUNCH_CHECK();
-  }
   // the 128-, 256- and 512-block inverses (reverse pass, triangular solves);
   // progressive: every block row's but the last were formed on `side`, the
   // last one's here on the main stream (idle after the last panel), then the

@@ -189,7 +189,13 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
     ctx->prof_count[i] = 0;
     ctx->prof_flops[i] = 0;
   }
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  // the main stream at the highest priority: when one of its launches (a
+  // Cholesky panel on the critical path) becomes ready together with a side
+  // stream's (the trailing update behind it), the panel's workgroups are
+  // dispatched first instead of waiting for CUs the GEMM took
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_greatest) != hipSuccess) {
     delete ctx;
     return SMG_ERR_HIP;
   }

@@ -26,11 +26,15 @@ __global__ void k_residual(const double* __restrict__ y, const double* __restric
 }
 
 // lp = n * NEG_LOG_SQRT_TWO_PI - 0.5 w.w + sum log(1/L_ii), one block, fixed order
-__global__ void k_mvn_lp(const double* __restrict__ w, const double* __restrict__ L, int ldl, int n,
-                         double* out) {
+// the value: part[2 b] = sum w_i^2, part[2 b + 1] = sum log(1 / L_ii) over
+// workgroup b's strided rows (MVN_LP_PARTS workgroups: the diagonal's
+// scattered loads and the logs spread over CUs), then one fixed-order sum
+constexpr int MVN_LP_PARTS = 32;
+__global__ __launch_bounds__(256) void k_mvn_lp_part(const double* __restrict__ w, const double* __restrict__ L,
+                                                     int ldl, int n, double* __restrict__ part) {
   __shared__ double lds[16];
   double q = 0.0, ld = 0.0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += MVN_LP_PARTS * 256) {
     q += w[i] * w[i];
     ld += log(1.0 / L[i + (size_t)i * ldl]);
   }
@@ -38,12 +42,22 @@ __global__ void k_mvn_lp(const double* __restrict__ w, const double* __restrict_
   __syncthreads();
   ld = block_sum(ld, lds);
   if (threadIdx.x == 0) {
-    const double neg_log_sqrt_two_pi = -log(sqrt(2.0 * M_PI));
-    double logp = neg_log_sqrt_two_pi * n;
-    logp -= 0.5 * q;
-    logp += ld;
-    out[0] = logp;
+    part[2 * blockIdx.x] = q;
+    part[2 * blockIdx.x + 1] = ld;
   }
+}
+__global__ void k_mvn_lp_final(const double* __restrict__ part, int n, double* out) {
+  if (threadIdx.x != 0) return;
+  double q = 0.0, ld = 0.0;
+  for (int b = 0; b < MVN_LP_PARTS; ++b) {
+    q += part[2 * b];
+    ld += part[2 * b + 1];
+  }
+  const double neg_log_sqrt_two_pi = -log(sqrt(2.0 * M_PI));
+  double logp = neg_log_sqrt_two_pi * n;
+  logp -= 0.5 * q;
+  logp += ld;
+  out[0] = logp;
 }
 
 // Ladj(i,j) += adj*(sd_i w_j) for i >= j;  Ladj(i,i) -= adj / L_ii
@@ -144,9 +158,10 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
   smg_prof_scope prof(ctx, SMG_FAM_MVN);
   double* w = ws;
   double* sd = ws + n;
-  double* r = smg_ws(ctx, SMG_WS_RED, 2 * (size_t)n);
+  double* r = smg_ws(ctx, SMG_WS_RED, 2 * (size_t)n + 2 * MVN_LP_PARTS);
   if (!r) return SMG_ERR_OOM;
   double* res = r + n;
+  double* part = r + 2 * (size_t)n;
   int rc;
   // the Cholesky forward's aux holds the 64- and 256-row diagonal-block
   // inverses (smg_cholesky_aux_doubles); without it, build the 64-row level
@@ -167,7 +182,8 @@ int smg_mvn_cholesky_fwd(smg_ctx* ctx, const double* y, const double* mu, const 
   if (rc) return rc;
   rc = smg_trsv_lower_impl(ctx, 1, L, ldl, Dinv, W256, W512, n, w, sd, r, n);  // sd = L^{-T} w
   if (rc) return rc;
-  hipLaunchKernelGGL(k_mvn_lp, dim3(1), dim3(1024), 0, ctx->stream, w, L, ldl, n, out_lp);
+  hipLaunchKernelGGL(k_mvn_lp_part, dim3(MVN_LP_PARTS), dim3(256), 0, ctx->stream, w, L, ldl, n, part);
+  hipLaunchKernelGGL(k_mvn_lp_final, dim3(1), dim3(64), 0, ctx->stream, part, n, out_lp);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

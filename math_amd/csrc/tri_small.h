@@ -101,6 +101,31 @@ __device__ inline void lds_mma64_8w(P C, CP A, CP B, double alpha = 1.0, double 
   __syncthreads();
 }
 
+// The 32-row tiles below a panel: C = alpha A B^T + beta C with A, C 32 x 64
+// (rows 0 .. 31 of the 64-row LDS layout), B 64 x 64.  8 waves: wave w owns
+// row stripe w & 1 and column tile w >> 1 (one accumulator; the SIMD's two
+// waves interleave).  Each element's k order is lds_mma64_8w's.  Safe when C
+// aliases A.
+template <typename P, typename CP>
+__device__ inline void lds_mma32_8w(P C, CP A, CP B, double alpha = 1.0, double beta = 0.0) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = l & 15, fk = l >> 4;
+  const int i = 16 * (w & 1) + fr, j = 16 * (w >> 1) + fr;
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < SMG_NB; k0 += 4) {
+    const int kk = k0 + fk;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[i * SMG_NBP + kk], B[j * SMG_NBP + kk], acc, 0, 0, 0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    auto c = &C[(16 * (w & 1) + fk + 4 * r) * SMG_NBP + 16 * (w >> 1) + fr];
+    *c = beta == 0.0 ? alpha * acc[r] : alpha * acc[r] + beta * *c;
+  }
+  __syncthreads();
+}
+
 // The panel chain's next diagonal block: C = C - A A^T (A, C: 64 x 64 in
 // LDS), written straight in the factorisation's input form -- lower triangle,
 // zero strict upper, identity padding beyond row / column b -- so no separate
@@ -615,6 +640,51 @@ __device__ __forceinline__ void wave_factor8_reg(double (&a)[8], int j0, bool& b
   }
 }
 
+// The same 8 columns two pivots at a time: for the 2x2 diagonal block
+// [[A, B], [B, C]] both reciprocal roots come from values known before
+// either is taken -- r1 = A^{-1/2} and rp = (AC - B^2)^{-1/2}, the second
+// pivot's l22^{-1} = sqrt(A) rp = A r1 rp -- so the two rsq + Newton chains
+// run side by side and the pivot chain is one root deep per PAIR of columns.
+// The rows' entries are pre-broadcast before the roots and scaled locally
+// (as in wave_factor8_reg).  Not bit-identical to wave_factor8_reg (l22 from
+// det / A instead of C - l21^2), same accuracy class.
+__device__ __forceinline__ void wave_factor8_pair(double (&a)[8], int j0, bool& bad) {
+  const int i = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 8; t += 2) {
+    double s0[8], s1[8];
+#pragma unroll
+    for (int c = t + 2; c < 8; ++c) {
+      s0[c] = bcast(a[t], j0 + c);
+      s1[c] = bcast(a[t + 1], j0 + c);
+    }
+    const double A = bcast(a[t], j0 + t);
+    const double B = bcast(a[t], j0 + t + 1);
+    const double C = bcast(a[t + 1], j0 + t + 1);
+    const double det = __builtin_fma(A, C, -(B * B));
+    bad |= !(A > 0.0 && A < INFINITY) || !(det > 0.0 && det < INFINITY);
+    double r1 = __builtin_amdgcn_rsq(A);
+    double rp = __builtin_amdgcn_rsq(det);
+    r1 = r1 * (1.5 - 0.5 * A * r1 * r1);
+    rp = rp * (1.5 - 0.5 * det * rp * rp);
+    r1 = r1 * (1.5 - 0.5 * A * r1 * r1);
+    rp = rp * (1.5 - 0.5 * det * rp * rp);
+    const double r2 = (A * r1) * rp;  // (C - l21^2)^{-1/2}
+    const double l21 = B * r1;
+    const double li0 = a[t] * r1;
+    const double li1 = (a[t + 1] - li0 * l21) * r2;
+    a[t] = li0;
+    a[t + 1] = li1;
+#pragma unroll
+    for (int c = t + 2; c < 8; ++c) {
+      const double lc0 = s0[c] * r1;
+      const double lc1 = (s1[c] - lc0 * l21) * r2;
+      a[c] = a[c] - li0 * lc0 - li1 * lc1;
+    }
+  }
+  (void)i;
+}
+
 // wave 0: factor panel columns j0..j0+7 (rows >= j0) of D in place, with NO
 // cross-lane traffic on the pivot chain: every lane factors the 8x8 diagonal
 // block redundantly in registers (left-looking), then solves its own row
@@ -684,24 +754,27 @@ __device__ __forceinline__ void wave_store8(P D, const double (&a)[8], int j0) {
 }
 
 // wave 0: load, factor (v_readlane broadcasts), store panel j0..j0+7
-template <typename P>
+template <bool PAIR = false, typename P>
 __device__ __forceinline__ void wave_panel8_rl(P D, int j0, bool& bad) {
   const int i = threadIdx.x & 63;
   double a[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) a[t] = (i >= j0) ? D[i * SMG_NBP + j0 + t] : 0.0;
-  wave_factor8_reg(a, j0, bad);
+  if (PAIR)
+    wave_factor8_pair(a, j0, bad);
+  else
+    wave_factor8_reg(a, j0, bad);
   wave_store8(D, a, j0);
 }
 
 // (templated on the pointer type: double* when inlined into a kernel, an
 // address_space(3) pointer when called out of line)
-template <typename P>
+template <bool PAIR = false, typename P>
 __device__ inline void lds_potrf64_lookahead(P D, int* status) {
   const int i = threadIdx.x & 63;
   const int g = threadIdx.x >> 6;
   bool bad = false;
-  if (g == 0) wave_panel8_rl(D, 0, bad);
+  if (g == 0) wave_panel8_rl<PAIR>(D, 0, bad);
   __syncthreads();
   for (int p = 0; p < 7; ++p) {
     const int j0 = 8 * p, c1 = j0 + 8, c2 = j0 + 16;
@@ -720,7 +793,7 @@ __device__ inline void lds_potrf64_lookahead(P D, int* status) {
     __syncthreads();
     // (B) wave 0 factors panel p+1 while waves 1..7 update columns >= c2
     if (g == 0) {
-      wave_panel8_rl(D, c1, bad);
+      wave_panel8_rl<PAIR>(D, c1, bad);
     } else if (c2 < 64) {
       // rank-8 trailing update of rows/cols >= c2 on the matrix cores: 16x16
       // tiles (ti >= tj) from 16-tile t0 = c2/16, 2 MFMAs each (K = 8); only
@@ -852,11 +925,12 @@ __device__ inline void lds_trtri64_mfma(CP D, P X, P T) {
 // column blocks p = 0..3 in order:
 //   Z = Y[w, p] - sum_{q < p} X[w, q] L[p, q]^T,   X[w, p] = Z Li_pp^T
 // (40 MFMAs on one dependency chain per wave; no barrier inside: a wave's
-// LDS accesses complete in order).  Waves >= 4 return at once.
+// LDS accesses complete in order).  Waves >= row_tiles return at once (Y's
+// first 16 row_tiles rows are solved).
 template <typename P, typename CP>
-__device__ inline void lds_trsm64_rt(P Y, CP L, CP Li) {
+__device__ inline void lds_trsm64_rt(P Y, CP L, CP Li, int row_tiles = 4) {
   const int w = threadIdx.x >> 6;
-  if (w >= 4) return;
+  if (w >= row_tiles) return;
   const int l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
   const int r0 = 16 * w;
 #pragma unroll

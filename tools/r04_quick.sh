@@ -18,6 +18,18 @@ for w in ${WLS:-gp gp_eigen}; do
   timeout -k 10 400 python bench.py --workload $w --steps $ST --no-cpu-baseline > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err || { tail $O/${TAG}_bench_$w.err; exit 1; }
   python -c "import json;d=json.load(open('$O/${TAG}_bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('eval_phases_ms', ''))"
 done
+if [ "${UBT:-0}" = 1 ]; then  # device-clock panel timeline of whole GP evaluations (tools/ubench_timeline.cpp)
+  timeout -k 10 120 ./tools/ubench_timeline > $O/${TAG}_ubt.txt 2>&1 || { tail $O/${TAG}_ubt.txt; exit 1; }
+  cat $O/${TAG}_ubt.txt
+fi
+if [ "${UBG:-0}" = 1 ]; then  # the GEMM shapes (tools/ubench_gemm.cpp + ubench_shapes.h)
+  timeout -k 10 120 ./tools/ubench_gemm > $O/${TAG}_ubg.txt 2>&1 || { tail $O/${TAG}_ubg.txt; exit 1; }
+  cat $O/${TAG}_ubg.txt
+fi
+if [ "${UBH:-0}" = 1 ]; then  # host enqueue vs device time of the factorisation (tools/ubench_host.cpp)
+  timeout -k 10 120 ./tools/ubench_host > $O/${TAG}_ubh.txt 2>&1 || { tail $O/${TAG}_ubh.txt; exit 1; }
+  cat $O/${TAG}_ubh.txt
+fi
 if [ "${UBP:-0}" = 1 ]; then  # the panel kernel's chain trace (tools/ubench_panel.hip) + its accuracy vs a host Cholesky
   timeout -k 10 120 ./tools/ubench_panel > $O/${TAG}_ubp.txt 2>&1 || { tail $O/${TAG}_ubp.txt; exit 1; }
   grep -E "panel kernel|potrf_diag" $O/${TAG}_ubp.txt
@@ -26,4 +38,13 @@ if [ "${PROF:-0}" = 1 ]; then  # kernel trace of the GP bench (rocprofv3; the pr
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-glm-strong > $O/${TAG}_prof.log 2>&1 || { tail $O/${TAG}_prof.log; exit 1; }
   echo prof ok
+fi
+if [ "${UBPH:-0}" = 1 ]; then  # the diagonal factorisation's pieces (tools/ubench_phase.hip)
+  timeout -k 10 60 ./tools/ubench_phase > $O/${TAG}_ubph.txt 2>&1 || { tail $O/${TAG}_ubph.txt; exit 1; }
+  cat $O/${TAG}_ubph.txt
+fi
+if [ "${HIPT:-0}" = 1 ]; then  # kernel + HIP API trace of a short GP bench (host enqueue costs)
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --hip-trace -d $O/${TAG}_hipt -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-glm-strong > $O/${TAG}_hipt.log 2>&1 || { tail $O/${TAG}_hipt.log; exit 1; }
+  echo hipt ok
 fi

@@ -40,11 +40,11 @@ int main(int argc, char** argv) {
     if (only >= 0 && int(si) != only) continue;
     const int lda = n, ldb = n, ldc = n;
     for (int w = 0; w < 3; ++w)
-      smg_gemm(ctx, sh.ta, sh.tb, sh.uplo, sh.m, sh.n, sh.k, -1e-3, A, lda, B, ldb, 1.0, C, ldc);
+      smg_gemm_tri(ctx, sh.ta, sh.tb, sh.uplo, sh.tri, sh.m, sh.n, sh.k, -1e-3, A, lda, B, ldb, 1.0, C, ldc);
     const int rr = sh.k == 4096 ? 5 : reps;
     hipEventRecord(e0, s);
     for (int r = 0; r < rr; ++r)
-      smg_gemm(ctx, sh.ta, sh.tb, sh.uplo, sh.m, sh.n, sh.k, -1e-3, A, lda, B, ldb, 1.0, C, ldc);
+      smg_gemm_tri(ctx, sh.ta, sh.tb, sh.uplo, sh.tri, sh.m, sh.n, sh.k, -1e-3, A, lda, B, ldb, 1.0, C, ldc);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
     hipEventElapsedTime(&ms, e0, e1);

@@ -21,7 +21,7 @@ int main(int argc, char** argv) {
   hipMalloc(&status, 4);
   hipMemset(flags, 0, 4096 * 4);
   hipMemset(status, 0, 4);
-  const int T = n / 64;
+  const int T = panel_tiles(n, J, K / 64);
   {  // the single-workgroup diagonal kernel alone, back to back
     hipMemcpy(dL, A.data(), 8ull * n * n, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
@@ -47,8 +47,8 @@ int main(int argc, char** argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    hipLaunchKernelGGL(k_chol_panel, dim3(T + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
-                       status, T);
+    hipLaunchKernelGGL(k_chol_panel, dim3(T + 1 + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
+                       status, T + 1);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
@@ -89,10 +89,10 @@ int main(int argc, char** argv) {
     hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_panel_trace), tr.size() * 8);
     hipMemcpyFromSymbol(cnt.data(), HIP_SYMBOL(g_panel_trace_n), cnt.size() * 4);
     unsigned long long t0 = ~0ull;
-    for (int w = 0; w < T + nh; ++w)
+    for (int w = 0; w < T + 1 + nh; ++w)
       for (int k = 0; k < cnt[w] && k < 64; ++k) t0 = std::min(t0, tr[w * 128 + 2 * k]);
-    for (int w : {0, 5, 6, 7, 10, T + 3, T + 4}) {
-      if (w >= T + nh) continue;
+    for (int w : {0, 1, 6, 7, 8, 11, T - 1, T, T + 4, T + 5}) {
+      if (w >= T + 1 + nh) continue;
       printf("WG %d:", w);
       for (int k = 0; k < cnt[w] && k < 64; ++k) {
         const unsigned long long c = tr[w * 128 + 2 * k + 1];

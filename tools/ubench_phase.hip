@@ -23,10 +23,13 @@ __global__ __launch_bounds__(512) void k_phase(double* g, long long* cyc) {
   long long t0 = stamp();
   if (threadIdx.x < 64) {
     if (WHICH == 0) wave_panel8_local(D, 0, bad);
-    if (WHICH == 1) {
+    if (WHICH == 1 || WHICH == 6) {
       double a[8];
       for (int t = 0; t < 8; ++t) a[t] = D[(threadIdx.x & 63) * SMG_NBP + t];
-      wave_factor8_reg(a, 0, bad);
+      if (WHICH == 1)
+        wave_factor8_reg(a, 0, bad);
+      else
+        wave_factor8_pair(a, 0, bad);
       wave_store8(D, a, 0);
     }
   }
@@ -35,6 +38,7 @@ __global__ __launch_bounds__(512) void k_phase(double* g, long long* cyc) {
   long long t2 = stamp();
   if (WHICH == 2) lds_potrf64_lookahead(D, (int*)(cyc + 60));
   if (WHICH == 3) lds_potrf64_lookahead(D, (int*)(cyc + 60));
+  if (WHICH == 7) lds_potrf64_lookahead<true>(D, (int*)(cyc + 60));
   if (WHICH == 4 || WHICH == 5) {
     __shared__ double X[SMG_NB * SMG_NBP];
     __shared__ double T[768];
@@ -78,6 +82,9 @@ int main() {
   };
   run("panel8 per-lane", k_phase<0>);
   run("panel8 readlane", k_phase<1>);
+  run("panel8 pairs", k_phase<6>);
+  std::vector<double> o7(4096);
+  for (int rep = 0; rep < 3; ++rep) run("lookahead potrf pairs", k_phase<7>, &o7);
   for (int rep = 0; rep < 3; ++rep) {
     run("lookahead potrf", k_phase<2>, &o2);
     run("pre-broadcast potrf", k_phase<3>, &o3);
@@ -109,4 +116,15 @@ int main() {
   for (int e = 0; e < 4096; ++e)
     if ((e >> 6) >= (e & 63) && o2[e] != o3[e]) ++diff;
   printf("lower-triangle entries differing: %d\n", diff);
+  {  // pairs vs per-pivot factor: max |diff| and |L L^T - A|
+    double md = 0, res = 0;
+    for (int r = 0; r < 64; ++r)
+      for (int c = 0; c <= r; ++c) {
+        md = std::max(md, std::abs(o7[r * 64 + c] - o2[r * 64 + c]));
+        double v = 0;
+        for (int k = 0; k <= c; ++k) v += o7[r * 64 + k] * o7[c * 64 + k];
+        res = std::max(res, std::abs(v - h[r + 64 * c]));
+      }
+    printf("pairs vs per-pivot: max |dL| %.2e, |L L^T - A| %.2e\n", md, res);
+  }
 }

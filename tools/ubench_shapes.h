@@ -6,6 +6,7 @@
 struct ub_shape {
   const char* name;
   int ta, tb, uplo, m, n, k;
+  int tri;  // SMG_TRI_* (smg_gemm_tri), 0: dense
 };
 static const ub_shape ub_shapes[] = {
     // forward: (a) next panel's columns (lower trapezoid), (b) the rest (SYRK)
@@ -28,6 +29,13 @@ static const ub_shape ub_shapes[] = {
     {"rev P*R NN (512,2048,512)", 0, 0, 0, 512, 2048, 512},
     {"rev P*R NN (512,3584,512)", 0, 0, 0, 512, 3584, 512},
     {"big NN (4096,4096,4096)", 0, 0, 0, 4096, 4096, 4096},
+    // progressive K^{-1} (chol_mvn.hip smg_inv_prog_row), block row k = 7 / 6
+    {"prog share TN lower (4096,4096,512)", 1, 0, 1, 4096, 4096, 512},
+    {"prog share NT lower (4096,4096,512)", 0, 1, 1, 4096, 4096, 512},
+    {"prog share TN lower (3584,3584,512)", 1, 0, 1, 3584, 3584, 512},
+    {"prog Y NN triB (512,3584,3584)", 0, 0, 0, 512, 3584, 3584, 4},
+    {"prog Y NN dense (512,3584,3584)", 0, 0, 0, 512, 3584, 3584},
+    {"prog W NN triA (512,3584,512)", 0, 0, 0, 512, 3584, 512, 1},
 };
 static const int ub_nshapes = sizeof(ub_shapes) / sizeof(ub_shapes[0]);
 static inline double ub_flops(const ub_shape& s) {
@@ -35,5 +43,5 @@ static inline double ub_flops(const ub_shape& s) {
     const double e = (double)s.n * (s.n + 1) / 2 + (double)(s.m - s.n) * s.n;
     return 2.0 * e * s.k;
   }
-  return 2.0 * s.m * s.n * s.k;
+  return (s.tri ? 1.0 : 2.0) * s.m * s.n * s.k;  // a triangular operand: ~half the products
 }
