@@ -453,6 +453,22 @@ int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long lon
  * form (the host layer's history per tape position). */
 int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                                       double* aux, double* ws, int* started);
+/* smg_cholesky_fwd_checked_mark_inv (ws may be NULL: no K^{-1}) that also
+ * streams the factor to the host while it is formed: once panel p (columns
+ * [512 p, min(512 (p + 1), n)); one panel when n <= 512) is final, its columns
+ * of the packed lower triangle (column-major, column j's rows j..n-1 from
+ * j n - j (j - 1) / 2) are packed into `packed` (device, n (n + 1) / 2
+ * doubles) and copied into host_dst (pinned host memory of the same size)
+ * on the context's zeroing stream, and marker marker_base + p is recorded
+ * behind the copy (smg_marker_wait).  smg_cholesky_stream_panels(n) markers;
+ * marker_base + that count <= 64.  The Eigen boundary's cholesky_decompose
+ * builds the factor's host varis panel by panel while the later panels are
+ * factored (the reference's cholesky_decompose returns an Eigen matrix of
+ * varis, rev/mat/fun/cholesky_decompose.hpp:378-427). */
+int smg_cholesky_stream_panels(int n);
+int smg_cholesky_fwd_checked_mark_stream(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                         double* aux, double* ws, int* started, double* packed, double* host_dst,
+                                         int marker_base);
 
 /* log_sum_exp(vector<var>) (rev/mat/fun/log_sum_exp.hpp:20-53):
  *   fwd: out = max + log(sum exp(x - max)); empty -> -inf; non-finite max -> max

@@ -202,6 +202,8 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int 
 //   Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}  (needs only panels <= k)
 // so that after the last panel only its own block row remains (its inverse,
 // -W_77 Y_7 and one rank-512 update) instead of V22, V12 and all of V V^T.
+// Each block row is four parts (W_kk; W_{k,0:k}; its K^{-1} share; Y_{k+1}),
+// queued by chol_fwd in budgets that fit beside the trailing updates.
 // ws: [W (n x n, ld n) | C (n x n, lower) | Y (P x n, ld P) | T (P/2 x 256)];
 // W's strict upper is never read outside its diagonal blocks (the triangular
 // K cuts stay inside a tile band), whose copies from aux carry stored zeros.
@@ -213,7 +215,7 @@ int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
   return SMG_OK;
 }
 
-int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k,
+int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k, int part,
                      bool inverses_here) {
   constexpr int P = SMG_NBR;
   const size_t nn = (size_t)n * n;
@@ -222,23 +224,40 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
   double* Y = C + nn;
   double* T = Y + (size_t)P * n;
   const int r0 = k * P, r1 = r0 + P;
-  int rc;
-  if (inverses_here) {  // (the solves after the factorisation wait for them: inv_ev_aux)
-    if ((rc = smg_block_inverses_rows(ctx, L, ldl, aux, n, r0, P, T))) return rc;
-    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->stream));
-  }
   const double* Wkk = aux + (size_t)n * SMG_AUX_W512 + r0;  // ld n, stored zeros above
-  SMG_HIP_TRY(hipMemcpy2DAsync(W + r0 + (size_t)r0 * n, n * sizeof(double), Wkk, n * sizeof(double),
-                               P * sizeof(double), P, hipMemcpyDeviceToDevice, ctx->stream));
-  if (k > 0) {  // W_{k,0:k} = -W_kk Y_k
-    if ((rc = smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y, P, 0.0, W + r0, n, SMG_TRI_A_LOWER))) return rc;
+  int rc;
+  switch (part) {
+    case 0:  // W_kk (the block row's 128/256/512 inverses first when asked)
+      if (inverses_here) {  // (the solves after the factorisation wait for them: inv_ev_aux)
+        if ((rc = smg_block_inverses_rows(ctx, L, ldl, aux, n, r0, P, T))) return rc;
+        SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->stream));
+      }
+      SMG_HIP_TRY(hipMemcpy2DAsync(W + r0 + (size_t)r0 * n, n * sizeof(double), Wkk, n * sizeof(double),
+                                   P * sizeof(double), P, hipMemcpyDeviceToDevice, ctx->stream));
+      return SMG_OK;
+    case 1:  // W_{k,0:k} = -W_kk Y_k
+      if (k == 0) return SMG_OK;
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y, P, 0.0, W + r0, n, SMG_TRI_A_LOWER);
+    case 2:  // C (lower, leading r1 x r1) += W_k^T W_k
+      return smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n);
+    default:  // Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}
+      if (r1 >= n) return SMG_OK;
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, r1, 1.0, L + r1, ldl, W, n, 0.0, Y, P, SMG_TRI_B_LOWER);
   }
-  // C (lower, leading r1 x r1) += W_k^T W_k
-  if ((rc = smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n))) return rc;
-  if (r1 < n) {  // Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}
-    if ((rc = smg_gemm_impl(ctx, 0, 0, 0, P, r1, r1, 1.0, L + r1, ldl, W, n, 0.0, Y, P, SMG_TRI_B_LOWER))) return rc;
+}
+
+// device time of part `part` of block row k, us: flops at the rate these
+// products reach beside the panels (~30 TF/s; tools/ubench_gemm's shapes
+// run at 33-46 alone) plus ~6 us per launch
+double smg_inv_prog_cost(int n, int k, int part, bool inverses_here) {
+  constexpr double P = SMG_NBR, rate = 30e6;  // flop per us
+  const double r0 = k * P, r1 = r0 + P;
+  switch (part) {
+    case 0: return inverses_here ? 60.0 : 6.0;
+    case 1: return k == 0 ? 0.0 : 6.0 + P * r0 * P / rate;
+    case 2: return 6.0 + r1 * r1 * P / rate;
+    default: return r1 >= n ? 0.0 : 6.0 + P * r1 * r1 / rate;
   }
-  return SMG_OK;
 }
 
 extern "C" {

@@ -293,12 +293,29 @@ extern "C" int smg_dev_timeline(smg_ctx* ctx, int stamp_slot, unsigned long long
 // spills inlined); the LDS pointers are typed address_space(3) so the
 // callees keep ds_ instructions (a generic pointer would turn them into flat
 // accesses).  Same arithmetic in the same order as inlined.
-// SMG_CHAIN_INLINE restores the inlined phases (A/B builds).
-#ifndef SMG_CHAIN_INLINE
+// the chain's factorisation takes its pivots two at a time (wave_factor8_pair)
+#ifndef SMG_FACTOR_PAIR
+#define SMG_FACTOR_PAIR 1
+#endif
 typedef __attribute__((address_space(3))) double lds_dbl;
-__device__ __noinline__ void chain_factor(lds_dbl* D, int* status) { lds_potrf64_lookahead(D, status); }
-__device__ __noinline__ void chain_leaves(const lds_dbl* D, lds_dbl* X) {
-  if ((threadIdx.x >> 6) < 4) trtri_leaf16(D, X, threadIdx.x >> 6);
+__device__ __noinline__ void chain_factor(lds_dbl* D, int* status) {
+  lds_potrf64_lookahead<SMG_FACTOR_PAIR != 0>(D, status);
+}
+// the chain's leaves also stored (sc1) into the diagonal 16 x 16 blocks of
+// Dinv_j (G = Dinv + cj, ld ldg; the inverter later writes the same bits
+// there), published with diag[j]: the panel tiles load them instead of
+// recomputing them
+__device__ __noinline__ void chain_leaves_pub(const lds_dbl* D, lds_dbl* X, double* G, int ldg, int b) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (w >= 4) return;
+  trtri_leaf16(D, X, w);
+  // the wave's whole leaf, 4 values per lane, rows fastest (128-byte column
+  // runs); read back from LDS after the wave's own writes
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = l + 64 * q, r = 16 * w + (e & 15), c = 16 * w + (e >> 4);
+    if (r < b && c < b) st_dev(&G[r + (size_t)c * ldg], X[r * SMG_NBP + c]);
+  }
 }
 __device__ __noinline__ void chain_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) { lds_trsm64_rt(Y, D, X); }
 __device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }
@@ -306,7 +323,7 @@ __device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const ld
   lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
 }
 #define CHAIN_FACTOR(D, st) chain_factor((lds_dbl*)(D), (st))
-#define CHAIN_LEAVES(D, X) chain_leaves((const lds_dbl*)(D), (lds_dbl*)(X))
+#define CHAIN_LEAVES_PUB(D, X, G, ldg, b) chain_leaves_pub((const lds_dbl*)(D), (lds_dbl*)(X), (G), (ldg), (b))
 #define CHAIN_TRSM(Y, D, X) chain_trsm((lds_dbl*)(Y), (const lds_dbl*)(D), (const lds_dbl*)(X))
 __device__ __noinline__ void below_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) {
   lds_trsm64_rt(Y, D, X, PANEL_BELOW_ROWS / 16);
@@ -322,17 +339,6 @@ __device__ __noinline__ void below_update(lds_dbl* Z, const lds_dbl* D, const ld
 #define BELOW_LTJ(Y, X) below_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
 #define BELOW_TRSM(Y, D, X) below_trsm((lds_dbl*)(Y), (const lds_dbl*)(D), (const lds_dbl*)(X))
 #define BELOW_UPDATE(Z, D, B) below_update((lds_dbl*)(Z), (const lds_dbl*)(D), (const lds_dbl*)(B))
-#else
-#define BELOW_LTJ(Y, X) lds_mma32_8w<double*, const double*>((Y), (Y), (X))
-#define BELOW_TRSM(Y, D, X) lds_trsm64_rt((Y), (D), (X), PANEL_BELOW_ROWS / 16)
-#define BELOW_UPDATE(Z, D, B) lds_mma32_8w<double*, const double*>((Z), (D), (B), -1.0, 1.0)
-#define CHAIN_FACTOR(D, st) lds_potrf64_lookahead((D), (st))
-#define CHAIN_LEAVES(D, X) \
-  if ((threadIdx.x >> 6) < 4) trtri_leaf16((D), (X), threadIdx.x >> 6)
-#define CHAIN_TRSM(Y, D, X) lds_trsm64_rt((Y), (D), (X))
-#define CHAIN_SYRK(Zn, Y, b) lds_syrk64_8w_next((Zn), (Y), (b))
-#define OWNER_UPDATE(Z, D, B) lds_mma64_8w<false, true>((Z), (D), (B), -1.0, 1.0)
-#endif
 
 // rows x cols block of a col-major matrix -> registers (8 per thread, 512
 // threads); branch-free: clamped addresses, out-of-range (and, with lower,
@@ -373,6 +379,31 @@ __device__ inline void panel_gstore(const double* D, double* A, int ld, int rows
     if (r < rows && c < cols && (!lower || r >= c)) st_dev(&A[r + (size_t)c * ld], D[r * SMG_NBP + c]);
   }
 }
+// the 4 diagonal 16 x 16 leaf inverses of Dinv_j (G, ld ldg; identity
+// beyond b, as the chain's identity-padded factor gives them) into the
+// diagonal blocks of Y (2 per thread; r fastest: 128-byte column runs)
+struct panel_leaves {
+  double v[2];
+};
+__device__ inline void panel_gload_leaves(panel_leaves& Rg, const double* G, int ldg, int b) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    const int w = e >> 8, c = (e >> 4) & 15, r = e & 15;
+    const int i = 16 * w + r, j = 16 * w + c;
+    const double v = ld_dev(&G[min(i, b - 1) + (size_t)min(j, b - 1) * ldg]);
+    Rg.v[q] = (i < b && j < b) ? v : (i == j ? 1.0 : 0.0);
+  }
+}
+__device__ inline void panel_lstore_leaves(double* Y, const panel_leaves& Rg) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+    const int w = e >> 8, c = (e >> 4) & 15, r = e & 15;
+    Y[(16 * w + r) * SMG_NBP + 16 * w + c] = Rg.v[q];
+  }
+}
+
 // a b x b lower triangle (loaded with lower = true) into LDS with identity
 // padding beyond b: the factor's leaf inverses stay finite
 __device__ inline void panel_lstore_id(double* D, const panel_regs& R, int b) {
@@ -528,7 +559,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
       PANEL_EV((j << 16) | (j << 8) | 15);
       if (more) load_next();
-      CHAIN_LEAVES(Dc, X);
+      CHAIN_LEAVES_PUB(Dc, X, Dinv + cj, ldd, bj);
       PANEL_EV((j << 16) | (j << 8) | 10);
       panel_publish(&diag[j], epoch);
       PANEL_EV((j << 16) | (j << 8) | 4);
@@ -579,10 +610,11 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
           panel_wait(&diag[j], epoch, status);
           PANEL_EV((j << 16) | (t << 8) | 6);
           panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
+          panel_leaves Rv;
+          panel_gload_leaves(Rv, Dinv + cj, ldd, bj);  // the chain's leaf inverses
           panel_lstore<R>(D, Ra);
           panel_lstore_id(X, Rd, bj);
-          __syncthreads();
-          CHAIN_LEAVES(X, Y);
+          panel_lstore_leaves(Y, Rv);
           __syncthreads();
           BELOW_TRSM(D, X, Y);
           __syncthreads();
@@ -624,10 +656,11 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       panel_wait(&diag[j], epoch, status);
       PANEL_EV((j << 16) | (t << 8) | 6);
       panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
+      panel_leaves Rv;
+      panel_gload_leaves(Rv, Dinv + cj, ldd, bj);  // the chain's leaf inverses
       panel_lstore(D, Ra);
       panel_lstore_id(X, Rd, bj);
-      __syncthreads();
-      CHAIN_LEAVES(X, Y);
+      panel_lstore_leaves(Y, Rv);
       __syncthreads();
       CHAIN_TRSM(D, X, Y);
       __syncthreads();
@@ -1007,8 +1040,15 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
   return SMG_OK;
 }
 
+// the factor streamed to the host panel by panel (smg_cholesky_fwd_checked_mark_stream)
+struct chol_stream_sink {
+  double* packed;   // device, tril_count(n) doubles
+  double* host;     // host (pinned), the same
+  int marker_base;  // marker slot of panel 0
+};
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym, bool mark = false, double* inv_ws = nullptr, int* inv_started = nullptr);
+             bool check_sym, bool mark = false, double* inv_ws = nullptr, int* inv_started = nullptr,
+             const chol_stream_sink* sink = nullptr);
 
 }  // namespace
 
@@ -1064,12 +1104,26 @@ int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, in
   return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started);
 }
 
+int smg_cholesky_stream_panels(int n) { return n <= 0 ? 0 : smg_ceil_div(n, n > SMG_NBF ? SMG_NBF : n); }
+
+int smg_cholesky_fwd_checked_mark_stream(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                         double* Dinv, double* ws, int* started, double* packed, double* host_dst,
+                                         int marker_base) {
+  if (!started || !packed || !host_dst || marker_base < 0) return SMG_ERR_ARG;
+  *started = 0;
+  if (ws && !Dinv) return SMG_ERR_ARG;
+  if (marker_base + smg_cholesky_stream_panels(n) > 64) return SMG_ERR_ARG;
+  if (!ctx || smg_zero_stream_begin(ctx) != SMG_OK) return SMG_ERR_HIP;
+  const chol_stream_sink sink{packed, host_dst, marker_base};
+  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started, &sink);
+}
+
 }  // extern "C"
 
 namespace {
 
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym, bool mark, double* inv_ws, int* inv_started) {
+             bool check_sym, bool mark, double* inv_ws, int* inv_started, const chol_stream_sink* sink) {
   if (!ctx || n < 0 || (n > 0 && (!A || !L || lda < n || ldl < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_FWD);
@@ -1120,14 +1174,39 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   // K^{-1} for the closed-form reverse under an MVN (chol_mvn.hip), formed
   // progressively: block row k of W = L^{-1} and its rank-512 share of
   // K^{-1} on `side` behind each panel's trailing update (b), so that after
-  // the last panel only that panel's own block row remains
+  // the last panel only that panel's own block row remains.  (On a stream of
+  // their own the rows ran 2x slower overall: with GPU_MAX_HW_QUEUES = 4 a
+  // fifth stream shares a hardware queue with another, here the panels'.)
   const bool prog = inv_ws && look && NB2 == SMG_NBR && smg_inv_prog_ok(n) && smg_inv_events(ctx) == SMG_OK;
-  if (prog) {
+  if (prog) {  // side follows the work queued so far (earlier readers of ws)
+    SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
+    SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
     smg_on_side on(ctx);
     if (int rc = smg_inv_prog_init(ctx, n, inv_ws)) return rc;
   }
   int nev = 0;       // pooled events used
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
+  // the block rows' parts (smg_inv_prog_row) queued on `side` behind each
+  // trailing update (b)_p within the slack before (b)_{p+1} becomes ready
+  // (the next panel and its look-ahead (a), minus (b)_p itself): queued
+  // whole, the growing rows held back (b)_{p+1}, the next (a) waiting for it,
+  // and with it the next panel; what does not fit goes after the last panel
+  int q_k = 0, q_part = 0;  // the next part to queue
+  const int rows_prog = prog ? n / SMG_NBR : 0;
+  auto queue_parts = [&](int kmax, double budget_us) -> int {  // budget < 0: all of rows <= kmax
+    while (q_k <= kmax && q_k < rows_prog - 1) {
+      const double c = smg_inv_prog_cost(n, q_k, q_part, true);
+      if (budget_us >= 0 && c > budget_us + 40.0) break;
+      budget_us -= c;
+      smg_on_side on(ctx);
+      if (int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, q_k, q_part, true)) return rc;
+      if (++q_part == 4) {
+        q_part = 0;
+        ++q_k;
+      }
+    }
+    return SMG_OK;
+  };
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
@@ -1137,16 +1216,28 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int grid = (T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID) + 1;
       const int epoch = ++ctx->flag_epoch;
       ctx->status_armed = 1;
-      // column helpers for panel tiles 3 .. nb-1 (SMG_PANEL_HELPERS=0: none)
-      static const bool use_helpers = [] {
-        const char* e = getenv("SMG_PANEL_HELPERS");
-        return !e || atoi(e) != 0;
-      }();
+      // column helpers for panel tiles 3 .. nb-1
       const int nbp = smg_ceil_div(K - J, SMG_NB);
-      int nh = use_helpers && nbp > 3 ? nbp - 3 : 0;
+      int nh = nbp > 3 ? nbp - 3 : 0;
       if (grid + nh > PANEL_MAX_GRID + 1 || nbp > T) nh = 0;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
+    }
+    if (sink) {  // columns [J, K) are final: packed and copied to the host on the zeroing stream
+      hipEvent_t Pe = smg_event(ctx, nev++), Me = nullptr;
+      if (!Pe) return SMG_ERR_HIP;
+      if (int rc = smg_marker_event(ctx, sink->marker_base + J / NB2, &Me)) return rc;
+      SMG_HIP_TRY(hipEventRecord(Pe, ctx->stream));
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, Pe, 0));
+      hipStream_t keep = ctx->stream;
+      ctx->stream = ctx->zero_stream;
+      const int prc = smg_pack_tril_cols(ctx, n, L, ldl, J, K, sink->packed);
+      ctx->stream = keep;
+      if (prc) return prc;
+      const size_t o0 = (size_t)J * n - (size_t)J * (J - 1) / 2, o1 = (size_t)K * n - (size_t)K * (K - 1) / 2;
+      SMG_HIP_TRY(hipMemcpyAsync(sink->host + o0, sink->packed + o0, (o1 - o0) * sizeof(double), hipMemcpyDeviceToHost,
+                                 ctx->zero_stream));
+      SMG_HIP_TRY(hipEventRecord(Me, ctx->zero_stream));
     }
     if (K >= n) break;
     const int m = n - K;
@@ -1183,10 +1274,17 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     } else if (prog) {  // no (b): the side stream still follows this panel
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
     }
-    if (prog) {  // block row J / P of W and K^{-1} (F is recorded before it: the next (a) does not wait for it)
-      smg_on_side on(ctx);
-      if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, J / NB2, true))) return rc;
+    if (prog) {  // (F is recorded before them: the next (a) does not wait for them)
+      // slack: the next panel (~22 us per 64-column step) and its (a), at
+      // ~30 TF/s, minus (b) at ~40 TF/s
+      const double m2 = n - K2, kk = K - J;
+      const double slack = 22.0 * (K2 - K) / SMG_NB + 6.0 + (double)(n - K) * (K2 - K) * kk / 30e6 -
+                           (K2 < n ? 6.0 + m2 * m2 * kk / 40e6 : 0.0);
+      if ((rc = queue_parts(J / NB2, slack))) return rc;
     }
+  }
+  if (prog) {  // the rest of the rows but the last
+    if (int rc0 = queue_parts(rows_prog - 2, -1.0)) return rc0;
   }
   // every launch that can latch the status (the symmetric check, the panels'
   // not-PD and hand-off bits) is enqueued: the status mark goes here, so a
@@ -1210,7 +1308,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
     {
       smg_on_side on(ctx);
-      if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, n / SMG_NBR - 1, false))) return rc;
+      for (int part = 0; part < 4; ++part)
+        if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, n / SMG_NBR - 1, part, false))) return rc;
     }
     // its writes to ws are joined before anything on the main stream may
     // touch ws (smg_cholesky_mvn_rev_v / smg_join_async)

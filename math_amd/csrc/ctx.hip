@@ -459,19 +459,39 @@ int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
   return SMG_OK;
 }
 
+int smg_zero_stream_begin(smg_ctx* ctx) {
+  if (ctx->zero_stream) return SMG_OK;
+  if (hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->zero_ev_main, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->zero_ev_done, hipEventDisableTiming) != hipSuccess) {
+    hipGetLastError();
+    ctx->zero_stream = nullptr;
+    return SMG_ERR_HIP;
+  }
+  return SMG_OK;
+}
+
+int smg_marker_event(smg_ctx* ctx, int slot, hipEvent_t* ev) {
+  if (slot < 0 || slot >= 64) return SMG_ERR_ARG;
+  while ((int)ctx->marker_ev.size() <= slot) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      ctx->host_status |= SMG_ERR_HIP;
+      return SMG_ERR_HIP;
+    }
+    ctx->marker_ev.push_back(e);
+  }
+  *ev = ctx->marker_ev[slot];
+  return SMG_OK;
+}
+
 int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes) {
   if (!ctx) return SMG_ERR_ARG;
   if (!bytes) return SMG_OK;
   if (!dst) return SMG_ERR_ARG;
-  if (!ctx->zero_stream) {
-    if (hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->zero_ev_main, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->zero_ev_done, hipEventDisableTiming) != hipSuccess) {
-      hipGetLastError();
-      ctx->zero_stream = nullptr;
-      SMG_HIP_TRY(hipMemsetAsync(dst, 0, bytes, ctx->stream));  // no second stream: in order
-      return SMG_OK;
-    }
+  if (smg_zero_stream_begin(ctx) != SMG_OK) {
+    SMG_HIP_TRY(hipMemsetAsync(dst, 0, bytes, ctx->stream));  // no second stream: in order
+    return SMG_OK;
   }
   // issued by smg_zero_flush: at the next latency-bound entry, the join, or a
   // rewind (the memory then still belongs to this tape)
@@ -507,16 +527,10 @@ int smg_join_async(smg_ctx* ctx) {
 }
 
 int smg_marker_record(smg_ctx* ctx, int slot) {
-  if (!ctx || slot < 0 || slot >= 64) return SMG_ERR_ARG;
-  while ((int)ctx->marker_ev.size() <= slot) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      ctx->host_status |= SMG_ERR_HIP;
-      return SMG_ERR_HIP;
-    }
-    ctx->marker_ev.push_back(e);
-  }
-  SMG_HIP_TRY(hipEventRecord(ctx->marker_ev[slot], ctx->stream));
+  if (!ctx) return SMG_ERR_ARG;
+  hipEvent_t e;
+  if (int rc = smg_marker_event(ctx, slot, &e)) return rc;
+  SMG_HIP_TRY(hipEventRecord(e, ctx->stream));
   return SMG_OK;
 }
 

@@ -536,8 +536,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
                      MODE == 4 ? t_ldc2 : 0);
   if (splits > 1) {
     const long long tot = (long long)m * n;
-    static const bool old_reduce = getenv("SMG_SPLITK_REDUCE1") != nullptr;  // dev A/B
-    if ((m & 1) == 0 && !old_reduce) {
+    if ((m & 1) == 0) {
       const long long pairs = tot / 2;
       const int nb = (int)(pairs / 256 < 2048 ? (pairs + 255) / 256 : 2048);
       hipLaunchKernelGGL(k_splitk_reduce2, dim3(nb), dim3(256), 0, ctx->stream, m, n, splits, slab, alpha, beta,
@@ -714,10 +713,6 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
     return smg_scale_impl(ctx, m, n, beta, C, ldc, uplo);
   }
   smg_prof_scope prof(ctx, SMG_FAM_GEMM);
-  {  // dev shape log (SMG_GEMM_LOG=1): one stderr line per product
-    static const bool log = getenv("SMG_GEMM_LOG") != nullptr;
-    if (log) fprintf(stderr, "gemm ta=%d tb=%d uplo=%d m=%d n=%d k=%d tri=%d\n", ta, tb, uplo, m, n, k, tri);
-  }
   if (ctx->prof_on) {
     // the K cuts of triangular operands execute about half (one) or a third
     // (two, as in V V^T with a triangle output) of the dense count

@@ -177,6 +177,18 @@ __global__ __launch_bounds__(256) void k_pack_tril(int mode, int n, const double
   }
 }
 
+// columns [j0, j1) of the packed lower triangle (a Cholesky panel's final
+// columns, streamed to the host while later panels factor): one column per
+// workgroup pass, reads and writes both column-contiguous
+__global__ __launch_bounds__(256) void k_pack_tril_cols(int n, const double* __restrict__ A, int lda, int j0, int j1,
+                                                        double* __restrict__ dst) {
+  for (int j = j0 + blockIdx.x; j < j1; j += gridDim.x) {
+    const double* a = A + (size_t)j * lda;
+    double* d = dst + tril_off(n, j) - j;
+    for (int i = j + threadIdx.x; i < n; i += 256) d[i] = a[i];
+  }
+}
+
 // tril(A) += unpack(src) (modes 0 / 1); A_ii += src[i] (mode 2)
 __global__ __launch_bounds__(256) void k_unpack_tril_add(int mode, int n, const double* __restrict__ src,
                                                          double* __restrict__ A, int lda) {
@@ -224,6 +236,14 @@ int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda) {
   if (!A || lda < n) return SMG_ERR_ARG;
   const int t = smg_ceil_div(n, TT);
   hipLaunchKernelGGL(k_sym_from_lower, dim3(t, t), dim3(256), 0, ctx->stream, n, A, lda);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_pack_tril_cols(smg_ctx* ctx, int n, const double* A, int lda, int j0, int j1, double* dst) {
+  if (j1 <= j0) return SMG_OK;
+  hipLaunchKernelGGL(k_pack_tril_cols, dim3(j1 - j0 < 1024 ? j1 - j0 : 1024), dim3(256), 0, ctx->stream, n, A, lda,
+                     j0, j1, dst);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

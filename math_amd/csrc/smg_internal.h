@@ -152,14 +152,18 @@ struct smg_on_side {
   }
   ~smg_on_side() { ctx->stream = ctx->main_stream; }
 };
+
 // chol_mvn.hip: K^{-1} for the closed-form reverse formed progressively
 // during the factorisation, block row k of W = L^{-1} once panel k is final
 // (queued by chol_fwd on `side`); ws: smg_cholesky_mvn_rev_ws_doubles(n)
 bool smg_inv_prog_ok(int n);
 int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws);
-// (inverses_here: the block row's 128/256/512 inverses first, then inv_ev_aux recorded)
-int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k,
+// part 0..3 of block row k (W_kk, W_{k,0:k}, the K^{-1} share, Y_{k+1});
+// inverses_here: part 0 forms the block row's 128/256/512 inverses first,
+// then records inv_ev_aux.  smg_inv_prog_cost: its device time estimate, us.
+int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k, int part,
                      bool inverses_here);
+double smg_inv_prog_cost(int n, int k, int part, bool inverses_here);
 // block inverses of the rows [row0, row0 + nrows) (multiples of 512), T: a
 // workspace (NULL: SMG_WS_TMP)
 int smg_block_inverses_rows(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0, int nrows,
@@ -179,6 +183,12 @@ int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* 
 int smg_status_mark_impl(smg_ctx* ctx);
 // issue the queued smg_memset_async zeroings on the zeroing stream (ctx.hip)
 extern "C" int smg_zero_flush(smg_ctx* ctx);
+// ensure the zeroing stream (also the device->host stream of the streamed
+// Cholesky output) and host-pipelining marker `slot` exist (ctx.hip)
+extern "C" int smg_zero_stream_begin(smg_ctx* ctx);
+extern "C" int smg_marker_event(smg_ctx* ctx, int slot, hipEvent_t* ev);
+// dst[tril_off(n, j) + i - j] = A(i, j) for j in [j0, j1), i >= j (matrix_util.hip)
+extern "C" int smg_pack_tril_cols(smg_ctx* ctx, int n, const double* A, int lda, int j0, int j1, double* dst);
 int smg_trtri_blocks_impl(smg_ctx* ctx, const double* L, int ldl, int n, double* W);
 int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux, int n);
 int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const double* W64,

@@ -153,11 +153,7 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
   const bool forward = (lower && !trans) || (!lower && trans);
   const bool wt = (trans != 0) != (lower == 0);  // X_p = W_p^T B_p
   int rc;
-  static const bool recursive = [] {  // dev A/B switch (SMG_TRSM_REC=0: the block loop)
-    const char* e = getenv("SMG_TRSM_REC");
-    return !e || atoi(e) != 0;
-  }();
-  if (recursive && lower && BSZ == SMG_NBR && m % SMG_NBR == 0) {
+  if (lower && BSZ == SMG_NBR && m % SMG_NBR == 0) {
     // Recursive halving: solve the first half, ONE update of the second half
     // by the whole first half (a rank-m/2 GEMM), solve the second half (for
     // the transposed solve the halves swap roles).  The same flops as the

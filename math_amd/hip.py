@@ -93,6 +93,8 @@ _SIGS = {
     "smg_cholesky_inv_t_async": (_I, [_P, _P, _I, _P, _I, _P, _I, _P]),
     "smg_cholesky_mvn_rev_v": (_I, [_P, _I, _P, _I, _L, _D, _P, _I, _P, _I]),
     "smg_cholesky_fwd_checked_mark_inv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
+    "smg_cholesky_stream_panels": (_I, [_I]),
+    "smg_cholesky_fwd_checked_mark_stream": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I]),
     "smg_log_sum_exp_fwd": (_I, [_P, _P, _L, _P]),
     "smg_log_sum_exp_rev": (_I, [_P, _P, _L, _D, _D, _P]),
     "smg_lgamma_fwd": (_I, [_P, _P, _L, _P]),

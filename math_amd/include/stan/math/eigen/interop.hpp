@@ -217,7 +217,10 @@ inline Eigen::Matrix<double, R, C> value_of(const Eigen::Matrix<var, R, C>& m) {
 /** rev/mat/fun/cholesky_decompose.hpp:378 signature: Matrix<var> -> Matrix<var>. */
 inline matrix_v cholesky_decompose(const matrix_v& A) {
   internal::check_square("cholesky_decompose", "A", int(A.rows()), int(A.cols()));
-  return to_host_matrix(cholesky_decompose(to_dev(A)));
+  matrix_v out(A.rows(), A.cols());
+  // the factor's varis are built as its panels finish (cholesky_decompose_impl)
+  internal::cholesky_decompose_impl(to_dev(A), out.data());
+  return out;
 }
 
 /**

@@ -299,7 +299,18 @@ inline dev_var_matrix add_diag(const dev_data<double>& A, const dev_var_matrix& 
   return internal::add_diag_dev(internal::operand(A), 0.0, nullptr, internal::operand(d));
 }
 
-inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
+namespace internal {
+/**
+ * cholesky_decompose on a device operand; with host_out (an n x n Eigen
+ * matrix of vars, column-major) also the Eigen boundary's output: the
+ * factor's host varis -- its lower triangle's, the strict upper on one dummy
+ * (cholesky_decompose.hpp:34-48, as internal::materialise) -- are built
+ * panel by panel as the factorisation streams each finished panel's columns
+ * to the host (smg_cholesky_fwd_checked_mark_stream), instead of after it.
+ * Varis built before a failed check are left unreferenced in the arena, as a
+ * throwing reference functor leaves its partial allocations.
+ */
+inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host_out) {
   const char* fn = "cholesky_decompose";
   internal::check_square(fn, "A", A.rows(), A.cols());
   const int n = A.rows();
@@ -316,10 +327,37 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   // status is read at the mark after the panels, so the block inverses that
   // follow run while the host builds the next node
   int inv_started = 0;
-  if (inv_ws)
+  const int panels = smg_cholesky_stream_panels(n);
+  host_block b{};
+  if (host_out && panels <= 64) {
+    b.node = L;
+    b.rows = b.cols = n;
+    b.dirty = false;
+    b.layout = layout_lower;
+    b.n = tril_count(size_t(n));
+    b.first = static_cast<vari*>(ChainableStack::instance_->memalloc_.alloc(b.n * sizeof(vari)));
+    b.dummy = new vari(0.0, vari::unstacked_tag{});
+    double* packed = amd::alloc_doubles(b.n);
+    double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
+    if (!stage) throw std::bad_alloc();
+    amd::check(smg_cholesky_fwd_checked_mark_stream(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started,
+                                                    packed, stage, 0),
+               fn);
+    fill_block_pointers(b, host_out);  // addresses only: while the first panel factors
+    const int nb2 = (n + panels - 1) / panels;
+    for (int p = 0; p < panels; ++p) {
+      const size_t J = size_t(p) * nb2, K = std::min(size_t(n), J + nb2);
+      const size_t o0 = J * n - J * (J - 1) / 2, o1 = K * n - K * (K - 1) / 2;
+      amd::check(smg_marker_wait(c, p), fn);
+      host_parallel_for(o1 - o0, [&](size_t s0, size_t s1) {
+        for (size_t i = o0 + s0; i < o0 + s1; ++i) ::new (static_cast<void*>(b.first + i)) vari(stage[i], vari::unstacked_tag{});
+      });
+    }
+  } else if (inv_ws) {
     amd::check(smg_cholesky_fwd_checked_mark_inv(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started), fn);
-  else
+  } else {
     amd::check(smg_cholesky_fwd_checked_mark(c, A.val_ptr(), n, n, L->val_, n, L->aux_), fn);
+  }
   int st = 0;
   amd::check(smg_status_mark_wait(c, &st), fn);
   if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
@@ -330,7 +368,17 @@ inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
     node->early_ = true;
     node->v_ready_ = node->c_ready_ = true;  // all of K^{-1} queued already
   }
+  if (b.node) {
+    push_block(b);
+  } else if (host_out) {  // (more than 64 panels: materialised after the factorisation)
+    materialise(L, [&](const host_block& hb) { fill_block_pointers(hb, host_out); });
+  }
   return dev_var_matrix(L);
+}
+}  // namespace internal
+
+inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
+  return internal::cholesky_decompose_impl(A, nullptr);
 }
 
 }  // namespace math

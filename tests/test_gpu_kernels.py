@@ -292,6 +292,47 @@ def test_cholesky_vs_oracle(ctx, N):
     near_rel(g, Aref, 1e-10, atol=1e-10 * np.abs(Aref).max(), what="grad_A")
 
 
+@pytest.mark.parametrize("N,with_ws", [(65, False), (600, False), (1536, True), (2048, False)])
+def test_cholesky_fwd_stream(ctx, N, with_ws):
+    """smg_cholesky_fwd_checked_mark_stream: the factor streamed to pinned
+    host memory panel by panel (the Eigen boundary's cholesky_decompose) --
+    every panel's marker lands, the host copy is the packed lower triangle of
+    the device factor bit for bit, and the factor equals the unstreamed entry's
+    bit for bit (with and without the progressive K^{-1} workspace)."""
+    import ctypes
+    rng = np.random.default_rng(N + 7)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + np.eye(N)
+    A = 0.5 * (A + A.T)
+    T = N * (N + 1) // 2
+    lib = ctx.lib
+    dA = ctx.put(F(A))
+    dL0, dD0 = ctx.zeros(N * N), ctx.zeros(lib.smg_cholesky_aux_doubles(N))
+    ctx.call("smg_cholesky_fwd_checked", dA, N, N, dL0, N, dD0)
+    L0 = ctx.get(dL0, N * N)
+    dL, dD, dP = ctx.zeros(N * N), ctx.zeros(lib.smg_cholesky_aux_doubles(N)), ctx.zeros(T)
+    ws = ctx.zeros(lib.smg_cholesky_mvn_rev_ws_doubles(N)) if with_ws else None
+    host = lib.smg_host_scratch(ctx.ptr, T * 8)
+    assert host
+    started = ctypes.c_int(-1)
+    ctx.call("smg_cholesky_fwd_checked_mark_stream", dA, N, N, dL, N, dD, ws, ctypes.byref(started), dP, host, 3)
+    npan = lib.smg_cholesky_stream_panels(N)
+    assert npan == (1 if N <= 512 else -(-N // 512))
+    for p in range(npan):
+        ctx.call("smg_marker_wait", 3 + p)
+    h = np.ctypeslib.as_array(ctypes.cast(host, ctypes.POINTER(ctypes.c_double)), shape=(T,)).copy()
+    st = ctypes.c_int(-1)
+    ctx.call("smg_status_mark_wait", ctypes.byref(st))
+    assert st.value == 0
+    ctx.call("smg_join_async")
+    L = ctx.get(dL, N * N)
+    assert np.array_equal(L, L0)
+    Lm = L.reshape(N, N).T  # row-major view of the column-major factor
+    packed = np.concatenate([Lm[j:, j] for j in range(N)])
+    assert np.array_equal(h, packed)
+    assert started.value == (2 if with_ws else 0)
+
+
 @pytest.mark.parametrize("N", [65, 300, 1024, 2048])
 def test_cholesky_mvn_closed_form_vs_oracle(ctx, N):
     """smg_cholesky_mvn_rev: cholesky_decompose's reverse for the MVN's

@@ -33,6 +33,10 @@ fi
 if [ "${UBP:-0}" = 1 ]; then  # the panel kernel's chain trace (tools/ubench_panel.hip) + its accuracy vs a host Cholesky
   timeout -k 10 120 ./tools/ubench_panel > $O/${TAG}_ubp.txt 2>&1 || { tail $O/${TAG}_ubp.txt; exit 1; }
   grep -E "panel kernel|potrf_diag" $O/${TAG}_ubp.txt
+  if [ -x ./tools/ubench_panel_old ]; then  # the A/B build (UB_OUT=tools/ubench_panel_old)
+    timeout -k 10 120 ./tools/ubench_panel_old > $O/${TAG}_ubp_old.txt 2>&1 || { tail $O/${TAG}_ubp_old.txt; exit 1; }
+    echo "A/B build:"; grep -E "panel kernel" $O/${TAG}_ubp_old.txt
+  fi
 fi
 if [ "${PROF:-0}" = 1 ]; then  # kernel trace of the GP bench (rocprofv3; the program itself after --)
   cd /tmp && export TMPDIR=/tmp

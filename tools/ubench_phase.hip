@@ -14,6 +14,11 @@ __device__ __forceinline__ long long stamp() {
   return t;
 }
 
+typedef __attribute__((address_space(3))) double lds_dbl;
+// the panel kernel's form: out of line, address_space(3) pointers
+__device__ __noinline__ void cf_pair(lds_dbl* D, int* st) { lds_potrf64_lookahead<true>(D, st); }
+__device__ __noinline__ void cf_old(lds_dbl* D, int* st) { lds_potrf64_lookahead<false>(D, st); }
+
 template <int WHICH>
 __global__ __launch_bounds__(512) void k_phase(double* g, long long* cyc) {
   __shared__ double D[SMG_NB * SMG_NBP];
@@ -36,6 +41,9 @@ __global__ __launch_bounds__(512) void k_phase(double* g, long long* cyc) {
   long long t1 = stamp();
   __syncthreads();
   long long t2 = stamp();
+  const long long r2 = __builtin_amdgcn_s_memrealtime();
+  if (WHICH == 8) cf_pair((lds_dbl*)D, (int*)(cyc + 60));
+  if (WHICH == 9) cf_old((lds_dbl*)D, (int*)(cyc + 60));
   if (WHICH == 2) lds_potrf64_lookahead(D, (int*)(cyc + 60));
   if (WHICH == 3) lds_potrf64_lookahead(D, (int*)(cyc + 60));
   if (WHICH == 7) lds_potrf64_lookahead<true>(D, (int*)(cyc + 60));
@@ -55,7 +63,8 @@ __global__ __launch_bounds__(512) void k_phase(double* g, long long* cyc) {
     for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) g[8192 + e] = X[(e >> 6) * SMG_NBP + (e & 63)];
   }
   long long t3 = stamp();
-  if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = t2 - t1; cyc[2] = t3 - t2; }
+  const long long r3 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = t2 - t1; cyc[2] = t3 - t2; cyc[3] = r3 - r2; }
   __syncthreads();
   for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) g[4096 + e] = D[(e >> 6) * SMG_NBP + (e & 63)];
   if (bad) g[0] = 0;
@@ -68,7 +77,7 @@ int main() {
   hipMalloc(&cyc, 4096);
   std::vector<double> h(4096);
   for (int j = 0; j < 64; ++j) for (int i = 0; i < 64; ++i) h[i + 64 * j] = (i == j ? 64.0 : 0.0) + 1.0 / (1 + i + j);
-  long long c[4];
+  long long c[4] = {0, 0, 0, 0};
   std::vector<double> o2(4096), o3(4096);
   auto run = [&](const char* nm, void (*k)(double*, long long*), std::vector<double>* out = nullptr) {
     for (int r = 0; r < 2; ++r) {
@@ -77,7 +86,7 @@ int main() {
       hipDeviceSynchronize();
       hipMemcpy(c, cyc, sizeof(c), hipMemcpyDeviceToHost);
     }
-    printf("%-22s w0 %lld  barrier %lld  full %lld\n", nm, c[0], c[1], c[2]);
+    printf("%-22s w0 %lld  barrier %lld  full %lld  (%.2f us real)\n", nm, c[0], c[1], c[2], c[3] / 100.0);
     if (out) hipMemcpy(out->data(), d + 4096, 4096 * 8, hipMemcpyDeviceToHost);
   };
   run("panel8 per-lane", k_phase<0>);
@@ -85,6 +94,10 @@ int main() {
   run("panel8 pairs", k_phase<6>);
   std::vector<double> o7(4096);
   for (int rep = 0; rep < 3; ++rep) run("lookahead potrf pairs", k_phase<7>, &o7);
+  for (int rep = 0; rep < 2; ++rep) {
+    run("out-of-line pairs", k_phase<8>);
+    run("out-of-line per-pivot", k_phase<9>);
+  }
   for (int rep = 0; rep < 3; ++rep) {
     run("lookahead potrf", k_phase<2>, &o2);
     run("pre-broadcast potrf", k_phase<3>, &o3);
