@@ -36,6 +36,24 @@ rf = calib_bytes / (mean(f["k_read8"]) * 1024.0)   # true bytes per reported byt
 rw = calib_bytes / (mean(w["k_write8"]) * 1024.0)
 res = {"calibration": {"kernel": "tools/calib_fetch.hip (8 B/lane, 1 GiB)", "fetch_scale": rf,
                        "write_scale": rw}}
+def per_dispatch(name):
+    """[(kernel short name, grid x, fetch-or-write KB)] per dispatch"""
+    dbs = glob.glob(BASE % (TAG, name)) or glob.glob(f"gpurun_out/pmc_{TAG}_{name}/*/*.db")
+    out = collections.defaultdict(float)
+    meta = {}
+    for db in dbs:
+        c = sqlite3.connect(db)
+        try:
+            rows = c.execute("select kernel_name, dispatch_id, grid_size_x, value from counters_collection").fetchall()
+        except sqlite3.OperationalError:
+            rows = [(kn, did, 0, v) for kn, did, v in
+                    c.execute("select kernel_name, dispatch_id, value from counters_collection")]
+        for kn, did, gx, v in rows:
+            out[did] += v
+            meta[did] = (kn.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0], gx)
+    return [(meta[d][0], meta[d][1], out[d]) for d in sorted(out)]
+
+
 for wl, kern in (("glm", "k_glm_reg"), ("gp", "k_gemm")):
     fk, wk = per_kernel(f"{wl}_fetch"), per_kernel(f"{wl}_write")
     fv = [v for k, vs in fk.items() if k.startswith(kern) for v in vs]
@@ -44,4 +62,31 @@ for wl, kern in (("glm", "k_glm_reg"), ("gp", "k_gemm")):
                "fetch_bytes_per_launch": mean(fv) * 1024.0 * rf,
                "write_bytes_per_launch": mean(wv) * 1024.0 * rw}
     res[wl]["traffic_bytes_per_launch"] = res[wl]["fetch_bytes_per_launch"] + res[wl]["write_bytes_per_launch"]
+# round 4: the dominant kernel (k_chol_panel) and the largest K^{-1} share
+# (C += W_k^T W_k of the last block row: k_gemm TN lower, the widest grid),
+# each beside its algorithmic bytes (N = 4096, 512-column panels)
+if glob.glob(BASE % (TAG, "gp_fetch")):
+    N, P = 4096, 512
+    fd, wd = per_dispatch("gp_fetch"), per_dispatch("gp_write")
+    pf = [v for k, g, v in fd if k.startswith("k_chol_panel")]
+    pw = [v for k, g, v in wd if k.startswith("k_chol_panel")]
+    # a panel reads its (N - J) x 512 columns and writes the factor back: 16 (N - J) 512 B, mean over the 8 panels
+    alg_panel = sum(16.0 * (N - J) * P for J in range(0, N, P)) / (N // P)
+    res["k_chol_panel"] = {"launches": len(pf), "fetch_bytes_per_launch": mean(pf) * 1024.0 * rf,
+                           "write_bytes_per_launch": mean(pw) * 1024.0 * rw, "algorithmic_bytes_per_launch": alg_panel}
+    res["k_chol_panel"]["waste_ratio"] = (res["k_chol_panel"]["fetch_bytes_per_launch"] +
+                                          res["k_chol_panel"]["write_bytes_per_launch"]) / alg_panel
+    share = [(g, v) for k, g, v in fd if k.startswith("k_gemm<64, 64, 16, true, false, 1")]
+    sharew = [(g, v) for k, g, v in wd if k.startswith("k_gemm<64, 64, 16, true, false, 1")]
+    if share:
+        gmax = max(g for g, v in share)
+        f1 = [v for g, v in share if g == gmax]
+        w1 = [v for g, v in sharew if g == gmax]
+        # W_7 (512 x N) read + C's lower triangle read and written: 8 (512 N + N^2) B
+        alg_share = 8.0 * (P * N + N * N)
+        res["k_gemm_share_last"] = {"grid": gmax, "launches": len(f1), "fetch_bytes_per_launch": mean(f1) * 1024.0 * rf,
+                                    "write_bytes_per_launch": mean(w1) * 1024.0 * rw,
+                                    "algorithmic_bytes_per_launch": alg_share}
+        res["k_gemm_share_last"]["waste_ratio"] = (res["k_gemm_share_last"]["fetch_bytes_per_launch"] +
+                                                   res["k_gemm_share_last"]["write_bytes_per_launch"]) / alg_share
 print(json.dumps(res, indent=1))

@@ -14,6 +14,6 @@ run calib_fetch FETCH_SIZE $GRAFT_REPO_ROOT/tools/calib_fetch || exit 1
 run calib_write WRITE_SIZE $GRAFT_REPO_ROOT/tools/calib_fetch || exit 1
 run glm_fetch FETCH_SIZE python3 $GRAFT_REPO_ROOT/bench.py --workload glm --steps 2 --warmup 1 --no-cpu-baseline || exit 1
 run glm_write WRITE_SIZE python3 $GRAFT_REPO_ROOT/bench.py --workload glm --steps 2 --warmup 1 --no-cpu-baseline || exit 1
-run gp_fetch FETCH_SIZE python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline || exit 1
-run gp_write WRITE_SIZE python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline || exit 1
+run gp_fetch FETCH_SIZE python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-glm-strong || exit 1
+run gp_write WRITE_SIZE python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-glm-strong || exit 1
 echo done
