@@ -467,7 +467,32 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // 2 .. gown - 1, column helpers gown ...
   const int nh = gridDim.x - gown;
   if (blockIdx.x == 1) {
+    // ... and, behind each Dinv_j, the aux 128 level of the previous full
+    // block pair (j - 2, j - 1): X = [[D1, 0], [-D2 L21 D1, D2]] (two 64^3
+    // LDS products; Y = D1, Z = D2 kept from the pair's own steps), so the
+    // doubling after the panel starts at 256 (chol_block_inverses skip128)
     __shared__ double Tin[3 * 256];
+    double* W128 = Dinv + (size_t)ldd * SMG_AUX_W128;
+    auto pair128 = [&](int j2) {  // blocks j2 - 1, j2 (Y, Z); both full
+      const int c1 = J + SMG_NB * (j2 - 1), c2 = c1 + SMG_NB;
+      panel_wait(&row[(j2 - 1) * S + j2], epoch, status);  // L_{j2, j2-1}, stored by tile j2's owner
+      panel_regs Rl;
+      panel_gload(Rl, L + c2 + (size_t)c1 * ldl, ldl, SMG_NB, SMG_NB, false);
+      __syncthreads();
+      panel_lstore(D, Rl);
+      __syncthreads();
+      lds_mma64_8w<false, false>(D, D, Y);        // T = L21 D1
+      lds_mma64_8w<false, false>(D, Z, D, -1.0);  // X21 = -D2 T
+      panel_gstore(Y, W128 + c1, ldd, SMG_NB, SMG_NB, false);
+      panel_gstore(Z, W128 + c2 + (size_t)SMG_NB * ldd, ldd, SMG_NB, SMG_NB, false);
+      panel_gstore(D, W128 + c2, ldd, SMG_NB, SMG_NB, false);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // the zero upper-right block
+        const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+        W128[c1 + (e & 63) + (size_t)(SMG_NB + (e >> 6)) * ldd] = 0.0;
+      }
+    };
+    auto full = [&](int j) { return j < nb && K - (J + SMG_NB * j) >= SMG_NB; };
     for (int j = 0; j < nb; ++j) {
       const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
       panel_wait(&diag[j], epoch, status);
@@ -480,7 +505,12 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       __syncthreads();
       panel_gstore_tri(X, Dinv + cj, ldd, bj);
       panel_publish(&dinvf[j], epoch);
+      if ((j & 1) == 0 && j >= 2 && full(j - 1)) pair128(j - 1);  // after Dinv_j: off the tiles' path
+      __syncthreads();
+      for (int e = threadIdx.x; e < SMG_NB * SMG_NBP; e += SMG_DIAG_THREADS) ((j & 1) ? Z : Y)[e] = X[e];
+      __syncthreads();
     }
+    if ((nb & 1) == 0 && full(nb - 1)) pair128(nb - 1);
     return;
   }
 
@@ -874,12 +904,13 @@ int chol_rev_blocks(smg_ctx* ctx, const double* L, int ldl, const double* Dv, in
 // (rows [row0, row0 + nrows) only, nrows < 0: all; T: workspace of
 // nrows / 2 x 256 doubles, NULL: SMG_WS_TMP)
 int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0 = 0,
-                        int nrows = -1, double* Tbuf = nullptr) {
+                        int nrows = -1, double* Tbuf = nullptr, bool skip128 = false) {
   if (nrows < 0) nrows = n;
   L += (size_t)row0 * (ldl + 1);
-  const double* Wi = aux + row0;
+  // skip128: the 128 level is already there (the panel kernel's inverter forms it)
+  const double* Wi = skip128 ? aux + (size_t)n * SMG_AUX_W128 + row0 : aux + row0;
   int ldi = n;
-  for (int s2 = 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
+  for (int s2 = skip128 ? 4 * SMG_NB : 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
     const int s = s2 / 2, nb = nrows / s2;
     if (nb == 0) return SMG_OK;
     const int off = s2 == 128 ? SMG_AUX_W128 : (s2 == 256 ? SMG_AUX_W256 : SMG_AUX_W512);
@@ -1059,7 +1090,7 @@ int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux,
 }
 int smg_block_inverses_rows(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0, int nrows,
                             double* T) {
-  return chol_block_inverses(ctx, L, ldl, aux, n, row0, nrows, T);
+  return chol_block_inverses(ctx, L, ldl, aux, n, row0, nrows, T, true);  // (behind chol_fwd's panels)
 }
 
 extern "C" {
@@ -1303,7 +1334,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   if (prog) {
     const int r0 = n - SMG_NBR;
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
-    if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, r0, SMG_NBR))) return rc;
+    if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, r0, SMG_NBR, nullptr, true))) return rc;
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
     {
@@ -1316,7 +1347,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
     ctx->inv_pending = 1;
     *inv_started = 2;
-  } else if ((rc = chol_block_inverses(ctx, L, ldl, aux, n))) {
+  } else if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, 0, -1, nullptr, true))) {
     return rc;
   }
   SMG_LAUNCH_CHECK();

@@ -16,7 +16,7 @@ int main(int argc, char** argv) {
   double *dL, *dD;
   int *flags, *status;
   hipMalloc(&dL, 8ull * n * n);
-  hipMalloc(&dD, 8ull * n * 64);
+  hipMalloc(&dD, 8ull * n * SMG_AUX_COLS);  // the whole aux: the inverter also writes the 128 level
   hipMalloc(&flags, 4096 * 4);
   hipMalloc(&status, 4);
   hipMemset(flags, 0, 4096 * 4);
