@@ -22,6 +22,7 @@
 #include "tri_small.h"
 #include "smg_sync.h"
 #include <cstdlib>
+#include <vector>
 
 namespace {
 
@@ -1222,9 +1223,49 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   // (the next panel and its look-ahead (a), minus (b)_p itself): queued
   // whole, the growing rows held back (b)_{p+1}, the next (a) waiting for it,
   // and with it the next panel; what does not fit goes after the last panel
-  int q_k = 0, q_part = 0;  // the next part to queue
+  int q_k = 0, q_part = 0;  // the next part to queue (all parts on `side`)
   const int rows_prog = prog ? n / SMG_NBR : 0;
+  // With the zeroing stream (idle during the panels): a row's chain of
+  // latency-bound parts -- its 256/512-level inverses (~8 small launches),
+  // W_{k,0:k} and Y_{k+1} -- runs there as soon as its panel is done (pe_ev);
+  // only the K^{-1} shares (part 2, the bulk) go on `side` within the slack,
+  // each after its row's W (w_ev).  C's accumulation order stays the rows'.
+  const bool zero_parts = prog && smg_zero_stream_begin(ctx) == SMG_OK;
+  std::vector<hipEvent_t> pe_ev(rows_prog, nullptr), w_ev(rows_prog, nullptr);
+  int z_k = 0, s_k = 0;  // next row for the zeroing stream's parts / the next share
+  auto queue_zero = [&](int kmax) -> int {
+    while (z_k <= kmax && z_k < rows_prog - 1) {
+      if (!pe_ev[z_k] || !(w_ev[z_k] = smg_event(ctx, nev++))) return SMG_ERR_HIP;
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, pe_ev[z_k], 0));
+      hipStream_t keep = ctx->stream;
+      ctx->stream = ctx->zero_stream;
+      int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 0, true);
+      if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 1, true);
+      if (!rc && hipEventRecord(w_ev[z_k], ctx->zero_stream) != hipSuccess) rc = SMG_ERR_HIP;
+      if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 3, true);
+      ctx->stream = keep;
+      if (rc) return rc;
+      ++z_k;
+    }
+    return SMG_OK;
+  };
+  auto queue_shares = [&](double budget_us) -> int {  // budget < 0: every row queued on zero so far
+    while (s_k < z_k) {
+      const double c = smg_inv_prog_cost(n, s_k, 2, true);
+      if (budget_us >= 0 && c > budget_us + 40.0) break;
+      budget_us -= c;
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, w_ev[s_k], 0));
+      smg_on_side on(ctx);
+      if (int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, s_k, 2, true)) return rc;
+      ++s_k;
+    }
+    return SMG_OK;
+  };
   auto queue_parts = [&](int kmax, double budget_us) -> int {  // budget < 0: all of rows <= kmax
+    if (zero_parts) {
+      if (int rc = queue_zero(kmax)) return rc;
+      return queue_shares(budget_us);
+    }
     while (q_k <= kmax && q_k < rows_prog - 1) {
       const double c = smg_inv_prog_cost(n, q_k, q_part, true);
       if (budget_us >= 0 && c > budget_us + 40.0) break;
@@ -1253,6 +1294,10 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if (grid + nh > PANEL_MAX_GRID + 1 || nbp > T) nh = 0;
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
+    }
+    if (zero_parts && J / NB2 < rows_prog) {  // this panel is final: its block row's inverses may start
+      if (!(pe_ev[J / NB2] = smg_event(ctx, nev++))) return SMG_ERR_HIP;
+      SMG_HIP_TRY(hipEventRecord(pe_ev[J / NB2], ctx->stream));
     }
     if (sink) {  // columns [J, K) are final: packed and copied to the host on the zeroing stream
       hipEvent_t Pe = smg_event(ctx, nev++), Me = nullptr;
@@ -1336,11 +1381,26 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
     if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, r0, SMG_NBR, nullptr, true))) return rc;
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
-    SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
-    {
+    const int klast = n / SMG_NBR - 1;
+    if (zero_parts) {  // W_last on the zeroing stream behind the last Y, its share on side
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->inv_ev_main, 0));
+      hipStream_t keep = ctx->stream;
+      ctx->stream = ctx->zero_stream;
+      rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 0, false);
+      if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 1, false);
+      ctx->stream = keep;
+      if (rc) return rc;
+      hipEvent_t We = smg_event(ctx, nev++);
+      if (!We) return SMG_ERR_HIP;
+      SMG_HIP_TRY(hipEventRecord(We, ctx->zero_stream));
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, We, 0));
+      smg_on_side on(ctx);
+      if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 2, false))) return rc;
+    } else {
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
       smg_on_side on(ctx);
       for (int part = 0; part < 4; ++part)
-        if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, n / SMG_NBR - 1, part, false))) return rc;
+        if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, part, false))) return rc;
     }
     // its writes to ws are joined before anything on the main stream may
     // touch ws (smg_cholesky_mvn_rev_v / smg_join_async)

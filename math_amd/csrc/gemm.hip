@@ -504,9 +504,12 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   splits = smg_ceil_div(k, kchunk);
   double* slab = nullptr;
   if (splits > 1) {
-    // the side stream has its own slab so concurrent split-K GEMMs never share one
-    slab = smg_ws(ctx, ctx->stream == ctx->side ? SMG_WS_GEMM_SIDE : SMG_WS_GEMM,
-                  (size_t)splits * m * n);
+    // the side and zeroing streams have their own slabs so concurrent split-K
+    // GEMMs never share one
+    const int slot = ctx->stream == ctx->side                                ? SMG_WS_GEMM_SIDE
+                     : (ctx->zero_stream && ctx->stream == ctx->zero_stream) ? SMG_WS_GEMM_ZERO
+                                                                             : SMG_WS_GEMM;
+    slab = smg_ws(ctx, slot, (size_t)splits * m * n);
     if (!slab) return SMG_ERR_OOM;
   }
   // XCD partition px x (8 / px) of a full tile grid minimising the per-XCD

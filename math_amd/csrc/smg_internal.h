@@ -85,8 +85,8 @@ struct smg_ctx {
   long long done_seq;
   unsigned int* red_counter_d;  // last-block-done counter of the fused reductions (device, self-resetting)
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[10];  // SMG_WS_COUNT
-  size_t ws_doubles[10];
+  double* ws[11];  // SMG_WS_COUNT
+  size_t ws_doubles[11];
   // profiling
   int prof_on;
   std::vector<smg_prof_slot> prof_pending;
@@ -132,7 +132,8 @@ struct smg_prof_scope {
 enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_ALIAS = 4,
        SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_RHS = 8,
        SMG_WS_GLM = 9,  // the GLM parameters [alpha, beta] (not the Cholesky aux's TMP2)
-       SMG_WS_COUNT = 10 };
+       SMG_WS_GEMM_ZERO = 10,  // split-K slabs of the GEMMs on the zeroing stream
+       SMG_WS_COUNT = 11 };
 static_assert(SMG_WS_COUNT == sizeof(((smg_ctx*)nullptr)->ws) / sizeof(double*), "workspace slots");
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 // spin on the host-coherent completion word until it reaches seq (then the
