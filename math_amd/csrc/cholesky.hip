@@ -1217,6 +1217,11 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     if (int rc = smg_inv_prog_init(ctx, n, inv_ws)) return rc;
   }
   int nev = 0;       // pooled events used
+  hipEvent_t init_ev = nullptr;  // C's zeroing on side (the zeroing stream's parts follow it)
+  if (prog) {
+    if (!(init_ev = smg_event(ctx, nev++))) return SMG_ERR_HIP;
+    SMG_HIP_TRY(hipEventRecord(init_ev, ctx->side));
+  }
   hipEvent_t F = nullptr;  // the pending (b) on the side stream
   // the block rows' parts (smg_inv_prog_row) queued on `side` behind each
   // trailing update (b)_p within the slack before (b)_{p+1} becomes ready
@@ -1236,6 +1241,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   auto queue_zero = [&](int kmax) -> int {
     while (z_k <= kmax && z_k < rows_prog - 1) {
       if (!pe_ev[z_k] || !(w_ev[z_k] = smg_event(ctx, nev++))) return SMG_ERR_HIP;
+      if (z_k == 0) SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, init_ev, 0));
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, pe_ev[z_k], 0));
       hipStream_t keep = ctx->stream;
       ctx->stream = ctx->zero_stream;
