@@ -292,6 +292,33 @@ def test_cholesky_vs_oracle(ctx, N):
     near_rel(g, Aref, 1e-10, atol=1e-10 * np.abs(Aref).max(), what="grad_A")
 
 
+@pytest.mark.parametrize("N", [300, 1000, 2048])
+def test_cholesky_aux_block_inverses(ctx, N):
+    """smg_cholesky_fwd's aux: every full 64/128/256/512-row diagonal block's
+    inverse (the 64 level and, since round 4, the 128 level from the panel
+    kernel's inverter workgroup; 256 / 512 by doubling after the panels) times
+    that block of L is the identity, with stored zeros above the diagonal."""
+    rng = np.random.default_rng(N + 11)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + np.eye(N)
+    A = 0.5 * (A + A.T)
+    lib = ctx.lib
+    dA, dL = ctx.put(F(A)), ctx.zeros(N * N)
+    naux = lib.smg_cholesky_aux_doubles(N)
+    dD = ctx.zeros(naux)
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
+    L = ctx.get(dL, N * N).reshape(N, N).T
+    aux = ctx.get(dD, naux).reshape(-1, N).T  # N rows, column blocks of the levels
+    off = 0
+    for s in (64, 128, 256, 512):
+        for b in range(0, N - s + 1, s):
+            X = aux[b:b + s, off:off + s]
+            assert np.abs(np.triu(X, 1)).max() == 0.0, (s, b)
+            E = X @ L[b:b + s, b:b + s] - np.eye(s)
+            assert np.abs(E).max() < 1e-11, (s, b, np.abs(E).max())
+        off += s
+
+
 @pytest.mark.parametrize("N,with_ws", [(65, False), (600, False), (1536, True), (2048, False)])
 def test_cholesky_fwd_stream(ctx, N, with_ws):
     """smg_cholesky_fwd_checked_mark_stream: the factor streamed to pinned
