@@ -66,6 +66,8 @@ def ref_bench(cfg, n, reps=1, timeout=300, threads=None):
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness" + ("_mt" if threads else ""))
     if not os.path.exists(exe):
         return None
+    from math_amd import srchash
+    srchash.check(exe, "ref")
     cmd = [exe, "bench", cfg, str(n), str(reps)] + ([str(threads)] if threads else [])
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=dict(os.environ, OMP_NUM_THREADS="1"))
     return json.loads(out.stdout.strip().splitlines()[-1])
@@ -81,18 +83,32 @@ def host_cores():
     return max(1, min(16, n))
 
 
-def pmc_traffic(workload):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (tools/pmc_traffic.sh + tools/pmc_traffic.py: separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes, calibrated on a known 8 B/lane
-    stream), or None when absent."""
-    path = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+def pmc_summary_path():
+    """The newest committed PMC summary, profiles/rNN_pmc_traffic.json (highest
+    round), or None."""
+    import glob
+    import re
+    best = None
+    for p in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")):
+        m = re.match(r"r(\d+)_pmc_traffic\.json$", os.path.basename(p))
+        if m and (best is None or int(m.group(1)) > best[0]):
+            best = (int(m.group(1)), p)
+    return best[1] if best else None
+
+
+def pmc_traffic(key):
+    """HBM bytes per launch of kernel `key` (fetch + write, and the entry
+    itself) from the newest committed PMC summary (tools/pmc_traffic.sh +
+    tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
+    calibrated on a known 8 B/lane stream), or (None, None, None)."""
+    path = pmc_summary_path()
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d[workload]["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+            e = json.load(f)[key]
+        t = e.get("traffic_bytes_per_launch", e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"])
+        return t, os.path.relpath(path, ROOT), e
+    except (OSError, KeyError, ValueError, TypeError):
+        return None, None, None
 
 
 def unif(seed, n, a, b):
@@ -106,7 +122,33 @@ def unif(seed, n, a, b):
     return a + (b - a) * ((z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0))
 
 
-def eval_roofline(wl, fams, steps, ms_per_step, traffic_src):
+def panel_roofline(fams, steps, n):
+    """The GP's dominant kernel, k_chol_panel (one persistent launch per 512
+    columns): its in-panel work m b^2 - 2 b^3 / 3 per launch (m rows from the
+    panel's top, b columns; SURVEY.md §8(d)'s N^3 / 3 forward, the part inside
+    the panels) / its average launch time from HIP events around each launch
+    (SMG_FAM_PANEL, the context stream in the profiled copy of the timed
+    region), with the PMC bytes per launch and the algorithmic bytes
+    16 (N - J) b per launch (read and write the panel once)."""
+    pms, pn, pfl = fams["panel"]
+    if pn <= 0 or pms <= 0:
+        return None
+    avg_ms = pms / pn
+    fl = pfl / pn
+    ach = fl / (avg_ms * 1e-3) / 1e12
+    traffic, src, e = pmc_traffic("k_chol_panel")
+    b = 512
+    alg_bytes = sum(16.0 * (n - j) * min(b, n - j) for j in range(0, n, b)) / max(1, -(-n // b))
+    return {"bound": "mfma", "kernel": "k_chol_panel", "achieved": ach, "peak": PEAK_FP64_TFLOPS,
+            "unit": "TFLOP/s", "frac": ach / PEAK_FP64_TFLOPS, "traffic": traffic,
+            "traffic_unit": "HBM bytes per k_chol_panel launch (PMC FETCH_SIZE + WRITE_SIZE)" if traffic else None,
+            "traffic_source": src, "algorithmic_bytes_per_launch": alg_bytes,
+            "traffic_over_algorithmic": traffic / alg_bytes if traffic else None,
+            "flops_per_launch": fl, "avg_launch_us": 1e3 * avg_ms, "launches_per_step": pn / steps,
+            "note": "latency-bound (the diagonal chain, DESIGN.md section 4), priced against the fp64 MFMA peak"}
+
+
+def eval_roofline(wl, fams, steps, ms_per_step):
     """algorithmic flops of ONE gradient eval (the unit a step
     processes) / the measured step time / the fp64 MFMA peak.  The GEMM kernel
     family (HIP events on the context stream) is reported beside it with the
@@ -115,11 +157,9 @@ def eval_roofline(wl, fams, steps, ms_per_step, traffic_src):
     fl = wl.eval_flops()
     ach = fl / (ms_per_step * 1e-3) / 1e12
     gms, gn, gfl = fams["gemm"]
-    traffic, src = traffic_src
     return {"bound": "mfma", "kernel": "whole gradient eval (algorithmic flops / step time)",
             "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP64_TFLOPS,
-            "traffic": traffic, "traffic_unit": "HBM bytes per k_gemm launch (PMC)" if traffic else None,
-            "traffic_source": src, "algorithmic_flops_per_eval": fl, "eval_flops": wl.eval_flops_expr,
+            "algorithmic_flops_per_eval": fl, "eval_flops": wl.eval_flops_expr,
             "gemm_family": {"launches_per_step": gn / steps, "avg_launch_ms": gms / max(gn, 1),
                             "executed_flops_per_launch": gfl / max(gn, 1),
                             "executed_tflops": gfl / (gms * 1e-3) / 1e12 if gms > 0 else None,
@@ -179,7 +219,12 @@ class GP(Workload):
         return float(self.N) ** 3
 
     def roofline(self, fams, steps, t_prof, ms_per_step):
-        return eval_roofline(self, fams, steps, ms_per_step, pmc_traffic("gp"))
+        ev = eval_roofline(self, fams, steps, ms_per_step)
+        pr = panel_roofline(fams, steps, self.N)
+        if pr is None:  # (a path without panel launches)
+            return ev
+        pr["eval"] = ev
+        return pr
 
     def extra(self, timed, steps):
         if type(self) is not GP:
@@ -348,7 +393,7 @@ class GLM(Workload):
         byts = self.rows * self.M * 8 + self.rows * 4  # one read of x and y
         avg = ms / max(n, 1)
         ach = byts / (avg * 1e-3) / 1e9 if avg > 0 else None
-        traffic, src = pmc_traffic("glm")
+        traffic, src, _ = pmc_traffic("glm")
         step_ms = t_prof * 1e3 / steps
         return {"bound": "hbm", "kernel": "k_glm_reg (one pass over x)", "achieved": ach,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS if ach else None,
@@ -418,7 +463,7 @@ class MulChol(Workload):
         return 7.0 * float(self.N) ** 3
 
     def roofline(self, fams, steps, t_prof, ms_per_step):
-        r = eval_roofline(self, fams, steps, ms_per_step, (None, None))
+        r = eval_roofline(self, fams, steps, ms_per_step)
         # the same step time priced on the flops this build executes: the Gram
         # product lower-only 2N^3 -> N^3 ... (A A^T: N^3, reverse GEMM 2N^3,
         # chol fwd N^3/3 + Murray adjoint N^3)
@@ -482,7 +527,7 @@ class HVP(GP):
         return 4.0 * float(self.N) ** 3
 
     def roofline(self, fams, steps, t_prof, ms_per_step):
-        r = eval_roofline(self, fams, steps, ms_per_step, (None, None))
+        r = eval_roofline(self, fams, steps, ms_per_step)
         # the same step time priced on the flops the GEMM family executes per
         # product (each launch's flops, triangular K cuts counted, summed over
         # the profiled steps): measured, not a formula
@@ -645,14 +690,44 @@ def glm_strong(bl, args, rank, world, local, dist, timed, lib, ctx):
     t = _timed_glm(g, steps, timed)
     lib.smg_profile_enable(ctx, 1)
     tp = _timed_glm(g, steps, timed)
-    fams = {f: hip_profile_read(lib, ctx, f) for f in ("glm",)}
+    fams = {f: hip_profile_read(lib, ctx, f) for f in ("glm", "comm")}
     lib.smg_profile_enable(ctx, 0)
     roof = g.roofline(fams, steps, tp, 1e3 * t / steps)
     return {"metric": g.metric, "value": steps / t, "unit": g.unit, "n_gpus": world, "steps": steps,
             "ms_per_step": 1e3 * t / steps, "scaling": "strong", "rows": int(a.rows), "covariates": g.M,
             "rows_per_rank": int(g.rows), "config": g.config(),
             "roofline": {k: roof[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
-                                              "bytes_per_launch", "avg_launch_ms", "step_minus_glm_kernels_us")}}
+                                              "bytes_per_launch", "avg_launch_ms", "step_minus_glm_kernels_us")},
+            "per_rank": glm_rank_breakdown(fams, steps, tp, dist, world)}
+
+
+def glm_rank_breakdown(fams, steps, t_prof, dist, world):
+    """Where one rank's GLM step goes, per rank of the profiled copy of the
+    timed region (HIP events on the context stream): the GLM kernels
+    (k_glm_params + k_glm_reg + k_glm_io_final), the ncclAllReduce of the
+    M + 2 sums, and the rest (host: the gradient() tape, the completion wait;
+    launch gaps) -- with the min / max over ranks, so that an N-GPU run can
+    attribute a shortfall to the kernel, the collective or the host."""
+    gms, gn, _ = fams["glm"]
+    cms, cn, _ = fams["comm"]
+    step_ms = 1e3 * t_prof / steps
+    mine = [gms / steps, 1e3 * cms / max(cn, 1), step_ms - gms / steps - cms / steps]
+    rows = [mine]
+    if dist is not None and world > 1:
+        import torch
+        out = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(out, torch.tensor(mine, dtype=torch.float64))
+        rows = [o.tolist() for o in out]
+    keys = ("glm_kernel_ms", "allreduce_us", "host_and_gaps_us")
+    scale = (1.0, 1.0, 1e3)
+
+    def col(i):
+        return [r[i] * scale[i] for r in rows]
+    return {"ranks": len(rows), "allreduces_per_step": cn / steps,
+            **{k: {"min": min(col(i)), "max": max(col(i)), "per_rank": col(i)} for i, k in enumerate(keys)},
+            "note": "glm_kernel_ms per step; allreduce_us per ncclAllReduce (HIP events around the call on the "
+                    "context stream: includes waiting for the other ranks); host_and_gaps_us per step = profiled "
+                    "step time - both"}
 
 
 def _timed_glm(g, steps, timed):
@@ -690,7 +765,10 @@ def main():
         dist.init_process_group("gloo")
 
     from math_amd import hip
-    bl = ctypes.CDLL(os.path.join(ROOT, "math_amd", "lib", "libsmg_bench.so"))
+    from math_amd import srchash
+    bl_path = os.path.join(ROOT, "math_amd", "lib", "libsmg_bench.so")
+    srchash.check(bl_path, "bench")  # (the GPU box cannot rebuild it: refuse a stale one)
+    bl = ctypes.CDLL(bl_path)
     bl.smg_bench_ctx.restype = ctypes.c_void_p
     bl.smg_bench_error.restype = ctypes.c_char_p
     lib = hip.lib()

@@ -133,7 +133,10 @@ int smg_status_inject(smg_ctx* ctx, int bits);
 enum smg_family {
   SMG_FAM_GEMM = 0, SMG_FAM_CHOL_FWD = 1, SMG_FAM_CHOL_REV = 2,
   SMG_FAM_GP = 3, SMG_FAM_MVN = 4, SMG_FAM_TRSV = 5, SMG_FAM_GLM = 6,
-  SMG_FAM_ELEMWISE = 7, SMG_FAM_COUNT = 8
+  SMG_FAM_ELEMWISE = 7,
+  SMG_FAM_PANEL = 8,  /* each k_chol_panel launch alone (flops: its in-panel work m b^2 - 2 b^3 / 3) */
+  SMG_FAM_COMM = 9,   /* each RCCL all-reduce (smg_comm_allreduce_sum) */
+  SMG_FAM_COUNT = 10
 };
 int smg_profile_enable(smg_ctx* ctx, int on);
 /* total milliseconds and number of timed regions per family since enable */
@@ -416,6 +419,21 @@ int smg_mvn_cholesky_rev(smg_ctx* ctx, const double* L, int ldl,
                          const double* aux, int n, const double* ws, double adj,
                          int lower_only, double* yadj, double* muadj,
                          double* Ladj, int ldla);
+/* The same forward on the factor's explicit inverse W = L^{-1} (lower, n x n,
+ * ld ldw; n % 64 == 0; W's strict upper is read only inside its diagonal
+ * 64 x 64 tiles, which must hold stored zeros there): w = W (y - mu),
+ * sd = W^T w as two passes over W's lower triangle -- the reference's own
+ * arithmetic, half = inv_L (y - mu), scaled_diff = half inv_L
+ * (prim/mat/prob/multi_normal_cholesky_lpdf.hpp:117-131) -- then the same
+ * out_lp and ws [w, sd] as smg_mvn_cholesky_fwd. */
+int smg_mvn_cholesky_fwd_inv(smg_ctx* ctx, const double* y, const double* mu,
+                             const double* L, int ldl, const double* W, int ldw, int n,
+                             double* ws, double* out_lp);
+/* The context's stream waits until W = L^{-1} of the latest factorisation
+ * that formed it progressively (smg_cholesky_fwd_checked_mark_inv with
+ * *started == 2, the first n^2 doubles of its ws) is complete, and every
+ * earlier one's.  SMG_ERR_ARG when no factorisation has formed one. */
+int smg_cholesky_inverse_wait(smg_ctx* ctx);
 /* cholesky_decompose's reverse (rev/mat/fun/cholesky_decompose.hpp:118-166)
  * for the one adjoint multi_normal_cholesky_lpdf gives a lower-structured
  * factor (the Ladj above with lower_only = 1: adj (tril(s w^T) - diag(1/L_ii)),
@@ -440,6 +458,24 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
  * also join it. */
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                              double* ws, int early_done, int* started);
+/* (smg_cholesky_mvn_rev / smg_cholesky_mvn_rev_v with Aadj == NULL only form
+ * K^{-1} (lower) into ws + n^2; s may then be NULL.)  The closed form's
+ * adjoint from that K^{-1} = C (ld n):
+ *   Aadj (lower) += adj Phi(sum_o s_o s_o^T - k C)   (the epilogue alone). */
+int smg_cholesky_inverse_adjoint(smg_ctx* ctx, const double* C, int ldc, int n, const double* s, int k,
+                                 long long s_stride, double adj, double* Aadj, int ldaa);
+/* The GP marginal's reverse through add_diag and gp_exp_quad_cov in one pass
+ * over K^{-1}'s lower triangle, when that closed-form adjoint
+ * G = adj Phi(sum_o s_o s_o^T - k C) is the only adjoint of add_diag(K0, d)
+ * and of K0 = gp_exp_quad_cov(x, sigma, l) (values K0, ld ldk; x D x n):
+ *   dadj (NULL skips) = sum_i G_ii                   (prim/mat/fun/add_diag.hpp:25-27)
+ *   out2 (NULL skips) = [2 sum_{i>=j} G_ij K0_ij / sigma,
+ *                        sum_{i>j} G_ij K0_ij d2_ij / l^3]
+ *                                                   (rev/mat/fun/gp_exp_quad_cov.hpp:96-112)
+ * written (not accumulated); fixed-order sums. */
+int smg_gp_inverse_adjoint(smg_ctx* ctx, const double* C, int ldc, int n, const double* s, int k,
+                           long long s_stride, double adj, const double* K0, int ldk, const double* x, int D,
+                           double sigma, double l, double* dadj, double* out2);
 int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long long s_stride, double adj,
                            double* Aadj, int ldaa, double* ws, int c_formed);
 /* smg_cholesky_fwd_checked_mark that also queues the top half's part of

@@ -157,6 +157,125 @@ __global__ void k_chol_mvn_adj(const double* __restrict__ C, int ldc, int n, con
   }
 }
 
+// The GP marginal's three reverses in one pass (gp_inverse_adjoint below):
+// per workgroup partials [sum_i g_ii, sum_{i>=j} g_ij K0_ij, sum_{i>j} g_ij
+// K0_ij d2_ij] with g = Phi(sum_o s_o s_o^T - k C) (adj factored out).  A
+// workgroup takes the column pair (j, n - 1 - j) (balanced: n + 1 rows), its
+// threads the rows at or below the diagonal; PAIRS: two rows per thread with
+// 16-byte loads (even n, 16-byte aligned operands, D == 1).
+template <bool PAIRS>
+__global__ __launch_bounds__(256) void k_gp_inv_reduce(const double* __restrict__ C, int ldc, int n,
+                                                      const double* __restrict__ s, int k, long long ss,
+                                                      const double* __restrict__ K0, int ldk,
+                                                      const double* __restrict__ x, int D,
+                                                      double* __restrict__ part) {
+  __shared__ double lds[16];
+  double sd = 0.0, sa = 0.0, sl = 0.0;
+  const int half = (n + 1) / 2;
+  for (int b = blockIdx.x; b < half; b += gridDim.x) {
+    for (int h = 0; h < 2; ++h) {
+      const int j = h == 0 ? b : n - 1 - b;
+      if (h == 1 && j == b) break;
+      const double* c = C + (size_t)j * ldc;
+      const double* kc = K0 + (size_t)j * ldk;
+      if (PAIRS) {
+        const double xj = x[j];
+        double sjs[4];
+        for (int o = 0; o < k && o < 4; ++o) sjs[o] = s[o * ss + j];
+        const double2* c2 = reinterpret_cast<const double2*>(c);
+        const double2* k2 = reinterpret_cast<const double2*>(kc);
+        const double2* x2 = reinterpret_cast<const double2*>(x);
+        for (int p = (j >> 1) + threadIdx.x; p < (n >> 1); p += 256) {
+          const double2 cv = c2[p], kv = k2[p], xv = x2[p];
+          double g0 = 0.0, g1 = 0.0;
+          for (int o = 0; o < k; ++o) {
+            const double2 sv = reinterpret_cast<const double2*>(s + o * ss)[p];
+            const double sj = o < 4 ? sjs[o] : s[o * ss + j];
+            g0 += sv.x * sj;
+            g1 += sv.y * sj;
+          }
+          g0 -= k * cv.x;
+          g1 -= k * cv.y;
+          const int i = 2 * p;
+          if (i > j) {
+            const double d = xv.x - xj;
+            const double t = g0 * kv.x;
+            sa += t;
+            sl += t * (d * d);
+          } else if (i == j) {
+            sd += 0.5 * g0;
+            sa += 0.5 * g0 * kv.x;
+          }
+          if (i + 1 > j) {
+            const double d = xv.y - xj;
+            const double t = g1 * kv.y;
+            sa += t;
+            sl += t * (d * d);
+          } else {  // i + 1 == j
+            sd += 0.5 * g1;
+            sa += 0.5 * g1 * kv.y;
+          }
+        }
+      } else {
+        for (int i = j + threadIdx.x; i < n; i += 256) {
+          double g = 0.0;
+          for (int o = 0; o < k; ++o) g += s[o * ss + i] * s[o * ss + j];
+          g -= k * c[i];
+          if (i == j) {
+            sd += 0.5 * g;
+            sa += 0.5 * g * kc[i];
+          } else {
+            double d2 = 0.0;
+            for (int d = 0; d < D; ++d) {
+              const double t = x[(size_t)i * D + d] - x[(size_t)j * D + d];
+              d2 += t * t;
+            }
+            const double t = g * kc[i];
+            sa += t;
+            sl += t * d2;
+          }
+        }
+      }
+    }
+  }
+  sd = block_sum(sd, lds);
+  __syncthreads();
+  sa = block_sum(sa, lds);
+  __syncthreads();
+  sl = block_sum(sl, lds);
+  if (threadIdx.x == 0) {
+    part[3 * blockIdx.x + 0] = sd;
+    part[3 * blockIdx.x + 1] = sa;
+    part[3 * blockIdx.x + 2] = sl;
+  }
+}
+
+// the fixed-order sum of k_gp_inv_reduce's partials: dadj = adj sum g_ii
+// (add_diag's d'), out2 = [2 adj sa / sigma, adj sl / l^3]
+// (rev/mat/fun/gp_exp_quad_cov.hpp:109-110)
+__global__ void k_gp_inv_final(const double* __restrict__ part, int nparts, double adj, double sigma, double l,
+                               double* dadj, double* out2) {
+  __shared__ double lds[16];
+  double sd = 0.0, sa = 0.0, sl = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    sd += part[3 * i];
+    sa += part[3 * i + 1];
+    sl += part[3 * i + 2];
+  }
+  sd = block_sum(sd, lds);
+  __syncthreads();
+  sa = block_sum(sa, lds);
+  __syncthreads();
+  sl = block_sum(sl, lds);
+  if (threadIdx.x == 0) {
+    if (dadj) dadj[0] = adj * sd;
+    if (out2) {
+      out2[0] = adj * sa * 2 / sigma;
+      out2[1] = adj * sl / (l * l * l);
+    }
+  }
+}
+
 inline int grid_for(long long tot) {
   long long g = (tot + 255) / 256;
   return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
@@ -194,24 +313,32 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int 
 }  // namespace
 
 // K^{-1} formed progressively during the factorisation (cholesky.hip
-// chol_fwd), one 512-row block row k of W = L^{-1} at a time, on the side
-// stream once panel k is final:
-//   W_kk = L_kk^{-1}                       (the block inverses of rows k P.., P = 512)
-//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}   (Y_k formed one panel earlier)
-//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k     (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
-//   Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}  (needs only panels <= k)
-// so that after the last panel only its own block row remains (its inverse,
-// -W_77 Y_7 and one rank-512 update) instead of V22, V12 and all of V V^T.
-// Each block row is four parts (W_kk; W_{k,0:k}; its K^{-1} share; Y_{k+1}),
-// queued by chol_fwd in budgets that fit beside the trailing updates.
-// ws: [W (n x n, ld n) | C (n x n, lower) | Y (P x n, ld P) | T (P/2 x 256)];
-// W's strict upper is never read outside its diagonal blocks (the triangular
-// K cuts stay inside a tile band), whose copies from aux carry stored zeros.
+// chol_fwd), one 512-row block row k of W = L^{-1} at a time, once panel k is
+// final:
+//   W_kk = L_kk^{-1}                        (the block inverses of rows k P.., P = 512)
+//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}
+//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k      (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
+// Y is accumulated right-looking, like the factorisation's trailing updates:
+// once W_k is formed, its contribution L_{r,k} W_{k,0:k+1} is added to every
+// later row's Y_r -- the next row's (r = k + 1, small: on the latency chain)
+// and the rest (r >= k + 2, the bulk: off it) as separate parts -- so that
+// after the last panel only its own block row remains (its inverse, -W_77 Y_7
+// and one rank-512 share), instead of forming Y_7 = L_{7,0:7} W_{0:7,0:7}
+// (6.6 GFLOP at n = 4096) there.
+// Parts of block row k: 0 W_kk; 1 W_{k,0:k}; 2 its K^{-1} share; 3 Y_{k+1} +=
+// L_{k+1,k} W_k; 4 Y_{k+2:} += L_{k+2:,k} W_k (part 1 of row r needs parts 3
+// of row r - 1 and 4 of rows <= r - 2).
+// ws: [W (n x n, ld n) | C (n x n, lower) | Y (n x n, ld n; block row r's
+// columns 0 .. r P) | T (P/2 x 256)]; W's strict upper is never read outside
+// its diagonal blocks (the triangular K cuts stay inside a tile band), whose
+// copies from aux carry stored zeros.
 bool smg_inv_prog_ok(int n) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR; }
 
 int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
   const size_t nn = (size_t)n * n;
-  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, nn * sizeof(double), ctx->stream));  // C accumulates
+  // C and Y accumulate (Y's column block k of row r first receives row k's
+  // contribution, after the earlier ones: one zeroing instead of a beta split)
+  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, 2 * nn * sizeof(double), ctx->stream));
   return SMG_OK;
 }
 
@@ -222,7 +349,7 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
   double* W = ws;
   double* C = ws + nn;
   double* Y = C + nn;
-  double* T = Y + (size_t)P * n;
+  double* T = Y + nn;
   const int r0 = k * P, r1 = r0 + P;
   const double* Wkk = aux + (size_t)n * SMG_AUX_W512 + r0;  // ld n, stored zeros above
   int rc;
@@ -237,12 +364,16 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
       return SMG_OK;
     case 1:  // W_{k,0:k} = -W_kk Y_k
       if (k == 0) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y, P, 0.0, W + r0, n, SMG_TRI_A_LOWER);
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y + r0, n, 0.0, W + r0, n, SMG_TRI_A_LOWER);
     case 2:  // C (lower, leading r1 x r1) += W_k^T W_k
       return smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n);
-    default:  // Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}
+    case 3:  // Y_{k+1}[:, 0:r1] (+)= L_{k+1,k} W_{k,0:r1}
       if (r1 >= n) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, r1, 1.0, L + r1, ldl, W, n, 0.0, Y, P, SMG_TRI_B_LOWER);
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, P, 1.0, L + r1 + (size_t)r0 * ldl, ldl, W + r0, n, 1.0, Y + r1, n);
+    default:  // Y_{k+2:}[:, 0:r1] (+)= L_{k+2:,k} W_{k,0:r1}
+      if (r1 + P >= n) return SMG_OK;
+      return smg_gemm_impl(ctx, 0, 0, 0, n - r1 - P, r1, P, 1.0, L + r1 + P + (size_t)r0 * ldl, ldl, W + r0, n, 1.0,
+                           Y + r1 + P, n);
   }
 }
 
@@ -256,21 +387,22 @@ double smg_inv_prog_cost(int n, int k, int part, bool inverses_here) {
     case 0: return inverses_here ? 60.0 : 6.0;
     case 1: return k == 0 ? 0.0 : 6.0 + P * r0 * P / rate;
     case 2: return 6.0 + r1 * r1 * P / rate;
-    default: return r1 >= n ? 0.0 : 6.0 + P * r1 * r1 / rate;
+    case 3: return r1 >= n ? 0.0 : 6.0 + 2.0 * P * r1 * P / rate;
+    default: return r1 + P >= n ? 0.0 : 6.0 + 2.0 * (n - r1 - P) * r1 * P / rate;
   }
 }
 
 extern "C" {
 
 size_t smg_cholesky_mvn_rev_ws_doubles(int n) {
-  return n > 0 ? 2 * (size_t)n * n + (size_t)SMG_NBR * n + SMG_NBR / 2 * 256 : 0;
+  return n > 0 ? 3 * (size_t)n * n + SMG_NBR / 2 * 256 : 0;
 }
 
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s, int k,
                          long long s_stride, double adj, double* Aadj, int ldaa, double* ws) {
   if (!ctx || n < 0 || k < 1 || (k > 1 && s_stride < n)) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
-  if (!L || !s || !Aadj || !ws || ldl < n || ldaa < n) return SMG_ERR_ARG;
+  if (!L || !ws || ldl < n || (Aadj && (!s || ldaa < n))) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
   const size_t nn = (size_t)n * n;
   double* V = ws;       // L^{-T} (upper), or W = L^{-1} on the general path
@@ -287,7 +419,54 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
     rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, V, n, V, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
   }
   if (rc) return rc;
+  if (!Aadj) return SMG_OK;  // K^{-1} only (the GP's fused reverse reads it)
   return mvn_adj_epilogue(ctx, C, n, s, k, s_stride, adj, Aadj, ldaa);
+}
+
+int smg_cholesky_inverse_adjoint(smg_ctx* ctx, const double* C, int ldc, int n, const double* s, int k,
+                                 long long s_stride, double adj, double* Aadj, int ldaa) {
+  if (!ctx || n < 0 || k < 1 || (k > 1 && s_stride < n)) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!C || !s || !Aadj || ldc != n || ldaa < n) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
+  return mvn_adj_epilogue(ctx, C, n, s, k, s_stride, adj, Aadj, ldaa);
+}
+
+int smg_gp_inverse_adjoint(smg_ctx* ctx, const double* C, int ldc, int n, const double* s, int k,
+                           long long s_stride, double adj, const double* K0, int ldk, const double* x, int D,
+                           double sigma, double l, double* dadj, double* out2) {
+  if (!ctx || n < 0 || k < 1 || (k > 1 && s_stride < n) || D < 1) return SMG_ERR_ARG;
+  if (n == 0) {
+    if (dadj || out2) {
+      const double z[2] = {0.0, 0.0};
+      if (dadj) SMG_HIP_TRY(hipMemcpyAsync(dadj, z, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+      if (out2) SMG_HIP_TRY(hipMemcpyAsync(out2, z, 2 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+      SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    return SMG_OK;
+  }
+  if (!out2) {  // the diagonal sum alone: K0 and x unused (any readable n x n / n operands)
+    if (!K0) K0 = C, ldk = ldc;
+    if (!x) x = s, D = 1;
+  }
+  if (!C || !s || !K0 || !x || ldc < n || ldk < n || (out2 && !(sigma > 0 && l > 0))) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GP);
+  const int half = (n + 1) / 2;
+  const int nb = half < 2048 ? half : 2048;
+  double* part = smg_ws(ctx, SMG_WS_RED, 3 * (size_t)nb);
+  if (!part) return SMG_ERR_OOM;
+  const bool pairs = D == 1 && n % 2 == 0 && ldc % 2 == 0 && ldk % 2 == 0 && (k == 1 || s_stride % 2 == 0) &&
+                     ((reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(s) |
+                       reinterpret_cast<uintptr_t>(K0) | reinterpret_cast<uintptr_t>(x)) & 15) == 0;
+  if (pairs)
+    hipLaunchKernelGGL(k_gp_inv_reduce<true>, dim3(nb), dim3(256), 0, ctx->stream, C, ldc, n, s, k, s_stride, K0, ldk,
+                       x, D, part);
+  else
+    hipLaunchKernelGGL(k_gp_inv_reduce<false>, dim3(nb), dim3(256), 0, ctx->stream, C, ldc, n, s, k, s_stride, K0,
+                       ldk, x, D, part);
+  hipLaunchKernelGGL(k_gp_inv_final, dim3(1), dim3(1024), 0, ctx->stream, part, nb, adj, sigma, l, dadj, out2);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
 }
 
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, double* ws,
@@ -321,7 +500,7 @@ int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long lon
                            int ldaa, double* ws, int c_formed) {
   if (!ctx || n < 0 || k < 1 || (k > 1 && s_stride < n)) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
-  if (!s || !Aadj || !ws || ldaa < n) return SMG_ERR_ARG;
+  if (!ws || (Aadj && (!s || ldaa < n))) return SMG_ERR_ARG;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
   if (ctx->inv_pending) {
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev, 0));
@@ -333,6 +512,7 @@ int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long lon
     int rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, ws, n, ws, n, 0.0, C, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER);
     if (rc) return rc;
   }
+  if (!Aadj) return SMG_OK;  // K^{-1} only
   return mvn_adj_epilogue(ctx, C, n, s, k, s_stride, adj, Aadj, ldaa);
 }
 

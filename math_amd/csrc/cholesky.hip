@@ -1073,6 +1073,15 @@ int chol_rev_two_level(smg_ctx* ctx, const double* L, int ldl, const double* aux
 }
 
 // the factor streamed to the host panel by panel (smg_cholesky_fwd_checked_mark_stream)
+// W = L^{-1} complete on stream s (the progressive rows' last part 1):
+// ctx->inv_ev_w, chained behind its previous recording
+int record_w_ready(smg_ctx* ctx, hipStream_t s) {
+  if (ctx->inv_w_recorded) SMG_HIP_TRY(hipStreamWaitEvent(s, ctx->inv_ev_w, 0));
+  SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_w, s));
+  ctx->inv_w_recorded = 1;
+  return SMG_OK;
+}
+
 struct chol_stream_sink {
   double* packed;   // device, tril_count(n) doubles
   double* host;     // host (pinned), the same
@@ -1134,6 +1143,13 @@ int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, in
   *started = 0;
   if (ws && !Dinv) return SMG_ERR_ARG;
   return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started);
+}
+
+int smg_cholesky_inverse_wait(smg_ctx* ctx) {
+  if (!ctx) return SMG_ERR_ARG;
+  if (!ctx->inv_w_recorded) return SMG_ERR_ARG;
+  SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_w, 0));
+  return SMG_OK;
 }
 
 int smg_cholesky_stream_panels(int n) { return n <= 0 ? 0 : smg_ceil_div(n, n > SMG_NBF ? SMG_NBF : n); }
@@ -1248,7 +1264,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 0, true);
       if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 1, true);
       if (!rc && hipEventRecord(w_ev[z_k], ctx->zero_stream) != hipSuccess) rc = SMG_ERR_HIP;
-      if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 3, true);
+      if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 3, true);  // the next row's Y
+      if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, z_k, 4, true);  // the later rows' Y
       ctx->stream = keep;
       if (rc) return rc;
       ++z_k;
@@ -1272,13 +1289,14 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if (int rc = queue_zero(kmax)) return rc;
       return queue_shares(budget_us);
     }
+    static const int order[5] = {0, 1, 3, 4, 2};  // W_k first, then its Y contributions, its share last
     while (q_k <= kmax && q_k < rows_prog - 1) {
-      const double c = smg_inv_prog_cost(n, q_k, q_part, true);
+      const double c = smg_inv_prog_cost(n, q_k, order[q_part], true);
       if (budget_us >= 0 && c > budget_us + 40.0) break;
       budget_us -= c;
       smg_on_side on(ctx);
-      if (int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, q_k, q_part, true)) return rc;
-      if (++q_part == 4) {
+      if (int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, q_k, order[q_part], true)) return rc;
+      if (++q_part == 5) {
         q_part = 0;
         ++q_k;
       }
@@ -1298,6 +1316,11 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int nbp = smg_ceil_div(K - J, SMG_NB);
       int nh = nbp > 3 ? nbp - 3 : 0;
       if (grid + nh > PANEL_MAX_GRID + 1 || nbp > T) nh = 0;
+      smg_prof_scope pprof(ctx, SMG_FAM_PANEL);  // (the launch alone: bench.py's dominant-kernel roofline)
+      if (ctx->prof_on) {  // in-panel work: the diagonal block's factor + the rows below's solve
+        const double m = n - J, b = K - J;
+        ctx->prof_flops[SMG_FAM_PANEL] += m * b * b - 2.0 * b * b * b / 3.0;
+      }
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
     }
@@ -1396,17 +1419,17 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 1, false);
       ctx->stream = keep;
       if (rc) return rc;
-      hipEvent_t We = smg_event(ctx, nev++);
-      if (!We) return SMG_ERR_HIP;
-      SMG_HIP_TRY(hipEventRecord(We, ctx->zero_stream));
-      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, We, 0));
+      if ((rc = record_w_ready(ctx, ctx->zero_stream))) return rc;
+      SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_w, 0));
       smg_on_side on(ctx);
       if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 2, false))) return rc;
     } else {
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
       smg_on_side on(ctx);
-      for (int part = 0; part < 4; ++part)
+      for (int part = 0; part < 3; ++part) {  // (the last row adds to no later row's Y)
         if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, part, false))) return rc;
+        if (part == 1 && (rc = record_w_ready(ctx, ctx->side))) return rc;
+      }
     }
     // its writes to ws are joined before anything on the main stream may
     // touch ws (smg_cholesky_mvn_rev_v / smg_join_async)

@@ -38,6 +38,7 @@ int smg_comm_init(smg_ctx* ctx, int nranks, int rank, const char* id) {
 int smg_comm_allreduce_sum(smg_ctx* ctx, double* buf, long long count) {
   if (!ctx || !ctx->comm || (count > 0 && !buf)) return SMG_ERR_ARG;
   if (count == 0) return SMG_OK;
+  smg_prof_scope prof(ctx, SMG_FAM_COMM);
   if (ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, (ncclComm_t)ctx->comm,
                     ctx->stream) != ncclSuccess)
     return SMG_ERR_HIP;

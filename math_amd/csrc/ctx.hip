@@ -116,7 +116,7 @@ int smg_side_begin(smg_ctx* ctx) {
 }
 
 int smg_inv_events(smg_ctx* ctx) {
-  for (hipEvent_t* e : {&ctx->inv_ev, &ctx->inv_ev_main, &ctx->inv_ev_aux})
+  for (hipEvent_t* e : {&ctx->inv_ev, &ctx->inv_ev_main, &ctx->inv_ev_aux, &ctx->inv_ev_w})
     if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
       *e = nullptr;
       ctx->host_status |= SMG_ERR_HIP;
@@ -180,8 +180,9 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->zero_stream = nullptr;
   ctx->zero_ev_main = ctx->zero_ev_done = nullptr;
   ctx->zero_pending = 0;
-  ctx->inv_ev = ctx->inv_ev_main = ctx->inv_ev_aux = nullptr;
+  ctx->inv_ev = ctx->inv_ev_main = ctx->inv_ev_aux = ctx->inv_ev_w = nullptr;
   ctx->inv_pending = 0;
+  ctx->inv_w_recorded = 0;
   ctx->side = nullptr;
   ctx->main_stream = nullptr;
   for (int i = 0; i < SMG_FAM_COUNT; ++i) {
@@ -254,7 +255,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
     hipStreamSynchronize(ctx->side);
     hipStreamDestroy(ctx->side);
   }
-  for (hipEvent_t e : {ctx->inv_ev, ctx->inv_ev_main, ctx->inv_ev_aux})
+  for (hipEvent_t e : {ctx->inv_ev, ctx->inv_ev_main, ctx->inv_ev_aux, ctx->inv_ev_w})
     if (e) hipEventDestroy(e);
   for (int i = 0; i < SMG_WS_COUNT; ++i)
     if (ctx->ws[i]) hipFree(ctx->ws[i]);

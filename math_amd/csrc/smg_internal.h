@@ -67,6 +67,11 @@ struct smg_ctx {
   // joined into `stream` by smg_cholesky_mvn_rev_v or smg_join_async
   hipEvent_t inv_ev, inv_ev_main, inv_ev_aux;
   int inv_pending;
+  // W = L^{-1} complete (all block rows) for the latest progressive
+  // factorisation; each recording first waits for the previous one, so
+  // waiting on it covers every earlier factorisation's W too
+  hipEvent_t inv_ev_w;
+  int inv_w_recorded;
   // cross-workgroup flags of the persistent panel kernels (device, zeroed at
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;
@@ -85,8 +90,8 @@ struct smg_ctx {
   long long done_seq;
   unsigned int* red_counter_d;  // last-block-done counter of the fused reductions (device, self-resetting)
   // persistent device workspaces (grow on demand; NOT arena-managed)
-  double* ws[11];  // SMG_WS_COUNT
-  size_t ws_doubles[11];
+  double* ws[12];  // SMG_WS_COUNT
+  size_t ws_doubles[12];
   // profiling
   int prof_on;
   std::vector<smg_prof_slot> prof_pending;
@@ -133,7 +138,8 @@ enum { SMG_WS_GEMM = 0, SMG_WS_RED = 1, SMG_WS_TMP = 2, SMG_WS_TMP2 = 3, SMG_WS_
        SMG_WS_GEMM_SIDE = 5, SMG_WS_INV = 6, SMG_WS_CW = 7, SMG_WS_RHS = 8,
        SMG_WS_GLM = 9,  // the GLM parameters [alpha, beta] (not the Cholesky aux's TMP2)
        SMG_WS_GEMM_ZERO = 10,  // split-K slabs of the GEMMs on the zeroing stream
-       SMG_WS_COUNT = 11 };
+       SMG_WS_MVN = 11,        // the tile partials of the MVN's passes over W = L^{-1} (mvn_inv.hip)
+       SMG_WS_COUNT = 12 };
 static_assert(SMG_WS_COUNT == sizeof(((smg_ctx*)nullptr)->ws) / sizeof(double*), "workspace slots");
 double* smg_ws(smg_ctx* ctx, int id, size_t doubles);
 // spin on the host-coherent completion word until it reaches seq (then the

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libsmg_hip.so")
 
 SMG_OK = 0
 STATUS = {1: "hip", 2: "not_pd", 4: "not_symmetric", 8: "nonfinite", 16: "arg", 32: "oom", 64: "not_positive"}
-FAMILIES = {"gemm": 0, "chol_fwd": 1, "chol_rev": 2, "gp": 3, "mvn": 4, "trsv": 5, "glm": 6, "elementwise": 7}
+FAMILIES = {"gemm": 0, "chol_fwd": 1, "chol_rev": 2, "gp": 3, "mvn": 4, "trsv": 5, "glm": 6, "elementwise": 7, "panel": 8, "comm": 9}
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -88,6 +88,10 @@ _SIGS = {
     "smg_multiply_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I]),
     "smg_mvn_cholesky_fwd": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
     "smg_mvn_cholesky_rev": (_I, [_P, _P, _I, _P, _I, _P, _D, _I, _P, _P, _P, _I]),
+    "smg_mvn_cholesky_fwd_inv": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _P, _P]),
+    "smg_cholesky_inverse_wait": (_I, [_P]),
+    "smg_cholesky_inverse_adjoint": (_I, [_P, _P, _I, _I, _P, _I, _L, _D, _P, _I]),
+    "smg_gp_inverse_adjoint": (_I, [_P, _P, _I, _I, _P, _I, _L, _D, _P, _I, _P, _I, _D, _D, _P, _P]),
     "smg_cholesky_mvn_rev_ws_doubles": (ctypes.c_size_t, [_I]),
     "smg_cholesky_mvn_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _L, _D, _P, _I, _P]),
     "smg_cholesky_inv_t_async": (_I, [_P, _P, _I, _P, _I, _P, _I, _P]),

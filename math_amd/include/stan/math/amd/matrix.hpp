@@ -40,17 +40,63 @@ enum class dev_structure : int {
                  // (i, j), (j, i) pair (gp_exp_quad_cov output)
 };
 
+/** A matrix adjoint in inverse form, G = adj Phi(sum_o s_o s_o^T - k C)
+ * (Phi: strict lower + half the diagonal, the reference's lower-entry
+ * convention; C = K^{-1} lower, ld n; s_o = s + o ss on the device): the
+ * closed-form reverse of cholesky_decompose under multi_normal_cholesky_lpdf
+ * (rev/fun/cholesky_decompose.hpp), handed to the producer of the factored
+ * matrix unexpanded. */
+struct inverse_adjoint {
+  const vari* owner = nullptr;  // the depositing node
+  const double* C = nullptr;
+  const double* s = nullptr;
+  int n = 0, k = 1;
+  long long ss = 0;
+  double adj = 0.0;
+  size_t sweep = 0;  // ChainableStack::sweep_ of the deposit
+  /** the dense form added into the lower triangle of Aadj (ld n) */
+  void expand_into(double* Aadj) const {
+    amd::check(smg_cholesky_inverse_adjoint(amd::ctx(), C, n, n, s, k, ss, adj, Aadj, n), "cholesky_decompose");
+  }
+};
+
+/** True when a node chained after tape position `pos`, other than `except`,
+ * may have written the device adjoint of matrix node `node`
+ * (vari::may_write_device_adjoint). */
+inline bool others_write_device_adjoint(size_t pos, const void* node, const vari* except) {
+  const auto& vs = ChainableStack::instance_->var_stack_;
+  for (size_t i = pos + 1; i < vs.size(); ++i)
+    if (vs[i] != except && vs[i]->may_write_device_adjoint(node)) return true;
+  return false;
+}
+
 /** A node that can take a consumer's adjoint contribution in structured
  * (unexpanded) form instead of as a dense device adjoint: cholesky_decompose
  * takes multi_normal_cholesky_lpdf's partials for its factor and applies
- * them in closed form (rev/fun/cholesky_decompose.hpp). */
+ * them in closed form (rev/fun/cholesky_decompose.hpp); add_diag and
+ * gp_exp_quad_cov take that closed form's inverse form (inverse_adjoint) for
+ * their outputs and reduce it in one pass (rev/fun/gp_exp_quad_cov.hpp). */
 class structured_adjoint_sink {
  public:
+  /** An inverse-form adjoint for the node's output (valid for the current
+   * sweep); dadj (device scalar, may be null): where a depositing add_diag
+   * wants its diagonal sum written.  True when taken. */
+  virtual bool take_inverse_adjoint(const inverse_adjoint& d, double* dadj) {
+    (void)d;
+    (void)dadj;
+    return false;
+  }
   /** owner: the consumer node; ws: its device [w, s] (smg_mvn_cholesky_fwd),
    * k of them 2n doubles apart (the array form's observations); adj: its
    * adjoint.  True when taken (the consumer then writes no dense adjoint for
    * the factor); false: the consumer writes it densely. */
-  virtual bool take_mvn_adjoint(const vari* owner, const double* ws, double adj, int k = 1) = 0;
+  virtual bool take_mvn_adjoint(const vari* owner, const double* ws, double adj, int k = 1) {
+    (void)owner;
+    (void)ws;
+    (void)adj;
+    (void)k;
+    return false;
+  }
   /** Called by such a consumer's forward pass before its own device work:
    * the node may start, on a side stream, what that reverse will need. */
   virtual void prepare_mvn_adjoint() {}
@@ -59,6 +105,12 @@ class structured_adjoint_sink {
    * that it holds what the reference's varis would (the closed form never
    * formed it). */
   virtual void expand_adjoint() {}
+  /** The factor's explicit inverse W = L^{-1} (device, n x n, ld n, lower;
+   * stored zeros above the diagonal inside its diagonal 64 x 64 tiles) when
+   * the factorisation formed it anyway, with the context's stream already
+   * ordered after its completion; null otherwise.  The consumer's forward
+   * then takes the reference's products with inv_L instead of two solves. */
+  virtual const double* inverse_factor() { return nullptr; }
 };
 
 class dev_matrix_vari {

@@ -195,6 +195,7 @@ static inline void zero_host_blocks(size_t from) {
 
 static inline void set_zero_all_adjoints() {
   auto* st = ChainableStack::instance_;
+  ++st->sweep_;  // (a structured adjoint of the last sweep is gone with the dense ones)
   for (auto* v : st->var_stack_) v->set_zero_adjoint();
   for (auto* v : st->var_nochain_stack_) v->set_zero_adjoint();
   for (auto& b : st->dev_adj_stack_) amd::zero(b.ptr, b.n);
@@ -207,6 +208,7 @@ static inline void set_zero_all_adjoints_nested() {
     throw std::logic_error(
         "empty_nested() must be false before calling set_zero_all_adjoints_nested()");
   auto* st = ChainableStack::instance_;
+  ++st->sweep_;
   const size_t s1 = st->nested_var_stack_sizes_.back();
   for (size_t i = (s1 == 0U) ? 0U : (s1 - 1); i < st->var_stack_.size(); ++i)
     st->var_stack_[i]->set_zero_adjoint();

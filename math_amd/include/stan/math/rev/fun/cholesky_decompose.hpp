@@ -35,17 +35,24 @@ namespace internal {
 /** B = A + diag(d) over the min(m, n) leading diagonal (prim/mat/fun/add_diag.hpp:20-55):
  * A a device var node or data; d a scalar (var or double) or a device vector
  * (var node or data). */
-class add_diag_dev_vari : public device_vari {
+class add_diag_dev_vari : public device_vari, public structured_adjoint_sink {
  public:
   dev_operand A_;
   dev_matrix_vari* B_;
   vari* d_vi_;    // scalar var diagonal (null otherwise)
   double* dadj_;  // its device adjoint
   dev_operand dv_;  // vector diagonal (dv_.rows == 0 when scalar)
+  size_t pos_;      // this node's index in var_stack_
+  // B's adjoint in inverse form (a Cholesky factorisation's closed form,
+  // cholesky_dev_vari): dep_ deposited in this sweep, exp_ consumed without
+  // forming B's dense adjoint (expand_adjoint writes it when read)
+  inverse_adjoint dep_, exp_;
 
   add_diag_dev_vari(const dev_operand& A, double d, vari* d_vi, const dev_operand& dv)
       : device_vari(0.0), A_(A), B_(new dev_matrix_vari(A.rows, A.cols)), d_vi_(d_vi),
-        dadj_(d_vi ? amd::alloc_doubles(1) : nullptr), dv_(dv) {
+        dadj_(d_vi ? amd::alloc_doubles(1) : nullptr), dv_(dv),
+        pos_(ChainableStack::instance_->var_stack_.size() - 1) {
+    if (A.rows == A.cols && !dv.rows) B_->sink_ = this;  // (square, scalar diagonal)
     smg_ctx* c = amd::ctx();
     const int m = A.rows, n = A.cols, k = m < n ? m : n;
     const double* dvec = dv_.rows ? dv_.val() : nullptr;
@@ -56,10 +63,47 @@ class add_diag_dev_vari : public device_vari {
       amd::check(smg_add_diag_fwd(c, B_->val_, m, k, d, dvec, B_->val_, m), "add_diag");
     }
   }
+  bool may_write_device_adjoint(const void* node) const override {
+    return (A_.vi && node == A_.vi) || (dv_.vi && node == dv_.vi);
+  }
+  bool take_inverse_adjoint(const inverse_adjoint& d, double*) override {
+    if (B_->sink_ != this) return false;
+    dep_ = d;
+    return true;
+  }
+  void expand_adjoint() override {
+    if (exp_.C && exp_.sweep == ChainableStack::instance_->sweep_) exp_.expand_into(B_->adj_);
+    exp_ = inverse_adjoint{};
+  }
+
   void chain() override {
     smg_ctx* c = amd::ctx();
     const int m = A_.rows, n = A_.cols, k = m < n ? m : n;
     if (!m || !n) return;
+    auto* st = ChainableStack::instance_;
+    if (dep_.C && dep_.sweep == st->sweep_) {
+      const inverse_adjoint d = dep_;
+      dep_ = inverse_adjoint{};
+      if (!others_write_device_adjoint(pos_, B_, d.owner)) {
+        // B's whole adjoint is the inverse form G: A' += G (passed on to A's
+        // producer when it takes it -- gp_exp_quad_cov reduces it in one pass
+        // and writes our d' -- else added densely), d' += sum_i G_ii
+        inverse_adjoint pass = d;
+        pass.owner = this;
+        const bool passed = A_.vi && A_.vi->sink_ && A_.vi->sink_->take_inverse_adjoint(pass, dadj_);
+        if (!passed) {
+          if (A_.adj()) pass.expand_into(A_.adj());
+          if (dadj_)
+            amd::check(smg_gp_inverse_adjoint(c, d.C, n, n, d.s, d.k, d.ss, d.adj, nullptr, n, nullptr, 1, 1.0, 1.0,
+                                              dadj_, nullptr),
+                       "add_diag");
+        }
+        if (d_vi_) add_pending_adjoint(d_vi_, dadj_);
+        exp_ = d;
+        return;
+      }
+      d.expand_into(B_->adj_);  // another node wrote B's adjoint too: the dense sum
+    }
     double* dadj = dv_.rows ? dv_.adj() : dadj_;
     if (dadj_) amd::check(smg_memset(c, dadj_, 0, sizeof(double)), "add_diag");
     const int vec = dv_.rows ? 1 : 0;
@@ -158,6 +202,9 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     L->sink_ = this;
   }
 
+  // chain() adds into A's device adjoint only
+  bool may_write_device_adjoint(const void* node) const override { return node == A_; }
+
   // When the factorisation did not already queue K^{-1} (no prediction yet,
   // or a size it cannot form progressively), L^{-T} is formed on the side
   // stream from the MVN's forward on, queued behind the MVN's latency-bound
@@ -174,6 +221,18 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
                "multi_normal_cholesky_lpdf");
     v_ready_ = started != 0;
     c_ready_ = v_ready_ && early_;
+  }
+
+  // W = L^{-1}: the first n^2 doubles of ws_ once the progressive K^{-1}
+  // (early_) has queued all of its block rows (chol_mvn.hip)
+  const double* inverse_factor() override {
+    static const bool off = [] {  // TEMP A/B switch (round 5)
+      const char* e = std::getenv("SMG_MVN_INV");
+      return e && e[0] == '0';
+    }();
+    if (off || !early_ || !ws_ || n_ % 64 != 0) return nullptr;
+    if (smg_cholesky_inverse_wait(amd::ctx()) != SMG_OK) return nullptr;
+    return ws_;
   }
 
   bool take_mvn_adjoint(const vari* owner, const double* ws, double adj, int k) override {
@@ -208,27 +267,36 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
     if (deposit) {
       const vari* owner = dep_owner_;
       dep_owner_ = nullptr;
-      bool dense = false;  // did any other node write L's adjoint?
-      for (size_t i = pos_ + 1; !dense && i < st->var_stack_.size(); ++i) {
-        const vari* v = st->var_stack_[i];
-        dense = v != owner && v->may_write_device_adjoint(L_);
-      }
+      const bool dense = others_write_device_adjoint(pos_, L_, owner);  // did any other node write L's adjoint?
       record(!dense);
       if (!dense) {
         exp_ws_ = dep_ws_;
         exp_adj_ = dep_adj_;
         exp_k_ = dep_k_;
         exp_sweep_ = st->sweep_;
+        // K^{-1} into ws_ + n^2, then its inverse form goes to A's producer
+        // when it takes it (add_diag / gp_exp_quad_cov: one fused pass),
+        // else the epilogue adds it into A's adjoint
         if (v_ready_) {
-          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_k_, 2LL * n_, dep_adj_, A_->adj_, n_, ws_,
+          amd::check(smg_cholesky_mvn_rev_v(c, n_, dep_ws_ + n_, dep_k_, 2LL * n_, dep_adj_, nullptr, n_, ws_,
                                             c_ready_ ? 1 : 0),
                      "cholesky_decompose");
         } else {
           if (!ws_) ws_ = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n_));
           amd::check(smg_cholesky_mvn_rev(c, L_->val_, n_, L_->aux_, n_, dep_ws_ + n_, dep_k_, 2LL * n_, dep_adj_,
-                                          A_->adj_, n_, ws_),
+                                          nullptr, n_, ws_),
                      "cholesky_decompose");
         }
+        inverse_adjoint d;
+        d.owner = this;
+        d.C = ws_ + size_t(n_) * n_;
+        d.s = dep_ws_ + n_;
+        d.n = n_;
+        d.k = dep_k_;
+        d.ss = 2LL * n_;
+        d.adj = dep_adj_;
+        d.sweep = st->sweep_;
+        if (!(A_->sink_ && A_->sink_->take_inverse_adjoint(d, nullptr))) d.expand_into(A_->adj_);
         return;
       }
       // expand the deposit: the MVN's own lower-only partials, added densely

@@ -30,7 +30,7 @@ inline void gp_check_positive(const char* fn, const char* name, double v) {
   }
 }
 
-class gp_exp_quad_cov_dev_vari : public device_vari {
+class gp_exp_quad_cov_dev_vari : public device_vari, public structured_adjoint_sink {
  public:
   const double* x_;  // D x n column-major (point i at x_ + i D)
   const int n_;
@@ -40,6 +40,11 @@ class gp_exp_quad_cov_dev_vari : public device_vari {
   vari* l_vi_;      // null when l is data
   dev_matrix_vari* K_;
   double* out2_;
+  size_t pos_;  // this node's index in var_stack_
+  // K's adjoint in inverse form (the GP marginal's closed form through
+  // add_diag, rev/fun/cholesky_decompose.hpp): its reduction was queued when
+  // it was deposited (dep_); exp_: consumed without forming K's dense adjoint
+  inverse_adjoint dep_, exp_;
 
   gp_exp_quad_cov_dev_vari(const double* x, int n, int D, double sigma, vari* sigma_vi, double l, vari* l_vi)
       : device_vari(0.0),
@@ -51,11 +56,44 @@ class gp_exp_quad_cov_dev_vari : public device_vari {
         sigma_vi_(sigma_vi),
         l_vi_(l_vi),
         K_(new dev_matrix_vari(n, n, dev_structure::symmetric)),
-        out2_(amd::alloc_doubles(2)) {
+        out2_(amd::alloc_doubles(2)),
+        pos_(ChainableStack::instance_->var_stack_.size() - 1) {
+    K_->sink_ = this;
     amd::check(smg_gp_exp_quad_cov_nd_fwd(amd::ctx(), x_, D_, n_, sigma_d_, l_d_, K_->val_, n_), "gp_exp_quad_cov");
   }
 
+  bool may_write_device_adjoint(const void*) const override { return false; }  // (host scalars only)
+
+  // The inverse form's reduction (this node's sigma', l' and the depositing
+  // add_diag's d') is queued right away, so that the d' a host node reads
+  // before this node's chain() is complete; chain() keeps sigma', l' only if
+  // no other node wrote K's adjoint, else it recomputes them from the dense sum.
+  bool take_inverse_adjoint(const inverse_adjoint& d, double* dadj) override {
+    if (d.n != n_) return false;
+    amd::check(smg_gp_inverse_adjoint(amd::ctx(), d.C, n_, n_, d.s, d.k, d.ss, d.adj, K_->val_, n_, x_, D_, sigma_d_,
+                                      l_d_, dadj, (sigma_vi_ || l_vi_) ? out2_ : nullptr),
+               "gp_exp_quad_cov");
+    dep_ = d;
+    return true;
+  }
+  void expand_adjoint() override {
+    if (exp_.C && exp_.sweep == ChainableStack::instance_->sweep_) exp_.expand_into(K_->adj_);
+    exp_ = inverse_adjoint{};
+  }
+
   void chain() override {
+    auto* st = ChainableStack::instance_;
+    if (dep_.C && dep_.sweep == st->sweep_) {
+      const inverse_adjoint d = dep_;
+      dep_ = inverse_adjoint{};
+      if (!others_write_device_adjoint(pos_, K_, d.owner)) {
+        if (sigma_vi_) add_pending_adjoint(sigma_vi_, out2_);
+        if (l_vi_) add_pending_adjoint(l_vi_, out2_ + 1);
+        exp_ = d;
+        return;
+      }
+      d.expand_into(K_->adj_);  // another node wrote K's adjoint too: the dense sum
+    }
     if (!sigma_vi_ && !l_vi_) return;
     smg_ctx* c = amd::ctx();
     amd::check(smg_memset(c, out2_, 0, 2 * sizeof(double)), "gp_exp_quad_cov");

@@ -102,7 +102,13 @@ inline var mvn_cholesky_dev(const double* y_d, const double* mu_d, int n, const 
   amd::check(smg_memset(c, lp_d + 1, 0, 2 * sizeof(double)), fn);
   if (mu_d) amd::check(smg_check_domain(c, mu_d, n, 1, lp_d + 1), fn);
   amd::check(smg_check_domain(c, y_d, n, 0, lp_d + 2), fn);
-  amd::check(smg_mvn_cholesky_fwd(c, y_d, mu_d, L.val_ptr(), n, L.vi_->aux_, n, ws, lp_d), fn);
+  // with the factor's explicit inverse at hand, the reference's own products
+  // (half = inv_L (y - mu), scaled_diff = half inv_L, :117-131)
+  const double* W = L.vi_->sink_ ? L.vi_->sink_->inverse_factor() : nullptr;
+  if (W)
+    amd::check(smg_mvn_cholesky_fwd_inv(c, y_d, mu_d, L.val_ptr(), n, W, n, n, ws, lp_d), fn);
+  else
+    amd::check(smg_mvn_cholesky_fwd(c, y_d, mu_d, L.val_ptr(), n, L.vi_->aux_, n, ws, lp_d), fn);
   if (L.vi_->sink_) L.vi_->sink_->prepare_mvn_adjoint();  // (behind the solves: overlaps their tail and the host)
   double out[3] = {0, 0, 0};
   amd::to_host(out, lp_d, 3);
@@ -178,8 +184,11 @@ inline vari* mvn_cholesky_multi(const dev_operand& L, const double* aux, bool lo
   smg_ctx* c = amd::ctx();
   double* ws = amd::alloc_doubles(2 * size_t(n) * size_t(k) + size_t(k));
   double* lp_d = ws + 2 * size_t(n) * size_t(k);
+  const double* W = lower_only && L.vi && L.vi->sink_ ? L.vi->sink_->inverse_factor() : nullptr;
   for (int i = 0; i < k; ++i)
-    amd::check(smg_mvn_cholesky_fwd(c, obs[i].y, obs[i].mu, L.val(), n, aux, n, ws + 2 * size_t(n) * i, lp_d + i),
+    amd::check(W ? smg_mvn_cholesky_fwd_inv(c, obs[i].y, obs[i].mu, L.val(), n, W, n, n, ws + 2 * size_t(n) * i,
+                                            lp_d + i)
+                 : smg_mvn_cholesky_fwd(c, obs[i].y, obs[i].mu, L.val(), n, aux, n, ws + 2 * size_t(n) * i, lp_d + i),
                fn);
   if (lower_only && L.vi && L.vi->sink_) L.vi->sink_->prepare_mvn_adjoint();  // (behind the solves)
   std::vector<double> lps(static_cast<size_t>(k));

@@ -59,6 +59,25 @@ def near_rel(actual, expected, rtol, atol=None, what=""):
     return float(rel[~small].max()) if np.any(~small) else 0.0
 
 
+# --------------------------------------------------------------- prebuilt binaries
+def prebuilt(path):
+    """path, after checking that the binary was built from the tree's sources
+    (math_amd/srchash.py): the GPU box runs these container-built binaries and
+    cannot rebuild them (no /root/reference there for Eigen)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from math_amd import srchash
+    name = os.path.basename(path)
+    if name == "libsmg_bench.so":
+        group = "bench"
+    elif name.startswith("ref_harness"):
+        group = "ref"
+    else:
+        group = "cpp:" + (name[3:-3] if name.startswith("lib") and name.endswith(".so") else name)
+    srchash.check(path, group)
+    return path
+
+
 # --------------------------------------------------------------- oracle
 _ORACLE = None
 _D = ctypes.POINTER(ctypes.c_double)

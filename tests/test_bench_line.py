@@ -30,3 +30,22 @@ def test_bench_default_line_carries_glm_strong():
     r = g["roofline"]
     assert r["bound"] == "hbm" and 0 < r["frac"] < 1.0
     assert abs(r["bytes_per_launch"] - (1e7 * 256 * 8 + 1e7 * 4)) < 1
+    # per-rank attribution of the GLM step (kernel / all-reduce / host), min / max over ranks
+    pr = g["per_rank"]
+    assert pr["ranks"] == 1 and abs(pr["allreduces_per_step"] - 1.0) < 1e-9
+    for k in ("glm_kernel_ms", "allreduce_us", "host_and_gaps_us"):
+        assert pr[k]["min"] <= pr[k]["max"] and len(pr[k]["per_rank"]) == 1
+    assert 0 < pr["glm_kernel_ms"]["min"] < g["ms_per_step"] * 1.5
+    assert pr["allreduce_us"]["min"] > 0
+    # the GP line's roofline: the dominant kernel (k_chol_panel) from HIP events,
+    # its PMC bytes from the newest committed summary, the whole eval beside it
+    gr = d["roofline"]
+    assert gr["kernel"] == "k_chol_panel" and gr["bound"] == "mfma" and 0 < gr["frac"] < 1.0
+    assert gr["avg_launch_us"] > 0 and abs(gr["launches_per_step"] - 8) < 1e-9
+    assert gr["algorithmic_bytes_per_launch"] == 18874368.0
+    import glob
+    import re
+    newest = max(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
+                 key=lambda p: int(re.match(r"r(\d+)_", os.path.basename(p)).group(1)))
+    assert gr["traffic_source"] == os.path.relpath(newest, ROOT)
+    assert 0 < gr["eval"]["frac"] < 1.0

@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from _util import ROOT, golden, near_rel
+from _util import ROOT, golden, near_rel, prebuilt
 
 BIN = os.path.join(ROOT, "tests", "cpp", "_bin", "test_boundary")
 RTOL = 1e-10
@@ -22,7 +22,7 @@ RTOL = 1e-10
 
 def _run(stdin, timeout=600, env=None):
     e = None if env is None else {**os.environ, **env}
-    p = subprocess.run([BIN], input=stdin, capture_output=True, text=True, timeout=timeout, env=e)
+    p = subprocess.run([prebuilt(BIN)], input=stdin, capture_output=True, text=True, timeout=timeout, env=e)
     assert p.returncode == 0, p.stderr[-3000:]
     return p.stdout
 

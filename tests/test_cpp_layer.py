@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from _util import ROOT, golden, near_rel
+from _util import ROOT, golden, near_rel, prebuilt
 
 BIN = os.path.join(ROOT, "tests", "cpp", "_bin")
 LIB = os.path.join(ROOT, "math_amd", "lib", "libsmg_hip.so")
@@ -38,6 +38,18 @@ def test_python_binding_covers_header():
     assert not missing, missing
 
 
+def test_prebuilt_binaries_match_sources():
+    """Every prebuilt binary the GPU box runs but cannot rebuild carries the
+    hash of the sources it was built from (math_amd/srchash.py), equal to the
+    tree's: libsmg_bench.so, tests/cpp/_bin/*, oracle/_ref/*."""
+    import glob
+    bins = [os.path.join(ROOT, "math_amd", "lib", "libsmg_bench.so")] + sorted(glob.glob(os.path.join(BIN, "*")))
+    bins += sorted(glob.glob(os.path.join(ROOT, "oracle", "_ref", "ref_harness*")))
+    assert len(bins) >= 6
+    for b in bins:
+        prebuilt(b)
+
+
 def test_cpp_programs_built():
     for name in ("test_gp_tape", "test_functors"):
         assert os.path.exists(os.path.join(BIN, name)), f"{name} not built (run __graft_entry__.build())"
@@ -45,7 +57,7 @@ def test_cpp_programs_built():
 
 def _run(name, stdin, args=(), env=None):
     e = None if env is None else {**os.environ, **env}
-    p = subprocess.run([os.path.join(BIN, name), *args], input=stdin, capture_output=True, text=True, timeout=300,
+    p = subprocess.run([prebuilt(os.path.join(BIN, name)), *args], input=stdin, capture_output=True, text=True, timeout=300,
                        env=e)
     assert p.returncode == 0, p.stderr[-2000:]
     return p.stdout

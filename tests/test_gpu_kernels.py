@@ -360,6 +360,111 @@ def test_cholesky_fwd_stream(ctx, N, with_ws):
     assert started.value == (2 if with_ws else 0)
 
 
+@pytest.mark.parametrize("N,mu", [(64, False), (320, True), (1000 // 64 * 64, False), (2048, True)])
+def test_mvn_cholesky_fwd_inv(ctx, N, mu):
+    """smg_mvn_cholesky_fwd_inv: w = W (y - mu), s = W^T w on an explicit
+    inverse W = L^{-1} (the reference's arithmetic, inv_L products) -- against
+    the solve-based smg_mvn_cholesky_fwd on the same factor (1e-12) and the
+    oracle's value (1e-10).  W's strict upper outside its diagonal 64 x 64
+    tiles holds NaN: it must never be read."""
+    rng = np.random.default_rng(N + 3)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + 0.3 * np.eye(N)
+    A = 0.5 * (A + A.T)
+    y = rng.uniform(-1, 1, N)
+    m = rng.uniform(-0.5, 0.5, N) if mu else None
+    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(N))
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
+    L = ctx.get(dL, N * N).reshape(N, N).T
+    W = np.linalg.inv(np.tril(L))
+    W = np.tril(W)
+    blk = np.arange(N) // 64
+    W[blk[:, None] < blk[None, :]] = np.nan  # above the diagonal tiles: never read
+    dy, dmu = ctx.put(y), (ctx.put(m) if mu else None)
+    ws0, lp0 = ctx.zeros(2 * N), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd", dy, dmu, dL, N, dD, N, ws0, lp0)
+    ws1, lp1 = ctx.zeros(2 * N), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd_inv", dy, dmu, dL, N, ctx.put(F(W)), N, N, ws1, lp1)
+    a0, a1 = ctx.get(ws0, 2 * N), ctx.get(ws1, 2 * N)
+    near_rel(a1, a0, 1e-12, atol=1e-12 * np.abs(a0).max(), what="[w, s]")
+    v0, v1 = ctx.get(lp0, 1)[0], ctx.get(lp1, 1)[0]
+    near_rel(np.array([v1]), np.array([v0]), 1e-12, what="lp")
+    r = y - (m if mu else 0.0)
+    w = np.linalg.solve(np.tril(L), r)
+    lp_ref = -0.5 * N * np.log(2 * np.pi) - 0.5 * w @ w - np.log(np.diag(L)).sum()
+    near_rel(np.array([v1]), np.array([lp_ref]), 1e-10, what="lp vs numpy")
+    assert ctx.lib.smg_mvn_cholesky_fwd_inv(ctx.ptr, dy, dmu, dL, N, ctx.put(F(W)), N - 1, N, ws1, lp1) != 0
+
+
+def test_mvn_inverse_from_progressive_factorisation(ctx):
+    """The factorisation's progressive W = L^{-1} (smg_cholesky_fwd_checked_mark_inv,
+    *started == 2) is what smg_mvn_cholesky_fwd_inv reads after
+    smg_cholesky_inverse_wait: the same [w, s] and lp as the solves (1e-12)."""
+    import ctypes
+    N = 2048
+    rng = np.random.default_rng(99)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + 0.2 * np.eye(N)
+    A = 0.5 * (A + A.T)
+    y = rng.uniform(-1, 1, N)
+    lib = ctx.lib
+    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(lib.smg_cholesky_aux_doubles(N))
+    ws = ctx.zeros(lib.smg_cholesky_mvn_rev_ws_doubles(N))
+    started = ctypes.c_int(-1)
+    ctx.call("smg_cholesky_fwd_checked_mark_inv", dA, N, N, dL, N, dD, ws, ctypes.byref(started))
+    assert started.value == 2
+    st = ctypes.c_int(-1)
+    ctx.call("smg_status_mark_wait", ctypes.byref(st))
+    assert st.value == 0
+    ctx.call("smg_cholesky_inverse_wait")
+    dy = ctx.put(y)
+    ws1, lp1 = ctx.zeros(2 * N), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd_inv", dy, None, dL, N, ws, N, N, ws1, lp1)
+    ws0, lp0 = ctx.zeros(2 * N), ctx.zeros(1)
+    ctx.call("smg_mvn_cholesky_fwd", dy, None, dL, N, dD, N, ws0, lp0)
+    ctx.call("smg_join_async")
+    a0, a1 = ctx.get(ws0, 2 * N), ctx.get(ws1, 2 * N)
+    near_rel(a1, a0, 1e-12, atol=1e-12 * np.abs(a0).max(), what="[w, s]")
+    near_rel(ctx.get(lp1, 1), ctx.get(lp0, 1), 1e-12, what="lp")
+
+
+@pytest.mark.parametrize("N,D,k", [(64, 1, 1), (301, 1, 1), (512, 3, 1), (1024, 1, 2), (257, 2, 3)])
+def test_gp_inverse_adjoint_vs_composition(ctx, N, D, k):
+    """smg_gp_inverse_adjoint (the GP marginal's three reverses in one pass
+    over K^{-1}) against their composition on the device: the closed form's
+    epilogue into Kd's adjoint (smg_cholesky_inverse_adjoint), add_diag's
+    reverse, gp_exp_quad_cov's reverse -- d', sigma', l' at 1e-12."""
+    rng = np.random.default_rng(N * 7 + D + k)
+    M = rng.uniform(-1, 1, (N, N))
+    C = M @ M.T / N + np.eye(N)
+    s = rng.uniform(-1, 1, (k, 2 * N))  # observation o's s at o * 2N (the MVN's [w, s] blocks: s_stride 2N)
+    x = rng.uniform(-3, 3, (N, D))
+    sig, ell, adj = 1.3, 0.7, 0.8
+    dC, ds, dx = ctx.put(F(C)), ctx.put(s.ravel()), ctx.put(x.ravel())
+    dK = ctx.zeros(N * N)
+    ctx.call("smg_gp_exp_quad_cov_nd_fwd", dx, D, N, sig, ell, dK, N)
+    # composition
+    dKd, dKa, dd0, o0 = ctx.zeros(N * N), ctx.zeros(N * N), ctx.zeros(1), ctx.zeros(2)
+    ctx.call("smg_cholesky_inverse_adjoint", dC, N, N, ds, k, 2 * N, adj, dKd, N)
+    ctx.call("smg_add_diag_rev", dKd, N, N, dKa, N, dd0, 0)
+    ctx.call("smg_gp_exp_quad_cov_nd_rev", dx, D, N, sig, ell, dKa, N, o0)
+    # fused
+    dd1, o1 = ctx.zeros(1), ctx.zeros(2)
+    ctx.call("smg_gp_inverse_adjoint", dC, N, N, ds, k, 2 * N, adj, dK, N, dx, D, sig, ell, dd1, o1)
+    dd2 = ctx.zeros(1)  # the diagonal sum alone (K0, x unused)
+    ctx.call("smg_gp_inverse_adjoint", dC, N, N, ds, k, 2 * N, adj, None, N, None, 1, 1.0, 1.0, dd2, None)
+    r0 = np.concatenate([ctx.get(dd0, 1), ctx.get(o0, 2)])
+    r1 = np.concatenate([ctx.get(dd1, 1), ctx.get(o1, 2)])
+    near_rel(r1, r0, 1e-12, what="[d', sigma', l']")
+    near_rel(ctx.get(dd2, 1), r0[:1], 1e-12, what="d' alone")
+    # the epilogue against numpy: Phi(sum_o s_o s_o^T - k C) adj on the lower triangle
+    S = sum(np.outer(s[o, :N], s[o, :N]) for o in range(k))
+    G = adj * (S - k * C)
+    G = np.tril(G, -1) + 0.5 * np.diag(np.diag(G))
+    Kd = ctx.get(dKd, N * N).reshape(N, N).T
+    near_rel(Kd, G, 1e-12, atol=1e-12 * np.abs(G).max(), what="epilogue")
+
+
 @pytest.mark.parametrize("N", [65, 300, 1024, 2048])
 def test_cholesky_mvn_closed_form_vs_oracle(ctx, N):
     """smg_cholesky_mvn_rev: cholesky_decompose's reverse for the MVN's

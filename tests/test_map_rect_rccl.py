@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import gen
-from _util import ROOT, golden, near_rel
+from _util import ROOT, golden, near_rel, prebuilt
 
 pytestmark = pytest.mark.gpu
 
@@ -27,7 +27,7 @@ _TAIL = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_
 
 
 def _lib():
-    lib = ctypes.CDLL(LIB)
+    lib = ctypes.CDLL(prebuilt(LIB))
     lib.maprect_hier.restype = ctypes.c_int
     lib.maprect_hier.argtypes = [ctypes.c_int, ctypes.c_int, _AG, ctypes.c_void_p] + _TAIL
     lib.maprect_hier_rccl.restype = ctypes.c_int

@@ -22,7 +22,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import gen
-from _util import ROOT, f64, golden, near_rel, oracle, ptr
+from _util import ROOT, f64, golden, near_rel, oracle, ptr, prebuilt
 
 GOLDEN_INC = 0x9E3779B97F4A7C15
 BENCH_LIB = os.path.join(ROOT, "math_amd", "lib", "libsmg_bench.so")
@@ -33,7 +33,7 @@ def _partition(R, world, rank, lib=None):
     that already loaded it) the glm_dist test library."""
     b0, b1 = ctypes.c_longlong(), ctypes.c_longlong()
     if lib is None:
-        ctypes.CDLL(BENCH_LIB).smg_bench_row_partition(ctypes.c_longlong(R), world, rank, ctypes.byref(b0),
+        ctypes.CDLL(prebuilt(BENCH_LIB)).smg_bench_row_partition(ctypes.c_longlong(R), world, rank, ctypes.byref(b0),
                                                        ctypes.byref(b1))
     else:
         lib.glm_dist_row_partition(ctypes.c_longlong(R), world, rank, ctypes.byref(b0), ctypes.byref(b1))
@@ -148,7 +148,7 @@ def _maprect_call(lib, world, rank, cb, xr, xi, th, mode):
 
 
 def _maprect_lib():
-    lib = ctypes.CDLL(MAPRECT_LIB)
+    lib = ctypes.CDLL(prebuilt(MAPRECT_LIB))
     lib.maprect_hier.restype = ctypes.c_int
     lib.maprect_hier.argtypes = [ctypes.c_int, ctypes.c_int, _AG, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -424,7 +424,7 @@ def _glm_dist_rank(rank, world, port, out):
         calls.append(count)
 
     ag, ar = _AG(allgather), _AR(allreduce)
-    lib = ctypes.CDLL(GLMDIST_LIB)
+    lib = ctypes.CDLL(prebuilt(GLMDIST_LIB))
     lib.glm_dist_eval.restype = ctypes.c_int
     res = {}
     for kind, name, bad in GLM_DIST_CASES:
