@@ -458,6 +458,15 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
  * also join it. */
 int smg_cholesky_inv_t_async(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n,
                              double* ws, int early_done, int* started);
+/* cholesky_decompose's reverse (rev/mat/fun/cholesky_decompose.hpp:118-166)
+ * for any factor adjoint Lbar (its lower triangle is read) in closed form on
+ * the factor's inverse W = L^{-1} (lower, zeros above; Wt = W^T, both ld ldw):
+ *   Abar (lower) += tril(G + G^T) - diag(G),  G = W^T Phi(L^T tril(Lbar)) W
+ * (Phi: lower triangle, half the diagonal): the same adjoint as
+ * smg_cholesky_rev's blocked (Murray) algorithm, in three large products.
+ * ws: 2 n^2 doubles. */
+int smg_cholesky_rev_inverse(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Wt, int ldw,
+                             const double* Ladj, int ldla, int n, double* Aadj, int ldaa, double* ws);
 /* (smg_cholesky_mvn_rev / smg_cholesky_mvn_rev_v with Aadj == NULL only form
  * K^{-1} (lower) into ws + n^2; s may then be NULL.)  The closed form's
  * adjoint from that K^{-1} = C (ld n):
@@ -502,6 +511,10 @@ int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, in
  * factored (the reference's cholesky_decompose returns an Eigen matrix of
  * varis, rev/mat/fun/cholesky_decompose.hpp:378-427). */
 int smg_cholesky_stream_panels(int n);
+/* The columns [*j0, *j1) panel p of the streamed factor covers (the packed
+ * triangle's offsets j n - j (j - 1) / 2 of those columns are what marker
+ * marker_base + p covers); SMG_ERR_ARG outside 0 <= p < smg_cholesky_stream_panels(n). */
+int smg_cholesky_stream_panel_cols(int n, int p, int* j0, int* j1);
 int smg_cholesky_fwd_checked_mark_stream(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                                          double* aux, double* ws, int* started, double* packed, double* host_dst,
                                          int marker_base);
@@ -635,6 +648,10 @@ int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda);
  * prim/mat/fun/add_diag.hpp:25-27).  unpack_tril_add: modes 0 / 1
  * tril(A) += unpack(src), mode 2 A_ii += src[i]. */
 int smg_pack_tril(smg_ctx* ctx, int mode, int n, const double* A, int lda, double* dst);
+/* out[0] = the sum of A's strict upper triangle (fixed order): what a
+ * cholesky_decompose factor's one dummy vari accumulates from every
+ * upper-element adjoint (rev/mat/fun/cholesky_decompose.hpp:34-48). */
+int smg_sum_strict_upper(smg_ctx* ctx, int n, const double* A, int lda, double* out);
 int smg_unpack_tril_add(smg_ctx* ctx, int mode, int n, const double* src, double* A, int lda);
 /* B (n x m) = A^T + beta B, A m x n (transpose(Matrix<var>): forward copy and
  * the reverse Aadj += Badj^T) */

@@ -276,6 +276,37 @@ __global__ void k_gp_inv_final(const double* __restrict__ part, int nparts, doub
   }
 }
 
+// Aadj (lower) += G + G^T below the diagonal and G_ii on it: one 64 x 64
+// tile of the lower triangle per workgroup, the mirror tile G(j0.., i0..)
+// read column-coalesced and transposed through LDS
+__global__ __launch_bounds__(256) void k_add_lower_sym(const double* __restrict__ G, int ldg, int n,
+                                                      double* __restrict__ A, int lda) {
+  const int bx = blockIdx.x, by = blockIdx.y;  // tile rows bx, cols by
+  if (bx < by) return;
+  __shared__ double t[64][65];
+  const int i0 = bx * 64, j0 = by * 64;
+  const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int c = c4; c < 64; c += 4) {  // t[r][c] = G(j0 + r, i0 + c) = G^T(i0 + c, j0 + r)
+    const int i = j0 + r, j = i0 + c;
+    t[r][c] = (i < n && j < n) ? G[i + (size_t)j * ldg] : 0.0;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int c = c4; c < 64; c += 4) {
+    const int i = i0 + r, j = j0 + c;
+    if (i < n && j < n && i >= j) {
+      double v = G[i + (size_t)j * ldg];
+      if (i != j) v += t[c][r];
+      A[i + (size_t)j * lda] += v;
+    }
+  }
+}
+
+__global__ void k_scale_diag(double* __restrict__ P, int ldp, int n, double f) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) P[i + (size_t)i * ldp] *= f;
+}
+
 inline int grid_for(long long tot) {
   long long g = (tot + 255) / 256;
   return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
@@ -313,32 +344,24 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int 
 }  // namespace
 
 // K^{-1} formed progressively during the factorisation (cholesky.hip
-// chol_fwd), one 512-row block row k of W = L^{-1} at a time, once panel k is
-// final:
-//   W_kk = L_kk^{-1}                        (the block inverses of rows k P.., P = 512)
-//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}
-//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k      (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
-// Y is accumulated right-looking, like the factorisation's trailing updates:
-// once W_k is formed, its contribution L_{r,k} W_{k,0:k+1} is added to every
-// later row's Y_r -- the next row's (r = k + 1, small: on the latency chain)
-// and the rest (r >= k + 2, the bulk: off it) as separate parts -- so that
-// after the last panel only its own block row remains (its inverse, -W_77 Y_7
-// and one rank-512 share), instead of forming Y_7 = L_{7,0:7} W_{0:7,0:7}
-// (6.6 GFLOP at n = 4096) there.
-// Parts of block row k: 0 W_kk; 1 W_{k,0:k}; 2 its K^{-1} share; 3 Y_{k+1} +=
-// L_{k+1,k} W_k; 4 Y_{k+2:} += L_{k+2:,k} W_k (part 1 of row r needs parts 3
-// of row r - 1 and 4 of rows <= r - 2).
-// ws: [W (n x n, ld n) | C (n x n, lower) | Y (n x n, ld n; block row r's
-// columns 0 .. r P) | T (P/2 x 256)]; W's strict upper is never read outside
-// its diagonal blocks (the triangular K cuts stay inside a tile band), whose
-// copies from aux carry stored zeros.
+// chol_fwd), one 512-row block row k of W = L^{-1} at a time, on the side
+// stream once panel k is final:
+//   W_kk = L_kk^{-1}                       (the block inverses of rows k P.., P = 512)
+//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}   (Y_k formed one panel earlier)
+//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k     (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
+//   Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}  (needs only panels <= k)
+// so that after the last panel only its own block row remains (its inverse,
+// -W_77 Y_7 and one rank-512 update) instead of V22, V12 and all of V V^T.
+// Each block row is four parts (W_kk; W_{k,0:k}; its K^{-1} share; Y_{k+1}),
+// queued by chol_fwd in budgets that fit beside the trailing updates.
+// ws: [W (n x n, ld n) | C (n x n, lower) | Y (P x n, ld P) | T (P/2 x 256)];
+// W's strict upper is never read outside its diagonal blocks (the triangular
+// K cuts stay inside a tile band), whose copies from aux carry stored zeros.
 bool smg_inv_prog_ok(int n) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR; }
 
 int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
   const size_t nn = (size_t)n * n;
-  // C and Y accumulate (Y's column block k of row r first receives row k's
-  // contribution, after the earlier ones: one zeroing instead of a beta split)
-  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, 2 * nn * sizeof(double), ctx->stream));
+  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, nn * sizeof(double), ctx->stream));  // C accumulates
   return SMG_OK;
 }
 
@@ -349,7 +372,7 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
   double* W = ws;
   double* C = ws + nn;
   double* Y = C + nn;
-  double* T = Y + nn;
+  double* T = Y + (size_t)P * n;
   const int r0 = k * P, r1 = r0 + P;
   const double* Wkk = aux + (size_t)n * SMG_AUX_W512 + r0;  // ld n, stored zeros above
   int rc;
@@ -364,16 +387,12 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
       return SMG_OK;
     case 1:  // W_{k,0:k} = -W_kk Y_k
       if (k == 0) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y + r0, n, 0.0, W + r0, n, SMG_TRI_A_LOWER);
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y, P, 0.0, W + r0, n, SMG_TRI_A_LOWER);
     case 2:  // C (lower, leading r1 x r1) += W_k^T W_k
       return smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n);
-    case 3:  // Y_{k+1}[:, 0:r1] (+)= L_{k+1,k} W_{k,0:r1}
+    default:  // Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}
       if (r1 >= n) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, P, 1.0, L + r1 + (size_t)r0 * ldl, ldl, W + r0, n, 1.0, Y + r1, n);
-    default:  // Y_{k+2:}[:, 0:r1] (+)= L_{k+2:,k} W_{k,0:r1}
-      if (r1 + P >= n) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, n - r1 - P, r1, P, 1.0, L + r1 + P + (size_t)r0 * ldl, ldl, W + r0, n, 1.0,
-                           Y + r1 + P, n);
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, r1, 1.0, L + r1, ldl, W, n, 0.0, Y, P, SMG_TRI_B_LOWER);
   }
 }
 
@@ -387,15 +406,14 @@ double smg_inv_prog_cost(int n, int k, int part, bool inverses_here) {
     case 0: return inverses_here ? 60.0 : 6.0;
     case 1: return k == 0 ? 0.0 : 6.0 + P * r0 * P / rate;
     case 2: return 6.0 + r1 * r1 * P / rate;
-    case 3: return r1 >= n ? 0.0 : 6.0 + 2.0 * P * r1 * P / rate;
-    default: return r1 + P >= n ? 0.0 : 6.0 + 2.0 * (n - r1 - P) * r1 * P / rate;
+    default: return r1 >= n ? 0.0 : 6.0 + P * r1 * r1 / rate;
   }
 }
 
 extern "C" {
 
 size_t smg_cholesky_mvn_rev_ws_doubles(int n) {
-  return n > 0 ? 3 * (size_t)n * n + SMG_NBR / 2 * 256 : 0;
+  return n > 0 ? 2 * (size_t)n * n + (size_t)SMG_NBR * n + SMG_NBR / 2 * 256 : 0;
 }
 
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s, int k,
@@ -421,6 +439,45 @@ int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* a
   if (rc) return rc;
   if (!Aadj) return SMG_OK;  // K^{-1} only (the GP's fused reverse reads it)
   return mvn_adj_epilogue(ctx, C, n, s, k, s_stride, adj, Aadj, ldaa);
+}
+
+// cholesky_decompose's reverse for ANY factor adjoint Lbar in closed form on
+// the factor's inverse W = L^{-1} (rev/mat/fun/cholesky_decompose.hpp:118-166
+// computes the same by Murray's blocked algorithm):
+//   P = Phi(L^T tril(Lbar)),  G = W^T P W,  Abar (lower) += tril(G + G^T)
+//   with G_ii on the diagonal
+// from <Lbar, dL> = <Phi(L^T Lbar), L^{-1} dA L^{-T}> (dL = L Phi(L^{-1} dA
+// L^{-T})).  4 n^3 / 3 flops in three large triangular-operand products
+// (P: n^3/3, T = P W: n^3/3, G = W^T T: 2 n^3/3) instead of Murray's 2 n^3 / 3
+// in ~n/64 dependent rounds.  ws: 2 n^2 doubles.
+int smg_cholesky_rev_inverse(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Wt, int ldw,
+                             const double* La, int ldla, int n, double* Aadj, int ldaa, double* ws) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!L || !W || !Wt || !La || !Aadj || !ws || ldl < n || ldw < n || ldla < n || ldaa < n) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_CHOL_REV);
+  const size_t nn = (size_t)n * n;
+  double* P = ws;
+  double* T = ws + nn;
+  int rc;
+  // T = tril(Lbar) (stored zeros above: the products' triangular K cuts read whole tiles)
+  if ((rc = smg_copy_tril(ctx, n, n, La, ldla, T, n))) return rc;
+  // P = Phi(L^T T) (lower): op(A) = L^T upper, op(B) = T lower
+  if ((rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, T, n, 0.0, P, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
+    return rc;
+  hipLaunchKernelGGL(k_scale_diag, dim3(smg_ceil_div(n, 256) < 64 ? smg_ceil_div(n, 256) : 64), dim3(256), 0,
+                     ctx->stream, P, n, n, 0.5);
+  SMG_LAUNCH_CHECK();
+  // T = P W (lower x lower: lower; T's strict upper keeps tril's zeros)
+  if ((rc = smg_gemm_impl(ctx, 0, 0, 1, n, n, n, 1.0, P, n, W, ldw, 0.0, T, n, SMG_TRI_A_LOWER | SMG_TRI_B_LOWER)))
+    return rc;
+  // G = W^T T (upper x lower: full) into P
+  if ((rc = smg_gemm_impl(ctx, 0, 0, 0, n, n, n, 1.0, Wt, ldw, T, n, 0.0, P, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
+    return rc;
+  const int tb = smg_ceil_div(n, 64);
+  hipLaunchKernelGGL(k_add_lower_sym, dim3(tb, tb), dim3(256), 0, ctx->stream, P, n, n, Aadj, ldaa);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
 }
 
 int smg_cholesky_inverse_adjoint(smg_ctx* ctx, const double* C, int ldc, int n, const double* s, int k,

@@ -1163,7 +1163,20 @@ int smg_cholesky_fwd_checked_mark_stream(smg_ctx* ctx, const double* A, int lda,
   if (marker_base + smg_cholesky_stream_panels(n) > 64) return SMG_ERR_ARG;
   if (!ctx || smg_zero_stream_begin(ctx) != SMG_OK) return SMG_ERR_HIP;
   const chol_stream_sink sink{packed, host_dst, marker_base};
-  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started, &sink);
+  const int rc = chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started, &sink);
+  // an error after some panel copies were queued: they still target host_dst,
+  // which the caller may free or regrow once this returns
+  if (rc != SMG_OK) hipStreamSynchronize(ctx->zero_stream);
+  return rc;
+}
+
+int smg_cholesky_stream_panel_cols(int n, int p, int* j0, int* j1) {
+  const int np = smg_cholesky_stream_panels(n);
+  if (!j0 || !j1 || p < 0 || p >= np) return SMG_ERR_ARG;
+  const int nb2 = n > SMG_NBF ? SMG_NBF : n;  // chol_fwd's panel width
+  *j0 = p * nb2;
+  *j1 = min(n, *j0 + nb2);
+  return SMG_OK;
 }
 
 }  // extern "C"

@@ -105,9 +105,23 @@ double* smg_ws(smg_ctx* ctx, int id, size_t doubles) {
   return ctx->ws[id];
 }
 
+// TEMP A/B (round 5): SMG_STREAM_PRIO=1 creates the side stream (trailing
+// updates, K^{-1} shares) at the least and the zeroing stream (the block rows'
+// latency chain) at the greatest priority
+static hipError_t create_aux_stream(hipStream_t* s, bool high) {
+  static const bool prio = [] {
+    const char* e = getenv("SMG_STREAM_PRIO");
+    return e && e[0] == '1';
+  }();
+  if (!prio) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, high ? greatest : least);
+}
+
 int smg_side_begin(smg_ctx* ctx) {
   if (ctx->side) return SMG_OK;
-  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+  if (create_aux_stream(&ctx->side, false) != hipSuccess) {
     ctx->side = nullptr;
     ctx->host_status |= SMG_ERR_HIP;
     return SMG_ERR_HIP;
@@ -343,9 +357,18 @@ size_t smg_arena_reserved(const smg_ctx* ctx) {
   return s;
 }
 
+// every stream that may still have a copy into / out of pinned host memory
+// in flight (the streamed factor's panel copies run on the zeroing stream)
+static void sync_all_streams(smg_ctx* ctx) {
+  hipStreamSynchronize(ctx->stream);
+  if (ctx->main_stream && ctx->main_stream != ctx->stream) hipStreamSynchronize(ctx->main_stream);
+  if (ctx->side) hipStreamSynchronize(ctx->side);
+  if (ctx->zero_stream) hipStreamSynchronize(ctx->zero_stream);
+}
+
 void* smg_host_scratch(smg_ctx* ctx, size_t bytes) {
   if (bytes > ctx->host_scratch_size) {
-    hipStreamSynchronize(ctx->stream);
+    sync_all_streams(ctx);
     hipHostFree(ctx->host_scratch);
     size_t n = ctx->host_scratch_size;
     while (n < bytes) n *= 2;
@@ -362,7 +385,7 @@ void* smg_host_scratch(smg_ctx* ctx, size_t bytes) {
 void* smg_pinned_io(smg_ctx* ctx, size_t bytes) {
   if (!ctx) return nullptr;
   if (bytes > ctx->pin_io_size) {
-    hipStreamSynchronize(ctx->stream);
+    sync_all_streams(ctx);
     if (ctx->pin_io) hipHostFree(ctx->pin_io);
     size_t n = ctx->pin_io_size ? ctx->pin_io_size : (size_t)1 << 16;
     while (n < bytes) n *= 2;
@@ -382,7 +405,7 @@ void* smg_pinned_io(smg_ctx* ctx, size_t bytes) {
 void* smg_pinned_result(smg_ctx* ctx, size_t bytes) {
   if (!ctx) return nullptr;
   if (bytes > ctx->res_h_size) {
-    hipStreamSynchronize(ctx->stream);
+    sync_all_streams(ctx);
     if (ctx->res_h) hipHostFree(ctx->res_h);
     size_t n = ctx->res_h_size ? ctx->res_h_size : (size_t)1 << 12;
     while (n < bytes) n *= 2;
@@ -462,7 +485,7 @@ int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
 
 int smg_zero_stream_begin(smg_ctx* ctx) {
   if (ctx->zero_stream) return SMG_OK;
-  if (hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking) != hipSuccess ||
+  if (create_aux_stream(&ctx->zero_stream, true) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->zero_ev_main, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->zero_ev_done, hipEventDisableTiming) != hipSuccess) {
     hipGetLastError();

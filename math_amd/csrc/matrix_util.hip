@@ -208,6 +208,20 @@ __global__ __launch_bounds__(256) void k_pack_diag(int n, const double* __restri
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) dst[i] = A[i + (size_t)i * lda];
 }
 
+// per-workgroup sums of the strict upper triangle (columns blockIdx.x,
+// + gridDim.x, ...; rows < column), in a fixed order
+__global__ __launch_bounds__(256) void k_upper_sums(int n, const double* __restrict__ A, int lda,
+                                                    double* __restrict__ part) {
+  __shared__ double lds[16];
+  double v = 0.0;
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double* a = A + (size_t)j * lda;
+    for (int i = threadIdx.x; i < j; i += 256) v += a[i];
+  }
+  v = block_sum(v, lds);
+  if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+
 inline int grid_for(long long tot, int cap = 4096) {
   long long g = (tot + 255) / 256;
   if (g > cap) g = cap;
@@ -259,6 +273,17 @@ int smg_pack_tril(smg_ctx* ctx, int mode, int n, const double* A, int lda, doubl
     const int t = smg_ceil_div(n, TT);
     hipLaunchKernelGGL(k_pack_tril, dim3(t, t), dim3(256), 0, ctx->stream, mode, n, A, lda, dst);
   }
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_sum_strict_upper(smg_ctx* ctx, int n, const double* A, int lda, double* out) {
+  if (!ctx || n < 0 || !out || (n > 0 && (!A || lda < n))) return SMG_ERR_ARG;
+  const int g = n < 1024 ? (n > 0 ? n : 1) : 1024;
+  double* part = smg_ws(ctx, SMG_WS_RED, g);
+  if (!part) return SMG_ERR_OOM;
+  hipLaunchKernelGGL(k_upper_sums, dim3(g), dim3(256), 0, ctx->stream, n, A, lda, part);
+  smg_reduce_partials(ctx, part, g, 1, out, 0);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -91,6 +91,7 @@ _SIGS = {
     "smg_mvn_cholesky_fwd_inv": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _P, _P]),
     "smg_cholesky_inverse_wait": (_I, [_P]),
     "smg_cholesky_inverse_adjoint": (_I, [_P, _P, _I, _I, _P, _I, _L, _D, _P, _I]),
+    "smg_cholesky_rev_inverse": (_I, [_P, _P, _I, _P, _P, _I, _P, _I, _I, _P, _I, _P]),
     "smg_gp_inverse_adjoint": (_I, [_P, _P, _I, _I, _P, _I, _L, _D, _P, _I, _P, _I, _D, _D, _P, _P]),
     "smg_cholesky_mvn_rev_ws_doubles": (ctypes.c_size_t, [_I]),
     "smg_cholesky_mvn_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _L, _D, _P, _I, _P]),
@@ -98,6 +99,8 @@ _SIGS = {
     "smg_cholesky_mvn_rev_v": (_I, [_P, _I, _P, _I, _L, _D, _P, _I, _P, _I]),
     "smg_cholesky_fwd_checked_mark_inv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
     "smg_cholesky_stream_panels": (_I, [_I]),
+    "smg_cholesky_stream_panel_cols": (_I, [_I, _I, _P, _P]),
+    "smg_sum_strict_upper": (_I, [_P, _I, _P, _I, _P]),
     "smg_cholesky_fwd_checked_mark_stream": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I]),
     "smg_log_sum_exp_fwd": (_I, [_P, _P, _L, _P]),
     "smg_log_sum_exp_rev": (_I, [_P, _P, _L, _D, _D, _P]),

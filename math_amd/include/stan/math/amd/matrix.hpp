@@ -64,9 +64,12 @@ struct inverse_adjoint {
  * may have written the device adjoint of matrix node `node`
  * (vari::may_write_device_adjoint). */
 inline bool others_write_device_adjoint(size_t pos, const void* node, const vari* except) {
-  const auto& vs = ChainableStack::instance_->var_stack_;
-  for (size_t i = pos + 1; i < vs.size(); ++i)
-    if (vs[i] != except && vs[i]->may_write_device_adjoint(node)) return true;
+  // only the nodes that can write device adjoints at all (the tape's
+  // dev_writers_, registered at construction), from the first one after pos
+  const auto& w = ChainableStack::instance_->dev_writers_;
+  auto it = std::upper_bound(w.begin(), w.end(), pos, [](size_t p, const dev_writer& d) { return p < d.pos; });
+  for (; it != w.end(); ++it)
+    if (it->v != except && it->v->may_write_device_adjoint(node)) return true;
   return false;
 }
 
@@ -111,6 +114,14 @@ class structured_adjoint_sink {
    * ordered after its completion; null otherwise.  The consumer's forward
    * then takes the reference's products with inv_L instead of two solves. */
   virtual const double* inverse_factor() { return nullptr; }
+  /** A consumer that formed the factor's inverse W = L^{-1} (lower, zeros
+   * above) and Wt = W^T (both n x n, ld n, device, living as long as the
+   * tape) offers them: the factor's reverse may then take the closed form on
+   * W for a dense adjoint (smg_cholesky_rev_inverse) instead of Murray's. */
+  virtual void provide_inverse(const double* W, const double* Wt) {
+    (void)W;
+    (void)Wt;
+  }
 };
 
 class dev_matrix_vari {
@@ -357,7 +368,9 @@ class dev_to_host_vari : public vari {
   size_t ran_ = 0;     // the sweep (ChainableStack::sweep_) of the last chain()
   bool wrote_ = false;  // whether that chain() added into the node's adjoint
   explicit dev_to_host_vari(size_t blk)
-      : vari(0.0), blk_(blk), pos_(ChainableStack::instance_->var_stack_.size() - 1) {}
+      : vari(0.0), blk_(blk), pos_(ChainableStack::instance_->var_stack_.size() - 1) {
+    local_adjoint_vari::register_dev_writer(this);  // (it adds gathered host adjoints into the node's)
+  }
   bool reads_other_adjoints() const override { return true; }
   bool touches_adjoints_in(const vari*, const vari*) const override { return false; }
   bool may_write_device_adjoint(const void* node) const override {
@@ -370,11 +383,10 @@ class dev_to_host_vari : public vari {
     wrote_ = false;
     const host_block b = st->host_blocks_[blk_];
     if (!b.n) return;
-    const vari* lo = b.first;
-    const vari* hi = b.first + b.n;
-    bool touched = b.dirty;
-    for (size_t i = pos_ + 1; !touched && i < st->var_stack_.size(); ++i)
-      touched = st->var_stack_[i]->touches_adjoints_in(lo, hi);
+    // a node chained before this one in the sweep (after it on the tape)
+    // added into the block's host adjoints (grad.hpp log_host_touches), or a
+    // device->host pending adjoint landed in one
+    const bool touched = b.dirty || b.touched_sweep == st->sweep_;
     if (!touched) return;
     wrote_ = true;
     smg_ctx* c = amd::ctx();
@@ -399,31 +411,52 @@ class dev_to_host_vari : public vari {
  * device node's adjoint written into the varis it owns -- what the
  * reference's varis hold after grad(): a symmetric block's shared vari the
  * sum of both elements' adjoints, a Cholesky factor's varis the partials its
- * consumers wrote (a closed-form reverse never formed them: expand_adjoint). */
+ * consumers wrote (a closed-form reverse never formed them: expand_adjoint),
+ * and its strict upper triangle's one dummy vari (cholesky_decompose.hpp:34-48)
+ * the sum of the adjoints device consumers wrote there.  Every block's pack
+ * and copy are queued first and land in ONE synchronisation. */
 inline void publish_block_adjoints(size_t from) {
   auto* st = ChainableStack::instance_;
   if (from >= st->host_blocks_.size() || !amd::has_ctx()) return;
   smg_ctx* c = amd::ctx();
   join_device_adjoints();
-  for (size_t k = from; k < st->host_blocks_.size(); ++k) {
+  const size_t nb = st->host_blocks_.size();
+  std::vector<size_t> off(nb + 1, 0);  // each block's doubles in the staging area (+1: a lower block's upper sum)
+  for (size_t k = from; k < nb; ++k) {
+    const host_block& b = st->host_blocks_[k];
+    off[k + 1] = off[k] + (b.n ? b.n + (b.layout == layout_lower ? 1 : 0) : 0);
+  }
+  if (off[nb] == 0) return;
+  double* stage = static_cast<double*>(smg_host_scratch(c, off[nb] * sizeof(double)));
+  if (!stage) throw std::bad_alloc();
+  for (size_t k = from; k < nb; ++k) {
     const host_block b = st->host_blocks_[k];
     if (!b.n) continue;
     auto* node = static_cast<dev_matrix_vari*>(b.node);
     if (node->sink_) node->sink_->expand_adjoint();
     const double* src = node->adj_;
     const int mode = block_pack_mode(b.layout);
+    const size_t cnt = off[k + 1] - off[k];
     if (mode >= 0) {
-      double* t = amd::alloc_doubles(b.n);
+      double* t = amd::alloc_doubles(cnt);
       amd::check(smg_pack_tril(c, mode, mode == 2 ? int(b.n) : b.rows, node->adj_, b.rows, t), "grad");
+      if (b.layout == layout_lower) amd::check(smg_sum_strict_upper(c, b.rows, node->adj_, b.rows, t + b.n), "grad");
       src = t;
     }
-    double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
-    if (!stage) throw std::bad_alloc();
-    amd::check(smg_memcpy_d2h(c, stage, src, b.n * sizeof(double)), "grad");
-    amd::check(smg_sync(c), "grad");
+    amd::check(smg_memcpy_d2h(c, stage + off[k], src, cnt * sizeof(double)), "grad");
+  }
+  amd::check(smg_sync(c), "grad");
+  for (size_t k = from; k < nb; ++k) {
+    host_block& b = st->host_blocks_[k];
+    if (!b.n) continue;
+    const double* h = stage + off[k];
     host_parallel_for(b.n, [&](size_t s, size_t e) {
-      for (size_t i = s; i < e; ++i) b.first[i].adj_ = stage[i];
+      for (size_t i = s; i < e; ++i) b.first[i].adj_ = h[i];
     });
+    if (b.layout == layout_lower && b.dummy) {  // (host nodes' contributions are already in it)
+      b.dummy->adj_ += h[b.n] - b.dummy_dev;
+      b.dummy_dev = h[b.n];
+    }
   }
 }
 

@@ -65,6 +65,20 @@ struct host_block {
   int layout = 0;
   long base = -1;
   vari* const* base_elems = nullptr;
+  // layout 1: the device's strict-upper adjoint sum already published into
+  // dummy (a later publish adds only what the device gained since)
+  double dummy_dev = 0.0;
+  // the sweep in which a node chained after the block's bridge added into
+  // one of its varis' host adjoints (grad.hpp log_host_touches)
+  size_t touched_sweep = 0;
+};
+/** A node that may add into some matrix node's DEVICE adjoint
+ * (vari::may_write_device_adjoint), with its var_stack_ position: the
+ * writers a structured reverse checks are the entries after its own
+ * position (a binary search), not the whole rest of the tape. */
+struct dev_writer {
+  size_t pos;
+  vari* v;
 };
 
 template <typename ChainableT, typename ChainableAllocT>
@@ -90,6 +104,11 @@ struct AutodiffStackSingleton {
     std::vector<pending_adjoint> pending_;
     std::vector<host_block> host_blocks_;
     std::vector<size_t> nested_host_block_sizes_;
+    std::vector<dev_writer> dev_writers_;  // in stack order (registered at construction)
+    // host_blocks_ indices ordered by address, rebuilt once per sweep that
+    // has blocks (the bisection of log_host_touches), and the sweep it is for
+    std::vector<size_t> block_order_;
+    size_t block_order_sweep_ = 0;
     // reverse sweeps started on this tape (grad()): a structured adjoint a
     // node deposits is valid for the sweep that deposited it only
     size_t sweep_ = 0;

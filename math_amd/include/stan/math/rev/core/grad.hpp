@@ -15,6 +15,7 @@
 #include <stan/math/amd/device.hpp>
 #include <stan/math/rev/core/vari.hpp>
 
+#include <algorithm>
 #include <cstdint>
 #include <typeinfo>
 #include <stdexcept>
@@ -77,6 +78,42 @@ inline void flush_pending(bool status = false) {
   if (armed) amd::throw_if_sync(*st, "grad", "the reverse sweep");
 }
 
+/** Record which host blocks' varis node v (just chained) may have added into
+ * (vari::touches_adjoints_in), stamping them with the sweep: a block's bridge
+ * (amd/matrix.hpp dev_to_host_vari) then knows without rescanning the rest of
+ * the tape whether any node after it touched its varis.  The blocks, ordered
+ * by address, are bisected: O(log B) range queries for a node touching one
+ * block, one query for a node touching none. */
+inline void log_host_touches(vari* v) {
+  auto* st = ChainableStack::instance_;
+  auto& blocks = st->host_blocks_;
+  if (typeid(*v) == typeid(vari)) return;  // (a leaf: its chain() is empty)
+  auto& order = st->block_order_;
+  if (st->block_order_sweep_ != st->sweep_) {
+    order.clear();
+    for (size_t k = 0; k < blocks.size(); ++k)
+      if (blocks[k].n) order.push_back(k);
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return blocks[a].first < blocks[b].first; });
+    st->block_order_sweep_ = st->sweep_;
+  }
+  struct bisect {
+    static void run(vari* v, std::vector<host_block>& blocks, const std::vector<size_t>& order, size_t a, size_t b,
+                    size_t sweep) {
+      const vari* lo = blocks[order[a]].first;
+      const host_block& last = blocks[order[b - 1]];
+      if (!v->touches_adjoints_in(lo, last.first + last.n)) return;
+      if (b - a == 1) {
+        blocks[order[a]].touched_sweep = sweep;
+        return;
+      }
+      const size_t m = a + (b - a) / 2;
+      run(v, blocks, order, a, m, sweep);
+      run(v, blocks, order, m, b, sweep);
+    }
+  };
+  if (!order.empty()) bisect::run(v, blocks, order, 0, order.size(), st->sweep_);
+}
+
 static inline bool empty_nested() {
   return ChainableStack::instance_->nested_var_stack_sizes_.empty();
 }
@@ -112,6 +149,7 @@ static void grad(vari* vi) {
       if (need) flush_pending();
     }
     (*it)->chain();
+    if (!st->host_blocks_.empty()) log_host_touches(*it);
   }
   flush_pending(true);
   if (st->publish_ && st->no_publish_ == 0) st->publish_(empty_nested() ? 0 : st->nested_host_block_sizes_.back());
@@ -143,6 +181,7 @@ static inline void recover_memory_nested() {
     throw std::logic_error("empty_nested() must be false before calling recover_memory_nested()");
   auto* st = ChainableStack::instance_;
   st->var_stack_.resize(st->nested_var_stack_sizes_.back());
+  while (!st->dev_writers_.empty() && st->dev_writers_.back().pos >= st->var_stack_.size()) st->dev_writers_.pop_back();
   st->nested_var_stack_sizes_.pop_back();
   st->var_nochain_stack_.resize(st->nested_var_nochain_stack_sizes_.back());
   st->nested_var_nochain_stack_sizes_.pop_back();
@@ -171,6 +210,7 @@ static inline void recover_memory() {
     throw std::logic_error("empty_nested() must be true before calling recover_memory()");
   auto* st = ChainableStack::instance_;
   st->var_stack_.clear();
+  st->dev_writers_.clear();
   st->var_nochain_stack_.clear();
   for (auto* a : st->var_alloc_stack_) delete a;
   st->var_alloc_stack_.clear();
@@ -189,6 +229,7 @@ static inline void zero_host_blocks(size_t from) {
     host_block& b = blocks[k];
     for (size_t i = 0; i < b.n; ++i) b.first[i].adj_ = 0.0;
     if (b.dummy) b.dummy->adj_ = 0.0;
+    b.dummy_dev = 0.0;
     b.dirty = false;
   }
 }

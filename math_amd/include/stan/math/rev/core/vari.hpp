@@ -94,15 +94,27 @@ class vari {
  * contribution need only land before it when it targets this node. */
 class local_adjoint_vari : public vari {
  public:
-  using vari::vari;
+  explicit local_adjoint_vari(double x) : vari(x) { register_dev_writer(this); }
+  local_adjoint_vari(double x, bool stacked) : vari(x, stacked) {
+    if (stacked) register_dev_writer(this);
+  }
   bool reads_other_adjoints() const override { return false; }
   bool may_write_device_adjoint(const void*) const override { return true; }
+  /** v (just pushed on var_stack_) may write device adjoints: the structured
+   * reverses' writer checks visit it (matrix.hpp others_write_device_adjoint) */
+  static void register_dev_writer(vari* v) {
+    auto* st = ChainableStack::instance_;
+    st->dev_writers_.push_back({st->var_stack_.size() - 1, v});
+  }
 };
 
 /** A library node whose chain() writes host adjoints only. */
 class host_local_vari : public local_adjoint_vari {
  public:
-  using local_adjoint_vari::local_adjoint_vari;
+  explicit host_local_vari(double x) : local_adjoint_vari(x) { ChainableStack::instance_->dev_writers_.pop_back(); }
+  host_local_vari(double x, bool stacked) : local_adjoint_vari(x, stacked) {
+    if (stacked) ChainableStack::instance_->dev_writers_.pop_back();
+  }
   bool may_write_device_adjoint(const void*) const override { return false; }
 };
 

@@ -152,6 +152,15 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   double exp_adj_ = 0.0;
   int exp_k_ = 1;
   size_t exp_sweep_ = 0;
+  // a consumer's W = L^{-1} and W^T (provide_inverse): the dense reverse in
+  // closed form on them instead of Murray's blocked algorithm
+  const double* inv_W_ = nullptr;
+  const double* inv_Wt_ = nullptr;
+
+  void provide_inverse(const double* W, const double* Wt) override {
+    inv_W_ = W;
+    inv_Wt_ = Wt;
+  }
 
   // the deposited partials written densely into L's adjoint (what the MVN
   // would have written: one smg_mvn_cholesky_rev per observation)
@@ -303,6 +312,16 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       expand(dep_ws_, dep_adj_, dep_k_);
     }
     if (!deposit) record(false);
+    static const bool inv_ok = [] {  // TEMP A/B (round 5)
+      const char* e = std::getenv("SMG_CHOL_REV_INV");
+      return !(e && e[0] == '0');
+    }();
+    if (inv_W_ && inv_ok) {  // Abar (lower) += tril(G + G^T) - diag(G), G = W^T Phi(L^T tril(Lbar)) W
+      double* ws = amd::alloc_doubles(2 * nn);
+      amd::check(smg_cholesky_rev_inverse(c, L_->val_, n_, inv_W_, inv_Wt_, n_, L_->adj_, n_, n_, A_->adj_, n_, ws),
+                 "cholesky_decompose");
+      return;
+    }
     // Murray's algorithm overwrites its input and reads only its lower triangle
     double* work = amd::alloc_doubles(nn);
     amd::check(smg_copy_tril(c, n_, n_, L_->adj_, n_, work, n_), "cholesky_decompose");
@@ -412,10 +431,10 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
                                                     packed, stage, 0),
                fn);
     fill_block_pointers(b, host_out);  // addresses only: while the first panel factors
-    const int nb2 = (n + panels - 1) / panels;
     for (int p = 0; p < panels; ++p) {
-      const size_t J = size_t(p) * nb2, K = std::min(size_t(n), J + nb2);
-      const size_t o0 = J * n - J * (J - 1) / 2, o1 = K * n - K * (K - 1) / 2;
+      int j0 = 0, j1 = 0;  // (the library's own panel bounds: what marker p covers)
+      amd::check(smg_cholesky_stream_panel_cols(n, p, &j0, &j1), fn);
+      const size_t o0 = tril_off(size_t(n), size_t(j0)), o1 = tril_off(size_t(n), size_t(j1));
       amd::check(smg_marker_wait(c, p), fn);
       host_parallel_for(o1 - o0, [&](size_t s0, size_t s1) {
         for (size_t i = o0 + s0; i < o0 + s1; ++i) ::new (static_cast<void*>(b.first + i)) vari(stage[i], vari::unstacked_tag{});

@@ -88,6 +88,10 @@ inline void map_rect_throw(const map_rect_check& c) {
       {"Size of one of the arrays of the job specific real data", "size of another array of the job specifc real data"},
       {"Size of one of the arrays of the job specific int data", "size of another array of the job specifc int data"}};
   if (c.code > 0 && c.code < 6) map_rect_size_match(what[c.code][0], c.a, what[c.code][1], c.b);
+  if (c.code == 6)
+    throw std::invalid_argument(
+        "map_rect: every rank must pass the same number of jobs, and a call_id's number of jobs must not change "
+        "between calls");
 }
 
 /** The checks; data_elsewhere: this rank left the job data to the root. */
@@ -269,7 +273,14 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
                                                   const map_rect_data& data, std::ostream* msgs, Eigen::Index rows,
                                                   const map_rect_check& chk) {
   const int W = amd::world_size(), rank = amd::world_rank();
-  const size_t J = job_params.size();
+  // the call_id's job count (equal on every rank: map_rect_fill_cache checks
+  // it), so that every rank's exchanges have the same size even when this
+  // rank was passed a different number of jobs -- that is reported in the
+  // first exchange and every rank throws together, instead of the others
+  // waiting in it
+  const size_t J = data.J;
+  map_rect_check c = chk;
+  if (!c.code && job_params.size() != J) c = {6, job_params.size(), J};
   const std::vector<int> chunks = map_rect_chunks(J, W);
   int first = 0, maxc = 0;
   for (int r = 0; r < W; ++r) {
@@ -278,7 +289,7 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
   }
   const int mine = chunks[size_t(rank)];
   std::vector<Eigen::MatrixXd> local(static_cast<size_t>(mine));
-  double ok = chk.code ? 0.0 : 1.0;  // (a failed check: nothing evaluated)
+  double ok = c.code ? 0.0 : 1.0;  // (a failed check: nothing evaluated)
   try {
     for (int i = 0; ok != 0.0 && i < mine; ++i) {
       const size_t j = size_t(first + i);
@@ -298,9 +309,9 @@ std::vector<Eigen::MatrixXd> map_rect_distributed(const Eigen::VectorXd& shared_
   const long long hn = 4 + maxc;
   std::vector<double> hdr(size_t(hn), 0.0), all_hdr(size_t(hn) * W);
   hdr[0] = ok;
-  hdr[1] = double(chk.code);
-  hdr[2] = double(chk.a);
-  hdr[3] = double(chk.b);
+  hdr[1] = double(c.code);
+  hdr[2] = double(c.a);
+  hdr[3] = double(c.b);
   if (ok != 0.0)
     for (int i = 0; i < mine; ++i) hdr[size_t(4 + i)] = double(local[size_t(i)].cols());
   amd::allgather(hdr.data(), hn, all_hdr.data());
@@ -362,18 +373,21 @@ map_rect(const Eigen::Matrix<T_shared, Eigen::Dynamic, 1>& shared_params,
   const bool dist = amd::distributed();
   const bool data_elsewhere = dist && amd::world_rank() != 0 && x_r.empty() && x_i.empty();
   const internal::map_rect_check chk = internal::map_rect_checks(job_params, x_r, x_i, data_elsewhere);
-  if (!dist || J == 0) internal::map_rect_throw(chk);  // (no exchange follows: throw here)
-  if (J == 0) return result_t();
+  if (!dist) internal::map_rect_throw(chk);  // (no exchange follows: throw here)
+  if (!dist && J == 0) return result_t();
 
   const Eigen::VectorXd shared_d = internal::map_rect_values(shared_params);
   std::vector<Eigen::MatrixXd> outs(J);
   if (dist) {
-    const Eigen::Index rows = 1 + (SV ? shared_params.size() : 0) + (JV ? job_params[0].size() : 0);
+    // every rank enters the exchanges, J == 0 included: a rank returning
+    // early would leave the others waiting in them
     internal::map_rect_data& data = internal::map_rect_cache<call_id>();
     if (!data.valid) internal::map_rect_fill_cache(data, J, x_r, x_i, chk);
-    if (data.J != J || data.world != amd::world_size())
+    if (data.world != amd::world_size())
       throw std::invalid_argument("map_rect: the number of jobs of a call_id must not change between calls");
+    const Eigen::Index rows = 1 + (SV ? shared_params.size() : 0) + (JV && J ? job_params[0].size() : 0);
     outs = internal::map_rect_distributed<F, SV, JV>(shared_d, job_params, data, msgs, rows, chk);
+    if (J == 0) return result_t();
   } else {
     for (size_t j = 0; j < J; ++j) {
       const Eigen::VectorXd job_d = internal::map_rect_values(job_params[j]);

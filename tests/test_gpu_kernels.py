@@ -428,6 +428,48 @@ def test_mvn_inverse_from_progressive_factorisation(ctx):
     near_rel(ctx.get(lp1, 1), ctx.get(lp0, 1), 1e-12, what="lp")
 
 
+@pytest.mark.parametrize("N", [64, 300, 1024, 2048])
+def test_cholesky_rev_inverse_vs_murray(ctx, N):
+    """smg_cholesky_rev_inverse (the closed form on W = L^{-1}: Abar lower +=
+    tril(G + G^T) - diag(G), G = W^T Phi(L^T tril(Lbar)) W) against the blocked
+    Murray reverse smg_cholesky_rev on the same factor and adjoint (1e-10,
+    the lower triangle; the strict upper of Lbar carries junk both ignore)."""
+    rng = np.random.default_rng(N + 5)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + 0.5 * np.eye(N)
+    A = 0.5 * (A + A.T)
+    dA, dL, dD = ctx.put(F(A)), ctx.zeros(N * N), ctx.zeros(ctx.lib.smg_cholesky_aux_doubles(N))
+    ctx.call("smg_cholesky_fwd", dA, N, N, dL, N, dD)
+    L = ctx.get(dL, N * N).reshape(N, N).T
+    W = np.tril(np.linalg.inv(np.tril(L)))
+    Lbar = rng.uniform(-1, 1, (N, N))
+    G0 = rng.uniform(-1, 1, (N, N))
+    # Murray (the reference's algorithm): overwrites its adjoint input
+    dLa, dG = ctx.put(F(Lbar)), ctx.put(F(G0))
+    ctx.call("smg_cholesky_rev", dL, N, dD, dLa, N, N, dG, N)
+    Gm = ctx.get(dG, N * N).reshape(N, N).T
+    dG2 = ctx.put(F(G0))
+    ctx.call("smg_cholesky_rev_inverse", dL, N, ctx.put(F(W)), ctx.put(F(W.T)), N, ctx.put(F(Lbar)), N, N, dG2, N,
+             ctx.zeros(2 * N * N))
+    Gi = ctx.get(dG2, N * N).reshape(N, N).T
+    low = np.tril(np.ones((N, N), bool))
+    ref = Gm[low] - G0[low]
+    near_rel(Gi[low] - G0[low], ref, 1e-10, atol=1e-10 * np.abs(ref).max(), what="Abar")
+    assert np.array_equal(Gi[~low], G0[~low])
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 300, 2049])
+def test_sum_strict_upper(ctx, n):
+    """smg_sum_strict_upper: the sum a Cholesky factor's dummy vari collects
+    from the strict upper triangle (fixed order; 1e-13 against numpy)."""
+    rng = np.random.default_rng(n)
+    A = rng.uniform(-1, 1, (n, n))
+    out = ctx.zeros(1)
+    ctx.call("smg_sum_strict_upper", n, ctx.put(F(A)), n, out)
+    ref = np.triu(A, 1).sum()
+    assert abs(ctx.get(out, 1)[0] - ref) <= 1e-13 * max(1.0, np.abs(np.triu(A, 1)).sum())
+
+
 @pytest.mark.parametrize("N,D,k", [(64, 1, 1), (301, 1, 1), (512, 3, 1), (1024, 1, 2), (257, 2, 3)])
 def test_gp_inverse_adjoint_vs_composition(ctx, N, D, k):
     """smg_gp_inverse_adjoint (the GP marginal's three reverses in one pass

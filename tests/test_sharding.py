@@ -387,6 +387,49 @@ def test_map_rect_argument_checks_agree_gloo(tmp_path):
         assert ranks[r]["good"][1] == ranks[r]["after"][1]
 
 
+def _maprect_jobcount_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(send, count, recv, _user):
+        t = torch.from_numpy(np.ctypeslib.as_array(send, shape=(count,)).copy())
+        parts = [torch.empty(count, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, t)
+        np.ctypeslib.as_array(recv, shape=(count * world,))[:] = torch.cat(parts).numpy()
+
+    cb = _AG(allgather)
+    lib = _maprect_lib()
+    xr, xi, th = gen.maprect_inputs(7)
+    short = (xr[:0], xi[:0], th[:2])  # rank 1 passes no jobs at all
+    res = {}
+    # (a) the first call of the call_id: the cache's size exchange sees the counts
+    res["fill"] = _maprect_ex(lib, world, rank, cb, _SC(), *(short if rank == 1 else (xr, xi, th)), 0, 1, 0)
+    # (b) a cached call_id: the status exchange carries it (sized by the cached count on every rank)
+    res["good"] = _maprect_ex(lib, world, rank, cb, _SC(), xr, xi, th, 0, 1, 0)
+    res["cached"] = _maprect_ex(lib, world, rank, cb, _SC(), *(short if rank == 1 else (xr, xi, th)), 0, 0, 0)
+    res["after"] = _maprect_ex(lib, world, rank, cb, _SC(), xr, xi, th, 0, 0, 0)
+    np.save(out + f".{rank}.npy", np.array(res, dtype=object), allow_pickle=True)
+    dist.destroy_process_group()
+
+
+def test_map_rect_job_count_mismatch_throws_on_every_rank_gloo(tmp_path):
+    """Rank 1 passes J = 0 jobs, rank 0 J = 7: every rank throws the same
+    invalid_argument -- on the first call of the call_id and on a cached one --
+    instead of rank 1 returning early while rank 0 waits in a collective;
+    good calls before and after agree."""
+    out = str(tmp_path / "jc")
+    _spawn(_maprect_jobcount_rank, 2, out)
+    ranks = [np.load(out + f".{r}.npy", allow_pickle=True).item() for r in range(2)]
+    for r in range(2):
+        rc, _, _, _, err = ranks[r]["fill"]
+        assert rc == 2 and err == "map_rect: every rank must pass the same number of jobs", (r, err)
+        rc, _, _, _, err = ranks[r]["cached"]
+        assert rc == 2 and err.startswith("map_rect: every rank must pass the same number of jobs"), (r, err)
+        for key in ("good", "after"):
+            assert ranks[r][key][0] == 0, (r, key, ranks[r][key][4])
+        assert ranks[r]["good"][1] == ranks[r]["after"][1]
+
+
 # ---------------------------------------------------------------- product GLM reducers, W = 2
 GLMDIST_LIB = os.path.join(ROOT, "tests", "cpp", "_bin", "libglm_dist.so")
 _AR = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.c_longlong, ctypes.c_void_p)
