@@ -288,7 +288,7 @@ class GPEigen(GP):
         return c
 
     def extra(self, timed, steps):
-        ph = np.zeros(8)
+        ph = np.zeros(32)
         self.bl.smg_bench_gp_eigen_phases.argtypes = [D, D]
         best = None
         for _ in range(3):
@@ -303,6 +303,13 @@ class GPEigen(GP):
                                    "recover": best[2] * 1e3, "gradient_call": best[3] * 1e3,
                                    "forward_K": best[4] * 1e3, "forward_Kd": best[5] * 1e3,
                                    "forward_L": best[6] * 1e3, "forward_mvn": best[7] * 1e3,
+                                   "forward_L_timeline_ms": {
+                                       "out_allocated": best[26] * 1e3, "input_recognised": best[27] * 1e3,
+                                       "staging_ready": best[28] * 1e3,
+                                       "enqueued": best[8] * 1e3, "pointers_filled": best[9] * 1e3,
+                                       "panels_arrived": [round(t * 1e3, 4) for t in best[10:26:2] if t > 0],
+                                       "panels_built": [round(t * 1e3, 4) for t in best[11:26:2] if t > 0],
+                                       "status_read": best[31] * 1e3},
                                    "note": "one evaluation split by hand (functor forward incl. three crossings; "
                                            "a top-level grad() to a device sync, which also publishes the "
                                            "intermediate blocks' adjoints into their varis; recover_memory), best "

@@ -164,7 +164,12 @@ int smg_bench_gp_eigen_step(const double* theta, double* fx, double* grad) {
  * top-level grad() (with the host blocks' adjoints published), out[2]
  * recover_memory, out[3] the whole evaluation (gradient()), out[4..7] the
  * forward's statements: K = gp_exp_quad_cov, Kd = add_diag, L =
- * cholesky_decompose, the MVN. */
+ * cholesky_decompose, the MVN; out[8..31] the L statement's host timeline
+ * from its start (amd::phase_mark: 0 the factorisation enqueued, 1 the
+ * pointer array filled, 2 + 2p / 3 + 2p panel p's values arrived / its varis
+ * built, 18 the output matrix allocated, 19 the input recognised, 20 the
+ * host staging buffer ready, 30 the status read; 0 where a point was not
+ * reached). */
 int smg_bench_gp_eigen_phases(const double* theta, double* out) {
   try {
     using namespace stan::math;
@@ -199,8 +204,17 @@ int smg_bench_gp_eigen_phases(const double* theta, double* out) {
       auto s1 = now();
       Eigen::Matrix<var, -1, -1> Kd = add_diag(K, square(tv2(2)));
       auto s2 = now();
+      amd::phase_log_t& pl = amd::phase_log();
+      for (double& t : pl.t) t = 0.0;
+      pl.on = true;
       Eigen::Matrix<var, -1, -1> L = cholesky_decompose(Kd);
+      pl.on = false;
       auto s3 = now();
+      const double base = std::chrono::duration<double>(s2.time_since_epoch()).count();
+      for (int k = 0; k < 24; ++k) {
+        const int src = k < 23 ? k : 30;
+        out[8 + k] = src >= 0 && pl.t[src] > 0 ? pl.t[src] - base : 0.0;
+      }
       Eigen::VectorXd mu = Eigen::VectorXd::Zero(g_n);
       var lp = multi_normal_cholesky_lpdf(g_yh, mu, L);
       auto s4 = now();

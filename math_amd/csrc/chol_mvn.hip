@@ -303,8 +303,14 @@ __global__ __launch_bounds__(256) void k_add_lower_sym(const double* __restrict_
   }
 }
 
-__global__ void k_scale_diag(double* __restrict__ P, int ldp, int n, double f) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) P[i + (size_t)i * ldp] *= f;
+// P = Phi(P) in place over a lower-output product: the diagonal halved, the
+// strict upper (never written by the product: stale workspace) zeroed, since
+// the next product's triangular K cut still reads whole diagonal tiles
+__global__ void k_phi_upper(double* __restrict__ P, int ldp, int n) {
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    double* c = P + (size_t)j * ldp;
+    for (int i = threadIdx.x; i <= j; i += blockDim.x) c[i] = i == j ? 0.5 * c[i] : 0.0;
+  }
 }
 
 inline int grid_for(long long tot) {
@@ -344,24 +350,32 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int 
 }  // namespace
 
 // K^{-1} formed progressively during the factorisation (cholesky.hip
-// chol_fwd), one 512-row block row k of W = L^{-1} at a time, on the side
-// stream once panel k is final:
-//   W_kk = L_kk^{-1}                       (the block inverses of rows k P.., P = 512)
-//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}   (Y_k formed one panel earlier)
-//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k     (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
-//   Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}  (needs only panels <= k)
-// so that after the last panel only its own block row remains (its inverse,
-// -W_77 Y_7 and one rank-512 update) instead of V22, V12 and all of V V^T.
-// Each block row is four parts (W_kk; W_{k,0:k}; its K^{-1} share; Y_{k+1}),
-// queued by chol_fwd in budgets that fit beside the trailing updates.
-// ws: [W (n x n, ld n) | C (n x n, lower) | Y (P x n, ld P) | T (P/2 x 256)];
-// W's strict upper is never read outside its diagonal blocks (the triangular
-// K cuts stay inside a tile band), whose copies from aux carry stored zeros.
+// chol_fwd), one 512-row block row k of W = L^{-1} at a time, once panel k is
+// final:
+//   W_kk = L_kk^{-1}                        (the block inverses of rows k P.., P = 512)
+//   W_{k,0:k} = -W_kk Y_k,  Y_k = L_{k,0:k} W_{0:k,0:k}
+//   C(0:(k+1)P, 0:(k+1)P) += W_k^T W_k      (C = K^{-1} = W^T W = sum_k W_k^T W_k, lower)
+// Y is accumulated right-looking, like the factorisation's trailing updates:
+// once W_k is formed, its contribution L_{r,k} W_{k,0:k+1} is added to every
+// later row's Y_r -- the next row's (r = k + 1, small: on the latency chain)
+// and the rest (r >= k + 2, the bulk: off it) as separate parts -- so that
+// after the last panel only its own block row remains (its inverse, -W_77 Y_7
+// and one rank-512 share), instead of forming Y_7 = L_{7,0:7} W_{0:7,0:7}
+// (6.6 GFLOP at n = 4096) there.
+// Parts of block row k: 0 W_kk; 1 W_{k,0:k}; 2 its K^{-1} share; 3 Y_{k+1} +=
+// L_{k+1,k} W_k; 4 Y_{k+2:} += L_{k+2:,k} W_k (part 1 of row r needs parts 3
+// of row r - 1 and 4 of rows <= r - 2).
+// ws: [W (n x n, ld n) | C (n x n, lower) | Y (n x n, ld n; block row r's
+// columns 0 .. r P) | T (P/2 x 256)]; W's strict upper is never read outside
+// its diagonal blocks (the triangular K cuts stay inside a tile band), whose
+// copies from aux carry stored zeros.
 bool smg_inv_prog_ok(int n) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR; }
 
 int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
   const size_t nn = (size_t)n * n;
-  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, nn * sizeof(double), ctx->stream));  // C accumulates
+  // C and Y accumulate (Y's column block k of row r first receives row k's
+  // contribution, after the earlier ones: one zeroing instead of a beta split)
+  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, 2 * nn * sizeof(double), ctx->stream));
   return SMG_OK;
 }
 
@@ -372,7 +386,7 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
   double* W = ws;
   double* C = ws + nn;
   double* Y = C + nn;
-  double* T = Y + (size_t)P * n;
+  double* T = Y + nn;
   const int r0 = k * P, r1 = r0 + P;
   const double* Wkk = aux + (size_t)n * SMG_AUX_W512 + r0;  // ld n, stored zeros above
   int rc;
@@ -387,12 +401,16 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
       return SMG_OK;
     case 1:  // W_{k,0:k} = -W_kk Y_k
       if (k == 0) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y, P, 0.0, W + r0, n, SMG_TRI_A_LOWER);
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y + r0, n, 0.0, W + r0, n, SMG_TRI_A_LOWER);
     case 2:  // C (lower, leading r1 x r1) += W_k^T W_k
       return smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n);
-    default:  // Y_{k+1} = L_{k+1,0:k+1} W_{0:k+1,0:k+1}
+    case 3:  // Y_{k+1}[:, 0:r1] (+)= L_{k+1,k} W_{k,0:r1}
       if (r1 >= n) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, r1, 1.0, L + r1, ldl, W, n, 0.0, Y, P, SMG_TRI_B_LOWER);
+      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, P, 1.0, L + r1 + (size_t)r0 * ldl, ldl, W + r0, n, 1.0, Y + r1, n);
+    default:  // Y_{k+2:}[:, 0:r1] (+)= L_{k+2:,k} W_{k,0:r1}
+      if (r1 + P >= n) return SMG_OK;
+      return smg_gemm_impl(ctx, 0, 0, 0, n - r1 - P, r1, P, 1.0, L + r1 + P + (size_t)r0 * ldl, ldl, W + r0, n, 1.0,
+                           Y + r1 + P, n);
   }
 }
 
@@ -406,14 +424,15 @@ double smg_inv_prog_cost(int n, int k, int part, bool inverses_here) {
     case 0: return inverses_here ? 60.0 : 6.0;
     case 1: return k == 0 ? 0.0 : 6.0 + P * r0 * P / rate;
     case 2: return 6.0 + r1 * r1 * P / rate;
-    default: return r1 >= n ? 0.0 : 6.0 + P * r1 * r1 / rate;
+    case 3: return r1 >= n ? 0.0 : 6.0 + 2.0 * P * r1 * P / rate;
+    default: return r1 + P >= n ? 0.0 : 6.0 + 2.0 * (n - r1 - P) * r1 * P / rate;
   }
 }
 
 extern "C" {
 
 size_t smg_cholesky_mvn_rev_ws_doubles(int n) {
-  return n > 0 ? 2 * (size_t)n * n + (size_t)SMG_NBR * n + SMG_NBR / 2 * 256 : 0;
+  return n > 0 ? 3 * (size_t)n * n + SMG_NBR / 2 * 256 : 0;
 }
 
 int smg_cholesky_mvn_rev(smg_ctx* ctx, const double* L, int ldl, const double* aux, int n, const double* s, int k,
@@ -465,8 +484,7 @@ int smg_cholesky_rev_inverse(smg_ctx* ctx, const double* L, int ldl, const doubl
   // P = Phi(L^T T) (lower): op(A) = L^T upper, op(B) = T lower
   if ((rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, T, n, 0.0, P, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
     return rc;
-  hipLaunchKernelGGL(k_scale_diag, dim3(smg_ceil_div(n, 256) < 64 ? smg_ceil_div(n, 256) : 64), dim3(256), 0,
-                     ctx->stream, P, n, n, 0.5);
+  hipLaunchKernelGGL(k_phi_upper, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, P, n, n);
   SMG_LAUNCH_CHECK();
   // T = P W (lower x lower: lower; T's strict upper keeps tril's zeros)
   if ((rc = smg_gemm_impl(ctx, 0, 0, 1, n, n, n, 1.0, P, n, W, ldw, 0.0, T, n, SMG_TRI_A_LOWER | SMG_TRI_B_LOWER)))

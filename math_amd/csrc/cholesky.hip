@@ -336,6 +336,7 @@ __device__ __noinline__ void below_update(lds_dbl* Z, const lds_dbl* D, const ld
   lds_mma32_8w<lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
 }
 #define CHAIN_SYRK(Zn, Y, b) chain_syrk((lds_dbl*)(Zn), (const lds_dbl*)(Y), (b))
+
 #define OWNER_UPDATE(Z, D, B) owner_update((lds_dbl*)(Z), (const lds_dbl*)(D), (const lds_dbl*)(B))
 #define BELOW_LTJ(Y, X) below_ltj((lds_dbl*)(Y), (const lds_dbl*)(X))
 #define BELOW_TRSM(Y, D, X) below_trsm((lds_dbl*)(Y), (const lds_dbl*)(D), (const lds_dbl*)(X))
@@ -362,16 +363,16 @@ __device__ inline void panel_gload(panel_regs& Rg, const double* A, int ld, int 
     Rg.ok |= (r < rows && c < cols && (!lower || r >= c)) ? (1u << q) : 0u;
   }
 }
-template <int R = 64>
-__device__ inline void panel_lstore(double* D, const panel_regs& Rg) {
+template <int R = 64, typename P = double*>
+__device__ inline void panel_lstore(P D, const panel_regs& Rg) {
 #pragma unroll
   for (int q = 0; q < R / 8; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
     D[(e % R) * SMG_NBP + e / R] = ((Rg.ok >> q) & 1u) ? Rg.v[q] : 0.0;
   }
 }
-template <int R = 64>
-__device__ inline void panel_gstore(const double* D, double* A, int ld, int rows, int cols,
+template <int R = 64, typename CP = const double*>
+__device__ inline void panel_gstore(CP D, double* A, int ld, int rows, int cols,
                                     bool lower) {
 #pragma unroll
   for (int q = 0; q < R / 8; ++q) {
@@ -396,7 +397,8 @@ __device__ inline void panel_gload_leaves(panel_leaves& Rg, const double* G, int
     Rg.v[q] = (i < b && j < b) ? v : (i == j ? 1.0 : 0.0);
   }
 }
-__device__ inline void panel_lstore_leaves(double* Y, const panel_leaves& Rg) {
+template <typename P = double*>
+__device__ inline void panel_lstore_leaves(P Y, const panel_leaves& Rg) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
@@ -407,7 +409,8 @@ __device__ inline void panel_lstore_leaves(double* Y, const panel_leaves& Rg) {
 
 // a b x b lower triangle (loaded with lower = true) into LDS with identity
 // padding beyond b: the factor's leaf inverses stay finite
-__device__ inline void panel_lstore_id(double* D, const panel_regs& R, int b) {
+template <typename P = double*>
+__device__ inline void panel_lstore_id(P D, const panel_regs& R, int b) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = threadIdx.x + SMG_DIAG_THREADS * q;
@@ -439,9 +442,98 @@ __device__ __forceinline__ bool panel_helped(int t, int c, int nb, int nh) {
   return t < nb && t >= 3 && t - 3 < nh && (c & 1) && c <= t - 2;
 }
 
+// A workgroup whose only tile t (>= nb) lies below the panel: every step of
+// that tile with its column blocks held in registers for the whole panel (the
+// accumulator layout of lds_mma32_8w: 4 doubles per lane per 32 x 64 block),
+// loaded once; each step's update A_tc -= L_tj L_cj^T is subtracted from them
+// in place, and block j goes out once, as L_tj -- instead of every later block
+// being loaded and stored again at every step (the kernel fetched 2.6x and
+// wrote 2.1x its algorithmic bytes).  Out of line, with the LDS products
+// inlined: its own register budget (the resident blocks live across the steps).
+__device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int n, int J, int K,
+                                            double* __restrict__ Dinv, int ldd, int* flags, int epoch, int* status,
+                                            int nb, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y) {
+  constexpr int S = PANEL_MAX_STEPS;
+  constexpr int R = PANEL_BELOW_ROWS;
+  static_assert(R == 32, "the resident layout is lds_mma32_8w's");
+  int* diag = flags;
+  int* row = flags + S;
+  int* dinvf = flags + S + 3 * S * S;
+  const int rt0 = J + SMG_NB * nb + R * (t - nb), rt = min(R, n - rt0);
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ar = 16 * (w & 1) + (l >> 4), ac = 16 * (w >> 1) + (l & 15);  // + 4 q: this lane's rows
+  double Rres[S][4];
+#pragma unroll
+  for (int c = 0; c < S; ++c) {  // the whole tile (final: rows are independent), once
+    const int cc = J + SMG_NB * c, bc = min(SMG_NB, K - cc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = ar + 4 * q;
+      const bool in = c < nb && r < rt && ac < bc;
+      const int col = c < nb ? cc + min(ac, bc - 1) : J;  // (clamped in range: loads are unconditional)
+      const double v = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
+      Rres[c][q] = in ? v : 0.0;
+    }
+  }
+  for (int j = 0; j < nb; ++j) {
+    const int cj = J + SMG_NB * j;
+    const int bj = min(SMG_NB, K - cj);
+    __syncthreads();  // LDS of the previous step fully consumed
+    PANEL_EV((j << 16) | (t << 8) | 5);
+#pragma unroll
+    for (int c = 0; c < S; ++c)  // block j into D (its current A_tj)
+      if (c == j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) D[(ar + 4 * q) * SMG_NBP + ac] = Rres[c][q];
+    panel_regs Rd;
+    if (j + 1 < nb) {
+      panel_wait(&dinvf[j], epoch, status);
+      PANEL_EV((j << 16) | (t << 8) | 6);
+      panel_gload(Rd, Dinv + cj, ldd, bj, bj, true);
+      panel_lstore(X, Rd);
+      __syncthreads();
+      lds_mma32_8w<lds_dbl*, const lds_dbl*>(D, D, X);  // L_tj = A_tj Dinv_j^T
+    } else {  // the last step: solve against L_jj (the chain's end, not the inverter's, bounds it)
+      panel_wait(&diag[j], epoch, status);
+      PANEL_EV((j << 16) | (t << 8) | 6);
+      panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
+      panel_leaves Rv;
+      panel_gload_leaves(Rv, Dinv + cj, ldd, bj);  // the chain's leaf inverses
+      panel_lstore_id(X, Rd, bj);
+      panel_lstore_leaves(Y, Rv);
+      __syncthreads();
+      lds_trsm64_rt(D, (const lds_dbl*)X, (const lds_dbl*)Y, R / 16);
+      __syncthreads();
+    }
+    panel_gstore<R>((const lds_dbl*)D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+    PANEL_EV((j << 16) | (t << 8) | 7);
+    if (j + 1 >= nb) break;
+    panel_wait_all(row + j * S, j + 1, nb - 1, 1, epoch, status);
+    panel_regs Ryn;
+    auto issue = [&](int c) {
+      const int cc = J + SMG_NB * c;
+      panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
+    };
+    issue(j + 1);
+    for (int c = j + 1; c < nb; ++c) {
+      __syncthreads();  // previous product's Y consumed
+      panel_lstore(Y, Ryn);
+      __syncthreads();
+      if (c + 1 < nb) issue(c + 1);  // in flight during this product
+      const d4 acc = lds_mma32_8w_acc((const lds_dbl*)D, (const lds_dbl*)Y);  // this wave's tile of L_tj L_cj^T
+#pragma unroll
+      for (int cr = 0; cr < S; ++cr)
+        if (cr == c)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Rres[cr][q] -= acc[q];
+      PANEL_EV((j << 16) | (t << 8) | (16 + c));
+    }
+  }
+}
+
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status, int gown) {
+                                                    int* flags, int epoch, int* status, int gown, int resident_ok) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -616,7 +708,19 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // the other workgroups: tiles t >= 1, owner(t) = 2 + (t - 1) mod (gown - 2);
   // every step of tile t.  At step t - 1 of a panel tile (t < nb) the owner
   // only computes, stores and publishes L_{t,t-1}: the chain applies the
-  // A_tt update privately
+  // A_tt update privately.
+  // A workgroup whose only tile is one below the panel keeps that tile's
+  // column blocks in registers for the whole panel (the accumulator layout of
+  // lds_mma32_8w: 4 doubles per lane per 32 x 64 block): loaded once, each
+  // step's update A_tc -= L_tj L_cj^T subtracted from the MFMA accumulator in
+  // place, and block j written out once, as L_tj -- instead of loading and
+  // storing every later block at every step (the kernel fetched 2.6x and
+  // wrote 2.1x its algorithmic bytes)
+  if (resident_ok && blockIdx.x - 1 >= nb && blockIdx.x - 1 + (gown - 2) >= T) {
+    below_resident(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb, blockIdx.x - 1, (lds_dbl*)D, (lds_dbl*)X,
+                   (lds_dbl*)Y);
+    return;
+  }
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
@@ -1334,8 +1438,12 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
         const double m = n - J, b = K - J;
         ctx->prof_flops[SMG_FAM_PANEL] += m * b * b - 2.0 * b * b * b / 3.0;
       }
+      static const int resident_ok = [] {  // TEMP A/B (round 5): SMG_PANEL_RESIDENT=0 keeps the reloading form
+        const char* e = getenv("SMG_PANEL_RESIDENT");
+        return e && e[0] == '0' ? 0 : 1;
+      }();
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, resident_ok);
     }
     if (zero_parts && J / NB2 < rows_prog) {  // this panel is final: its block row's inverses may start
       if (!(pe_ev[J / NB2] = smg_event(ctx, nev++))) return SMG_ERR_HIP;

@@ -105,23 +105,9 @@ double* smg_ws(smg_ctx* ctx, int id, size_t doubles) {
   return ctx->ws[id];
 }
 
-// TEMP A/B (round 5): SMG_STREAM_PRIO=1 creates the side stream (trailing
-// updates, K^{-1} shares) at the least and the zeroing stream (the block rows'
-// latency chain) at the greatest priority
-static hipError_t create_aux_stream(hipStream_t* s, bool high) {
-  static const bool prio = [] {
-    const char* e = getenv("SMG_STREAM_PRIO");
-    return e && e[0] == '1';
-  }();
-  if (!prio) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-  int least = 0, greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, high ? greatest : least);
-}
-
 int smg_side_begin(smg_ctx* ctx) {
   if (ctx->side) return SMG_OK;
-  if (create_aux_stream(&ctx->side, false) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
     ctx->side = nullptr;
     ctx->host_status |= SMG_ERR_HIP;
     return SMG_ERR_HIP;
@@ -485,7 +471,7 @@ int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
 
 int smg_zero_stream_begin(smg_ctx* ctx) {
   if (ctx->zero_stream) return SMG_OK;
-  if (create_aux_stream(&ctx->zero_stream, true) != hipSuccess ||
+  if (hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->zero_ev_main, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->zero_ev_done, hipEventDisableTiming) != hipSuccess) {
     hipGetLastError();

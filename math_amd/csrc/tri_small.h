@@ -126,6 +126,24 @@ __device__ inline void lds_mma32_8w(P C, CP A, CP B, double alpha = 1.0, double 
   __syncthreads();
 }
 
+// This wave's 16 x 16 tile of the 32 x 64 product A B^T (A: 32 x 64, B:
+// 64 x 64 in LDS), returned in the accumulator layout lds_mma32_8w stores:
+// lane l of wave w holds rows 16 (w & 1) + (l >> 4) + 4 r, column
+// 16 (w >> 1) + (l & 15).  No barrier: the caller owns the ordering.
+template <typename CP>
+__device__ inline d4 lds_mma32_8w_acc(CP A, CP B) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = l & 15, fk = l >> 4;
+  const int i = 16 * (w & 1) + fr, j = 16 * (w >> 1) + fr;
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < SMG_NB; k0 += 4) {
+    const int kk = k0 + fk;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[i * SMG_NBP + kk], B[j * SMG_NBP + kk], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
 // The panel chain's next diagonal block: C = C - A A^T (A, C: 64 x 64 in
 // LDS), written straight in the factorisation's input form -- lower triangle,
 // zero strict upper, identity padding beyond row / column b -- so no separate

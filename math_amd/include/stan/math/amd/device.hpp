@@ -15,6 +15,7 @@
 // std::invalid_argument for size mismatches; std::bad_alloc for OOM;
 // std::runtime_error for HIP failures).
 
+#include <chrono>
 #include <smg_hip.h>
 
 #include <cmath>
@@ -202,6 +203,23 @@ inline void to_host(double* dst, const double* src, size_t n) {
   check(smg_sync(c), "to_host");
   if (armed) throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
   __builtin_memcpy(dst, stage, n * sizeof(double));
+}
+
+/** Dev instrumentation: host timestamps (steady clock, seconds) at numbered
+ * points of one evaluation, taken only while phase_log_on() (the bench's
+ * phase split sets it around one evaluation). */
+struct phase_log_t {
+  bool on = false;
+  double t[32] = {};
+};
+inline phase_log_t& phase_log() {
+  static phase_log_t p;
+  return p;
+}
+inline void phase_mark(int k) {
+  phase_log_t& p = phase_log();
+  if (p.on && k >= 0 && k < 32)
+    p.t[k] = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 inline void zero(double* p, size_t n) {

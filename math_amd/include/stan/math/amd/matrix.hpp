@@ -338,6 +338,11 @@ inline dev_matrix_vari* recognise_block(const var* d, size_t n, int rows, int co
   return k < 0 ? nullptr : static_cast<dev_matrix_vari*>(ChainableStack::instance_->host_blocks_[size_t(k)].node);
 }
 
+/** varis first[i] = vari(val[i]) (unstacked) for i in [b, e) */
+inline void construct_varis(vari* first, const double* val, size_t b, size_t e) {
+  for (size_t i = b; i < e; ++i) ::new (static_cast<void*>(first + i)) vari(val[i], vari::unstacked_tag{});
+}
+
 /** Write block b's element varis into d (column-major rows x cols). */
 inline void fill_block_pointers(const host_block& b, var* d) {
   const std::vector<host_block>& blocks = ChainableStack::instance_->host_blocks_;
@@ -487,9 +492,7 @@ inline void stream_varis(vari* first, const double* src, size_t n, const std::fu
     const size_t b = size_t(k) * chunk, e = std::min(n, b + chunk);
     amd::check(smg_marker_wait(c, k), "to_host");
     if (k == 0 && armed) amd::throw_if_sync(*reinterpret_cast<int*>(stage + n), "to_host", "a persistent solve");
-    host_parallel_for(e - b, [&](size_t s0, size_t s1) {
-      for (size_t i = b + s0; i < b + s1; ++i) ::new (static_cast<void*>(first + i)) vari(stage[i], vari::unstacked_tag{});
-    });
+    host_parallel_for(e - b, [&](size_t s0, size_t s1) { construct_varis(first, stage, b + s0, b + s1); });
   }
 }
 

@@ -218,8 +218,11 @@ inline Eigen::Matrix<double, R, C> value_of(const Eigen::Matrix<var, R, C>& m) {
 inline matrix_v cholesky_decompose(const matrix_v& A) {
   internal::check_square("cholesky_decompose", "A", int(A.rows()), int(A.cols()));
   matrix_v out(A.rows(), A.cols());
+  amd::phase_mark(18);
   // the factor's varis are built as its panels finish (cholesky_decompose_impl)
-  internal::cholesky_decompose_impl(to_dev(A), out.data());
+  const dev_var_matrix Ad = to_dev(A);
+  amd::phase_mark(19);
+  internal::cholesky_decompose_impl(Ad, out.data());
   return out;
 }
 

@@ -235,11 +235,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   // W = L^{-1}: the first n^2 doubles of ws_ once the progressive K^{-1}
   // (early_) has queued all of its block rows (chol_mvn.hip)
   const double* inverse_factor() override {
-    static const bool off = [] {  // TEMP A/B switch (round 5)
-      const char* e = std::getenv("SMG_MVN_INV");
-      return e && e[0] == '0';
-    }();
-    if (off || !early_ || !ws_ || n_ % 64 != 0) return nullptr;
+    if (!early_ || !ws_ || n_ % 64 != 0) return nullptr;
     if (smg_cholesky_inverse_wait(amd::ctx()) != SMG_OK) return nullptr;
     return ws_;
   }
@@ -312,9 +308,12 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       expand(dep_ws_, dep_adj_, dep_k_);
     }
     if (!deposit) record(false);
-    static const bool inv_ok = [] {  // TEMP A/B (round 5)
+    // SMG_CHOL_REV_INV=1: the closed form on a consumer's W = L^{-1}
+    // (2/3 N^3 multiply-adds on three triangular-cut products) instead of
+    // Murray's blocked reverse -- measured slower on the HVP
+    static const bool inv_ok = [] {
       const char* e = std::getenv("SMG_CHOL_REV_INV");
-      return !(e && e[0] == '0');
+      return e && e[0] == '1';
     }();
     if (inv_W_ && inv_ok) {  // Abar (lower) += tril(G + G^T) - diag(G), G = W^T Phi(L^T tril(Lbar)) W
       double* ws = amd::alloc_doubles(2 * nn);
@@ -427,18 +426,21 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
     double* packed = amd::alloc_doubles(b.n);
     double* stage = static_cast<double*>(smg_host_scratch(c, b.n * sizeof(double)));
     if (!stage) throw std::bad_alloc();
+    amd::phase_mark(20);
     amd::check(smg_cholesky_fwd_checked_mark_stream(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started,
                                                     packed, stage, 0),
                fn);
+    amd::phase_mark(0);
     fill_block_pointers(b, host_out);  // addresses only: while the first panel factors
+    amd::phase_mark(1);
     for (int p = 0; p < panels; ++p) {
       int j0 = 0, j1 = 0;  // (the library's own panel bounds: what marker p covers)
       amd::check(smg_cholesky_stream_panel_cols(n, p, &j0, &j1), fn);
       const size_t o0 = tril_off(size_t(n), size_t(j0)), o1 = tril_off(size_t(n), size_t(j1));
       amd::check(smg_marker_wait(c, p), fn);
-      host_parallel_for(o1 - o0, [&](size_t s0, size_t s1) {
-        for (size_t i = o0 + s0; i < o0 + s1; ++i) ::new (static_cast<void*>(b.first + i)) vari(stage[i], vari::unstacked_tag{});
-      });
+      amd::phase_mark(2 + 2 * p);
+      host_parallel_for(o1 - o0, [&](size_t s0, size_t s1) { construct_varis(b.first, stage, o0 + s0, o0 + s1); });
+      amd::phase_mark(3 + 2 * p);
     }
   } else if (inv_ws) {
     amd::check(smg_cholesky_fwd_checked_mark_inv(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started), fn);
@@ -447,6 +449,7 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
   }
   int st = 0;
   amd::check(smg_status_mark_wait(c, &st), fn);
+  amd::phase_mark(30);
   if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
   if (st) amd::throw_status(st, fn, "m");
   auto* node = new internal::cholesky_dev_vari(A.vi_, L);

@@ -433,7 +433,8 @@ def test_cholesky_rev_inverse_vs_murray(ctx, N):
     """smg_cholesky_rev_inverse (the closed form on W = L^{-1}: Abar lower +=
     tril(G + G^T) - diag(G), G = W^T Phi(L^T tril(Lbar)) W) against the blocked
     Murray reverse smg_cholesky_rev on the same factor and adjoint (1e-10,
-    the lower triangle; the strict upper of Lbar carries junk both ignore)."""
+    the lower triangle; the strict upper of Lbar carries junk both ignore).
+    The workspace starts as NaN: a stale value the products read would show."""
     rng = np.random.default_rng(N + 5)
     B = rng.uniform(-1, 1, (N, N))
     A = B @ B.T / N + 0.5 * np.eye(N)
@@ -450,7 +451,7 @@ def test_cholesky_rev_inverse_vs_murray(ctx, N):
     Gm = ctx.get(dG, N * N).reshape(N, N).T
     dG2 = ctx.put(F(G0))
     ctx.call("smg_cholesky_rev_inverse", dL, N, ctx.put(F(W)), ctx.put(F(W.T)), N, ctx.put(F(Lbar)), N, N, dG2, N,
-             ctx.zeros(2 * N * N))
+             ctx.put(np.full(2 * N * N, np.nan)))
     Gi = ctx.get(dG2, N * N).reshape(N, N).T
     low = np.tril(np.ones((N, N), bool))
     ref = Gm[low] - G0[low]
