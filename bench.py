@@ -304,9 +304,9 @@ class GPEigen(GP):
                                    "forward_K": best[4] * 1e3, "forward_Kd": best[5] * 1e3,
                                    "forward_L": best[6] * 1e3, "forward_mvn": best[7] * 1e3,
                                    "forward_L_timeline_ms": {
-                                       "out_allocated": best[26] * 1e3, "input_recognised": best[27] * 1e3,
-                                       "staging_ready": best[28] * 1e3,
-                                       "enqueued": best[8] * 1e3, "pointers_filled": best[9] * 1e3,
+                                       "out_allocated": best[26] * 1e3, "candidate_found": best[27] * 1e3,
+                                       "staging_ready": best[28] * 1e3, "enqueued": best[8] * 1e3,
+                                       "input_verified": best[29] * 1e3, "pointers_filled": best[9] * 1e3,
                                        "panels_arrived": [round(t * 1e3, 4) for t in best[10:26:2] if t > 0],
                                        "panels_built": [round(t * 1e3, 4) for t in best[11:26:2] if t > 0],
                                        "status_read": best[31] * 1e3},

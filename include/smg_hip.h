@@ -108,6 +108,10 @@ int smg_memset(smg_ctx* ctx, void* dst, int value, size_t bytes);
 int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes);
 int smg_join_async(smg_ctx* ctx);
 int smg_sync(smg_ctx* ctx);
+/* Block the host until every stream of the context (main, side, zeroing) is
+ * idle: work queued on a speculation that is then discarded (the Eigen
+ * boundary's cholesky_decompose of a block that turns out modified). */
+int smg_sync_all(smg_ctx* ctx);
 /* Host-side pipelining: record marker `slot` (0..63) on the context stream
  * after the work enqueued so far; smg_marker_wait blocks the host until the
  * stream reaches it (e.g. a large device->host copy issued in chunks whose

@@ -167,9 +167,9 @@ int smg_bench_gp_eigen_step(const double* theta, double* fx, double* grad) {
  * cholesky_decompose, the MVN; out[8..31] the L statement's host timeline
  * from its start (amd::phase_mark: 0 the factorisation enqueued, 1 the
  * pointer array filled, 2 + 2p / 3 + 2p panel p's values arrived / its varis
- * built, 18 the output matrix allocated, 19 the input recognised, 20 the
- * host staging buffer ready, 30 the status read; 0 where a point was not
- * reached). */
+ * built, 18 the output matrix allocated, 19 the input's candidate block
+ * found, 20 the host staging buffer ready, 21 the speculative input verified,
+ * 30 the status read; 0 where a point was not reached). */
 int smg_bench_gp_eigen_phases(const double* theta, double* out) {
   try {
     using namespace stan::math;

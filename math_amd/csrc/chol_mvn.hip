@@ -375,8 +375,8 @@ int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
   const size_t nn = (size_t)n * n;
   // C and Y accumulate (Y's column block k of row r first receives row k's
   // contribution, after the earlier ones: one zeroing instead of a beta split)
-  SMG_HIP_TRY(hipMemsetAsync(ws + nn, 0, 2 * nn * sizeof(double), ctx->stream));
-  return SMG_OK;
+  const std::pair<void*, size_t> r(ws + nn, 2 * nn * sizeof(double));
+  return smg_zero_ranges_impl(ctx, ctx->stream, &r, 1);
 }
 
 int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k, int part,
@@ -396,9 +396,7 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
         if ((rc = smg_block_inverses_rows(ctx, L, ldl, aux, n, r0, P, T))) return rc;
         SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->stream));
       }
-      SMG_HIP_TRY(hipMemcpy2DAsync(W + r0 + (size_t)r0 * n, n * sizeof(double), Wkk, n * sizeof(double),
-                                   P * sizeof(double), P, hipMemcpyDeviceToDevice, ctx->stream));
-      return SMG_OK;
+      return smg_copy_impl(ctx, P, P, Wkk, n, W + r0 + (size_t)r0 * n, n, 1.0, 0);
     case 1:  // W_{k,0:k} = -W_kk Y_k
       if (k == 0) return SMG_OK;
       return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y + r0, n, 0.0, W + r0, n, SMG_TRI_A_LOWER);

@@ -18,6 +18,7 @@
 // The partition differs from the reference's bottom-aligned block_size_ only
 // in where the block seams fall; Murray's recurrence is exact for any
 // partition, so results agree to round-off.  Aadj(lower) += L_adj(lower).
+#include <chrono>
 #include "smg_internal.h"
 #include "tri_small.h"
 #include "smg_sync.h"
@@ -276,6 +277,15 @@ struct panel_tl_end {
 __global__ void k_tl_stamp(int slot) {
   if (threadIdx.x == 0) g_panel_tl[128 + slot] = __builtin_amdgcn_s_memrealtime();
 }
+// host steady-clock time (us) of each panel launch call, by epoch
+double g_panel_host_us[64];
+static inline void panel_host_stamp(int epoch) {
+  g_panel_host_us[epoch & 63] =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+extern "C" void smg_dev_timeline_host(double* out) {
+  for (int i = 0; i < 64; ++i) out[i] = g_panel_host_us[i];
+}
 extern "C" int smg_dev_timeline(smg_ctx* ctx, int stamp_slot, unsigned long long* out) {
   if (stamp_slot >= 0) {
     hipLaunchKernelGGL(k_tl_stamp, dim3(1), dim3(64), 0, ctx->stream, stamp_slot & 63);
@@ -285,6 +295,7 @@ extern "C" int smg_dev_timeline(smg_ctx* ctx, int stamp_slot, unsigned long long
 }
 #else
 #define PANEL_TL()
+static inline void panel_host_stamp(int) {}
 #endif
 
 // hand-off primitives (st_dev / panel_publish / panel_wait): smg_sync.h
@@ -1442,6 +1453,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
         const char* e = getenv("SMG_PANEL_RESIDENT");
         return e && e[0] == '0' ? 0 : 1;
       }();
+      panel_host_stamp(epoch);
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
                          n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, resident_ok);
     }
@@ -1488,15 +1500,31 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const int m2 = n - K2;
       const double* P2 = L + K2 + (size_t)J * ldl;
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
+      // TEMP A/B (round 5): SMG_SPLIT_B=1 splits (b) into (b1), the columns
+      // of the panel after next (all the next look-ahead (a) waits for: F),
+      // and (b2), the rest behind it
+      static const bool split_b = [] {
+        const char* e = getenv("SMG_SPLIT_B");
+        return e && e[0] == '1';
+      }();
+      const int K3 = split_b ? min(K2 + NB2, n) : n;
       {
         smg_on_side on(ctx);
-        rc = smg_gemm_impl(ctx, 0, 1, 1, m2, m2, K - J, -1.0, P2, ldl, P2, ldl, 1.0,
+        rc = smg_gemm_impl(ctx, 0, 1, 1, m2, K3 - K2, K - J, -1.0, P2, ldl, P2, ldl, 1.0,
                            L + K2 + (size_t)K2 * ldl, ldl);
       }
       if (rc) return rc;
       F = smg_event(ctx, nev++);
       if (!F) return SMG_ERR_HIP;
       SMG_HIP_TRY(hipEventRecord(F, ctx->side));
+      if (K3 < n) {  // (b2)
+        const int m3 = n - K3;
+        const double* P3 = L + K3 + (size_t)J * ldl;
+        smg_on_side on(ctx);
+        if ((rc = smg_gemm_impl(ctx, 0, 1, 1, m3, m3, K - J, -1.0, P3, ldl, P3, ldl, 1.0, L + K3 + (size_t)K3 * ldl,
+                                ldl)))
+          return rc;
+      }
     } else if (prog) {  // no (b): the side stream still follows this panel
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
     }

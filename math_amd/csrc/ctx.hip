@@ -33,6 +33,53 @@ __global__ __launch_bounds__(256) void k_publish(const double* __restrict__ src,
   if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// zero up to ZR_MAX device ranges in one launch (16-byte stores; a range of
+// an odd number of doubles gets its last one from the range's first lane):
+// the adjoint zeroings and workspace clears without a runtime fill per buffer
+constexpr int ZR_MAX = 16;
+struct zero_ranges {
+  double* p[ZR_MAX];
+  unsigned long long n[ZR_MAX];  // doubles
+  int count;
+};
+__global__ __launch_bounds__(256) void k_zero_ranges(zero_ranges z) {
+  const unsigned long long tid = blockIdx.x * 256ull + threadIdx.x, stride = gridDim.x * 256ull;
+  const double2 zz = {0.0, 0.0};
+  for (int r = 0; r < z.count; ++r) {
+    double* q = z.p[r];
+    unsigned long long n = z.n[r];
+    if (reinterpret_cast<uintptr_t>(q) & 8) {  // (a head double up to the 16-byte boundary)
+      if (tid == 0) q[0] = 0.0;
+      ++q;
+      --n;
+    }
+    double2* p = reinterpret_cast<double2*>(q);
+    const unsigned long long n2 = n >> 1;
+    for (unsigned long long i = tid; i < n2; i += stride) p[i] = zz;
+    if ((n & 1) && tid == 0) q[n - 1] = 0.0;
+  }
+}
+
+// small device -> pinned host copies (the context's host staging buffer) as a
+// kernel with system-scope stores instead of a runtime copy launch
+__global__ __launch_bounds__(256) void k_copy_to_host(const double* __restrict__ src, long long n, double* dst) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += gridDim.x * 256ll)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// copy the status word to host memory (pinned, device-visible) and clear it:
+// one launch instead of a runtime copy and fill
+__global__ void k_status_take(int* st, int* host_dst) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(host_dst, st[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    st[0] = 0;
+  }
+}
+
+__global__ void k_status_copy(const int* st, int* host_dst) {
+  if (threadIdx.x == 0) __hip_atomic_store(host_dst, st[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr int GATHER_MAX = 64;  // scalars per launch (kernel-argument array)
 struct gather_args {
   const double* p[GATHER_MAX];
@@ -451,8 +498,23 @@ int smg_memcpy_h2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
   return SMG_OK;
 }
 
+// dst inside the context's pinned host staging buffer (device-accessible)
+static bool in_host_scratch(const smg_ctx* ctx, const void* p, size_t bytes) {
+  const char* b = static_cast<const char*>(ctx->host_scratch);
+  const char* c = static_cast<const char*>(p);
+  return b && c >= b && c + bytes <= b + ctx->host_scratch_size;
+}
+
 int smg_memcpy_d2h(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (!bytes) return SMG_OK;
+  if (bytes <= 65536 && !((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | bytes) & 7) &&
+      in_host_scratch(ctx, dst, bytes)) {
+    const long long n = (long long)(bytes / 8);
+    hipLaunchKernelGGL(k_copy_to_host, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                       static_cast<const double*>(src), n, static_cast<double*>(dst));
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
   SMG_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   return SMG_OK;
 }
@@ -465,9 +527,45 @@ int smg_memcpy_d2d(smg_ctx* ctx, void* dst, const void* src, size_t bytes) {
 
 int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
   if (!bytes) return SMG_OK;
+  if (v == 0) {
+    const std::pair<void*, size_t> r(dst, bytes);
+    return smg_zero_ranges_impl(ctx, ctx->stream, &r, 1);
+  }
   SMG_HIP_TRY(hipMemsetAsync(dst, v, bytes, ctx->stream));
   return SMG_OK;
 }
+
+}  // extern "C"
+
+int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count) {
+  zero_ranges z{};
+  size_t most = 0;
+  auto launch = [&]() -> int {
+    if (!z.count) return SMG_OK;
+    const size_t g = (most / 2 + 255) / 256;
+    hipLaunchKernelGGL(k_zero_ranges, dim3(g < 2048 ? (g < 1 ? 1 : (unsigned)g) : 2048u), dim3(256), 0, stream, z);
+    SMG_LAUNCH_CHECK();
+    z.count = 0;
+    most = 0;
+    return SMG_OK;
+  };
+  for (int i = 0; i < count; ++i) {
+    const size_t b = r[i].second;
+    if (!b) continue;
+    if ((reinterpret_cast<uintptr_t>(r[i].first) & 7) || (b & 7)) {  // (not a range of doubles)
+      SMG_HIP_TRY(hipMemsetAsync(r[i].first, 0, b, stream));
+      continue;
+    }
+    z.p[z.count] = static_cast<double*>(r[i].first);
+    z.n[z.count] = b / 8;
+    most = b / 8 > most ? b / 8 : most;
+    if (++z.count == ZR_MAX)
+      if (int rc = launch()) return rc;
+  }
+  return launch();
+}
+
+extern "C" {
 
 int smg_zero_stream_begin(smg_ctx* ctx) {
   if (ctx->zero_stream) return SMG_OK;
@@ -499,9 +597,9 @@ int smg_memset_async(smg_ctx* ctx, void* dst, size_t bytes) {
   if (!ctx) return SMG_ERR_ARG;
   if (!bytes) return SMG_OK;
   if (!dst) return SMG_ERR_ARG;
-  if (smg_zero_stream_begin(ctx) != SMG_OK) {
-    SMG_HIP_TRY(hipMemsetAsync(dst, 0, bytes, ctx->stream));  // no second stream: in order
-    return SMG_OK;
+  if (smg_zero_stream_begin(ctx) != SMG_OK) {  // no second stream: in order
+    const std::pair<void*, size_t> r(dst, bytes);
+    return smg_zero_ranges_impl(ctx, ctx->stream, &r, 1);
   }
   // issued by smg_zero_flush: at the next latency-bound entry, the join, or a
   // rewind (the memory then still belongs to this tape)
@@ -516,7 +614,8 @@ int smg_zero_flush(smg_ctx* ctx) {
   hipStream_t main = (ctx->side && ctx->stream == ctx->side) ? ctx->main_stream : ctx->stream;
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_main, main));
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_ev_main, 0));
-  for (const auto& z : ctx->zero_queue) SMG_HIP_TRY(hipMemsetAsync(z.first, 0, z.second, ctx->zero_stream));
+  if (int rc = smg_zero_ranges_impl(ctx, ctx->zero_stream, ctx->zero_queue.data(), (int)ctx->zero_queue.size()))
+    return rc;
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_done, ctx->zero_stream));
   ctx->zero_queue.clear();
   ctx->zero_pending = 1;
@@ -550,6 +649,14 @@ int smg_marker_wait(smg_ctx* ctx, int slot) {
   return SMG_OK;
 }
 
+int smg_sync_all(smg_ctx* ctx) {
+  if (!ctx) return SMG_ERR_ARG;
+  sync_all_streams(ctx);
+  SMG_HIP_TRY(hipGetLastError());
+  if (ctx->prof_on) prof_drain(ctx);
+  return SMG_OK;
+}
+
 int smg_sync(smg_ctx* ctx) {
   SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (ctx->prof_on) prof_drain(ctx);
@@ -557,9 +664,8 @@ int smg_sync(smg_ctx* ctx) {
 }
 
 int smg_status(smg_ctx* ctx, int* status) {
-  SMG_HIP_TRY(hipMemcpyAsync(ctx->status_h, ctx->status_d, sizeof(int),
-                             hipMemcpyDeviceToHost, ctx->stream));
-  SMG_HIP_TRY(hipMemsetAsync(ctx->status_d, 0, sizeof(int), ctx->stream));
+  hipLaunchKernelGGL(k_status_take, dim3(1), dim3(64), 0, ctx->stream, ctx->status_d, ctx->status_h);
+  SMG_LAUNCH_CHECK();
   SMG_HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (ctx->prof_on) prof_drain(ctx);
   int s = ctx->status_h[0] | ctx->host_status;
@@ -576,8 +682,8 @@ int smg_status_mark_impl(smg_ctx* ctx) {
     ctx->status_ev = nullptr;
     return SMG_ERR_HIP;
   }
-  SMG_HIP_TRY(hipMemcpyAsync(ctx->status_h + 1, ctx->status_d, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  SMG_HIP_TRY(hipMemsetAsync(ctx->status_d, 0, sizeof(int), ctx->stream));
+  hipLaunchKernelGGL(k_status_take, dim3(1), dim3(64), 0, ctx->stream, ctx->status_d, ctx->status_h + 1);
+  SMG_LAUNCH_CHECK();
   SMG_HIP_TRY(hipEventRecord(ctx->status_ev, ctx->stream));
   ctx->status_mark = 1;
   return SMG_OK;
@@ -608,7 +714,12 @@ int smg_status_armed(smg_ctx* ctx, int* armed) {
 
 int smg_status_enqueue(smg_ctx* ctx, int* host_dst) {
   if (!ctx || !host_dst) return SMG_ERR_ARG;
-  SMG_HIP_TRY(hipMemcpyAsync(host_dst, ctx->status_d, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  if (in_host_scratch(ctx, host_dst, sizeof(int))) {
+    hipLaunchKernelGGL(k_status_copy, dim3(1), dim3(64), 0, ctx->stream, ctx->status_d, host_dst);
+    SMG_LAUNCH_CHECK();
+  } else {
+    SMG_HIP_TRY(hipMemcpyAsync(host_dst, ctx->status_d, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  }
   ctx->status_armed = 0;
   return SMG_OK;
 }

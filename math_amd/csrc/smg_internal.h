@@ -188,6 +188,9 @@ int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, 
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
 int smg_status_mark_impl(smg_ctx* ctx);
+// zero `count` device ranges (pointer, bytes) on `stream`: batched launches of
+// one kernel (ranges of doubles on 16 bytes), the runtime fill otherwise (ctx.hip)
+int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count);
 // issue the queued smg_memset_async zeroings on the zeroing stream (ctx.hip)
 extern "C" int smg_zero_flush(smg_ctx* ctx);
 // ensure the zeroing stream (also the device->host stream of the streamed

@@ -42,6 +42,7 @@ _SIGS = {
     "smg_memset_async": (_I, [_P, _P, _S]),
     "smg_join_async": (_I, [_P]),
     "smg_sync": (_I, [_P]),
+    "smg_sync_all": (_I, [_P]),
     "smg_status": (_I, [_P, ctypes.POINTER(_I)]),
     "smg_status_armed": (_I, [_P, ctypes.POINTER(_I)]),
     "smg_status_enqueue": (_I, [_P, _P]),

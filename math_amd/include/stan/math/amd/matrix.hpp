@@ -253,12 +253,13 @@ inline size_t tril_count(size_t n) { return n * (n + 1) / 2; }
 
 inline void block_column_ptrs(const std::vector<host_block>& blocks, const host_block& b, size_t j, vari** out);
 
-/** f(i, v) for every row i of column j of host block b, in order: v is the
- * vari the reference's matrix holds at (i, j) (host_block's layouts).
- * blocks: the tape's host_blocks_ (passed in: the host pool's workers have
- * no tape of their own). */
+/** f(i, v) for every row i of column j of a dense, lower or symmetric block
+ * (no base block), in order.  The symmetric layout's rows above the diagonal
+ * step through the packed columns incrementally: element (i, j), i < j, is
+ * packed column i's entry j - i at tril_off(r, i) + j - i, and
+ * tril_off(r, i + 1) - tril_off(r, i) = r - i. */
 template <typename F>
-inline void block_column(const std::vector<host_block>& blocks, const host_block& b, size_t j, F&& f) {
+inline void block_column_own(const host_block& b, size_t j, F&& f) {
   const size_t r = size_t(b.rows);
   switch (b.layout) {
     case layout_lower: {
@@ -268,28 +269,45 @@ inline void block_column(const std::vector<host_block>& blocks, const host_block
       break;
     }
     case layout_sym: {
-      for (size_t i = 0; i < j && i < r; ++i) f(i, b.first + tril_off(r, i) + (j - i));
+      vari* p = b.first + j;  // (i = 0: tril_off(r, 0) + j)
+      for (size_t i = 0; i < j && i < r; ++i) {
+        f(i, p);
+        p += r - i - 1;
+      }
       vari* c = b.first + tril_off(r, j) - j;
       for (size_t i = j; i < r; ++i) f(i, c + i);
-      break;
-    }
-    case layout_diag: {
-      vari* own = j < b.n ? b.first + j : nullptr;
-      if (b.base >= 0) {  // (the base's column through a buffer: no recursive instantiation)
-        thread_local std::vector<vari*> col;
-        col.resize(r);
-        block_column_ptrs(blocks, blocks[size_t(b.base)], j, col.data());
-        for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : col[i]);
-      } else {
-        vari* const* e = b.base_elems + j * r;
-        for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : e[i]);
-      }
       break;
     }
     default: {
       vari* c = b.first + j * r;
       for (size_t i = 0; i < r; ++i) f(i, c + i);
     }
+  }
+}
+
+/** f(i, v) for every row i of column j of host block b, in order: v is the
+ * vari the reference's matrix holds at (i, j) (host_block's layouts).
+ * blocks: the tape's host_blocks_ (passed in: the host pool's workers have
+ * no tape of their own). */
+template <typename F>
+inline void block_column(const std::vector<host_block>& blocks, const host_block& b, size_t j, F&& f) {
+  if (b.layout != layout_diag) return block_column_own(b, j, f);
+  const size_t r = size_t(b.rows);
+  vari* own = j < b.n ? b.first + j : nullptr;
+  if (b.base >= 0) {
+    const host_block& base = blocks[size_t(b.base)];
+    if (base.layout != layout_diag) {  // (the common case: add_diag of a materialised node)
+      block_column_own(base, j, [&](size_t i, vari* v) { f(i, i == j && own ? own : v); });
+      return;
+    }
+    // (the base's column through a buffer: no recursive instantiation)
+    thread_local std::vector<vari*> col;
+    col.resize(r);
+    block_column_ptrs(blocks, base, j, col.data());
+    for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : col[i]);
+  } else {
+    vari* const* e = b.base_elems + j * r;
+    for (size_t i = 0; i < r; ++i) f(i, i == j && own ? own : e[i]);
   }
 }
 
@@ -309,7 +327,8 @@ inline size_t col_grain(int rows) { return std::max<size_t>(1, (size_t(1) << 18)
  * (column-major rows x cols) by the block's layout, or -1.  The full pointer
  * check runs on every call (a caller may have replaced single elements); it
  * is one parallel read of n pointers. */
-inline long recognise_block_index(const var* d, size_t n, int rows, int cols) {
+/** The host block d[0..n) may be (its first vari and shape; O(1)), or -1. */
+inline long candidate_block_index(const var* d, size_t n, int rows, int cols) {
   if (n == 0) return -1;
   auto& blocks = ChainableStack::instance_->host_blocks_;
   const vari* v0 = d[0].vi_;
@@ -317,21 +336,31 @@ inline long recognise_block_index(const var* d, size_t n, int rows, int cols) {
     const host_block& b = blocks[k];
     if (b.first != v0) continue;
     if (b.rows != rows || b.cols != cols || size_t(rows) * size_t(cols) != n) return -1;
-    const size_t r = size_t(rows);
-    const bool ok = host_parallel_all(
-        size_t(cols),
-        [&](size_t j0, size_t j1) {
-          bool good = true;
-          for (size_t j = j0; good && j < j1; ++j) {
-            const var* col = d + j * r;
-            block_column(blocks, b, j, [&](size_t i, vari* v) { good &= col[i].vi_ == v; });
-          }
-          return good;
-        },
-        col_grain(rows));
-    return ok ? long(k) : -1;
+    return long(k);
   }
   return -1;
+}
+/** Whether d (column-major, block k's shape) holds exactly block k's varis:
+ * one parallel read of its pointers. */
+inline bool block_matches(const var* d, size_t k) {
+  auto& blocks = ChainableStack::instance_->host_blocks_;
+  const host_block& b = blocks[k];
+  const size_t r = size_t(b.rows);
+  return host_parallel_all(
+      size_t(b.cols),
+      [&](size_t j0, size_t j1) {
+        bool good = true;
+        for (size_t j = j0; good && j < j1; ++j) {
+          const var* col = d + j * r;
+          block_column(blocks, b, j, [&](size_t i, vari* v) { good &= col[i].vi_ == v; });
+        }
+        return good;
+      },
+      col_grain(b.rows));
+}
+inline long recognise_block_index(const var* d, size_t n, int rows, int cols) {
+  const long k = candidate_block_index(d, n, rows, cols);
+  return k >= 0 && block_matches(d, size_t(k)) ? k : -1;
 }
 inline dev_matrix_vari* recognise_block(const var* d, size_t n, int rows, int cols) {
   const long k = recognise_block_index(d, n, rows, cols);

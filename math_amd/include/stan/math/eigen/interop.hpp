@@ -219,10 +219,19 @@ inline matrix_v cholesky_decompose(const matrix_v& A) {
   internal::check_square("cholesky_decompose", "A", int(A.rows()), int(A.cols()));
   matrix_v out(A.rows(), A.cols());
   amd::phase_mark(18);
-  // the factor's varis are built as its panels finish (cholesky_decompose_impl)
-  const dev_var_matrix Ad = to_dev(A);
+  // the factor's varis are built as its panels finish (cholesky_decompose_impl).
+  // A materialised node (the usual case) is factorised speculatively: the
+  // full pointer check runs on the host while the first panels factor, and a
+  // mismatch (an element replaced) discards that factorisation for the
+  // gathered copy's
+  const long k = internal::candidate_block_index(A.data(), size_t(A.size()), int(A.rows()), int(A.cols()));
   amd::phase_mark(19);
-  internal::cholesky_decompose_impl(Ad, out.data());
+  if (k >= 0) {
+    auto* node = static_cast<dev_matrix_vari*>(ChainableStack::instance_->host_blocks_[size_t(k)].node);
+    const std::function<bool()> verify = [&] { return internal::block_matches(A.data(), size_t(k)); };
+    if (internal::cholesky_decompose_impl(dev_var_matrix(node), out.data(), &verify).vi_) return out;
+  }
+  internal::cholesky_decompose_impl(to_dev(A), out.data());
   return out;
 }
 

@@ -396,11 +396,19 @@ namespace internal {
  * Varis built before a failed check are left unreferenced in the arena, as a
  * throwing reference functor leaves its partial allocations.
  */
-inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host_out) {
+inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host_out,
+                                              const std::function<bool()>* verify = nullptr) {
   const char* fn = "cholesky_decompose";
   internal::check_square(fn, "A", A.rows(), A.cols());
   const int n = A.rows();
   smg_ctx* c = amd::ctx();
+  // verify: A is speculative (its host matrix still to be checked); an empty
+  // result if the check fails.  It runs once the factorisation is queued when
+  // the factor streams to the host, before anything is queued otherwise.
+  if (verify && !(host_out && n > 0 && smg_cholesky_stream_panels(n) <= 64)) {
+    if (!(*verify)()) return dev_var_matrix();
+    verify = nullptr;
+  }
   if (n == 0) return dev_var_matrix(new dev_matrix_vari(0, 0, dev_structure::lower));
   auto* L = new dev_matrix_vari(n, n, dev_structure::lower);
   L->aux_ = amd::alloc_doubles(size_t(smg_cholesky_aux_doubles(n)));
@@ -431,6 +439,13 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
                                                     packed, stage, 0),
                fn);
     amd::phase_mark(0);
+    if (verify && !(*verify)()) {  // (rejected: the queued work drains, its results are dropped)
+      amd::check(smg_sync_all(c), fn);
+      int st = 0;
+      amd::check(smg_status_mark_wait(c, &st), fn);
+      return dev_var_matrix();
+    }
+    amd::phase_mark(21);
     fill_block_pointers(b, host_out);  // addresses only: while the first panel factors
     amd::phase_mark(1);
     for (int p = 0; p < panels; ++p) {

@@ -203,6 +203,33 @@ def test_gp_intermediate_adjoints(N, variant, closed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("closed", ["1", "0"])
+@pytest.mark.parametrize("N", [64, 256])
+def test_gp_intermediate_replaced_element(N, closed):
+    """cholesky_decompose of an Eigen matrix that is a materialised node but
+    for one replaced element (Kd(N-1, N/2) = 0.5 (x + x), a new vari of the
+    same value): the factorisation started speculatively on the node is
+    discarded once the host's pointer check fails, and the gathered copy's
+    result is the reference's unmodified one (gp_intermediate_N*.json
+    variant 0, 1e-10): the same lp, theta gradient, K / Kd / L adjoints and
+    L values; the identity entries but those of Kd's sharing (one new vari)."""
+    d = golden(f"gp_intermediate_N{N}")
+    th = d["theta"]
+    env = None if closed == "1" else {"SMG_CHOL_MVN_CLOSED_FORM": "0"}
+    res = _parse(_run(f"gp_inter {N} 3 {_num(d['x'])} {_num(d['y'])} {_num(th)}\n", env=env))
+    got, want = res["gpi"], np.concatenate([[d["fx_v0"]], d["v0"]])
+    near_rel(got[0], want[0], 1e-12, what="lp")
+    g, w = _gpi_split(got[1:], N), _gpi_split(want[1:], N)
+    near_rel(g[0], w[0], RTOL, what="grad theta")
+    for name, a, b in zip(("K adj", "Kd diag adj", "L adj", "L val"), g[1:5], w[1:5]):
+        near_rel(a, b, RTOL, atol=RTOL * float(np.abs(b).max()), what=name)
+    gi, wi = list(g[5]), list(w[5])
+    assert [gi[q] for q in (0, 3, 4, 6)] == [wi[q] for q in (0, 3, 4, 6)], ("identity", gi, wi)
+    assert gi[1] == 0.0 and gi[5] == wi[5] + 1  # (Kd no longer shares K's vari there: one more vari)
+    assert list(res["stack"]) == [0.0, 0.0]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N", [1024, 4096])
 def test_gp_codegen_1d_golden(N):
     """The Stan-codegen GP marginal (1-D x, Eigen::Matrix<var> K, Kd, L, the
