@@ -463,7 +463,7 @@ __device__ __forceinline__ bool panel_helped(int t, int c, int nb, int nh) {
 // inlined: its own register budget (the resident blocks live across the steps).
 __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int n, int J, int K,
                                             double* __restrict__ Dinv, int ldd, int* flags, int epoch, int* status,
-                                            int nb, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y) {
+                                            int nb, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y, int Jp) {
   constexpr int S = PANEL_MAX_STEPS;
   constexpr int R = PANEL_BELOW_ROWS;
   static_assert(R == 32, "the resident layout is lds_mma32_8w's");
@@ -474,15 +474,21 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ar = 16 * (w & 1) + (l >> 4), ac = 16 * (w >> 1) + (l & 15);  // + 4 q: this lane's rows
   double Rres[S][4];
+  // fused look-ahead (look): the other workgroups apply (a) to these rows in
+  // memory (panel_lookahead, column block c published as aflag[rb S + c]);
+  // Rres then accumulates only this panel's updates, and block j is loaded at
+  // step j, once its look-ahead tile is in
+  const bool look = Jp < J;
+  const int rb = nb + (R * (t - nb)) / SMG_NB;  // (its 64-row look-ahead tile)
 #pragma unroll
   for (int c = 0; c < S; ++c) {  // the whole tile (final: rows are independent), once
     const int cc = J + SMG_NB * c, bc = min(SMG_NB, K - cc);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = ar + 4 * q;
-      const bool in = c < nb && r < rt && ac < bc;
+      const bool in = c < nb && r < rt && ac < bc && !look;
       const int col = c < nb ? cc + min(ac, bc - 1) : J;  // (clamped in range: loads are unconditional)
-      const double v = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
+      const double v = look ? 0.0 : ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
       Rres[c][q] = in ? v : 0.0;
     }
   }
@@ -491,6 +497,19 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
     const int bj = min(SMG_NB, K - cj);
     __syncthreads();  // LDS of the previous step fully consumed
     PANEL_EV((j << 16) | (t << 8) | 5);
+    if (look) {  // block j after (a): memory + this panel's updates so far
+      panel_wait(&flags[S + 4 * S * S + rb * S + j], epoch, status);
+      const int col = cj + min(ac, bj - 1);
+#pragma unroll
+      for (int c = 0; c < S; ++c)
+        if (c == j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int r = ar + 4 * q;
+            const double v = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
+            Rres[c][q] = (r < rt && ac < bj) ? v + Rres[c][q] : 0.0;
+          }
+    }
 #pragma unroll
     for (int c = 0; c < S; ++c)  // block j into D (its current A_tj)
       if (c == j)
@@ -542,9 +561,84 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
   }
 }
 
+// The look-ahead update (a) of panel [J, K) by the previous panel [Jp, J),
+// fused into the panel's launch: A[J:, J:K] -= L[J:, Jp:J] L[J:K, Jp:J]^T in
+// 64 x 64 tiles by workgroups 0 .. na - 1, each tile published (aflag[r S +
+// c]): first the diagonal block's lower tiles (the chain's and the panel
+// tiles' rows, needed at once), then the rows below column block by column
+// block (block c is needed at step c: below_resident waits for it there).
+// Out of line: its own register budget.
+__device__ __noinline__ void panel_lookahead(double* __restrict__ L, int ldl, int n, int J, int K, int Jp, int na,
+                                             int nb, int* aflag, int epoch, lds_dbl* X, lds_dbl* Y) {
+  constexpr int S = PANEL_MAX_STEPS;
+  const int nr = (n - J + SMG_NB - 1) / SMG_NB;  // 64-row tiles from J
+  const int ntri = nb * (nb + 1) / 2, nq = ntri + (nr - nb) * nb;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, fr = l & 15, fk = l >> 4;
+  const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
+  for (int q = blockIdx.x; q < nq; q += na) {
+    int r, c;
+    if (q < ntri) {
+      r = 0;
+      while ((r + 1) * (r + 2) / 2 <= q) ++r;
+      c = q - r * (r + 1) / 2;
+    } else {  // column-major below the diagonal block
+      c = (q - ntri) / (nr - nb);
+      r = nb + (q - ntri) % (nr - nb);
+    }
+    const int r0 = J + SMG_NB * r, c0 = J + SMG_NB * c;
+    const int rr = min(SMG_NB, n - r0), cb = min(SMG_NB, K - c0);
+    d4 acc[2];
+    acc[0] = d4{0.0, 0.0, 0.0, 0.0};
+    acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+    panel_regs Ra, Rb;
+    panel_gload(Ra, L + r0 + (size_t)Jp * ldl, ldl, rr, min(SMG_NB, J - Jp), false);
+    panel_gload(Rb, L + c0 + (size_t)Jp * ldl, ldl, cb, min(SMG_NB, J - Jp), false);
+    for (int k0 = Jp; k0 < J; k0 += SMG_NB) {
+      __syncthreads();  // the previous chunk's product has read X / Y
+      panel_lstore(X, Ra);
+      panel_lstore(Y, Rb);
+      __syncthreads();
+      const int k1 = k0 + SMG_NB;
+      if (k1 < J) {  // the next chunk in flight during this product
+        panel_gload(Ra, L + r0 + (size_t)k1 * ldl, ldl, rr, min(SMG_NB, J - k1), false);
+        panel_gload(Rb, L + c0 + (size_t)k1 * ldl, ldl, cb, min(SMG_NB, J - k1), false);
+      }
+#pragma unroll 4
+      for (int kq = 0; kq < SMG_NB; kq += 4) {
+        const int kk = kq + fk;
+        const double a = X[i * SMG_NBP + kk];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const double b = Y[(16 * (t0 + t) + fr) * SMG_NBP + kk];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int row = 16 * (w & 3) + fk + 4 * q4, col = 16 * (t0 + t) + fr;
+        if (row < rr && col < cb && (r != c || row >= col)) {
+          double* pc = L + r0 + row + (size_t)(c0 + col) * ldl;
+          st_dev(pc, ld_dev(pc) - acc[t][q4]);
+        }
+      }
+    panel_publish(&aflag[r * S + c], epoch);
+  }
+}
+
+// a workgroup's wait for the fused look-ahead tiles of 64-row tile r (all
+// the panel's column blocks it has), before its first read of those rows
+__device__ inline void wait_look(const int* flags, int r, int nb, int epoch, int* status) {
+  constexpr int S = PANEL_MAX_STEPS;
+  panel_wait_all(flags + S + 4 * S * S + r * S, 0, min(r, nb - 1), 1, epoch, status);
+}
+
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status, int gown, int resident_ok) {
+                                                    int* flags, int epoch, int* status, int gown, int resident_ok,
+                                                    int Jp, int na) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -558,6 +652,21 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   int* dinvf = flags + S + 3 * S * S;  // dinvf[j]: Dinv_j stored (the inverter workgroup)
   const int nb = (K - J + SMG_NB - 1) / SMG_NB;
   const int T = panel_tiles(n, J, nb);
+  // flags + S + 4 S^2 + r S + c: look-ahead tile (r, c) stored (na > 0: panel_lookahead / wait_look)
+  // The look-ahead update (a) of this panel's columns by the previous panel
+  // [Jp, J) (A[J:, J:K] -= L[J:, Jp:J] L[J:K, Jp:J]^T, lower trapezoid),
+  // when fused (na > 0): workgroups 0 .. na - 1 compute its 64 x 64 tiles,
+  // the diagonal block's rows first, and publish each; every other
+  // workgroup waits for the tiles of the rows it reads before its first
+  // read of them.  They are dispatched before the panel's workgroups and wait
+  // on nothing, so the grid needs no co-residency beyond the panel's own;
+  // the chain starts once the first rows' tiles are in, instead of behind a
+  // separate launch of the whole update.
+  if ((int)blockIdx.x < na) {
+    panel_lookahead(L, ldl, n, J, K, Jp, na, nb, flags + S + 4 * S * S, epoch, (lds_dbl*)X, (lds_dbl*)Y);
+    return;
+  }
+  const unsigned bid = blockIdx.x - (unsigned)na;  // the panel's own workgroup index
   // Column helpers: panel tile t >= 3 (t < nb) gets workgroup gown + t - 3,
   // which applies the updates of its odd column blocks c <= t - 2 (panel_helped);
   // the owner of t does the rest, its L_tj, and waits hflag[(j-1) S + t]
@@ -569,8 +678,8 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // cheaper product beats the solve), the panel tiles solve against L_jj
   // (the chain needs their updates sooner).  Owners are workgroups
   // 2 .. gown - 1, column helpers gown ...
-  const int nh = gridDim.x - gown;
-  if (blockIdx.x == 1) {
+  const int nh = gridDim.x - na - gown;
+  if (bid == 1) {
     // ... and, behind each Dinv_j, the aux 128 level of the previous full
     // block pair (j - 2, j - 1): X = [[D1, 0], [-D2 L21 D1, D2]] (two 64^3
     // LDS products; Y = D1, Z = D2 kept from the pair's own steps), so the
@@ -618,10 +727,11 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     return;
   }
 
-  if (blockIdx.x >= gown) {
-    const int t = 3 + (blockIdx.x - gown);
+  if (bid >= gown) {
+    const int t = 3 + (bid - gown);
     if (t >= nb) return;
     const int rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
+    if (na > 0) wait_look(flags, t, nb, epoch, status);
     for (int j = 0; j + 2 <= t; ++j) {
       const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
       int c0 = j + 1;
@@ -655,7 +765,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     return;
   }
 
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     // the diagonal chain: factor block j, then apply step j to tile j + 1
     // (a private L_{j+1,j} and the A_{j+1,j+1} update) so that block j + 1 is
     // ready in LDS without a hand-off.  Tile j + 1's owner computes the same
@@ -665,7 +775,16 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     // it with L_{j+1,j} only after seeing diag[j].
     double* Dc = D;  // current diagonal block (LDS)
     double* Zn = Z;  // next one
-    lds_load_block(Dc, L + J + (size_t)J * ldl, ldl, min(SMG_NB, K - J), true);
+    if (na > 0) {
+      wait_look(flags, 0, nb, epoch, status);
+      if (nb > 1) wait_look(flags, 1, nb, epoch, status);  // (step 0 reads tile 1's rows before any owner has)
+    }
+    {
+      panel_regs R0;
+      const int b0 = min(SMG_NB, K - J);
+      panel_gload(R0, L + J + (size_t)J * ldl, ldl, b0, b0, true);
+      panel_lstore_id(Dc, R0, b0);
+    }
     __syncthreads();
     for (int j = 0; j < nb; ++j) {
       const int cj = J + SMG_NB * j;
@@ -727,16 +846,19 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // place, and block j written out once, as L_tj -- instead of loading and
   // storing every later block at every step (the kernel fetched 2.6x and
   // wrote 2.1x its algorithmic bytes)
-  if (resident_ok && blockIdx.x - 1 >= nb && blockIdx.x - 1 + (gown - 2) >= T) {
-    below_resident(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb, blockIdx.x - 1, (lds_dbl*)D, (lds_dbl*)X,
-                   (lds_dbl*)Y);
+  if (resident_ok && bid - 1 >= nb && bid - 1 + (gown - 2) >= T) {
+    below_resident(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb, (int)bid - 1, (lds_dbl*)D, (lds_dbl*)X,
+                   (lds_dbl*)Y, na > 0 ? Jp : J);
     return;
   }
+  // (fused look-ahead only with every tile its own workgroup, those below the
+  // panel resident: here only panel tiles, which wait for their rows' tiles)
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
-    for (int t = 1 + (blockIdx.x - 2); t < T; t += gown - 2) {
+    for (int t = 1 + (bid - 2); t < T; t += gown - 2) {
       if (t <= j) continue;  // done
+      if (j == 0 && na > 0 && t < nb) wait_look(flags, t, nb, epoch, status);
       if (t >= nb) {  // a 32-row tile below the panel: L_tj = A_tj Dinv_j^T, then A_tc -= L_tj L_cj^T (c < nb)
         constexpr int R = PANEL_BELOW_ROWS;
         const int rt0 = J + SMG_NB * nb + R * (t - nb), rt = min(R, n - rt0);
@@ -1431,6 +1553,37 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     }
     return SMG_OK;
   };
+  // SMG_PANEL_RESIDENT=0: the rows below the panel reload and store every
+  // column block at every step (the round-4 form; tools/ubench_panel's
+  // before / after traces).  SMG_FUSED_A=1: the look-ahead (a) inside the next
+  // panel's launch (panel_lookahead) -- gaps between panels of 12-20 us, but
+  // slower overall (342-346 against 357-362 evals/s): its
+  // workgroups take CUs the concurrent trailing update and K^{-1} work need
+  static const int resident_ok = [] {
+    const char* e = getenv("SMG_PANEL_RESIDENT");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  static const bool fuse_env = [] {
+    const char* e = getenv("SMG_FUSED_A");
+    return e && e[0] == '1';
+  }();
+  // the look-ahead workgroups of the panel launch at column Jx (0: (a) runs
+  // as its own GEMM before it): only with every tile its own workgroup (the
+  // tiles below then register-resident: they wait for each column block's
+  // look-ahead at its step)
+  auto fused_at = [&](int Jx) -> int {
+    if (!fuse_env || !look || Jx <= 0 || !resident_ok) return 0;
+    const int Kx = min(Jx + NB2, n), nbx = smg_ceil_div(Kx - Jx, SMG_NB), Tx = panel_tiles(n, Jx, nbx);
+    if (Tx >= PANEL_MAX_GRID) return 0;
+    const int nr = smg_ceil_div(n - Jx, SMG_NB);
+    constexpr int S = PANEL_MAX_STEPS;
+    if (S + 4 * S * S + nr * S > 4096) return 0;  // (the flag buffer)
+    const int ntri = nbx * (nbx + 1) / 2, nq = ntri + (nr - nbx) * nbx;
+    int nhx = nbx > 3 ? nbx - 3 : 0;
+    if (Tx + 1 + nhx > PANEL_MAX_GRID + 1 || nbx > Tx) nhx = 0;
+    // the CUs the panel leaves, at least one workgroup per diagonal tile
+    return min(nq, max(ntri, PANEL_MAX_GRID - (Tx + 1) - nhx));
+  };
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
@@ -1449,13 +1602,10 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
         const double m = n - J, b = K - J;
         ctx->prof_flops[SMG_FAM_PANEL] += m * b * b - 2.0 * b * b * b / 3.0;
       }
-      static const int resident_ok = [] {  // TEMP A/B (round 5): SMG_PANEL_RESIDENT=0 keeps the reloading form
-        const char* e = getenv("SMG_PANEL_RESIDENT");
-        return e && e[0] == '0' ? 0 : 1;
-      }();
+      const int na = fused_at(J);
       panel_host_stamp(epoch);
-      hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, resident_ok);
+      hipLaunchKernelGGL(k_chol_panel, dim3(na + grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, resident_ok, J - NB2, na);
     }
     if (zero_parts && J / NB2 < rows_prog) {  // this panel is final: its block row's inverses may start
       if (!(pe_ev[J / NB2] = smg_event(ctx, nev++))) return SMG_ERR_HIP;
@@ -1473,8 +1623,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       ctx->stream = keep;
       if (prc) return prc;
       const size_t o0 = (size_t)J * n - (size_t)J * (J - 1) / 2, o1 = (size_t)K * n - (size_t)K * (K - 1) / 2;
-      SMG_HIP_TRY(hipMemcpyAsync(sink->host + o0, sink->packed + o0, (o1 - o0) * sizeof(double), hipMemcpyDeviceToHost,
-                                 ctx->zero_stream));
+      if (int rc = smg_d2h_impl(ctx, ctx->zero_stream, sink->host + o0, sink->packed + o0, (o1 - o0) * sizeof(double)))
+        return rc;
       SMG_HIP_TRY(hipEventRecord(Me, ctx->zero_stream));
     }
     if (K >= n) break;
@@ -1490,22 +1640,24 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     hipEvent_t E = smg_event(ctx, nev++);
     if (!E) return SMG_ERR_HIP;
     if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
-    // (a) the next panel's columns (lower trapezoid), main stream
-    int rc = smg_gemm_impl(ctx, 0, 1, 1, m, K2 - K, K - J, -1.0, P, ldl, P, ldl, 1.0,
-                           L + K + (size_t)K * ldl, ldl);
-    if (rc) return rc;
+    int rc = 0;
+    // (a) the next panel's columns (lower trapezoid), main stream -- or in
+    // the next panel's launch (fused_at)
+    if (!fused_at(K) &&
+        (rc = smg_gemm_impl(ctx, 0, 1, 1, m, K2 - K, K - J, -1.0, P, ldl, P, ldl, 1.0, L + K + (size_t)K * ldl, ldl)))
+      return rc;
     SMG_HIP_TRY(hipEventRecord(E, ctx->stream));
     F = nullptr;
     if (K2 < n) {  // (b) the rest, side stream
       const int m2 = n - K2;
       const double* P2 = L + K2 + (size_t)J * ldl;
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
-      // TEMP A/B (round 5): SMG_SPLIT_B=1 splits (b) into (b1), the columns
-      // of the panel after next (all the next look-ahead (a) waits for: F),
-      // and (b2), the rest behind it
+      // (b) in two: (b1), the columns of the panel after next (all the next
+      // look-ahead (a) waits for: F), and (b2), the rest behind it (GP
+      // 355-358 -> 358-360 evals/s in a same-box A/B; SMG_SPLIT_B=0: one (b))
       static const bool split_b = [] {
         const char* e = getenv("SMG_SPLIT_B");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
       }();
       const int K3 = split_b ? min(K2 + NB2, n) : n;
       {

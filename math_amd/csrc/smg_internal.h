@@ -191,6 +191,8 @@ int smg_status_mark_impl(smg_ctx* ctx);
 // zero `count` device ranges (pointer, bytes) on `stream`: batched launches of
 // one kernel (ranges of doubles on 16 bytes), the runtime fill otherwise (ctx.hip)
 int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count);
+// device -> host copy of `bytes` on `stream` (ctx.hip)
+extern "C" int smg_d2h_impl(smg_ctx* ctx, hipStream_t stream, void* dst, const void* src, size_t bytes);
 // issue the queued smg_memset_async zeroings on the zeroing stream (ctx.hip)
 extern "C" int smg_zero_flush(smg_ctx* ctx);
 // ensure the zeroing stream (also the device->host stream of the streamed
