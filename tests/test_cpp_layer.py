@@ -125,6 +125,25 @@ def test_gp_gradient_through_tape(N):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split_b", ["1", "0"])
+@pytest.mark.parametrize("N", [1024, 4096])
+def test_gp_gradient_fused_lookahead(N, split_b):
+    """The opt-in look-ahead inside the next panel's launch (SMG_FUSED_A=1:
+    the diagonal block's tiles and the rows below column block by column
+    block, published per tile; the resident rows load each block at its
+    step), with the trailing update split or whole: the reference's golden
+    gradient at 1e-10, three evaluations each."""
+    d = golden(f"gp_N{N}")
+    lines = [l.split() for l in _run("test_gp_tape", _gp_stdin(d),
+                                     env={"SMG_FUSED_A": "1", "SMG_SPLIT_B": split_b}).strip().splitlines()]
+    for row in lines[:3]:
+        vals = np.array([float(v) for v in row])
+        near_rel(vals[0], d["fx"], 1e-12, what="fx")
+        near_rel(vals[1:], d["grad"], 1e-10, what="grad")
+    assert lines[3] == ["stack", "0", "0"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N", [64, 1024])
 def test_gp_cholesky_reverse_closed_form_vs_murray(N):
     """The GP's factor has one consumer, the MVN: cholesky_decompose's reverse
