@@ -302,6 +302,10 @@ int smg_ctx_destroy(smg_ctx* ctx) {
     hipStreamSynchronize(ctx->side);
     hipStreamDestroy(ctx->side);
   }
+  if (ctx->copy_stream) {
+    hipStreamSynchronize(ctx->copy_stream);
+    hipStreamDestroy(ctx->copy_stream);
+  }
   for (hipEvent_t e : {ctx->inv_ev, ctx->inv_ev_main, ctx->inv_ev_aux, ctx->inv_ev_w})
     if (e) hipEventDestroy(e);
   for (int i = 0; i < SMG_WS_COUNT; ++i)
@@ -397,6 +401,7 @@ static void sync_all_streams(smg_ctx* ctx) {
   if (ctx->main_stream && ctx->main_stream != ctx->stream) hipStreamSynchronize(ctx->main_stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
   if (ctx->zero_stream) hipStreamSynchronize(ctx->zero_stream);
+  if (ctx->copy_stream) hipStreamSynchronize(ctx->copy_stream);
 }
 
 void* smg_host_scratch(smg_ctx* ctx, size_t bytes) {

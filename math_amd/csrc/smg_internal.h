@@ -55,6 +55,10 @@ struct smg_ctx {
   // are cleared there, overlapping the forward pass, and joined into `stream`
   // before the reverse sweep
   hipStream_t zero_stream;
+  // the streamed factor's panel packs and device->host copies (created on
+  // first use): off the zeroing stream, whose block-row chain the side
+  // stream's K^{-1} shares and with them the trailing updates wait for
+  hipStream_t copy_stream;
   hipEvent_t zero_ev_main, zero_ev_done;
   int zero_pending;
   // zeroings requested but not yet issued: they are issued at the next
