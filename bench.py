@@ -382,7 +382,21 @@ class GLM(Workload):
         fx0, g0 = self.fx.copy(), self.g.copy()
         self.step()
         ok = np.isfinite(fx0[0]) and fx0[0] == self.fx[0] and np.array_equal(g0, self.g)
-        return ok, f"fx {fx0[0]!r} vs {self.fx[0]!r}"
+        msg = f"fx {fx0[0]!r} vs {self.fx[0]!r}"
+        # at config 4's size: the value and gradient of the whole job (all
+        # ranks, after the all-reduce) against the CPU restatement over row
+        # blocks (tests/golden/make_glm_full.py), fx 1e-12, gradient 1e-10
+        path = os.path.join(ROOT, "tests", "golden", f"glm_R{self.R}_M{self.M}.json")
+        if ok and os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            want = np.array(d["grad"])
+            efx = abs(self.fx[0] - d["fx"]) / abs(d["fx"])
+            eg = float(np.max(np.abs(self.g - want) / (np.abs(want) + np.abs(want).max())))
+            ok = efx <= 1e-12 and eg <= 1e-10
+            msg += f"; vs glm_R{self.R}_M{self.M}: fx rel {efx:.2e}, grad rel {eg:.2e}"
+            self.reference_check = {"fixture": os.path.basename(path), "fx_rel": efx, "grad_rel": eg}
+        return ok, msg
 
     def units_per_step(self):
         return 1  # one full-data gradient per step across all ranks
@@ -705,7 +719,8 @@ def glm_strong(bl, args, rank, world, local, dist, timed, lib, ctx):
             "rows_per_rank": int(g.rows), "config": g.config(),
             "roofline": {k: roof[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
                                               "bytes_per_launch", "avg_launch_ms", "step_minus_glm_kernels_us")},
-            "per_rank": glm_rank_breakdown(fams, steps, tp, dist, world)}
+            "per_rank": glm_rank_breakdown(fams, steps, tp, dist, world),
+            "reference_check": getattr(g, "reference_check", None)}
 
 
 def glm_rank_breakdown(fams, steps, t_prof, dist, world):
@@ -855,6 +870,8 @@ def main():
         line.update(wl.extra(timed, args.steps))
     if getattr(wl, "parity", None):
         line["parity"] = wl.parity
+    if getattr(wl, "reference_check", None):
+        line["reference_check"] = wl.reference_check
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = wl.cpu_baseline()

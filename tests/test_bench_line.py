@@ -37,6 +37,9 @@ def test_bench_default_line_carries_glm_strong():
         assert pr[k]["min"] <= pr[k]["max"] and len(pr[k]["per_rank"]) == 1
     assert 0 < pr["glm_kernel_ms"]["min"] < g["ms_per_step"] * 1.5
     assert pr["allreduce_us"]["min"] > 0
+    # the whole job's value and gradient against the full-size fixture (guard passed, so within tolerance)
+    rc = g["reference_check"]
+    assert rc["fixture"] == "glm_R10000000_M256.json" and rc["fx_rel"] <= 1e-12 and rc["grad_rel"] <= 1e-10
     # the GP line's roofline: the dominant kernel (k_chol_panel) from HIP events,
     # its PMC bytes from the newest committed summary, the whole eval beside it
     gr = d["roofline"]
