@@ -371,12 +371,31 @@ int mvn_adj_epilogue(smg_ctx* ctx, const double* C, int n, const double* s, int 
 // copies from aux carry stored zeros.
 bool smg_inv_prog_ok(int n) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR; }
 
+// C and Y accumulate without a zeroing beforehand: C's rows k P .. (k+1) P
+// (lower) first receive row k's share, Y's column block k (every row r > k)
+// first receives row k's parts 3 / 4, so those products take beta = 0 from
+// that row / column on (smg_gemm_bz_impl) and beta = 1 before it.  Zeroing
+// the 2 n^2 doubles instead (SMG_PROG_ZERO=1, dev A/B) put 268 MB of stores
+// beside the first panel.
+static bool prog_zero() {
+  static const bool z = getenv("SMG_PROG_ZERO") && atoi(getenv("SMG_PROG_ZERO")) == 1;
+  return z;
+}
+
 int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
+  if (!prog_zero()) return SMG_OK;
   const size_t nn = (size_t)n * n;
-  // C and Y accumulate (Y's column block k of row r first receives row k's
-  // contribution, after the earlier ones: one zeroing instead of a beta split)
   const std::pair<void*, size_t> r(ws + nn, 2 * nn * sizeof(double));
   return smg_zero_ranges_impl(ctx, ctx->stream, &r, 1);
+}
+
+// the accumulated products of the parts: beta = 1 before the boundary bz
+// (rows bz > 0 / columns -bz < 0), 0 from it on; k = 0 has no earlier terms
+static int prog_acc(smg_ctx* ctx, int ta, int uplo, int m, int nc, int kk, const double* A, int lda,
+                    const double* B, int ldb, double* C, int ldc, int bz, bool first) {
+  if (prog_zero()) return smg_gemm_impl(ctx, ta, 0, uplo, m, nc, kk, 1.0, A, lda, B, ldb, 1.0, C, ldc);
+  if (first) return smg_gemm_impl(ctx, ta, 0, uplo, m, nc, kk, 1.0, A, lda, B, ldb, 0.0, C, ldc);
+  return smg_gemm_bz_impl(ctx, ta, 0, uplo, m, nc, kk, 1.0, A, lda, B, ldb, 1.0, C, ldc, 0, bz);
 }
 
 int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, double* ws, int k, int part,
@@ -400,15 +419,15 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
     case 1:  // W_{k,0:k} = -W_kk Y_k
       if (k == 0) return SMG_OK;
       return smg_gemm_impl(ctx, 0, 0, 0, P, r0, P, -1.0, Wkk, n, Y + r0, n, 0.0, W + r0, n, SMG_TRI_A_LOWER);
-    case 2:  // C (lower, leading r1 x r1) += W_k^T W_k
-      return smg_gemm_impl(ctx, 1, 0, 1, r1, r1, P, 1.0, W + r0, n, W + r0, n, 1.0, C, n);
+    case 2:  // C (lower, leading r1 x r1) += W_k^T W_k (rows r0.. first written here)
+      return prog_acc(ctx, 1, 1, r1, r1, P, W + r0, n, W + r0, n, C, n, r0, k == 0);
     case 3:  // Y_{k+1}[:, 0:r1] (+)= L_{k+1,k} W_{k,0:r1}
       if (r1 >= n) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, P, r1, P, 1.0, L + r1 + (size_t)r0 * ldl, ldl, W + r0, n, 1.0, Y + r1, n);
+      return prog_acc(ctx, 0, 0, P, r1, P, L + r1 + (size_t)r0 * ldl, ldl, W + r0, n, Y + r1, n, -r0, k == 0);
     default:  // Y_{k+2:}[:, 0:r1] (+)= L_{k+2:,k} W_{k,0:r1}
       if (r1 + P >= n) return SMG_OK;
-      return smg_gemm_impl(ctx, 0, 0, 0, n - r1 - P, r1, P, 1.0, L + r1 + P + (size_t)r0 * ldl, ldl, W + r0, n, 1.0,
-                           Y + r1 + P, n);
+      return prog_acc(ctx, 0, 0, n - r1 - P, r1, P, L + r1 + P + (size_t)r0 * ldl, ldl, W + r0, n, Y + r1 + P, n, -r0,
+                      k == 0);
   }
 }
 

@@ -550,13 +550,15 @@ int smg_memset(smg_ctx* ctx, void* dst, int v, size_t bytes) {
 
 }  // extern "C"
 
-int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count) {
+int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count,
+                         unsigned max_grid) {
   zero_ranges z{};
   size_t most = 0;
   auto launch = [&]() -> int {
     if (!z.count) return SMG_OK;
     const size_t g = (most / 2 + 255) / 256;
-    hipLaunchKernelGGL(k_zero_ranges, dim3(g < 2048 ? (g < 1 ? 1 : (unsigned)g) : 2048u), dim3(256), 0, stream, z);
+    hipLaunchKernelGGL(k_zero_ranges, dim3(g < max_grid ? (g < 1 ? 1 : (unsigned)g) : max_grid), dim3(256), 0, stream,
+                       z);
     SMG_LAUNCH_CHECK();
     z.count = 0;
     most = 0;
@@ -627,7 +629,11 @@ int smg_zero_flush(smg_ctx* ctx) {
   hipStream_t main = (ctx->side && ctx->stream == ctx->side) ? ctx->main_stream : ctx->stream;
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_main, main));
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_ev_main, 0));
-  if (int rc = smg_zero_ranges_impl(ctx, ctx->zero_stream, ctx->zero_queue.data(), (int)ctx->zero_queue.size()))
+  // (dev A/B: SMG_ZERO_GRID caps the workgroups of these zeroings, which run
+  // beside the first panel)
+  static const unsigned grid = getenv("SMG_ZERO_GRID") ? (unsigned)atoi(getenv("SMG_ZERO_GRID")) : 2048u;
+  if (int rc = smg_zero_ranges_impl(ctx, ctx->zero_stream, ctx->zero_queue.data(), (int)ctx->zero_queue.size(),
+                                    grid < 1 ? 1u : grid))
     return rc;
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_done, ctx->zero_stream));
   ctx->zero_queue.clear();

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
     int m, int n, int k, double alpha, const double* __restrict__ A, int lda,
     const double* __restrict__ B, int ldb, double beta, double* __restrict__ C,
     int ldc, int tiles_m, int ntiles, int kchunk, double* __restrict__ slab, long long sA,
-    long long sB, long long sC, int px, int ntp, int tri, double* __restrict__ C2, int ldc2) {
+    long long sB, long long sC, int px, int ntp, int tri, double* __restrict__ C2, int ldc2, int bz) {
   constexpr bool LOWT = MODE == 1 || MODE == 3;  // lower-triangle tiles
   constexpr bool UPT = MODE == 2;
   constexpr bool TRIC = LOWT || UPT;
@@ -306,7 +306,9 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
   // e = tid + 256 q -> (i = e % BM, j = e / BM), the same as the store
   constexpr int EPT = BM * BN / NT;
   constexpr bool PREFETCH_C = EPT <= 16;
-  const bool use_c = !slab && beta != 0.0;
+  // bz: tiles from row bz (bz > 0) or column -bz (bz < 0) on take beta = 0
+  // (the first contribution to a region of an accumulated product: C is not read)
+  const bool use_c = !slab && beta != 0.0 && !(bz > 0 && i0 >= bz) && !(bz < 0 && j0 >= -bz);
   double cpre[PREFETCH_C ? EPT : 1];
   if (PREFETCH_C) {
 #pragma unroll
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
 
 __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restrict__ slab,
                                 double alpha, double beta, double* __restrict__ C,
-                                int ldc, int lower) {
+                                int ldc, int lower, int bz) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long long)m * n) return;
   const int i = (int)(idx % m), j = (int)(idx / m);
@@ -431,6 +433,7 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
   double s = 0.0;
   for (int t = 0; t < splits; ++t) s += slab[(size_t)t * m * n + idx];
   double* c = C + i + (size_t)j * ldc;
+  if ((bz > 0 && i >= bz) || (bz < 0 && j >= -bz)) beta = 0.0;  // (k_gemm's bz)
   *c = (beta == 0.0) ? alpha * s : alpha * s + beta * *c;
 }
 
@@ -441,7 +444,7 @@ __global__ void k_splitk_reduce(int m, int n, int splits, const double* __restri
 // four 512 x 2560 slabs)
 __global__ __launch_bounds__(256) void k_splitk_reduce2(int m, int n, int splits, const double* __restrict__ slab,
                                                         double alpha, double beta, double* __restrict__ C, int ldc,
-                                                        int lower) {
+                                                        int lower, int bz) {
   const long long tot = (long long)m * n;
   for (smg_mn w(m >> 1, n); w.ok(); w.next()) {
     const int i = 2 * w.i, j = w.j;
@@ -463,8 +466,10 @@ __global__ __launch_bounds__(256) void k_splitk_reduce2(int m, int n, int splits
     for (; t < splits; ++t) s += *reinterpret_cast<const d2v*>(slab + (size_t)t * tot + e);
     double* c = C + i + (size_t)j * ldc;
     const bool w0 = !(lower == 1 && i < j), w1 = !(lower == 2 && i + 1 > j);
-    if (w0) c[0] = (beta == 0.0) ? alpha * s[0] : alpha * s[0] + beta * c[0];
-    if (w1) c[1] = (beta == 0.0) ? alpha * s[1] : alpha * s[1] + beta * c[1];
+    // (k_gemm's bz; an even row boundary keeps both rows of the pair on one side)
+    const double b = ((bz > 0 && i >= bz) || (bz < 0 && j >= -bz)) ? 0.0 : beta;
+    if (w0) c[0] = (b == 0.0) ? alpha * s[0] : alpha * s[0] + b * c[0];
+    if (w1) c[1] = (b == 0.0) ? alpha * s[1] : alpha * s[1] + b * c[1];
   }
 }
 
@@ -472,6 +477,8 @@ __global__ __launch_bounds__(256) void k_splitk_reduce2(int m, int n, int splits
 // time per host thread issues a MODE-4 GEMM)
 thread_local double* t_c2 = nullptr;
 thread_local int t_ldc2 = 0;
+// the beta-zero boundary of the next product (k_gemm's bz; smg_gemm_bz_impl)
+thread_local int t_bz = 0;
 
 template <int BM, int BN, int BK, bool TA, bool TB, int MODE, int KS = 1>
 int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
@@ -536,17 +543,17 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE, KS>), dim3(ntp * splits, batch), dim3(256 * KS), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
                      ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri, MODE == 4 ? t_c2 : nullptr,
-                     MODE == 4 ? t_ldc2 : 0);
+                     MODE == 4 ? t_ldc2 : 0, t_bz);
   if (splits > 1) {
     const long long tot = (long long)m * n;
     if ((m & 1) == 0) {
       const long long pairs = tot / 2;
       const int nb = (int)(pairs / 256 < 2048 ? (pairs + 255) / 256 : 2048);
       hipLaunchKernelGGL(k_splitk_reduce2, dim3(nb), dim3(256), 0, ctx->stream, m, n, splits, slab, alpha, beta,
-                         C, ldc, MODE);
+                         C, ldc, MODE, t_bz);
     } else {
       hipLaunchKernelGGL(k_splitk_reduce, dim3(smg_ceil_div(tot, 256)), dim3(256), 0,
-                         ctx->stream, m, n, splits, slab, alpha, beta, C, ldc, MODE);
+                         ctx->stream, m, n, splits, slab, alpha, beta, C, ldc, MODE, t_bz);
     }
   }
   SMG_LAUNCH_CHECK();
@@ -584,7 +591,7 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   const bool alias_a = overlaps(A, lda, TA ? k : m, TA ? m : k, C, ldc, m, n);
   const bool alias_b = overlaps(B, ldb, TB ? n : k, TB ? k : n, C, ldc, m, n);
   if (alias_a || alias_b) {
-    if (MODE == 3 || MODE == 4) return SMG_ERR_ARG;  // (the symbolic step's products never alias)
+    if (MODE == 3 || MODE == 4 || t_bz) return SMG_ERR_ARG;  // (the symbolic step's products never alias)
     if (MODE == 0 && alias_a && !alias_b && n <= 64)
       return launch<32, 64, 32, TA, TB, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
     if (MODE == 0 && alias_b && !alias_a && m <= 64)
@@ -745,6 +752,19 @@ int smg_gemm_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k,
   if (!ta && tb) return dispatch_tile<false, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   if (ta && !tb) return dispatch_tile<true, false, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   return dispatch_tile<true, true, 0>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+}
+
+// smg_gemm_impl with beta taken as 0 for C's rows from bz on (bz > 0) or its
+// columns from -bz on (bz < 0): the first contribution to that region of an
+// accumulated product, which then needs no zeroing beforehand.  |bz| must be a
+// multiple of 128 (every tile lies on one side of it).
+int smg_gemm_bz_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k, double alpha, const double* A,
+                     int lda, const double* B, int ldb, double beta, double* C, int ldc, int tri, int bz) {
+  if (bz % 128) return SMG_ERR_ARG;
+  t_bz = bz;
+  const int rc = smg_gemm_impl(ctx, ta, tb, uplo, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  t_bz = 0;
+  return rc;
 }
 
 // C = alpha op(A) op(B) + beta C (full) and C2 = tril(C) with halved diagonal

@@ -194,7 +194,8 @@ int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* 
 int smg_status_mark_impl(smg_ctx* ctx);
 // zero `count` device ranges (pointer, bytes) on `stream`: batched launches of
 // one kernel (ranges of doubles on 16 bytes), the runtime fill otherwise (ctx.hip)
-int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count);
+int smg_zero_ranges_impl(smg_ctx* ctx, hipStream_t stream, const std::pair<void*, size_t>* r, int count,
+                         unsigned max_grid = 2048);
 // device -> host copy of `bytes` on `stream` (ctx.hip)
 extern "C" int smg_d2h_impl(smg_ctx* ctx, hipStream_t stream, void* dst, const void* src, size_t bytes);
 // issue the queued smg_memset_async zeroings on the zeroing stream (ctx.hip)
@@ -218,6 +219,9 @@ int smg_trsv_lower_impl(smg_ctx* ctx, int trans, const double* L, int ldl, const
 int smg_gemm_impl(smg_ctx* ctx, int transA, int transB, int uplo, int m, int n,
                   int k, double alpha, const double* A, int lda, const double* B,
                   int ldb, double beta, double* C, int ldc, int tri = 0);
+// the same with beta taken as 0 from row bz (bz > 0) / column -bz (bz < 0) of C on
+int smg_gemm_bz_impl(smg_ctx* ctx, int ta, int tb, int uplo, int m, int n, int k, double alpha, const double* A,
+                     int lda, const double* B, int ldb, double beta, double* C, int ldc, int tri, int bz);
 
 // C = alpha op(A) op(B) + beta C and C2 = tril(C) with halved diagonal (one pass)
 int smg_gemm_dual_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda,
