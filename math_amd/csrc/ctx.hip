@@ -629,9 +629,11 @@ int smg_zero_flush(smg_ctx* ctx) {
   hipStream_t main = (ctx->side && ctx->stream == ctx->side) ? ctx->main_stream : ctx->stream;
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_main, main));
   SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_ev_main, 0));
-  // (dev A/B: SMG_ZERO_GRID caps the workgroups of these zeroings, which run
-  // beside the first panel)
-  static const unsigned grid = getenv("SMG_ZERO_GRID") ? (unsigned)atoi(getenv("SMG_ZERO_GRID")) : 2048u;
+  // at most 128 workgroups: these zeroings (the N^2 adjoints of a GP's K, K + dI
+  // and L: 400 MB at N = 4096) run beside the first panel, and at full width
+  // they had stretched it 177 -> 230 us; GP 367 -> 369-372 evals/s against 2048
+  // (same box; 64 / 32: the same within noise).  SMG_ZERO_GRID: dev A/B.
+  static const unsigned grid = getenv("SMG_ZERO_GRID") ? (unsigned)atoi(getenv("SMG_ZERO_GRID")) : 128u;
   if (int rc = smg_zero_ranges_impl(ctx, ctx->zero_stream, ctx->zero_queue.data(), (int)ctx->zero_queue.size(),
                                     grid < 1 ? 1u : grid))
     return rc;
