@@ -1055,6 +1055,121 @@ __global__ void k_inv_double_diag(int nb, int s2, const double* __restrict__ Wi,
   }
 }
 
+// The 256- and 512-level inverses of ONE 512-row block row from its 128-level
+// ones in one launch: chol_block_inverses' doubling steps
+//   level 256 (pairs q = 0, 1):  T_q = L21_q X11_q,  X21_q = -X22_q T_q
+//   level 512:                   T = L21 W256_0,     X21 = -W256_1 T
+// as four phases over IB_WG workgroups with a grid-wide counter between them
+// (the fence-free hand-off of smg_sync.h: sc1 payload stores, every wave's
+// vmcnt(0), a barrier, one counter add; sc1 loads after the poll).  Six
+// dependent launches of 32-128 tiles each took 66 us after the last panel,
+// sharing their CUs with the K^{-1} shares.  Every phase is 32 x 32 output
+// tiles on 16 x 16 x 4 f64 MFMAs (one 16 x 16 quadrant per wave); the
+// diagonal-block copies of both levels ride along.  Aux strips: ld n; L at
+// the block row's diagonal origin.
+constexpr int IB_WG = 64;
+constexpr int IB_PHASES = 4;
+
+__device__ inline void ib_sync(unsigned* ctr, unsigned target, int* status) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        atomicOr(status, (int)SMG_ERR_SYNC);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// C[32 x 32 at C] = alpha A[32 x K] B[K x 32] (column-major, sc1 loads and
+// stores); wave w takes the 16 x 16 quadrant (w & 1, w >> 1)
+__device__ inline void ib_tile(const double* A, int lda, const double* B, int ldb, int K, double alpha, double* C,
+                               int ldc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wi = (w & 1) * 16, wj = (w >> 1) * 16;
+  const int fr = lane & 15, fk = lane >> 4;
+  const double* a = A + wi + fr + (size_t)fk * lda;
+  const double* b = B + fk + (size_t)(wj + fr) * ldb;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  constexpr int U = 16;  // k-steps of 4 whose loads are all issued before their MFMAs
+  for (int k = 0; k < K; k += 4 * U) {
+    double av[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      av[u] = ld_dev(a + (size_t)(k + 4 * u) * lda);
+      bv[u] = ld_dev(b + k + 4 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) st_dev(C + (wi + fk + 4 * r) + (size_t)(wj + fr) * ldc, alpha * acc[r]);
+}
+
+// dst[rows x cols] = src (or zero when src is null); the workgroup's share
+// `part` of `parts` of the elements, sc1 loads / stores
+__device__ inline void ib_copy(const double* src, int lds, double* dst, int ldd, int rows, int cols, int part,
+                               int parts) {
+  const int tot = rows * cols;
+  for (int e = part * 256 + (int)threadIdx.x; e < tot; e += parts * 256) {
+    const int r = e % rows, c = e / rows;
+    st_dev(dst + r + (size_t)c * ldd, src ? ld_dev(src + r + (size_t)c * lds) : 0.0);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_inv_block512(const double* __restrict__ Lb, int ldl, const double* Wi,
+                                                      double* W256, double* W512, int ldw, double* T,
+                                                      unsigned* ctr, unsigned base, int* status) {
+  const int g = blockIdx.x;
+  // phase 1: T_q = L21_q X11_q (2 x 16 tiles, K = 128); the level-256 diagonal copies
+  if (g < 32) {
+    const int q = g >> 4, t = g & 15, ti = (t & 3) * 32, tj = (t >> 2) * 32;
+    const int o = q * 256;
+    ib_tile(Lb + (o + 128 + ti) + (size_t)o * ldl, ldl, Wi + o + (size_t)tj * ldw, ldw, 128, 1.0,
+            T + q * 128 * 128 + ti + (size_t)tj * 128, 128);
+  } else {  // X11 (rows o.., cols 0..128), X22 (rows o + 128.., cols 128..256), the upper-right block zero
+    const int p = g - 32;  // 32 workgroups: (q, piece) = (p >> 4, p & 15)
+    const int q = p >> 4, o = q * 256, piece = p & 15;
+    ib_copy(Wi + o, ldw, W256 + o, ldw, 128, 128, piece, 16);
+    ib_copy(Wi + o + 128, ldw, W256 + o + 128 + (size_t)128 * ldw, ldw, 128, 128, piece, 16);
+    ib_copy(nullptr, 0, W256 + o + (size_t)128 * ldw, ldw, 128, 128, piece, 16);
+  }
+  ib_sync(ctr, base + 1 * IB_WG, status);
+  // phase 2: X21_q = -X22_q T_q (2 x 16 tiles, K = 128)
+  if (g < 32) {
+    const int q = g >> 4, t = g & 15, ti = (t & 3) * 32, tj = (t >> 2) * 32;
+    const int o = q * 256;
+    ib_tile(Wi + o + 128 + ti, ldw, T + q * 128 * 128 + (size_t)tj * 128, 128, 128, -1.0,
+            W256 + o + 128 + ti + (size_t)tj * ldw, ldw);
+  }
+  ib_sync(ctr, base + 2 * IB_WG, status);
+  // phase 3: T = L21 W256_0 (64 tiles, K = 256; T reused: phase 2 has read it);
+  // the level-512 diagonal copies
+  {
+    const int ti = (g & 7) * 32, tj = (g >> 3) * 32;
+    ib_tile(Lb + 256 + ti, ldl, W256 + (size_t)tj * ldw, ldw, 256, 1.0, T + ti + (size_t)tj * 256, 256);
+    ib_copy(W256, ldw, W512, ldw, 256, 256, g, IB_WG);
+    ib_copy(W256 + 256, ldw, W512 + 256 + (size_t)256 * ldw, ldw, 256, 256, g, IB_WG);
+    ib_copy(nullptr, 0, W512 + (size_t)256 * ldw, ldw, 256, 256, g, IB_WG);
+  }
+  ib_sync(ctr, base + 3 * IB_WG, status);
+  // phase 4: X21 = -W256_1 T (64 tiles, K = 256)
+  {
+    const int ti = (g & 7) * 32, tj = (g >> 3) * 32;
+    ib_tile(W256 + 256 + ti, ldw, T + (size_t)tj * 256, 256, 256, -1.0, W512 + 256 + ti + (size_t)tj * ldw, ldw);
+  }
+  // (the fourth count: the next launch on this slot starts from base + IB_PHASES * IB_WG)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // G = tril(X) (n x n dense, ld n)
 __global__ void k_tril_copy(const double* __restrict__ X, int ldx, int n, double* __restrict__ G) {
   for (smg_mn it(n, n); it.ok(); it.next()) {
@@ -1148,6 +1263,21 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int
   // skip128: the 128 level is already there (the panel kernel's inverter forms it)
   const double* Wi = skip128 ? aux + (size_t)n * SMG_AUX_W128 + row0 : aux + row0;
   int ldi = n;
+  static_assert(SMG_NBR == 512 && SMG_NB == 64, "k_inv_block512's phases");
+  static const bool fused = !(getenv("SMG_INV_FUSED") && getenv("SMG_INV_FUSED")[0] == '0');  // dev A/B
+  if (fused && skip128 && nrows == SMG_NBR) {  // one block row: one launch (k_inv_block512)
+    double* T = Tbuf ? Tbuf : smg_ws(ctx, SMG_WS_TMP, (size_t)256 * 256);
+    if (!T) return SMG_ERR_OOM;
+    const long long e = ctx->inv_launches++;
+    unsigned* ctr = ctx->inv_ctr_d + e % SMG_INV_CTRS;
+    const unsigned base = (unsigned)((unsigned long long)(e / SMG_INV_CTRS) * (IB_PHASES * IB_WG));
+    ctx->status_armed = 1;
+    hipLaunchKernelGGL(k_inv_block512, dim3(IB_WG), dim3(256), 0, ctx->stream, L, ldl, Wi,
+                       aux + (size_t)n * SMG_AUX_W256 + row0, aux + (size_t)n * SMG_AUX_W512 + row0, n, T, ctr,
+                       base, ctx->status_d);
+    SMG_LAUNCH_CHECK();
+    return SMG_OK;
+  }
   for (int s2 = skip128 ? 4 * SMG_NB : 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
     const int s = s2 / 2, nb = nrows / s2;
     if (nb == 0) return SMG_OK;

@@ -264,6 +264,8 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   hipMemset(ctx->status_d, 0, SMG_STATUS_BYTES);
   ctx->flags_d = ctx->status_d + 64;
   ctx->flag_epoch = 0;
+  ctx->inv_ctr_d = reinterpret_cast<unsigned*>(ctx->flags_d + 4096);
+  ctx->inv_launches = 0;
   ctx->host_scratch_size = 1u << 20;
   if (hipHostMalloc(&ctx->host_scratch, ctx->host_scratch_size, hipHostMallocDefault) != hipSuccess) {
     delete ctx;

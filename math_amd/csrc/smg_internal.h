@@ -23,7 +23,9 @@ struct smg_prof_slot {
 };
 
 // device status allocation: the status word, then the panel-kernel flags
-constexpr size_t SMG_STATUS_BYTES = 256 + 4096 * sizeof(int);
+// (+ the counter ring of k_inv_block512's grid barriers: SMG_INV_CTRS slots)
+constexpr int SMG_INV_CTRS = 64;
+constexpr size_t SMG_STATUS_BYTES = 256 + 4096 * sizeof(int) + SMG_INV_CTRS * sizeof(int);
 
 struct smg_ctx {
   int device;
@@ -80,6 +82,10 @@ struct smg_ctx {
   // creation; a launch's flags count as set when they hold its epoch)
   int* flags_d;
   int flag_epoch;
+  // k_inv_block512 (cholesky.hip): a ring of monotonic grid-barrier counters
+  // after the flags, and the launches issued so far (slot = launch % ring)
+  unsigned* inv_ctr_d;
+  long long inv_launches;
   // pinned host scratch
   void* host_scratch;
   size_t host_scratch_size;

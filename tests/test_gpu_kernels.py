@@ -428,6 +428,50 @@ def test_mvn_inverse_from_progressive_factorisation(ctx):
     near_rel(ctx.get(lp1, 1), ctx.get(lp0, 1), 1e-12, what="lp")
 
 
+def test_progressive_inverses_from_nan_workspace(ctx):
+    """The progressive factorisation's by-products against numpy, from a
+    workspace and an aux buffer that start as NaN: every 512-row block row's
+    256- and 512-level diagonal-block inverses (one k_inv_block512 launch per
+    row: aux columns 64 + 128 .. and 64 + 128 + 256 .., ld N), W = L^{-1}
+    (lower) and C = K^{-1} (lower: the shares and Y accumulate with beta = 0 on
+    their first contribution, nothing is cleared beforehand).  1e-10."""
+    import ctypes
+    N = 2048
+    rng = np.random.default_rng(7)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + 0.2 * np.eye(N)
+    A = 0.5 * (A + A.T)
+    lib = ctx.lib
+    naux = lib.smg_cholesky_aux_doubles(N)
+    nws = lib.smg_cholesky_mvn_rev_ws_doubles(N)
+    dA, dL = ctx.put(F(A)), ctx.zeros(N * N)
+    dD, ws = ctx.put(np.full(naux, np.nan)), ctx.put(np.full(nws, np.nan))
+    started = ctypes.c_int(-1)
+    ctx.call("smg_cholesky_fwd_checked_mark_inv", dA, N, N, dL, N, dD, ws, ctypes.byref(started))
+    assert started.value == 2
+    st = ctypes.c_int(-1)
+    ctx.call("smg_status_mark_wait", ctypes.byref(st))
+    assert st.value == 0
+    ctx.call("smg_cholesky_inverse_wait")
+    ctx.call("smg_join_async")
+    L = np.tril(ctx.get(dL, N * N).reshape(N, N, order="F"))
+    aux = ctx.get(dD, naux).reshape(-1, N).T  # aux[:, c]: column c of the n x SMG_AUX_COLS strip set
+    for off, s2 in ((64 + 128, 256), (64 + 128 + 256, 512)):
+        for r0 in range(0, N, s2):
+            got = aux[r0:r0 + s2, off:off + s2]
+            want = np.linalg.inv(L[r0:r0 + s2, r0:r0 + s2])
+            assert np.all(np.isfinite(got)), (s2, r0)
+            near_rel(np.tril(got), np.tril(want), 1e-10, atol=1e-10 * np.abs(want).max(), what=f"W{s2} row {r0}")
+            assert not np.any(np.triu(got, 1)), (s2, r0)  # stored zeros above
+    W = ctx.get(ws, N * N).reshape(N, N, order="F")
+    Winv = np.linalg.inv(L)
+    near_rel(np.tril(W), np.tril(Winv), 1e-10, atol=1e-10 * np.abs(Winv).max(), what="W")
+    C = ctx.get(ws + 8 * N * N, N * N).reshape(N, N, order="F")
+    Kinv = np.linalg.inv(A)
+    assert np.all(np.isfinite(np.tril(C)))
+    near_rel(np.tril(C), np.tril(Kinv), 1e-9, atol=1e-10 * np.abs(Kinv).max(), what="K^-1")
+
+
 @pytest.mark.parametrize("N", [64, 300, 1024, 2048])
 def test_cholesky_rev_inverse_vs_murray(ctx, N):
     """smg_cholesky_rev_inverse (the closed form on W = L^{-1}: Abar lower +=
