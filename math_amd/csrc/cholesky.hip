@@ -1268,7 +1268,7 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int
   if (fused && skip128 && nrows == SMG_NBR) {  // one block row: one launch (k_inv_block512)
     double* T = Tbuf ? Tbuf : smg_ws(ctx, SMG_WS_TMP, (size_t)256 * 256);
     if (!T) return SMG_ERR_OOM;
-    const long long e = ctx->inv_launches++;
+    const long long e = ctx->inv_launches;  // (counted once the launch is in: a failed one adds nothing to its slot)
     unsigned* ctr = ctx->inv_ctr_d + e % SMG_INV_CTRS;
     const unsigned base = (unsigned)((unsigned long long)(e / SMG_INV_CTRS) * (IB_PHASES * IB_WG));
     ctx->status_armed = 1;
@@ -1276,6 +1276,7 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int
                        aux + (size_t)n * SMG_AUX_W256 + row0, aux + (size_t)n * SMG_AUX_W512 + row0, n, T, ctr,
                        base, ctx->status_d);
     SMG_LAUNCH_CHECK();
+    ctx->inv_launches = e + 1;
     return SMG_OK;
   }
   for (int s2 = skip128 ? 4 * SMG_NB : 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
