@@ -1828,7 +1828,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       const double slack = 22.0 * (K2 - K) / SMG_NB + 6.0 + (double)(n - K) * (K2 - K) * kk / 30e6 -
                            (K2 < n ? 6.0 + m2 * m2 * kk / 40e6 : 0.0);
       // queued against HALF that estimate: since the K^{-1} / Y parts stopped clearing their outputs and
-      // the block-row inverses became one launch, fuller budgets delayed the next (b1) and with it (a)
+      // the block-row inverses became one launch, the full estimate measures slower
       // (same-box A/Bs of the scale, r05y / r05z2 / r05z3: 0.5 380.5 and 379.9, 0.65 379.0, 1.0 374.8
       // and 376.0, 0.4 371, 0.25 373.6, 0 370.6 evals/s; SMG_SLACK_SCALE: dev override)
       static const double slack_scale = getenv("SMG_SLACK_SCALE") ? atof(getenv("SMG_SLACK_SCALE")) : 0.5;
