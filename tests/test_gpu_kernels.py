@@ -1019,6 +1019,58 @@ def test_gp_marginal_golden(ctx, N):
     near_rel(g, d["grad"], RTOL, what="grad")
 
 
+def gp_gradient_abi_closed_form(ctx, x, y, theta):
+    """The same functor on the schedule the product takes at N % 512 == 0
+    (the C++ layer's predicted closed form): the factorisation forms W = L^{-1}
+    and K^{-1} progressively (smg_cholesky_fwd_checked_mark_inv, *started ==
+    2), the MVN's forward runs on W (smg_mvn_cholesky_fwd_inv), and the
+    reverse is one pass over K^{-1} for the three hyperparameter adjoints
+    (smg_gp_inverse_adjoint) -- no Murray reverse, no add_diag / GP reverse."""
+    import ctypes
+    n = len(x)
+    a, r, s = theta
+    lib = ctx.lib
+    dx, dy = ctx.put(f64(x)), ctx.put(f64(y))
+    K, Kd, L = ctx.zeros(n * n), ctx.zeros(n * n), ctx.zeros(n * n)
+    Dinv = ctx.zeros(lib.smg_cholesky_aux_doubles(n))
+    inv_ws = ctx.zeros(lib.smg_cholesky_mvn_rev_ws_doubles(n))
+    ws, lp = ctx.zeros(2 * n), ctx.zeros(1)
+    ctx.call("smg_gp_exp_quad_cov_fwd", dx, n, a, r, K, n)
+    ctx.call("smg_add_diag_fwd", K, n, n, s * s, None, Kd, n)
+    started = ctypes.c_int(-1)
+    ctx.call("smg_cholesky_fwd_checked_mark_inv", Kd, n, n, L, n, Dinv, inv_ws, ctypes.byref(started))
+    assert started.value == 2
+    st = ctypes.c_int(-1)
+    ctx.call("smg_status_mark_wait", ctypes.byref(st))
+    assert st.value == 0
+    ctx.call("smg_cholesky_inverse_wait")
+    ctx.call("smg_mvn_cholesky_fwd_inv", dy, None, L, n, inv_ws, n, n, ws, lp)
+    fx = ctx.get(lp, 1)[0]
+    dadj, hyp = ctx.zeros(1), ctx.zeros(2)
+    s_vec = ws + 8 * n  # [w, s]: s = W^T w = K^{-1} y
+    ctx.call("smg_cholesky_mvn_rev_v", n, s_vec, 1, 2 * n, 1.0, None, n, inv_ws, 1)  # joins K^{-1}
+    ctx.call("smg_gp_inverse_adjoint", inv_ws + 8 * n * n, n, n, s_vec, 1, 2 * n, 1.0, K, n, dx, 1, a, r, dadj, hyp)
+    h = ctx.get(hyp, 2)
+    sa = ctx.get(dadj, 1)[0]
+    return fx, np.array([h[0], h[1], sa * 2 * s])
+
+
+@pytest.mark.parametrize("N", [1024, 4096])
+def test_gp_marginal_golden_closed_form(ctx, N):
+    """The headline's own schedule through the C-ABI against the reference's
+    golden value and gradient (test_gp_marginal_golden composes Murray's
+    reverse instead), twice on one context: bit-identical."""
+    d = golden(f"gp_N{N}")
+    m0 = ctx.mark()
+    fx, g = gp_gradient_abi_closed_form(ctx, d["x"], d["y"], d["theta"])
+    assert ctx.status() == 0
+    near_rel(fx, d["fx"], 1e-12, what="fx")
+    near_rel(g, d["grad"], RTOL, what="grad")
+    ctx.rewind(m0)
+    fx2, g2 = gp_gradient_abi_closed_form(ctx, d["x"], d["y"], d["theta"])
+    assert fx2 == fx and np.array_equal(g2, g)
+
+
 def test_handoff_stress_repeat_under_load(ctx):
     """The persistent kernels' fence-free hand-offs (smg_sync.h: sc1 payload,
     flag after every wave's vmcnt(0), sc1 loads after the poll) under uneven
