@@ -130,6 +130,14 @@ int smg_status_armed(smg_ctx* ctx, int* armed);
 int smg_status_enqueue(smg_ctx* ctx, int* host_dst);
 /* test hook: OR `bits` into the device status word (arms it) */
 int smg_status_inject(smg_ctx* ctx, int bits);
+/* test hook: the 256/512-level block inverses of a progressive block row by
+ * mode 0: one launch (k_inv_block512, 64 workgroups behind grid-wide counters)
+ *         when the device holds them beside a panel launch (occupancy, checked
+ *         once per context), else the six-launch chain;
+ * mode 1: always the six-launch chain */
+int smg_set_inv_block_mode(smg_ctx* ctx, int mode);
+/* 1 when mode 0 takes the one-launch form on this device, 0 if not, -1 on a null ctx */
+int smg_inv_block_fused(smg_ctx* ctx);
 
 /* ------------------------------------------------------- instrumentation ---
  * HIP-event timing of the kernel families on the context stream (used by

@@ -375,25 +375,19 @@ bool smg_inv_prog_ok(int n) { return n % SMG_NBR == 0 && n >= 2 * SMG_NBR; }
 // (lower) first receive row k's share, Y's column block k (every row r > k)
 // first receives row k's parts 3 / 4, so those products take beta = 0 from
 // that row / column on (smg_gemm_bz_impl) and beta = 1 before it.  Zeroing
-// the 2 n^2 doubles instead (SMG_PROG_ZERO=1, dev A/B) put 268 MB of stores
-// beside the first panel.
-static bool prog_zero() {
-  static const bool z = getenv("SMG_PROG_ZERO") && atoi(getenv("SMG_PROG_ZERO")) == 1;
-  return z;
-}
-
+// the 2 n^2 doubles instead put 268 MB of stores beside the first panel
+// (GP 356-362 -> 365-368 evals/s without it).
 int smg_inv_prog_init(smg_ctx* ctx, int n, double* ws) {
-  if (!prog_zero()) return SMG_OK;
-  const size_t nn = (size_t)n * n;
-  const std::pair<void*, size_t> r(ws + nn, 2 * nn * sizeof(double));
-  return smg_zero_ranges_impl(ctx, ctx->stream, &r, 1);
+  (void)ctx;
+  (void)n;
+  (void)ws;
+  return SMG_OK;
 }
 
 // the accumulated products of the parts: beta = 1 before the boundary bz
 // (rows bz > 0 / columns -bz < 0), 0 from it on; k = 0 has no earlier terms
 static int prog_acc(smg_ctx* ctx, int ta, int uplo, int m, int nc, int kk, const double* A, int lda,
                     const double* B, int ldb, double* C, int ldc, int bz, bool first) {
-  if (prog_zero()) return smg_gemm_impl(ctx, ta, 0, uplo, m, nc, kk, 1.0, A, lda, B, ldb, 1.0, C, ldc);
   if (first) return smg_gemm_impl(ctx, ta, 0, uplo, m, nc, kk, 1.0, A, lda, B, ldb, 0.0, C, ldc);
   return smg_gemm_bz_impl(ctx, ta, 0, uplo, m, nc, kk, 1.0, A, lda, B, ldb, 1.0, C, ldc, 0, bz);
 }

@@ -463,7 +463,7 @@ __device__ __forceinline__ bool panel_helped(int t, int c, int nb, int nh) {
 // inlined: its own register budget (the resident blocks live across the steps).
 __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int n, int J, int K,
                                             double* __restrict__ Dinv, int ldd, int* flags, int epoch, int* status,
-                                            int nb, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y, int Jp) {
+                                            int nb, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y) {
   constexpr int S = PANEL_MAX_STEPS;
   constexpr int R = PANEL_BELOW_ROWS;
   static_assert(R == 32, "the resident layout is lds_mma32_8w's");
@@ -474,21 +474,15 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ar = 16 * (w & 1) + (l >> 4), ac = 16 * (w >> 1) + (l & 15);  // + 4 q: this lane's rows
   double Rres[S][4];
-  // fused look-ahead (look): the other workgroups apply (a) to these rows in
-  // memory (panel_lookahead, column block c published as aflag[rb S + c]);
-  // Rres then accumulates only this panel's updates, and block j is loaded at
-  // step j, once its look-ahead tile is in
-  const bool look = Jp < J;
-  const int rb = nb + (R * (t - nb)) / SMG_NB;  // (its 64-row look-ahead tile)
 #pragma unroll
   for (int c = 0; c < S; ++c) {  // the whole tile (final: rows are independent), once
     const int cc = J + SMG_NB * c, bc = min(SMG_NB, K - cc);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = ar + 4 * q;
-      const bool in = c < nb && r < rt && ac < bc && !look;
+      const bool in = c < nb && r < rt && ac < bc;
       const int col = c < nb ? cc + min(ac, bc - 1) : J;  // (clamped in range: loads are unconditional)
-      const double v = look ? 0.0 : ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
+      const double v = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
       Rres[c][q] = in ? v : 0.0;
     }
   }
@@ -497,19 +491,6 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
     const int bj = min(SMG_NB, K - cj);
     __syncthreads();  // LDS of the previous step fully consumed
     PANEL_EV((j << 16) | (t << 8) | 5);
-    if (look) {  // block j after (a): memory + this panel's updates so far
-      panel_wait(&flags[S + 4 * S * S + rb * S + j], epoch, status);
-      const int col = cj + min(ac, bj - 1);
-#pragma unroll
-      for (int c = 0; c < S; ++c)
-        if (c == j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int r = ar + 4 * q;
-            const double v = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
-            Rres[c][q] = (r < rt && ac < bj) ? v + Rres[c][q] : 0.0;
-          }
-    }
 #pragma unroll
     for (int c = 0; c < S; ++c)  // block j into D (its current A_tj)
       if (c == j)
@@ -561,84 +542,9 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
   }
 }
 
-// The look-ahead update (a) of panel [J, K) by the previous panel [Jp, J),
-// fused into the panel's launch: A[J:, J:K] -= L[J:, Jp:J] L[J:K, Jp:J]^T in
-// 64 x 64 tiles by workgroups 0 .. na - 1, each tile published (aflag[r S +
-// c]): first the diagonal block's lower tiles (the chain's and the panel
-// tiles' rows, needed at once), then the rows below column block by column
-// block (block c is needed at step c: below_resident waits for it there).
-// Out of line: its own register budget.
-__device__ __noinline__ void panel_lookahead(double* __restrict__ L, int ldl, int n, int J, int K, int Jp, int na,
-                                             int nb, int* aflag, int epoch, lds_dbl* X, lds_dbl* Y) {
-  constexpr int S = PANEL_MAX_STEPS;
-  const int nr = (n - J + SMG_NB - 1) / SMG_NB;  // 64-row tiles from J
-  const int ntri = nb * (nb + 1) / 2, nq = ntri + (nr - nb) * nb;
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, fr = l & 15, fk = l >> 4;
-  const int i = 16 * (w & 3) + fr, t0 = 2 * (w >> 2);
-  for (int q = blockIdx.x; q < nq; q += na) {
-    int r, c;
-    if (q < ntri) {
-      r = 0;
-      while ((r + 1) * (r + 2) / 2 <= q) ++r;
-      c = q - r * (r + 1) / 2;
-    } else {  // column-major below the diagonal block
-      c = (q - ntri) / (nr - nb);
-      r = nb + (q - ntri) % (nr - nb);
-    }
-    const int r0 = J + SMG_NB * r, c0 = J + SMG_NB * c;
-    const int rr = min(SMG_NB, n - r0), cb = min(SMG_NB, K - c0);
-    d4 acc[2];
-    acc[0] = d4{0.0, 0.0, 0.0, 0.0};
-    acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-    panel_regs Ra, Rb;
-    panel_gload(Ra, L + r0 + (size_t)Jp * ldl, ldl, rr, min(SMG_NB, J - Jp), false);
-    panel_gload(Rb, L + c0 + (size_t)Jp * ldl, ldl, cb, min(SMG_NB, J - Jp), false);
-    for (int k0 = Jp; k0 < J; k0 += SMG_NB) {
-      __syncthreads();  // the previous chunk's product has read X / Y
-      panel_lstore(X, Ra);
-      panel_lstore(Y, Rb);
-      __syncthreads();
-      const int k1 = k0 + SMG_NB;
-      if (k1 < J) {  // the next chunk in flight during this product
-        panel_gload(Ra, L + r0 + (size_t)k1 * ldl, ldl, rr, min(SMG_NB, J - k1), false);
-        panel_gload(Rb, L + c0 + (size_t)k1 * ldl, ldl, cb, min(SMG_NB, J - k1), false);
-      }
-#pragma unroll 4
-      for (int kq = 0; kq < SMG_NB; kq += 4) {
-        const int kk = kq + fk;
-        const double a = X[i * SMG_NBP + kk];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const double b = Y[(16 * (t0 + t) + fr) * SMG_NBP + kk];
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const int row = 16 * (w & 3) + fk + 4 * q4, col = 16 * (t0 + t) + fr;
-        if (row < rr && col < cb && (r != c || row >= col)) {
-          double* pc = L + r0 + row + (size_t)(c0 + col) * ldl;
-          st_dev(pc, ld_dev(pc) - acc[t][q4]);
-        }
-      }
-    panel_publish(&aflag[r * S + c], epoch);
-  }
-}
-
-// a workgroup's wait for the fused look-ahead tiles of 64-row tile r (all
-// the panel's column blocks it has), before its first read of those rows
-__device__ inline void wait_look(const int* flags, int r, int nb, int epoch, int* status) {
-  constexpr int S = PANEL_MAX_STEPS;
-  panel_wait_all(flags + S + 4 * S * S + r * S, 0, min(r, nb - 1), 1, epoch, status);
-}
-
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status, int gown, int resident_ok,
-                                                    int Jp, int na) {
+                                                    int* flags, int epoch, int* status, int gown) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -652,21 +558,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   int* dinvf = flags + S + 3 * S * S;  // dinvf[j]: Dinv_j stored (the inverter workgroup)
   const int nb = (K - J + SMG_NB - 1) / SMG_NB;
   const int T = panel_tiles(n, J, nb);
-  // flags + S + 4 S^2 + r S + c: look-ahead tile (r, c) stored (na > 0: panel_lookahead / wait_look)
-  // The look-ahead update (a) of this panel's columns by the previous panel
-  // [Jp, J) (A[J:, J:K] -= L[J:, Jp:J] L[J:K, Jp:J]^T, lower trapezoid),
-  // when fused (na > 0): workgroups 0 .. na - 1 compute its 64 x 64 tiles,
-  // the diagonal block's rows first, and publish each; every other
-  // workgroup waits for the tiles of the rows it reads before its first
-  // read of them.  They are dispatched before the panel's workgroups and wait
-  // on nothing, so the grid needs no co-residency beyond the panel's own;
-  // the chain starts once the first rows' tiles are in, instead of behind a
-  // separate launch of the whole update.
-  if ((int)blockIdx.x < na) {
-    panel_lookahead(L, ldl, n, J, K, Jp, na, nb, flags + S + 4 * S * S, epoch, (lds_dbl*)X, (lds_dbl*)Y);
-    return;
-  }
-  const unsigned bid = blockIdx.x - (unsigned)na;  // the panel's own workgroup index
+  const unsigned bid = blockIdx.x;
   // Column helpers: panel tile t >= 3 (t < nb) gets workgroup gown + t - 3,
   // which applies the updates of its odd column blocks c <= t - 2 (panel_helped);
   // the owner of t does the rest, its L_tj, and waits hflag[(j-1) S + t]
@@ -678,7 +570,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // cheaper product beats the solve), the panel tiles solve against L_jj
   // (the chain needs their updates sooner).  Owners are workgroups
   // 2 .. gown - 1, column helpers gown ...
-  const int nh = gridDim.x - na - gown;
+  const int nh = gridDim.x - gown;
   if (bid == 1) {
     // ... and, behind each Dinv_j, the aux 128 level of the previous full
     // block pair (j - 2, j - 1): X = [[D1, 0], [-D2 L21 D1, D2]] (two 64^3
@@ -731,7 +623,6 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     const int t = 3 + (bid - gown);
     if (t >= nb) return;
     const int rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
-    if (na > 0) wait_look(flags, t, nb, epoch, status);
     for (int j = 0; j + 2 <= t; ++j) {
       const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
       int c0 = j + 1;
@@ -775,10 +666,6 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
     // it with L_{j+1,j} only after seeing diag[j].
     double* Dc = D;  // current diagonal block (LDS)
     double* Zn = Z;  // next one
-    if (na > 0) {
-      wait_look(flags, 0, nb, epoch, status);
-      if (nb > 1) wait_look(flags, 1, nb, epoch, status);  // (step 0 reads tile 1's rows before any owner has)
-    }
     {
       panel_regs R0;
       const int b0 = min(SMG_NB, K - J);
@@ -846,19 +733,16 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // place, and block j written out once, as L_tj -- instead of loading and
   // storing every later block at every step (the kernel fetched 2.6x and
   // wrote 2.1x its algorithmic bytes)
-  if (resident_ok && bid - 1 >= nb && bid - 1 + (gown - 2) >= T) {
+  if (bid - 1 >= nb && bid - 1 + (gown - 2) >= T) {
     below_resident(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb, (int)bid - 1, (lds_dbl*)D, (lds_dbl*)X,
-                   (lds_dbl*)Y, na > 0 ? Jp : J);
+                   (lds_dbl*)Y);
     return;
   }
-  // (fused look-ahead only with every tile its own workgroup, those below the
-  // panel resident: here only panel tiles, which wait for their rows' tiles)
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
     for (int t = 1 + (bid - 2); t < T; t += gown - 2) {
       if (t <= j) continue;  // done
-      if (j == 0 && na > 0 && t < nb) wait_look(flags, t, nb, epoch, status);
       if (t >= nb) {  // a 32-row tile below the panel: L_tj = A_tj Dinv_j^T, then A_tc -= L_tj L_cj^T (c < nb)
         constexpr int R = PANEL_BELOW_ROWS;
         const int rt0 = J + SMG_NB * nb + R * (t - nb), rt = min(R, n - rt0);
@@ -1061,7 +945,14 @@ __global__ void k_inv_double_diag(int nb, int s2, const double* __restrict__ Wi,
 //   level 512:                   T = L21 W256_0,     X21 = -W256_1 T
 // as four phases over IB_WG workgroups with a grid-wide counter between them
 // (the fence-free hand-off of smg_sync.h: sc1 payload stores, every wave's
-// vmcnt(0), a barrier, one counter add; sc1 loads after the poll).  Six
+// vmcnt(0), a barrier, one counter add; sc1 loads after the poll).  The
+// counter needs the 64 workgroups co-resident: the kernel is used only when
+// the device can hold them beside the persistent panel kernel (inv_fused_ok:
+// occupancy x CUs, checked once per context); else the six launches.  A
+// ticketed work queue (each workgroup takes its next item from an atomic
+// counter, waits only for lower tickets: deadlock-free at any residency) was
+// measured 41-56 -> 67-83 us per launch (returning device-scope atomics on one
+// address serialise beyond the XCD L2s) and GP 383 -> 358 evals/s; dropped.  Six
 // dependent launches of 32-128 tiles each took 66 us after the last panel,
 // sharing their CUs with the K^{-1} shares.  Every phase is 32 x 32 output
 // tiles on 16 x 16 x 4 f64 MFMAs (one 16 x 16 quadrant per wave); the
@@ -1251,6 +1142,38 @@ int chol_rev_blocks(smg_ctx* ctx, const double* L, int ldl, const double* Dv, in
   return SMG_OK;
 }
 
+// k_inv_block512's counter barriers need its IB_WG workgroups co-resident.
+// Nothing it runs beside waits on it, so they all get a slot once those
+// kernels drain -- unless the device cannot hold IB_WG of them at all next to
+// the persistent panel kernel's workgroups (one per CU, LDS-bound).  Checked
+// once per context from the occupancy API; the test hook smg_set_inv_block_mode
+// forces the six-launch chain.
+bool inv_fused_ok(smg_ctx* ctx) {
+  if (ctx->inv_mode == 1) return false;
+  if (ctx->inv_fused_ok < 0) {
+    // room for k_inv_block512's workgroups with a panel launch of the widest
+    // grid resident: the CUs it leaves hold `per_cu` each; a CU holding a
+    // panel workgroup (SMG_DIAG_THREADS threads: two waves per SIMD) takes one
+    // more (one wave per SIMD) when its VGPRs fit in what the panel leaves of
+    // the 512 per SIMD lane
+    int per_cu = 0, cus = 0;
+    hipFuncAttributes ai{}, ap{};
+    const bool q = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_inv_block512, 256, 0) == hipSuccess &&
+                   hipFuncGetAttributes(&ai, reinterpret_cast<const void*>(k_inv_block512)) == hipSuccess &&
+                   hipFuncGetAttributes(&ap, reinterpret_cast<const void*>(k_chol_panel)) == hipSuccess &&
+                   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess;
+    long long room = 0;
+    if (q) {
+      const int panel_cus = min(cus, PANEL_MAX_GRID + 8);
+      const int panel_waves_per_simd = SMG_DIAG_THREADS / 64 / 4;
+      const bool beside = 512 - panel_waves_per_simd * ap.numRegs >= ai.numRegs;
+      room = (long long)per_cu * (cus - panel_cus) + (beside ? panel_cus : 0);
+    }
+    ctx->inv_fused_ok = room >= IB_WG ? 1 : 0;
+  }
+  return ctx->inv_fused_ok == 1;
+}
+
 // Inverses of the full 128-, 256- and 512-row diagonal blocks of L by
 // recursive doubling from the SMG_NB-block inverses: aux (ld n) holds the
 // levels at the SMG_AUX_W* column offsets (smg_cholesky_aux_doubles).
@@ -1264,8 +1187,7 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int
   const double* Wi = skip128 ? aux + (size_t)n * SMG_AUX_W128 + row0 : aux + row0;
   int ldi = n;
   static_assert(SMG_NBR == 512 && SMG_NB == 64, "k_inv_block512's phases");
-  static const bool fused = !(getenv("SMG_INV_FUSED") && getenv("SMG_INV_FUSED")[0] == '0');  // dev A/B
-  if (fused && skip128 && nrows == SMG_NBR) {  // one block row: one launch (k_inv_block512)
+  if (skip128 && nrows == SMG_NBR && inv_fused_ok(ctx)) {  // one block row: one launch (k_inv_block512)
     double* T = Tbuf ? Tbuf : smg_ws(ctx, SMG_WS_TMP, (size_t)256 * 256);
     if (!T) return SMG_ERR_OOM;
     const long long e = ctx->inv_launches;  // (counted once the launch is in: a failed one adds nothing to its slot)
@@ -1475,6 +1397,8 @@ extern "C" {
 
 int smg_cholesky_block_size(int n) { return SMG_NB; }
 
+int smg_inv_block_fused(smg_ctx* ctx) { return ctx ? (inv_fused_ok(ctx) ? 1 : 0) : -1; }
+
 // aux = the 64-, 128-, 256- and 512-row diagonal-block inverses, n rows each, ld n
 long long smg_cholesky_aux_doubles(int n) {
   return (long long)(n > 0 ? n : 0) * SMG_AUX_COLS;
@@ -1657,9 +1581,9 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     return SMG_OK;
   };
   auto queue_shares = [&](double budget_us) -> int {  // budget < 0: every row queued on zero so far
-    // (a share may overrun the budget by this much; SMG_SHARE_TOL: dev A/B -- r05z5, three same-box
-    // pairs: 40 379.8, 0 374.4, 80 374.5, 150 375.3 evals/s)
-    static const double tol = getenv("SMG_SHARE_TOL") ? atof(getenv("SMG_SHARE_TOL")) : 40.0;
+    // (a share may overrun the budget by this much -- r05z5, three same-box pairs: 40 379.8, 0 374.4,
+    // 80 374.5, 150 375.3 evals/s)
+    constexpr double tol = 40.0;
     while (s_k < z_k) {
       const double c = smg_inv_prog_cost(n, s_k, 2, true);
       if (budget_us >= 0 && c > budget_us + tol) break;
@@ -1690,37 +1614,6 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     }
     return SMG_OK;
   };
-  // SMG_PANEL_RESIDENT=0: the rows below the panel reload and store every
-  // column block at every step (the round-4 form; tools/ubench_panel's
-  // before / after traces).  SMG_FUSED_A=1: the look-ahead (a) inside the next
-  // panel's launch (panel_lookahead) -- gaps between panels of 12-20 us, but
-  // slower overall (342-346 against 357-362 evals/s): its
-  // workgroups take CUs the concurrent trailing update and K^{-1} work need
-  static const int resident_ok = [] {
-    const char* e = getenv("SMG_PANEL_RESIDENT");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  static const bool fuse_env = [] {
-    const char* e = getenv("SMG_FUSED_A");
-    return e && e[0] == '1';
-  }();
-  // the look-ahead workgroups of the panel launch at column Jx (0: (a) runs
-  // as its own GEMM before it): only with every tile its own workgroup (the
-  // tiles below then register-resident: they wait for each column block's
-  // look-ahead at its step)
-  auto fused_at = [&](int Jx) -> int {
-    if (!fuse_env || !look || Jx <= 0 || !resident_ok) return 0;
-    const int Kx = min(Jx + NB2, n), nbx = smg_ceil_div(Kx - Jx, SMG_NB), Tx = panel_tiles(n, Jx, nbx);
-    if (Tx >= PANEL_MAX_GRID) return 0;
-    const int nr = smg_ceil_div(n - Jx, SMG_NB);
-    constexpr int S = PANEL_MAX_STEPS;
-    if (S + 4 * S * S + nr * S > 4096) return 0;  // (the flag buffer)
-    const int ntri = nbx * (nbx + 1) / 2, nq = ntri + (nr - nbx) * nbx;
-    int nhx = nbx > 3 ? nbx - 3 : 0;
-    if (Tx + 1 + nhx > PANEL_MAX_GRID + 1 || nbx > Tx) nhx = 0;
-    // the CUs the panel leaves, at least one workgroup per diagonal tile
-    return min(nq, max(ntri, PANEL_MAX_GRID - (Tx + 1) - nhx));
-  };
   for (int J = 0; J < n; J += NB2) {
     const int K = min(J + NB2, n);
     {  // the whole panel in one persistent launch (k_chol_panel)
@@ -1739,10 +1632,9 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
         const double m = n - J, b = K - J;
         ctx->prof_flops[SMG_FAM_PANEL] += m * b * b - 2.0 * b * b * b / 3.0;
       }
-      const int na = fused_at(J);
       panel_host_stamp(epoch);
-      hipLaunchKernelGGL(k_chol_panel, dim3(na + grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, resident_ok, J - NB2, na);
+      hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
     }
     if (zero_parts && J / NB2 < rows_prog) {  // this panel is final: its block row's inverses may start
       if (!(pe_ev[J / NB2] = smg_event(ctx, nev++))) return SMG_ERR_HIP;
@@ -1785,10 +1677,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     if (!E) return SMG_ERR_HIP;
     if (F) SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, F, 0));
     int rc = 0;
-    // (a) the next panel's columns (lower trapezoid), main stream -- or in
-    // the next panel's launch (fused_at)
-    if (!fused_at(K) &&
-        (rc = smg_gemm_impl(ctx, 0, 1, 1, m, K2 - K, K - J, -1.0, P, ldl, P, ldl, 1.0, L + K + (size_t)K * ldl, ldl)))
+    // (a) the next panel's columns (lower trapezoid), main stream
+    if ((rc = smg_gemm_impl(ctx, 0, 1, 1, m, K2 - K, K - J, -1.0, P, ldl, P, ldl, 1.0, L + K + (size_t)K * ldl, ldl)))
       return rc;
     SMG_HIP_TRY(hipEventRecord(E, ctx->stream));
     F = nullptr;
@@ -1798,12 +1688,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, E, 0));
       // (b) in two: (b1), the columns of the panel after next (all the next
       // look-ahead (a) waits for: F), and (b2), the rest behind it (GP
-      // 355-358 -> 358-360 evals/s in a same-box A/B; SMG_SPLIT_B=0: one (b))
-      static const bool split_b = [] {
-        const char* e = getenv("SMG_SPLIT_B");
-        return !(e && e[0] == '0');
-      }();
-      const int K3 = split_b ? min(K2 + NB2, n) : n;
+      // 355-358 -> 358-360 evals/s in a same-box A/B)
+      const int K3 = min(K2 + NB2, n);
       {
         smg_on_side on(ctx);
         rc = smg_gemm_impl(ctx, 0, 1, 1, m2, K3 - K2, K - J, -1.0, P2, ldl, P2, ldl, 1.0,
@@ -1833,9 +1719,8 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       // queued against HALF that estimate: since the K^{-1} / Y parts stopped clearing their outputs and
       // the block-row inverses became one launch, the full estimate measures slower
       // (same-box A/Bs of the scale, r05y / r05z2 / r05z3: 0.5 380.5 and 379.9, 0.65 379.0, 1.0 374.8
-      // and 376.0, 0.4 371, 0.25 373.6, 0 370.6 evals/s; SMG_SLACK_SCALE: dev override)
-      static const double slack_scale = getenv("SMG_SLACK_SCALE") ? atof(getenv("SMG_SLACK_SCALE")) : 0.5;
-      if ((rc = queue_parts(J / NB2, slack * slack_scale))) return rc;
+      // and 376.0, 0.4 371, 0.25 373.6, 0 370.6 evals/s)
+      if ((rc = queue_parts(J / NB2, 0.5 * slack))) return rc;
     }
   }
   if (prog) {  // the rest of the rows but the last

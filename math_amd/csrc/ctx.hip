@@ -266,6 +266,8 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->flag_epoch = 0;
   ctx->inv_ctr_d = reinterpret_cast<unsigned*>(ctx->flags_d + 4096);
   ctx->inv_launches = 0;
+  ctx->inv_fused_ok = -1;
+  ctx->inv_mode = 0;
   ctx->host_scratch_size = 1u << 20;
   if (hipHostMalloc(&ctx->host_scratch, ctx->host_scratch_size, hipHostMallocDefault) != hipSuccess) {
     delete ctx;
@@ -634,10 +636,8 @@ int smg_zero_flush(smg_ctx* ctx) {
   // at most 128 workgroups: these zeroings (the N^2 adjoints of a GP's K, K + dI
   // and L: 400 MB at N = 4096) run beside the first panel, and at full width
   // they had stretched it 177 -> 230 us; GP 367 -> 369-372 evals/s against 2048
-  // (same box; 64 / 32: the same within noise).  SMG_ZERO_GRID: dev A/B.
-  static const unsigned grid = getenv("SMG_ZERO_GRID") ? (unsigned)atoi(getenv("SMG_ZERO_GRID")) : 128u;
-  if (int rc = smg_zero_ranges_impl(ctx, ctx->zero_stream, ctx->zero_queue.data(), (int)ctx->zero_queue.size(),
-                                    grid < 1 ? 1u : grid))
+  // (same box; 64 / 32: the same within noise)
+  if (int rc = smg_zero_ranges_impl(ctx, ctx->zero_stream, ctx->zero_queue.data(), (int)ctx->zero_queue.size(), 128u))
     return rc;
   SMG_HIP_TRY(hipEventRecord(ctx->zero_ev_done, ctx->zero_stream));
   ctx->zero_queue.clear();
@@ -669,6 +669,12 @@ int smg_marker_record(smg_ctx* ctx, int slot) {
 int smg_marker_wait(smg_ctx* ctx, int slot) {
   if (!ctx || slot < 0 || slot >= (int)ctx->marker_ev.size()) return SMG_ERR_ARG;
   SMG_HIP_TRY(hipEventSynchronize(ctx->marker_ev[slot]));
+  return SMG_OK;
+}
+
+int smg_set_inv_block_mode(smg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 1) return SMG_ERR_ARG;
+  ctx->inv_mode = mode;
   return SMG_OK;
 }
 

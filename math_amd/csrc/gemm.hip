@@ -491,7 +491,6 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   int splits = 1;
   const int target = 512;
   constexpr int KMIN = 64;  // shortest K chunk of a split
-  static const bool nosplit = getenv("SMG_GEMM_NOSPLIT") != nullptr;  // dev (tools/ubench_gemm)
   // (a grid that already covers every CU once keeps K whole while K is short:
   // 512^3 with 32 x 32 tiles, 256 tiles: 12.3 us unsplit vs 15.9 us split
   // in two plus the reduction)
@@ -499,7 +498,7 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   // (triangular operands: every tile has its own K range, no split)
   // (MODE 3 / 4 products -- the symbolic step's, with triangular operands --
   // never split)
-  if (!nosplit && !tri && MODE != 3 && MODE != 4 && batch == 1 && ntiles < target && !covers &&
+  if (!tri && MODE != 3 && MODE != 4 && batch == 1 && ntiles < target && !covers &&
       k >= 2 * KMIN) {
     splits = smg_ceil_div(target, ntiles);
     const int maxs = k / KMIN;
@@ -616,24 +615,6 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   const long long t64 = smg_ceil_div(m, 64);
   const long long mid_tiles =
       (!FULLC && m == n) ? t64 * (t64 + 1) / 2 : t64 * smg_ceil_div(n, 64);
-  {  // dev override for tile studies (tools/ubench_gemm): SMG_GEMM_TILE=128|12864|64|32
-    static const int forced = [] {
-      const char* e = getenv("SMG_GEMM_TILE");
-      return e ? atoi(e) : 0;
-    }();
-    if (forced == 128)
-      return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-    if (forced == 12864)
-      return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-    if (forced == 64)
-      return launch<64, 64, BK64, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-    if (forced == 32)
-      return launch<32, 32, 32, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-    if (forced == 6402)
-      return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-    if (forced == 3202)
-      return launch<32, 32, 32, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-  }
   // (triangle modes keep 64 x 64 tiles: half the 128-tile grid would sit on
   // the diagonal, and the split-K those few tiles need costs a reduction; at
   // N = K = 4096 the 528-tile 128 triangle -- 2.06 waves over the CUs -- ran
@@ -661,20 +642,6 @@ int dispatch_tile(smg_ctx* ctx, int m, int n, int k, double alpha, const double*
   //   (512,512,512) 11.5 (32x32) / 10.2 (32x32 KS=2)
   // (and a 64 x 64 grid below 256 tiles, split over K or not, loses to 32 x 32:
   // (3584,256,256) 18.6 vs 28 us)
-  {  // dev: the tile of the large triangle outputs (HVP's N x N lower products)
-    static const int tri_tile = [] {
-      const char* e = getenv("SMG_GEMM_TRI");
-      return e ? atoi(e) : 0;
-    }();
-    if (!FULLC && mid_tiles > SMG_GEMM_KS2_MAX && tri_tile) {
-      if (tri_tile == 12864)
-        return launch<128, 64, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-      if (tri_tile == 128)
-        return launch<128, 128, 16, TA, TB, MODE>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-      if (tri_tile == 6402)
-        return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);
-    }
-  }
   if (mid_tiles >= 512) {
     if (mid_tiles <= SMG_GEMM_KS2_MAX)
       return launch<64, 64, BK64, TA, TB, MODE, 2>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, 0, 0, tri);

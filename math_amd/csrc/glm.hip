@@ -30,8 +30,8 @@
 // is still on chip.  Each workgroup keeps per-column accumulators in
 // registers and writes one [logp, alpha', beta'(M)] partial; a fixed-order
 // second pass sums the partials (deterministic).  The default kernel is
-// k_glm_reg (the tile stays in registers); k_glm_fused (the tile staged
-// through LDS) is kept behind SMG_GLM_REG=0 for A/B runs.
+// k_glm_reg (the tile stays in registers); the LDS-staged form measured
+// slower (below) and lives in git history.
 //
 // Measured at 1e7 x 256 on MI355X (bench.py --workload glm, same box):
 //   k_glm_fused 32 rows x 256 threads, 512 WGs   5.08 TB/s
@@ -57,119 +57,6 @@ constexpr int MMAX = 256;         // fused path: M <= 256
 // redirected, no select on the loaded value
 __device__ double g_glm_zero[2] = {0.0, 0.0};
 
-template <int RB, int KIND>
-__global__ __launch_bounds__(256) void k_glm_fused(const void* __restrict__ yv,
-                                                   const double* __restrict__ x, long long R,
-                                                   int M, long long ldx,
-                                                   const double* __restrict__ ab,
-                                                   double* __restrict__ part) {
-  const int* __restrict__ y = static_cast<const int*>(yv);
-  const double* __restrict__ yd = static_cast<const double*>(yv);
-  constexpr int XS = RB + 1;  // LDS column stride (bank-conflict free)
-  constexpr int PER = RB * MMAX / 256;
-  constexpr int G = 256 / RB;  // column groups of the eta pass
-  __shared__ double X[MMAX * XS];
-  __shared__ double beta[MMAX];
-  __shared__ double etap[G * RB];
-  __shared__ double thd[RB];
-  __shared__ double lds[16];
-  const int t = threadIdx.x;
-  if (t < M) beta[t] = ab[1 + t];
-  const double alpha = ab[0];
-  const double inv_sigma = KIND == 1 ? 1.0 / ab[1 + M] : 0.0;  // ab = [alpha, beta(M), sigma]
-  const long long ntiles = (R + RB - 1) / RB;
-  double gacc = 0.0;                 // column t's beta' accumulator (t < M)
-  double lp_acc = 0.0, ga_acc = 0.0; // rows' logp / alpha' (threads < RB)
-  double c_acc = 0.0;                // KIND 2: rows' lgamma(y + 1)
-  double reg[PER];
-
-  auto load = [&](long long tile) {
-    const long long r0 = tile * RB;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int e = t + 256 * q;
-      const int r = e % RB, c = e / RB;
-      const long long gr = r0 + r;
-      reg[q] = (c < M && gr < R) ? x[gr + (size_t)c * ldx] : 0.0;
-    }
-  };
-
-  long long tile = blockIdx.x;
-  if (tile < ntiles) load(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
-    __syncthreads();  // previous tile fully consumed
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int e = t + 256 * q;
-      X[(e / RB) * XS + (e % RB)] = reg[q];
-    }
-    __syncthreads();
-    const long long next = tile + gridDim.x;
-    if (next < ntiles) load(next);  // in flight during the compute below
-    // eta: thread (r, g) sums columns c = g, g + G, ...
-    {
-      const int r = t % RB, g = t / RB;
-      double s = 0.0;
-      for (int c = g; c < M; c += G) s += X[c * XS + r] * beta[c];
-      etap[g * RB + r] = s;
-    }
-    __syncthreads();
-    if (t < RB) {
-      const long long gr = tile * RB + t;
-      double th = 0.0;
-      if (gr < R) {
-        double eta = 0.0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) eta += etap[g * RB + t];
-        if (KIND == 0) {
-          const double sgn = 2.0 * y[gr] - 1.0;
-          const double yt = sgn * (eta + alpha);
-          const double e = exp(-yt);
-          lp_acc += yt > 20.0 ? -e : (yt < -20.0 ? yt : -log1p(e));
-          th = yt > 20.0 ? -e : (yt < -20.0 ? sgn : sgn * e / (e + 1));
-        } else if (KIND == 1) {
-          const double ys = (yd[gr] - eta - alpha) * inv_sigma;
-          lp_acc += ys * ys;
-          th = ys * inv_sigma;
-        } else {
-          const double yi = (double)y[gr];
-          const double theta = eta + alpha;
-          const double e = exp(theta);
-          lp_acc += yi * theta - e;
-          th = yi - e;
-          c_acc += lgamma(yi + 1.0);
-        }
-        ga_acc += th;
-      }
-      thd[t] = th;
-    }
-    __syncthreads();
-    if (t < M) {
-      double s = 0.0;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) s += X[t * XS + r] * thd[r];
-      gacc += s;
-    }
-  }
-  // per-block partial [logp, alpha', beta'(M) (, lgamma sum)]
-  const int W = M + 2 + (KIND == 2);
-  double* p = part + (size_t)blockIdx.x * W;
-  __syncthreads();
-  const double lp = block_sum(lp_acc, lds);
-  __syncthreads();
-  const double ga = block_sum(ga_acc, lds);
-  double cs = 0.0;
-  if (KIND == 2) {
-    __syncthreads();
-    cs = block_sum(c_acc, lds);
-  }
-  if (t == 0) {
-    p[0] = lp;
-    p[1] = ga;
-    if (KIND == 2) p[M + 2] = cs;
-  }
-  if (t < M) p[2 + t] = gacc;
-}
 
 // Register-resident variant: the tile never goes through LDS.  512 threads:
 // thread t holds row r = t & 31 of the tile and the 16 columns c = g + 16q
@@ -382,39 +269,11 @@ int glm_blocks(long long R) {
   return (int)nb;
 }
 
-// dev A/B switches: SMG_GLM_REG selects the streaming kernel (0: LDS-staged
-// k_glm_fused; 1: k_glm_reg 32 rows x 512 threads, nontemporal x loads;
-// 2: 16 x 256; 3: 16 x 512; 4: as 1 with ordinary loads),
-// SMG_GLM_NB caps the number of workgroups (<= glm_blocks(R), the workspace size)
-inline int glm_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 template <int KIND>
 int glm_launch(hipStream_t st, const void* y, const double* x, long long R, int M, long long ldx,
                const double* ab, double* ws, int check_y = 0) {
-  static const int variant = glm_env("SMG_GLM_REG", 1);
-  static const int nb_cap = glm_env("SMG_GLM_NB", 0);
-  int nb = glm_blocks(R);
-  if (nb_cap > 0 && nb_cap < nb) nb = nb_cap;
-  switch (variant) {
-    case 0:
-      hipLaunchKernelGGL((k_glm_fused<GLM_RB, KIND>), dim3(nb), dim3(256), 0, st, y, x, R, M, ldx, ab, ws);
-      break;
-    case 2:
-      hipLaunchKernelGGL((k_glm_reg<KIND, 16, 256>), dim3(nb), dim3(256), 0, st, y, x, R, M, ldx, ab, ws);
-      break;
-    case 3:
-      hipLaunchKernelGGL((k_glm_reg<KIND, 16, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
-      break;
-    case 4:
-      hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws);
-      break;
-    default:
-      hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512, true>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws,
-                         check_y);
-  }
+  const int nb = glm_blocks(R);
+  hipLaunchKernelGGL((k_glm_reg<KIND, 32, 512, true>), dim3(nb), dim3(512), 0, st, y, x, R, M, ldx, ab, ws, check_y);
   return nb;
 }
 
@@ -630,8 +489,7 @@ int smg_bernoulli_logit_glm_checked(smg_ctx* ctx, const int* y, const double* x,
                                     long long ldx, const double* ab, double* ws, double* out) {
   if (!ctx || R < 0 || M < 0 || !ab || !ws || !out) return SMG_ERR_ARG;
   if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
-  static const int variant = glm_env("SMG_GLM_REG", 1);
-  if (M > MMAX || variant != 1 || R == 0) {  // the other variants: a separate bound check
+  if (M > MMAX || R == 0) {  // the general path: a separate bound check
     int rc = smg_memset(ctx, out + M + 2, 0, sizeof(double));
     if (!rc) rc = smg_check_bounded_int(ctx, y, R, 0, 1, out + M + 2);
     if (!rc) rc = R > 0 ? smg_bernoulli_logit_glm(ctx, y, x, R, M, ldx, ab, ws, out)
@@ -649,10 +507,7 @@ int smg_bernoulli_logit_glm_io(smg_ctx* ctx, const int* y, const double* x, long
                                double alpha, const double* beta, double* ws, double* out, double* out_h) {
   if (!ctx || R < 0 || M < 0 || !ws || !out || (M > 0 && !beta)) return SMG_ERR_ARG;
   if (R > 0 && (!y || (M > 0 && (!x || ldx < R)))) return SMG_ERR_ARG;
-  static const int variant = glm_env("SMG_GLM_REG", 1);
-  static const int nb_cap = glm_env("SMG_GLM_NB", 0);
-  static const int io = glm_env("SMG_GLM_IO", 1);  // dev A/B switch: 0 = always the general path
-  if (M > MMAX || variant != 1 || R == 0 || !io) {  // the general path, then one copy back and a synchronisation
+  if (M > MMAX || R == 0) {  // the general path, then one copy back and a synchronisation
     double* ab = smg_ws(ctx, SMG_WS_GLM, (size_t)M + 1);
     double* h = (double*)smg_host_scratch(ctx, sizeof(double) * (M + 1));
     if (!ab || !h) return SMG_ERR_OOM;
@@ -667,8 +522,7 @@ int smg_bernoulli_logit_glm_io(smg_ctx* ctx, const int* y, const double* x, long
   glm_ab_arg a;
   a.v[0] = alpha;
   for (int j = 0; j < M; ++j) a.v[1 + j] = beta[j];
-  int nb = glm_blocks(R);
-  if (nb_cap > 0 && nb_cap < nb) nb = nb_cap;
+  const int nb = glm_blocks(R);
   const long long seq = out_h ? ++ctx->done_seq : 0;
   {  // (the profiling scope closes before the host waits)
     smg_prof_scope prof(ctx, SMG_FAM_GLM);

@@ -114,14 +114,6 @@ class structured_adjoint_sink {
    * ordered after its completion; null otherwise.  The consumer's forward
    * then takes the reference's products with inv_L instead of two solves. */
   virtual const double* inverse_factor() { return nullptr; }
-  /** A consumer that formed the factor's inverse W = L^{-1} (lower, zeros
-   * above) and Wt = W^T (both n x n, ld n, device, living as long as the
-   * tape) offers them: the factor's reverse may then take the closed form on
-   * W for a dense adjoint (smg_cholesky_rev_inverse) instead of Murray's. */
-  virtual void provide_inverse(const double* W, const double* Wt) {
-    (void)W;
-    (void)Wt;
-  }
 };
 
 class dev_matrix_vari {

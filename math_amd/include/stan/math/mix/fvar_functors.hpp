@@ -333,7 +333,6 @@ class chol_tangent_dev_vari : public device_vari {
     P_ = amd::alloc_doubles(nn);
     amd::check(smg_chol_tangent_fwd(amd::ctx(), L_->val_, n, L_->aux_, Ad_->val_, n, n, W_, Wt_, Y_, P_, Ld_->val_, n),
                "cholesky_decompose");
-    if (L_->sink_) L_->sink_->provide_inverse(W_, Wt_);  // (the value factor's reverse: closed form on W)
   }
   void chain() override {
     const int n = L_->rows_;

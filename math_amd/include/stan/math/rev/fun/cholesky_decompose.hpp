@@ -66,14 +66,21 @@ class add_diag_dev_vari : public device_vari, public structured_adjoint_sink {
   bool may_write_device_adjoint(const void* node) const override {
     return (A_.vi && node == A_.vi) || (dv_.vi && node == dv_.vi);
   }
+  // one deposit per sweep (a second factorisation of B writes its G densely)
   bool take_inverse_adjoint(const inverse_adjoint& d, double*) override {
     if (B_->sink_ != this) return false;
+    if (dep_.C && dep_.sweep == ChainableStack::instance_->sweep_) return false;
     dep_ = d;
     return true;
   }
+  // B's adjoint read: this sweep's deposit written densely, consumed (exp_)
+  // or not yet chained (dep_), as gp_exp_quad_cov_dev_vari::expand_adjoint
   void expand_adjoint() override {
-    if (exp_.C && exp_.sweep == ChainableStack::instance_->sweep_) exp_.expand_into(B_->adj_);
+    const size_t sw = ChainableStack::instance_->sweep_;
+    if (exp_.C && exp_.sweep == sw) exp_.expand_into(B_->adj_);
     exp_ = inverse_adjoint{};
+    if (dep_.C && dep_.sweep == sw) dep_.expand_into(B_->adj_);
+    dep_ = inverse_adjoint{};
   }
 
   void chain() override {
@@ -152,16 +159,6 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   double exp_adj_ = 0.0;
   int exp_k_ = 1;
   size_t exp_sweep_ = 0;
-  // a consumer's W = L^{-1} and W^T (provide_inverse): the dense reverse in
-  // closed form on them instead of Murray's blocked algorithm
-  const double* inv_W_ = nullptr;
-  const double* inv_Wt_ = nullptr;
-
-  void provide_inverse(const double* W, const double* Wt) override {
-    inv_W_ = W;
-    inv_Wt_ = Wt;
-  }
-
   // the deposited partials written densely into L's adjoint (what the MVN
   // would have written: one smg_mvn_cholesky_rev per observation)
   void expand(const double* ws, double adj, int k) const {
@@ -308,19 +305,6 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
       expand(dep_ws_, dep_adj_, dep_k_);
     }
     if (!deposit) record(false);
-    // SMG_CHOL_REV_INV=1: the closed form on a consumer's W = L^{-1}
-    // (2/3 N^3 multiply-adds on three triangular-cut products) instead of
-    // Murray's blocked reverse -- measured slower on the HVP
-    static const bool inv_ok = [] {
-      const char* e = std::getenv("SMG_CHOL_REV_INV");
-      return e && e[0] == '1';
-    }();
-    if (inv_W_ && inv_ok) {  // Abar (lower) += tril(G + G^T) - diag(G), G = W^T Phi(L^T tril(Lbar)) W
-      double* ws = amd::alloc_doubles(2 * nn);
-      amd::check(smg_cholesky_rev_inverse(c, L_->val_, n_, inv_W_, inv_Wt_, n_, L_->adj_, n_, n_, A_->adj_, n_, ws),
-                 "cholesky_decompose");
-      return;
-    }
     // Murray's algorithm overwrites its input and reads only its lower triangle
     double* work = amd::alloc_doubles(nn);
     amd::check(smg_copy_tril(c, n_, n_, L_->adj_, n_, work, n_), "cholesky_decompose");

@@ -68,17 +68,28 @@ class gp_exp_quad_cov_dev_vari : public device_vari, public structured_adjoint_s
   // add_diag's d') is queued right away, so that the d' a host node reads
   // before this node's chain() is complete; chain() keeps sigma', l' only if
   // no other node wrote K's adjoint, else it recomputes them from the dense sum.
+  // One deposit per sweep: a second producer (K shared by two add_diag /
+  // cholesky chains, or passed to cholesky and add_diag) is refused and
+  // writes its G densely, and chain() expands the kept deposit on top of it.
   bool take_inverse_adjoint(const inverse_adjoint& d, double* dadj) override {
     if (d.n != n_) return false;
+    if (dep_.C && dep_.sweep == ChainableStack::instance_->sweep_) return false;
     amd::check(smg_gp_inverse_adjoint(amd::ctx(), d.C, n_, n_, d.s, d.k, d.ss, d.adj, K_->val_, n_, x_, D_, sigma_d_,
                                       l_d_, dadj, (sigma_vi_ || l_vi_) ? out2_ : nullptr),
                "gp_exp_quad_cov");
     dep_ = d;
     return true;
   }
+  // K's adjoint read: the deposit of this sweep is written densely whether
+  // chain() consumed it (exp_) or has not run (dep_: a nested sweep whose
+  // window holds the depositing factor but not this node, or a read before
+  // this node's turn -- chain() then takes the dense path on the sum)
   void expand_adjoint() override {
-    if (exp_.C && exp_.sweep == ChainableStack::instance_->sweep_) exp_.expand_into(K_->adj_);
+    const size_t sw = ChainableStack::instance_->sweep_;
+    if (exp_.C && exp_.sweep == sw) exp_.expand_into(K_->adj_);
     exp_ = inverse_adjoint{};
+    if (dep_.C && dep_.sweep == sw) dep_.expand_into(K_->adj_);
+    dep_ = inverse_adjoint{};
   }
 
   void chain() override {

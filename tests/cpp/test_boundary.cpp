@@ -10,6 +10,9 @@
 //   bridge N touch                                       host-block bookkeeping of the
 //                                                        device <-> Eigen round trip
 //   chol_nan_arena N                                     cholesky gradient after NaN-poisoned arena
+//   gp_share N mode reps                                 one K with two inverse-form consumers / a
+//                                                        nested window (closed form vs dense)
+//   gp_inter_rep N variant reps x y theta                bnd::run_gp_intermediate, repeated
 #include <stan/math.hpp>
 #include <algorithm>
 
@@ -266,6 +269,78 @@ static void cmd_chol_mvn_ladj() {
   recover_memory_nested();
 }
 
+// One gp_exp_quad_cov output K with two consumers that each take an
+// inverse-form adjoint (device API, x_i = 1.1 i: a well-conditioned K):
+//   mode 0: two noise terms, K -> add_diag(K, s1) -> chol -> MVN(y1) and
+//           K -> add_diag(K, s2) -> chol -> MVN(y2)
+//   mode 1: K factored directly and through add_diag(K, s1)
+//   mode 2: a nested sweep whose window holds only the Cholesky and MVN
+//           nodes: K and Kd = add_diag(K, s1) built outside it (their nodes
+//           are not chained), the factor's deposit must still reach Kd.adj()
+// `reps` evaluations (the later ones take the predicted closed form with the
+// progressive K^{-1}); for the last: "share<mode> lp th' (sigma, l, s1, s2)
+// sum / sum of squares of K.adj() and Kd.adj()".  Compared closed form against
+// SMG_CHOL_MVN_CLOSED_FORM=0 (tests/test_boundary.py).
+static void cmd_gp_share() {
+  int N, mode, reps;
+  std::cin >> N >> mode >> reps;
+  std::vector<double> x(N), y1(N), y2(N);
+  for (int i = 0; i < N; ++i) {
+    x[i] = 1.1 * i;
+    y1[i] = std::sin(0.3 * i);
+    y2[i] = std::cos(0.7 * i) * 0.5;
+  }
+  for (int r = 0; r < reps; ++r) {
+    start_nested();
+    var sigma = 1.2, l = 0.9, s1 = 0.35, s2 = 0.6;
+    dev_var_matrix K = gp_exp_quad_cov(x, sigma, l);
+    dev_var_matrix Kd = add_diag(K, s1);
+    var lp;
+    if (mode == 2) {
+      start_nested();
+      dev_var_matrix L = cholesky_decompose(Kd);
+      lp = multi_normal_cholesky_lpdf(to_dev_data(y1), L);
+      grad(lp.vi_);
+    } else {
+      dev_var_matrix L1 = cholesky_decompose(Kd);
+      dev_var_matrix L2 = cholesky_decompose(mode == 0 ? add_diag(K, s2) : K);
+      lp = multi_normal_cholesky_lpdf(to_dev_data(y1), L1) + multi_normal_cholesky_lpdf(to_dev_data(y2), L2);
+      lp.grad();
+    }
+    std::vector<double> out = {sigma.adj(), l.adj(), s1.adj(), s2.adj()};
+    for (const auto& v : {K.adj(), Kd.adj()}) {
+      double a = 0.0, q = 0.0;
+      for (double e : v) {
+        a += e;
+        q += e * e;
+      }
+      out.push_back(a);
+      out.push_back(q);
+    }
+    if (r + 1 == reps) print("share" + std::to_string(mode), lp.val(), out);
+    if (mode == 2) recover_memory_nested();
+    recover_memory_nested();
+  }
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->host_blocks_.size());
+}
+
+// bnd::run_gp_intermediate `reps` times on the same inputs (from the second
+// evaluation on the factorisation predicts the closed form and forms K^{-1}
+// progressively with its panels); the last one's "gpi lp out..."
+static void cmd_gp_inter_rep() {
+  int N, variant, reps;
+  std::cin >> N >> variant >> reps;
+  std::vector<double> x = read_vec(size_t(N)), yv = read_vec(size_t(N)), th = read_vec(3);
+  Eigen::VectorXd y = Eigen::Map<Eigen::VectorXd>(yv.data(), N);
+  for (int r = 0; r < reps; ++r)
+    bnd::run_gp_intermediate(x, y, th.data(), variant, [&](const std::string& name, double f, const std::vector<double>& g) {
+      if (r + 1 == reps) print(name, f, g);
+    });
+  std::printf("stack %zu %zu\n", ChainableStack::instance_->var_stack_.size(),
+              ChainableStack::instance_->host_blocks_.size());
+}
+
 // bnd::run_gp_intermediate on the fixture's inputs: "gpi lp out..."
 static void cmd_gp_inter() {
   int N, variant;
@@ -308,6 +383,8 @@ int main() {
     else if (cmd == "chol_mvn_ladj") cmd_chol_mvn_ladj();
     else if (cmd == "gp_inter") cmd_gp_inter();
     else if (cmd == "gp_1d") cmd_gp_1d();
+    else if (cmd == "gp_share") cmd_gp_share();
+    else if (cmd == "gp_inter_rep") cmd_gp_inter_rep();
     else {
       std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
       return 2;

@@ -203,6 +203,60 @@ def test_gp_intermediate_adjoints(N, variant, closed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("N", [300, 1024])
+def test_gp_kernel_two_inverse_consumers(N, mode):
+    """One gp_exp_quad_cov output with two consumers that each take the
+    Cholesky closed form's inverse-form adjoint (mode 0: two add_diag ->
+    cholesky -> MVN terms; mode 1: K factored directly and through add_diag)
+    and a nested sweep whose window holds only the factor and the MVN (mode 2:
+    the deposit's receivers are not chained, Kd.adj() must still hold it).
+    Two evaluations (the second on the predicted closed form, at N = 1024
+    with the progressive K^{-1}); the hyperparameter gradient and the K / Kd
+    adjoint sums equal the dense Cholesky reverse's (SMG_CHOL_MVN_CLOSED_FORM=0)
+    at 1e-10 relative."""
+    def run(env):
+        return _parse(_run(f"gp_share {N} {mode} 2\n", env=env))
+    a, b = run(None), run({"SMG_CHOL_MVN_CLOSED_FORM": "0"})
+    tag = f"share{mode}"
+    near_rel(a[tag][0], b[tag][0], 1e-12, what="lp")
+    near_rel(a[tag][1:], b[tag][1:], RTOL, what="theta' and adjoint sums")
+    assert abs(b[tag][8]) > 0  # Kd's adjoint holds the deposit
+    if mode != 2:
+        assert np.all(np.abs(b[tag][5:9]) > 0)
+    assert list(a["stack"]) == [0.0, 0.0] and list(b["stack"]) == [0.0, 0.0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_gp_intermediate_adjoints_N1024(variant):
+    """bnd::run_gp_intermediate at N = 1024 (a 512-multiple: the second
+    evaluation forms K^{-1} progressively with the panels and deposits the
+    inverse-form adjoint through add_diag into gp_exp_quad_cov), with the
+    intermediate adjoints read after the sweep (variant 0), host consumers of
+    L (variant 1: the dense reverse) and of K / Kd (variant 2: the deposit
+    expanded into K's dense adjoint on the progressive path).  The theta
+    gradient of variant 0 against the reference's (gp_N1024.json, the same
+    model) and every intermediate adjoint against the dense Cholesky reverse
+    (SMG_CHOL_MVN_CLOSED_FORM=0), 1e-10."""
+    N = 1024
+    d = golden(f"gp_N{N}")
+    cmd = f"gp_inter_rep {N} {variant} 2 {_num(d['x'])} {_num(d['y'])} {_num(d['theta'])}\n"
+    a = _parse(_run(cmd))
+    b = _parse(_run(cmd, env={"SMG_CHOL_MVN_CLOSED_FORM": "0"}))
+    ga, gb = _gpi_split(a["gpi"][1:], N), _gpi_split(b["gpi"][1:], N)
+    near_rel(a["gpi"][0], b["gpi"][0], 1e-12, what="lp")
+    if variant == 0:
+        near_rel(a["gpi"][0], d["fx"], 1e-12, what="lp vs reference")
+        near_rel(ga[0], d["grad"], RTOL, what="grad theta vs reference")
+    near_rel(ga[0], gb[0], RTOL, what="grad theta")
+    for name, x, y in zip(("K adj", "Kd diag adj", "L adj", "L val"), ga[1:5], gb[1:5]):
+        near_rel(x, y, RTOL, atol=RTOL * float(np.abs(y).max()), what=name)
+    assert list(ga[5]) == list(gb[5])
+    assert list(a["stack"]) == [0.0, 0.0]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("closed", ["1", "0"])
 @pytest.mark.parametrize("N", [64, 256])
 def test_gp_intermediate_replaced_element(N, closed):

@@ -428,13 +428,27 @@ def test_mvn_inverse_from_progressive_factorisation(ctx):
     near_rel(ctx.get(lp1, 1), ctx.get(lp0, 1), 1e-12, what="lp")
 
 
-def test_progressive_inverses_from_nan_workspace(ctx):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_progressive_inverses_from_nan_workspace(ctx, mode):
     """The progressive factorisation's by-products against numpy, from a
     workspace and an aux buffer that start as NaN: every 512-row block row's
-    256- and 512-level diagonal-block inverses (one k_inv_block512 launch per
-    row: aux columns 64 + 128 .. and 64 + 128 + 256 .., ld N), W = L^{-1}
-    (lower) and C = K^{-1} (lower: the shares and Y accumulate with beta = 0 on
-    their first contribution, nothing is cleared beforehand).  1e-10."""
+    256- and 512-level diagonal-block inverses (aux columns 64 + 128 .. and
+    64 + 128 + 256 .., ld N), W = L^{-1} (lower) and C = K^{-1} (lower: the
+    shares and Y accumulate with beta = 0 on their first contribution, nothing
+    is cleared beforehand).  1e-10.  mode 0: one k_inv_block512 launch per
+    row (its occupancy guard must pass on an MI355X), running beside the
+    panels and the trailing-update GEMMs; mode 1: the six-launch chain, the
+    fallback when the guard fails."""
+    ctx.call("smg_set_inv_block_mode", mode)
+    try:
+        if mode == 0:
+            assert ctx.lib.smg_inv_block_fused(ctx.ptr) == 1
+        _progressive_inverses_check(ctx)
+    finally:
+        ctx.call("smg_set_inv_block_mode", 0)
+
+
+def _progressive_inverses_check(ctx):
     import ctypes
     N = 2048
     rng = np.random.default_rng(7)

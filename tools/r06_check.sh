@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-6: targeted GPU tests, smoke, then the baseline measurements (tools/r06_base.sh)
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O
+cd $GRAFT_REPO_ROOT
+TAG=${1:-r06b}
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ${TESTS:--k "two_inverse or N1024 or progressive_inverses or intermediate or closed_form"} > $O/${TAG}_pytest.log 2>&1 || { tail -40 $O/${TAG}_pytest.log; exit 1; }
+tail -3 $O/${TAG}_pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 || { tail $O/${TAG}_smoke.log; exit 1; }
+cat $O/${TAG}_smoke.log
+[ "${BASE:-1}" = 1 ] && bash tools/r06_base.sh $TAG

@@ -47,9 +47,8 @@ int main(int argc, char** argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    const char* ur = getenv("SMG_PANEL_RESIDENT");  // (the library's switch: 0 = the reloading form)
     hipLaunchKernelGGL(k_chol_panel, dim3(T + 1 + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
-                       status, T + 1, ur && ur[0] == '0' ? 0 : 1, 0, 0);
+                       status, T + 1);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
