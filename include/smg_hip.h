@@ -136,8 +136,9 @@ int smg_status_inject(smg_ctx* ctx, int bits);
  *         once per context), else the six-launch chain;
  * mode 1: always the six-launch chain */
 int smg_set_inv_block_mode(smg_ctx* ctx, int mode);
-/* 1 when mode 0 takes the one-launch form on this device, 0 if not, -1 on a null ctx */
-int smg_inv_block_fused(smg_ctx* ctx);
+/* 1 when mode 0 takes the one-launch form for an n x n factorisation on this
+ * device, 0 if not, -1 on a null ctx or n <= 0 */
+int smg_inv_block_fused(smg_ctx* ctx, int n);
 
 /* ------------------------------------------------------- instrumentation ---
  * HIP-event timing of the kernel families on the context stream (used by

@@ -1145,33 +1145,23 @@ int chol_rev_blocks(smg_ctx* ctx, const double* L, int ldl, const double* Dv, in
 // k_inv_block512's counter barriers need its IB_WG workgroups co-resident.
 // Nothing it runs beside waits on it, so they all get a slot once those
 // kernels drain -- unless the device cannot hold IB_WG of them at all next to
-// the persistent panel kernel's workgroups (one per CU, LDS-bound).  Checked
-// once per context from the occupancy API; the test hook smg_set_inv_block_mode
-// forces the six-launch chain.
-bool inv_fused_ok(smg_ctx* ctx) {
+// a panel launch of this factorisation, whose workgroups take one CU each
+// (LDS-bound; its VGPRs fill the SIMDs): the CUs the widest panel grid (the
+// first panel's) leaves must hold IB_WG.  The occupancy is queried once per
+// context; the test hook smg_set_inv_block_mode forces the six-launch chain.
+bool inv_fused_ok(smg_ctx* ctx, int n) {
   if (ctx->inv_mode == 1) return false;
-  if (ctx->inv_fused_ok < 0) {
-    // room for k_inv_block512's workgroups with a panel launch of the widest
-    // grid resident: the CUs it leaves hold `per_cu` each; a CU holding a
-    // panel workgroup (SMG_DIAG_THREADS threads: two waves per SIMD) takes one
-    // more (one wave per SIMD) when its VGPRs fit in what the panel leaves of
-    // the 512 per SIMD lane
+  if (ctx->inv_per_cu < 0) {
     int per_cu = 0, cus = 0;
-    hipFuncAttributes ai{}, ap{};
-    const bool q = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_inv_block512, 256, 0) == hipSuccess &&
-                   hipFuncGetAttributes(&ai, reinterpret_cast<const void*>(k_inv_block512)) == hipSuccess &&
-                   hipFuncGetAttributes(&ap, reinterpret_cast<const void*>(k_chol_panel)) == hipSuccess &&
-                   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess;
-    long long room = 0;
-    if (q) {
-      const int panel_cus = min(cus, PANEL_MAX_GRID + 8);
-      const int panel_waves_per_simd = SMG_DIAG_THREADS / 64 / 4;
-      const bool beside = 512 - panel_waves_per_simd * ap.numRegs >= ai.numRegs;
-      room = (long long)per_cu * (cus - panel_cus) + (beside ? panel_cus : 0);
-    }
-    ctx->inv_fused_ok = room >= IB_WG ? 1 : 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_inv_block512, 256, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+      per_cu = cus = 0;
+    ctx->inv_per_cu = per_cu;
+    ctx->inv_cus = cus;
   }
-  return ctx->inv_fused_ok == 1;
+  const int nb0 = smg_ceil_div(min(n, SMG_NBF), SMG_NB), t0 = panel_tiles(n, 0, nb0);
+  const int panel_grid = min(t0, PANEL_MAX_GRID) + 1 + (nb0 > 3 ? nb0 - 3 : 0);
+  return (long long)ctx->inv_per_cu * max(0, ctx->inv_cus - panel_grid) >= IB_WG;
 }
 
 // Inverses of the full 128-, 256- and 512-row diagonal blocks of L by
@@ -1187,7 +1177,7 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int
   const double* Wi = skip128 ? aux + (size_t)n * SMG_AUX_W128 + row0 : aux + row0;
   int ldi = n;
   static_assert(SMG_NBR == 512 && SMG_NB == 64, "k_inv_block512's phases");
-  if (skip128 && nrows == SMG_NBR && inv_fused_ok(ctx)) {  // one block row: one launch (k_inv_block512)
+  if (skip128 && nrows == SMG_NBR && inv_fused_ok(ctx, n)) {  // one block row: one launch (k_inv_block512)
     double* T = Tbuf ? Tbuf : smg_ws(ctx, SMG_WS_TMP, (size_t)256 * 256);
     if (!T) return SMG_ERR_OOM;
     const long long e = ctx->inv_launches;  // (counted once the launch is in: a failed one adds nothing to its slot)
@@ -1397,7 +1387,7 @@ extern "C" {
 
 int smg_cholesky_block_size(int n) { return SMG_NB; }
 
-int smg_inv_block_fused(smg_ctx* ctx) { return ctx ? (inv_fused_ok(ctx) ? 1 : 0) : -1; }
+int smg_inv_block_fused(smg_ctx* ctx, int n) { return ctx && n > 0 ? (inv_fused_ok(ctx, n) ? 1 : 0) : -1; }
 
 // aux = the 64-, 128-, 256- and 512-row diagonal-block inverses, n rows each, ld n
 long long smg_cholesky_aux_doubles(int n) {

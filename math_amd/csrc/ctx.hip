@@ -266,7 +266,7 @@ int smg_ctx_create(int device, size_t initial, smg_ctx** out) {
   ctx->flag_epoch = 0;
   ctx->inv_ctr_d = reinterpret_cast<unsigned*>(ctx->flags_d + 4096);
   ctx->inv_launches = 0;
-  ctx->inv_fused_ok = -1;
+  ctx->inv_per_cu = ctx->inv_cus = -1;
   ctx->inv_mode = 0;
   ctx->host_scratch_size = 1u << 20;
   if (hipHostMalloc(&ctx->host_scratch, ctx->host_scratch_size, hipHostMallocDefault) != hipSuccess) {

@@ -86,7 +86,7 @@ struct smg_ctx {
   // after the flags, and the launches issued so far (slot = launch % ring)
   unsigned* inv_ctr_d;
   long long inv_launches;
-  int inv_fused_ok;  // k_inv_block512's workgroups fit beside a panel launch (-1: not yet checked)
+  int inv_per_cu, inv_cus;  // k_inv_block512's occupancy per CU and the CUs (-1: not yet queried)
   int inv_mode;      // 1: the block inverses by the six-launch chain (smg_set_inv_block_mode, a test hook)
   // pinned host scratch
   void* host_scratch;

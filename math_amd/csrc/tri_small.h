@@ -846,6 +846,210 @@ __device__ inline void lds_potrf64_lookahead(P D, int* status) {
   if (bad) atomicOr(status, (int)SMG_ERR_NOT_PD);
 }
 
+// ---------------------------------------------------------------------------
+// x^{-1/2} to ~1 ulp: v_rsq_f64 (about 2^-22 relative) and ONE third-order
+// (Halley-type) correction r (1 + e/2 + 3 e^2 / 8), e = 1 - x r^2 -- four
+// dependent operations instead of two Newton steps' eight
+__device__ __forceinline__ double rsq_h(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  const double t = x * r;
+  const double e = __builtin_fma(-t, r, 1.0);
+  const double s = r * e;
+  const double p = __builtin_fma(0.375, e, 0.5);
+  return __builtin_fma(s, p, r);
+}
+
+// wave_factor8_pair with rsq_h roots
+__device__ __forceinline__ void wave_factor8_pair_h(double (&a)[8], int j0, bool& bad) {
+#pragma unroll
+  for (int t = 0; t < 8; t += 2) {
+    double s0[8], s1[8];
+#pragma unroll
+    for (int c = t + 2; c < 8; ++c) {
+      s0[c] = bcast(a[t], j0 + c);
+      s1[c] = bcast(a[t + 1], j0 + c);
+    }
+    const double A = bcast(a[t], j0 + t);
+    const double B = bcast(a[t], j0 + t + 1);
+    const double C = bcast(a[t + 1], j0 + t + 1);
+    const double det = __builtin_fma(A, C, -(B * B));
+    bad |= !(A > 0.0 && A < INFINITY) || !(det > 0.0 && det < INFINITY);
+    const double r1 = rsq_h(A);
+    const double rp = rsq_h(det);
+    const double r2 = (A * r1) * rp;
+    const double l21 = B * r1;
+    const double li0 = a[t] * r1;
+    const double li1 = (a[t + 1] - li0 * l21) * r2;
+    a[t] = li0;
+    a[t + 1] = li1;
+#pragma unroll
+    for (int c = t + 2; c < 8; ++c) {
+      const double lc0 = s0[c] * r1;
+      const double lc1 = (s1[c] - lc0 * l21) * r2;
+      a[c] = a[c] - li0 * lc0 - li1 * lc1;
+    }
+  }
+}
+
+// wave 0: panel j0..j0+7 with the 8 x 8 diagonal block factored UNIFORMLY
+// (every lane the same values, read as LDS broadcasts: no cross-lane traffic
+// on the pivot chain), pivots in pairs (wave_factor8_pair's 2 x 2 leading
+// minors) with rsq_h roots, then each lane solves its own row against it:
+// x_t = (a_t - sum_{q<t} x_q L_tq) / L_tt.  The diagonal rows store the
+// uniform factor.  Same accuracy class as wave_factor8_pair.
+template <typename P>
+__device__ __forceinline__ void wave_panel8_uniform(P D, int j0, bool& bad) {
+  const int i = threadIdx.x & 63;
+  double a[8], d[8][8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a[t] = D[i * SMG_NBP + j0 + t];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c <= r; ++c) d[r][c] = D[(j0 + r) * SMG_NBP + j0 + c];  // (broadcast)
+  double rinv[8];
+#pragma unroll
+  for (int t = 0; t < 8; t += 2) {
+    const double A = d[t][t], B = d[t + 1][t], C = d[t + 1][t + 1];
+    const double det = __builtin_fma(A, C, -(B * B));
+    bad |= !(A > 0.0 && A < INFINITY) || !(det > 0.0 && det < INFINITY);
+    const double r1 = rsq_h(A);
+    const double rp = rsq_h(det);
+    const double r2 = (A * r1) * rp;  // (C - l21^2)^{-1/2}
+    const double l21 = B * r1;
+    d[t][t] = A * r1;
+    d[t + 1][t] = l21;
+    d[t + 1][t + 1] = (det * rp) * r1;  // sqrt(det / A)
+    rinv[t] = r1;
+    rinv[t + 1] = r2;
+#pragma unroll
+    for (int c = t + 2; c < 8; ++c) {
+      const double lc0 = d[c][t] * r1;
+      d[c][t] = lc0;
+      d[c][t + 1] = (d[c][t + 1] - lc0 * l21) * r2;
+    }
+#pragma unroll
+    for (int c = t + 2; c < 8; ++c)
+#pragma unroll
+      for (int c2 = t + 2; c2 <= c; ++c2) d[c][c2] = d[c][c2] - d[c][t] * d[c2][t] - d[c][t + 1] * d[c2][t + 1];
+  }
+  double x[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    double v = a[t];
+#pragma unroll
+    for (int q = 0; q < t; ++q) v -= x[q] * d[t][q];
+    x[t] = v * rinv[t];
+  }
+  if (i >= j0 + 8) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) D[i * SMG_NBP + j0 + t] = x[t];
+  } else if (i >= j0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (i == j0 + r)
+#pragma unroll
+        for (int t = 0; t <= r; ++t) D[i * SMG_NBP + j0 + t] = d[r][t];
+  }
+}
+
+// The look-ahead factor with selectable pieces (tools/ubench_factor):
+//   PANEL 0: wave_factor8_pair (readlane broadcasts, Newton roots)
+//         1: wave_factor8_pair_h (readlane broadcasts, rsq_h roots)
+//         2: wave_panel8_uniform (uniform diagonal block, rsq_h roots)
+//   AMFMA:  the next panel's rank-8 update (A) on the matrix cores (waves
+//           1..4, one 16-row tile each, 2 MFMAs) instead of one element per
+//           thread of waves 1..7 (17 LDS loads each)
+template <int PANEL, bool AMFMA, typename P>
+__device__ inline void lds_potrf64_v3(P D, int* status) {
+  const int i = threadIdx.x & 63;
+  const int g = threadIdx.x >> 6;
+  bool bad = false;
+  auto panel = [&](int j0) {
+    if (PANEL == 2) {
+      wave_panel8_uniform(D, j0, bad);
+    } else {
+      double a[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) a[t] = (i >= j0) ? D[i * SMG_NBP + j0 + t] : 0.0;
+      if (PANEL == 1)
+        wave_factor8_pair_h(a, j0, bad);
+      else
+        wave_factor8_pair(a, j0, bad);
+      wave_store8(D, a, j0);
+    }
+  };
+  if (g == 0) panel(0);
+  __syncthreads();
+  for (int p = 0; p < 7; ++p) {
+    const int j0 = 8 * p, c1 = j0 + 8, c2 = j0 + 16;
+    if (AMFMA) {
+      // (A): rows >= c1 of columns c1..c1+7 -= L[:, j0:j0+8] L[c1:c1+8, j0:j0+8]^T,
+      // 16-row tiles ti = (c1 >> 4) + g - 1 on waves g = 1..; B's columns past
+      // c1 + 7 are clamped rows (their outputs are dropped)
+      const int ti = (c1 >> 4) + g - 1;
+      if (g >= 1 && ti < 4) {
+        const int fr = i & 15, fk = i >> 4;
+        const int brow = min(c1 + fr, 63);
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < 8; k0 += 4) {
+          const double av = D[(16 * ti + fr) * SMG_NBP + j0 + k0 + fk];
+          const double bv = D[brow * SMG_NBP + j0 + k0 + fk];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        const int col = c1 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ti + fk + 4 * r;
+          if (fr < 8 && row >= col) D[row * SMG_NBP + col] -= acc[r];
+        }
+      }
+    } else if (g > 0) {
+      const int e = threadIdx.x - 64;
+      const int r = c1 + (e >> 3), c = c1 + (e & 7);
+      if (r < 64 && r >= c) {
+        double v = D[r * SMG_NBP + c];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v -= D[r * SMG_NBP + j0 + t] * D[c * SMG_NBP + j0 + t];
+        D[r * SMG_NBP + c] = v;
+      }
+    }
+    __syncthreads();
+    // (B) wave 0 factors panel p+1 while waves 1..7 update columns >= c2
+    if (g == 0) {
+      panel(c1);
+    } else if (c2 < 64) {
+      const int t0 = c2 >> 4, nt = 4 - t0, ntiles = nt * (nt + 1) / 2;
+      const int fr = i & 15, fk = i >> 4;
+      for (int q = g - 1; q < ntiles; q += 7) {
+        int ti = 0, rem = q;
+        while (rem > ti) {
+          rem -= ti + 1;
+          ++ti;
+        }
+        const int tj = rem + t0;
+        ti += t0;
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < 8; k0 += 4) {
+          const double av = D[(16 * ti + fr) * SMG_NBP + j0 + k0 + fk];
+          const double bv = D[(16 * tj + fr) * SMG_NBP + j0 + k0 + fk];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        const int col = 16 * tj + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ti + fk + 4 * r;
+          if (col >= c2 && row >= col) D[row * SMG_NBP + col] -= acc[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (bad) atomicOr(status, (int)SMG_ERR_NOT_PD);
+}
+
 // Pieces of X = L^{-1} (64x64) on 16x16 blocks, shared by lds_trtri64_mfma
 // and the fused lds_potrf_trtri64 (same arithmetic, same order: same bits).
 // Leaf k (one wave, lane c < 16 owns column c): X_kk = L_kk^{-1} by

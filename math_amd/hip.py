@@ -48,7 +48,7 @@ _SIGS = {
     "smg_status_enqueue": (_I, [_P, _P]),
     "smg_status_inject": (_I, [_P, _I]),
     "smg_set_inv_block_mode": (_I, [_P, _I]),
-    "smg_inv_block_fused": (_I, [_P]),
+    "smg_inv_block_fused": (_I, [_P, _I]),
     "smg_pinned_io": (_P, [_P, _S]),
     "smg_pinned_result": (_P, [_P, _S]),
     "smg_gather_scalars": (_I, [_P, _P, _I, _P, _P]),

@@ -442,7 +442,7 @@ def test_progressive_inverses_from_nan_workspace(ctx, mode):
     ctx.call("smg_set_inv_block_mode", mode)
     try:
         if mode == 0:
-            assert ctx.lib.smg_inv_block_fused(ctx.ptr) == 1
+            assert ctx.lib.smg_inv_block_fused(ctx.ptr, 2048) == 1 and ctx.lib.smg_inv_block_fused(ctx.ptr, 4096) == 1
         _progressive_inverses_check(ctx)
     finally:
         ctx.call("smg_set_inv_block_mode", 0)
