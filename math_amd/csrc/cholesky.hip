@@ -305,29 +305,21 @@ static inline void panel_host_stamp(int) {}
 // spills inlined); the LDS pointers are typed address_space(3) so the
 // callees keep ds_ instructions (a generic pointer would turn them into flat
 // accesses).  Same arithmetic in the same order as inlined.
-// the chain's factorisation takes its pivots two at a time (wave_factor8_pair)
-#ifndef SMG_FACTOR_PAIR
-#define SMG_FACTOR_PAIR 1
-#endif
 typedef __attribute__((address_space(3))) double lds_dbl;
-__device__ __noinline__ void chain_factor(lds_dbl* D, int* status) {
-  lds_potrf64_lookahead<SMG_FACTOR_PAIR != 0>(D, status);
-}
+// the chain's factorisation: 8-column panels whose pivots are taken two at a
+// time (wave_factor8_pair2: the 2 x 2 leading minors' two roots side by side,
+// rsq_h roots, the later columns updated with the factor's own entries
+// broadcast from the lanes that form them)
+__device__ __noinline__ void chain_factor(lds_dbl* D, int* status) { lds_potrf64_v3<3, false>(D, status); }
 // the chain's leaves also stored (sc1) into the diagonal 16 x 16 blocks of
 // Dinv_j (G = Dinv + cj, ld ldg; the inverter later writes the same bits
 // there), published with diag[j]: the panel tiles load them instead of
 // recomputing them
 __device__ __noinline__ void chain_leaves_pub(const lds_dbl* D, lds_dbl* X, double* G, int ldg, int b) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
   if (w >= 4) return;
   trtri_leaf16(D, X, w);
-  // the wave's whole leaf, 4 values per lane, rows fastest (128-byte column
-  // runs); read back from LDS after the wave's own writes
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = l + 64 * q, r = 16 * w + (e & 15), c = 16 * w + (e >> 4);
-    if (r < b && c < b) st_dev(&G[r + (size_t)c * ldg], X[r * SMG_NBP + c]);
-  }
+  leaf16_store((const lds_dbl*)X, G, ldg, b, w);
 }
 __device__ __noinline__ void chain_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) { lds_trsm64_rt(Y, D, X); }
 __device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }

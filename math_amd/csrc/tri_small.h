@@ -891,6 +891,41 @@ __device__ __forceinline__ void wave_factor8_pair_h(double (&a)[8], int j0, bool
   }
 }
 
+// The pairs with the fewest operations: rsq_h roots, and the later columns
+// updated with the factor's own entries broadcast from the lanes that form
+// them (li0 / li1 of lane j0 + c are L[c][t] / L[c][t+1]): per column and pair
+// two FMAs (wave_factor8_pair recomputes both entries on every lane from
+// pre-broadcast raw values: five operations).  PRE: the next pair's two
+// columns' entries are broadcast first, the rest after their update.
+template <bool PRE = true>
+__device__ __forceinline__ void wave_factor8_pair2(double (&a)[8], int j0, bool& bad) {
+#pragma unroll
+  for (int t = 0; t < 8; t += 2) {
+    const double A = bcast(a[t], j0 + t);
+    const double B = bcast(a[t], j0 + t + 1);
+    const double C = bcast(a[t + 1], j0 + t + 1);
+    const double det = __builtin_fma(A, C, -(B * B));
+    bad |= !(A > 0.0 && A < INFINITY) || !(det > 0.0 && det < INFINITY);
+    const double r1 = rsq_h(A);
+    const double rp = rsq_h(det);
+    const double r2 = (A * r1) * rp;
+    const double l21 = B * r1;
+    const double li0 = a[t] * r1;
+    const double li1 = (a[t + 1] - li0 * l21) * r2;
+    a[t] = li0;
+    a[t + 1] = li1;
+    if (PRE && t + 2 < 8) {  // the next pair's columns first (its pivots' chain)
+#pragma unroll
+      for (int c = t + 2; c < t + 4; ++c) a[c] = a[c] - li0 * bcast(li0, j0 + c) - li1 * bcast(li1, j0 + c);
+#pragma unroll
+      for (int c = t + 4; c < 8; ++c) a[c] = a[c] - li0 * bcast(li0, j0 + c) - li1 * bcast(li1, j0 + c);
+    } else {
+#pragma unroll
+      for (int c = t + 2; c < 8; ++c) a[c] = a[c] - li0 * bcast(li0, j0 + c) - li1 * bcast(li1, j0 + c);
+    }
+  }
+}
+
 // wave 0: panel j0..j0+7 with the 8 x 8 diagonal block factored UNIFORMLY
 // (every lane the same values, read as LDS broadcasts: no cross-lane traffic
 // on the pivot chain), pivots in pairs (wave_factor8_pair's 2 x 2 leading
@@ -957,6 +992,7 @@ __device__ __forceinline__ void wave_panel8_uniform(P D, int j0, bool& bad) {
 //   PANEL 0: wave_factor8_pair (readlane broadcasts, Newton roots)
 //         1: wave_factor8_pair_h (readlane broadcasts, rsq_h roots)
 //         2: wave_panel8_uniform (uniform diagonal block, rsq_h roots)
+//         3: wave_factor8_pair2 (the factor's own entries broadcast, rsq_h roots)
 //   AMFMA:  the next panel's rank-8 update (A) on the matrix cores (waves
 //           1..4, one 16-row tile each, 2 MFMAs) instead of one element per
 //           thread of waves 1..7 (17 LDS loads each)
@@ -974,6 +1010,8 @@ __device__ inline void lds_potrf64_v3(P D, int* status) {
       for (int t = 0; t < 8; ++t) a[t] = (i >= j0) ? D[i * SMG_NBP + j0 + t] : 0.0;
       if (PANEL == 1)
         wave_factor8_pair_h(a, j0, bad);
+      else if (PANEL == 3)
+        wave_factor8_pair2(a, j0, bad);
       else
         wave_factor8_pair(a, j0, bad);
       wave_store8(D, a, j0);
@@ -1050,6 +1088,13 @@ __device__ inline void lds_potrf64_v3(P D, int* status) {
   if (bad) atomicOr(status, (int)SMG_ERR_NOT_PD);
 }
 
+// A wave's 16 x 16 leaf inverse k (the diagonal block of X written by
+// trtri_leaf16) stored (sc1) into G (ld ldg; rows / columns < b): 4 values
+// per lane, rows fastest (128-byte column runs), read back from LDS after the
+// wave's own writes
+template <typename P>
+__device__ __forceinline__ void leaf16_store(const P X, double* G, int ldg, int b, int k);
+
 // Pieces of X = L^{-1} (64x64) on 16x16 blocks, shared by lds_trtri64_mfma
 // and the fused lds_potrf_trtri64 (same arithmetic, same order: same bits).
 // Leaf k (one wave, lane c < 16 owns column c): X_kk = L_kk^{-1} by
@@ -1073,6 +1118,43 @@ __device__ __forceinline__ void trtri_leaf16(CP D, P X, int k) {
     x[r] = x[r] * rv[r];
 #pragma unroll
     for (int q = r + 1; q < 16; ++q) x[q] -= D[(r0 + q) * SMG_NBP + r0 + r] * x[r];
+  }
+  if (l < 16)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) X[(r0 + r) * SMG_NBP + r0 + l] = x[r];
+}
+// trtri_leaf16 with its LDS reads pipelined: every diagonal entry at the
+// start, then column r + 1's entries below the diagonal issued before step r's
+// FMAs consume column r's (the compiler's own schedule waited for the LDS
+// after nearly every read: ~3 us per leaf).  Same arithmetic, same order.
+template <typename CP, typename P>
+__device__ __forceinline__ void trtri_leaf16_p(CP D, P X, int k) {
+  const int l = threadIdx.x & 63;
+  const int r0 = 16 * k;
+  double x[16], rv[16], cur[16], nxt[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rv[r] = D[(r0 + r) * SMG_NBP + r0 + r];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) cur[q] = D[(r0 + q) * SMG_NBP + r0];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const double dd = rv[r];
+    double rr = __builtin_amdgcn_rcp(dd);
+    rr = rr * (2.0 - dd * rr);
+    rv[r] = rr * (2.0 - dd * rr);
+    x[r] = (l == r) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (r + 1 < 16) {
+#pragma unroll
+      for (int q = r + 2; q < 16; ++q) nxt[q] = D[(r0 + q) * SMG_NBP + r0 + r + 1];
+    }
+    x[r] = x[r] * rv[r];
+#pragma unroll
+    for (int q = r + 1; q < 16; ++q) x[q] -= cur[q] * x[r];
+#pragma unroll
+    for (int q = r + 2; q < 16; ++q) cur[q] = nxt[q];
   }
   if (l < 16)
 #pragma unroll
@@ -1138,6 +1220,18 @@ __device__ inline void lds_trtri64_mfma(CP D, P X, P T) {
     __syncthreads();
     if (w < p) trtri_x_tile(X, T, p, w);
     __syncthreads();
+  }
+}
+
+template <typename P>
+__device__ __forceinline__ void leaf16_store(const P X, double* G, int ldg, int b, int k) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = l + 64 * q, r = 16 * k + (e & 15), c = 16 * k + (e >> 4);
+    if (r < b && c < b)
+      __hip_atomic_store(&G[r + (size_t)c * ldg], (double)X[r * SMG_NBP + c], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

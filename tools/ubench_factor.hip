@@ -25,6 +25,7 @@ template <int V> __device__ __noinline__ void fac(lds_dbl* D, int* st) {
   if (V == 3) lds_potrf64_v3<0, true>(D, st);
   if (V == 4) lds_potrf64_v3<1, true>(D, st);
   if (V == 5) lds_potrf64_v3<2, true>(D, st);
+  if (V == 6) lds_potrf64_v3<3, false>(D, st);
 }
 template <int V>
 __global__ __launch_bounds__(512) void k_fac(const double* g, double* out, long long* cyc, int* st) {
@@ -39,10 +40,30 @@ __global__ __launch_bounds__(512) void k_fac(const double* g, double* out, long 
   for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) out[e] = D[(e >> 6) * SMG_NBP + (e & 63)];
 }
 
+template <int V>
+__global__ __launch_bounds__(512) void k_leaf(const double* g, double* out, long long* cyc) {
+  __shared__ double D[SMG_NB * SMG_NBP];
+  __shared__ double X[SMG_NB * SMG_NBP];
+  lds_load_block(D, g, 64, 64, true);
+  for (int e = threadIdx.x; e < SMG_NB * SMG_NBP; e += blockDim.x) X[e] = 0.0;
+  __syncthreads();
+  if (threadIdx.x < 64) lds_potrf64_lookahead<true>((lds_dbl*)D, (int*)(cyc + 8));
+  __syncthreads();
+  const long long t0 = stamp();
+  const int w = threadIdx.x >> 6;
+  if (V == 0 && w < 4) trtri_leaf16((const lds_dbl*)D, (lds_dbl*)X, w);
+  if (V == 1 && w < 4) trtri_leaf16_p((const lds_dbl*)D, (lds_dbl*)X, w);
+  if (V == 2 && w == 0) trtri_leaf16_p((const lds_dbl*)D, (lds_dbl*)X, 3);
+  __syncthreads();
+  const long long t1 = stamp();
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) out[e] = X[(e >> 6) * SMG_NBP + (e & 63)];
+}
+
 int main() {
-  const char* names[6] = {"lookahead pairs (lib)", "pairs + rsq_h", "uniform + rsq_h", "pairs + MFMA (A)",
-                          "pairs rsq_h + MFMA (A)", "uniform + MFMA (A)"};
-  void (*ks[6])(const double*, double*, long long*, int*) = {k_fac<0>, k_fac<1>, k_fac<2>, k_fac<3>, k_fac<4>, k_fac<5>};
+  const char* names[7] = {"lookahead pairs (lib)", "pairs + rsq_h", "uniform + rsq_h", "pairs + MFMA (A)",
+                          "pairs rsq_h + MFMA (A)", "uniform + MFMA (A)", "pair2 (own entries bcast)"};
+  void (*ks[7])(const double*, double*, long long*, int*) = {k_fac<0>, k_fac<1>, k_fac<2>, k_fac<3>, k_fac<4>, k_fac<5>, k_fac<6>};
   double *dA, *dO;
   long long* dc;
   int* dst;
@@ -74,7 +95,7 @@ int main() {
     for (auto v : Lr) lmax = std::max(lmax, std::fabs(v));
     hipMemcpy(dA, h.data(), 4096 * 8, hipMemcpyHostToDevice);
     std::printf("%s block:\n", mat == 0 ? "diagonally dominant" : "GP kernel (l = 0.3, jitter 1e-4)");
-    for (int v = 0; v < 6; ++v) {
+    for (int v = 0; v < 7; ++v) {
       long long best = 1LL << 60;
       std::vector<double> o(4096);
       for (int rep = 0; rep < 5; ++rep) {
@@ -93,6 +114,30 @@ int main() {
         for (int c = 0; c <= r; ++c) err = std::max(err, std::fabs((long double)o[r * 64 + c] - Lr[r * 64 + c]));
       std::printf("  %-24s %6lld cycles (%.2f us)  max|L - L_ref| / max|L| %.2e  status %d\n", names[v], best,
                   best / 2400.0, (double)(err / lmax), st);
+    }
+  }
+  {  // leaf inverses: the library's trtri_leaf16 vs the pipelined one (4 waves / one wave)
+    std::vector<double> h(4096), o0(4096), o1(4096);
+    for (int j = 0; j < 64; ++j)
+      for (int i = 0; i < 64; ++i) h[i + 64 * j] = (i == j ? 64.0 : 0.0) + 1.0 / (1 + i + j);
+    hipMemcpy(dA, h.data(), 4096 * 8, hipMemcpyHostToDevice);
+    void (*kl[3])(const double*, double*, long long*) = {k_leaf<0>, k_leaf<1>, k_leaf<2>};
+    const char* nl[3] = {"trtri_leaf16 x4 waves", "trtri_leaf16_p x4 waves", "trtri_leaf16_p one leaf"};
+    for (int v = 0; v < 3; ++v) {
+      long long best = 1LL << 60;
+      for (int rep = 0; rep < 5; ++rep) {
+        hipLaunchKernelGGL(kl[v], dim3(1), dim3(512), 0, 0, dA, dO, dc);
+        hipDeviceSynchronize();
+        long long c;
+        hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+        best = std::min(best, c);
+      }
+      hipMemcpy(v == 0 ? o0.data() : o1.data(), dO, 4096 * 8, hipMemcpyDeviceToHost);
+      int diff = 0;
+      if (v == 1)
+        for (int e = 0; e < 4096; ++e) diff += o0[e] != o1[e];
+      std::printf("  %-24s %6lld cycles (%.2f us)%s\n", nl[v], best, best / 2400.0,
+                  v == 1 ? (diff ? "  DIFFERENT bits" : "  same bits") : "");
     }
   }
   return 0;
