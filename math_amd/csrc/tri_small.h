@@ -1123,43 +1123,6 @@ __device__ __forceinline__ void trtri_leaf16(CP D, P X, int k) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) X[(r0 + r) * SMG_NBP + r0 + l] = x[r];
 }
-// trtri_leaf16 with its LDS reads pipelined: every diagonal entry at the
-// start, then column r + 1's entries below the diagonal issued before step r's
-// FMAs consume column r's (the compiler's own schedule waited for the LDS
-// after nearly every read: ~3 us per leaf).  Same arithmetic, same order.
-template <typename CP, typename P>
-__device__ __forceinline__ void trtri_leaf16_p(CP D, P X, int k) {
-  const int l = threadIdx.x & 63;
-  const int r0 = 16 * k;
-  double x[16], rv[16], cur[16], nxt[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) rv[r] = D[(r0 + r) * SMG_NBP + r0 + r];
-#pragma unroll
-  for (int q = 1; q < 16; ++q) cur[q] = D[(r0 + q) * SMG_NBP + r0];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const double dd = rv[r];
-    double rr = __builtin_amdgcn_rcp(dd);
-    rr = rr * (2.0 - dd * rr);
-    rv[r] = rr * (2.0 - dd * rr);
-    x[r] = (l == r) ? 1.0 : 0.0;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    if (r + 1 < 16) {
-#pragma unroll
-      for (int q = r + 2; q < 16; ++q) nxt[q] = D[(r0 + q) * SMG_NBP + r0 + r + 1];
-    }
-    x[r] = x[r] * rv[r];
-#pragma unroll
-    for (int q = r + 1; q < 16; ++q) x[q] -= cur[q] * x[r];
-#pragma unroll
-    for (int q = r + 2; q < 16; ++q) cur[q] = nxt[q];
-  }
-  if (l < 16)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) X[(r0 + r) * SMG_NBP + r0 + l] = x[r];
-}
 // T_q = -L[p, q:p] X[q:p, q] accumulated over k in [kb, ke) (multiples of 8,
 // from 16q): two MFMA chains (even / odd k-steps of 4), summed at the store
 template <typename CP, typename XP>

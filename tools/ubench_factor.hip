@@ -47,13 +47,12 @@ __global__ __launch_bounds__(512) void k_leaf(const double* g, double* out, long
   lds_load_block(D, g, 64, 64, true);
   for (int e = threadIdx.x; e < SMG_NB * SMG_NBP; e += blockDim.x) X[e] = 0.0;
   __syncthreads();
-  if (threadIdx.x < 64) lds_potrf64_lookahead<true>((lds_dbl*)D, (int*)(cyc + 8));
+  lds_potrf64_lookahead<true>((lds_dbl*)D, (int*)(cyc + 8));
   __syncthreads();
   const long long t0 = stamp();
   const int w = threadIdx.x >> 6;
   if (V == 0 && w < 4) trtri_leaf16((const lds_dbl*)D, (lds_dbl*)X, w);
-  if (V == 1 && w < 4) trtri_leaf16_p((const lds_dbl*)D, (lds_dbl*)X, w);
-  if (V == 2 && w == 0) trtri_leaf16_p((const lds_dbl*)D, (lds_dbl*)X, 3);
+  if (V >= 1 && w == 0) trtri_leaf16((const lds_dbl*)D, (lds_dbl*)X, 3);
   __syncthreads();
   const long long t1 = stamp();
   if (threadIdx.x == 0) cyc[0] = t1 - t0;
@@ -121,9 +120,9 @@ int main() {
     for (int j = 0; j < 64; ++j)
       for (int i = 0; i < 64; ++i) h[i + 64 * j] = (i == j ? 64.0 : 0.0) + 1.0 / (1 + i + j);
     hipMemcpy(dA, h.data(), 4096 * 8, hipMemcpyHostToDevice);
-    void (*kl[3])(const double*, double*, long long*) = {k_leaf<0>, k_leaf<1>, k_leaf<2>};
-    const char* nl[3] = {"trtri_leaf16 x4 waves", "trtri_leaf16_p x4 waves", "trtri_leaf16_p one leaf"};
-    for (int v = 0; v < 3; ++v) {
+    void (*kl[4])(const double*, double*, long long*) = {k_leaf<0>, k_leaf<1>, k_leaf<2>, k_leaf<3>};
+    const char* nl[4] = {"trtri_leaf16 x4 waves", "trtri_leaf16 leaf 3", "(same)", "(same)"};
+    for (int v = 0; v < 4; ++v) {
       long long best = 1LL << 60;
       for (int rep = 0; rep < 5; ++rep) {
         hipLaunchKernelGGL(kl[v], dim3(1), dim3(512), 0, 0, dA, dO, dc);
@@ -134,10 +133,32 @@ int main() {
       }
       hipMemcpy(v == 0 ? o0.data() : o1.data(), dO, 4096 * 8, hipMemcpyDeviceToHost);
       int diff = 0;
-      if (v == 1)
-        for (int e = 0; e < 4096; ++e) diff += o0[e] != o1[e];
+      double md = 0.0;
+      if (v >= 1)
+        for (int e = 0; e < 4096; ++e) {
+          diff += o0[e] != o1[e];
+          md = std::max(md, std::fabs(o0[e] - o1[e]));
+        }
+      if (v >= 1) std::printf("  (%d entries differ, max |d| %.2e)\n", diff, md);
+      {  // |X_k L_k - I| per leaf, L from the factor (dumped by k_fac<0> on the same input)
+        std::vector<double> Lf(4096);
+        hipLaunchKernelGGL(ks[0], dim3(1), dim3(512), 0, 0, dA, dO, dc, dst);
+        hipDeviceSynchronize();
+        hipMemcpy(Lf.data(), dO, 4096 * 8, hipMemcpyDeviceToHost);
+        const std::vector<double>& Xo = v == 0 ? o0 : o1;
+        double res = 0;
+        for (int k = 0; k < 4; ++k)
+          for (int r = 0; r < 16; ++r)
+            for (int c = 0; c < 16; ++c) {
+              double acc = 0;
+              for (int q = 0; q < 16; ++q)
+                acc += Xo[(16 * k + r) * 64 + 16 * k + q] * (q >= c ? Lf[(16 * k + q) * 64 + 16 * k + c] : 0.0);
+              res = std::max(res, std::fabs(acc - (r == c ? 1.0 : 0.0)));
+            }
+        std::printf("  |X L - I| = %.2e\n", res);
+      }
       std::printf("  %-24s %6lld cycles (%.2f us)%s\n", nl[v], best, best / 2400.0,
-                  v == 1 ? (diff ? "  DIFFERENT bits" : "  same bits") : "");
+                  v >= 1 ? (diff ? "  DIFFERENT bits" : "  same bits") : "");
     }
   }
   return 0;
