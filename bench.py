@@ -299,6 +299,24 @@ class GPEigen(GP):
         out = np.zeros(5)
         if self.bl.smg_bench_bridge_cost(self.N, 3, ptr(out)) != 0:
             raise SystemExit(f"bridge cost failed: {self.bl.smg_bench_error().decode()}")
+        # host-memory roofline of the three crossings: the bytes each writes
+        # (varis + the Eigen pointer array) and reads (the staged values),
+        # against a same-process probe of the same host pool's bandwidth
+        bw = np.zeros(4)
+        self.bl.smg_bench_host_bw.argtypes = [ctypes.c_longlong, ctypes.c_int, D]
+        if self.bl.smg_bench_host_bw(1 << 29, 3, ptr(bw)) != 0:
+            raise SystemExit(f"host bandwidth probe failed: {self.bl.smg_bench_error().decode()}")
+        N, sv = self.N, float(bw[3])
+        tri, nn = N * (N + 1) / 2, float(N) * N
+        moved = {"forward_K": (tri * sv + nn * 8, tri * 8),     # K's own varis, pointers; staged values
+                 "forward_Kd": (N * sv + nn * 8, 0.0),          # Kd's diagonal varis, pointers (K's shared)
+                 "forward_L": (tri * sv + nn * 8, tri * 8)}     # L's varis, pointers; streamed values
+        crossings = {}
+        for k, (wb, rb) in moved.items():
+            t = best[{"forward_K": 4, "forward_Kd": 5, "forward_L": 6}[k]]
+            floor = (wb + rb) / (bw[0] * 1e9)
+            crossings[k] = {"ms": t * 1e3, "bytes_written": wb, "bytes_read": rb,
+                            "ms_at_probe_bandwidth": floor * 1e3, "frac_of_probe": floor / t if t > 0 else None}
         return {"eval_phases_ms": {"forward": best[0] * 1e3, "reverse_published": best[1] * 1e3,
                                    "recover": best[2] * 1e3, "gradient_call": best[3] * 1e3,
                                    "forward_K": best[4] * 1e3, "forward_Kd": best[5] * 1e3,
@@ -315,6 +333,11 @@ class GPEigen(GP):
                                            "intermediate blocks' adjoints into their varis; recover_memory), best "
                                            "of 3; gradient_call: the same evaluation through stan::math::gradient "
                                            "(nothing published); forward_*: the forward's four statements"},
+                "host_roofline": {"probe_write_GBps": bw[0], "probe_copy_GBps": bw[1], "pool_threads": int(bw[2]),
+                                  "vari_bytes": int(bw[3]), "crossings": crossings,
+                                  "note": "each crossing's bytes (written: varis + the Eigen pointer array; read: "
+                                          "the staged values) at the probe's write bandwidth, over its measured "
+                                          "time (forward_L overlaps the factorisation it streams from)"},
                 "bridge_cost_ms": {"to_host_matrix": out[0] * 1e3, "to_dev_recognised": out[1] * 1e3,
                                    "to_dev_gathered_copy": out[2] * 1e3, "reverse_gather_touched": out[3] * 1e3,
                                    "reverse_untouched_sweep": out[4] * 1e3,

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <exception>
@@ -225,6 +226,54 @@ int smg_bench_gp_eigen_phases(const double* theta, double* out) {
       (void)lp;
       recover_memory_nested();
     }
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e);
+  }
+}
+
+/* The host pool's memory bandwidth on the cores the Eigen boundary's
+ * crossings use (the same persistent pool, the same partition): out[0] GB/s
+ * of a write-only pass laid out like a crossing (24-byte vari records, then
+ * an 8-byte pointer array), out[1] GB/s of a read + write pass; best of
+ * `reps` over a `bytes` buffer whose pages are faulted in first; out[2] the
+ * pool's thread count, out[3] sizeof(vari). */
+int smg_bench_host_bw(long long bytes, int reps, double* out) {
+  try {
+    using namespace stan::math;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto sec = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
+    const size_t nrec = size_t(bytes) / 32;  // 24 + 8 bytes per element, as a crossing writes
+    std::vector<char> buf(nrec * 32);
+    std::memset(buf.data(), 0, buf.size());
+    struct rec {
+      void* vt;
+      double val, adj;
+    };
+    rec* R = reinterpret_cast<rec*>(buf.data());
+    void** P = reinterpret_cast<void**>(buf.data() + nrec * sizeof(rec));
+    static_assert(sizeof(rec) == 24, "record");
+    double wbest = 1e30, cbest = 1e30;
+    for (int r = 0; r < reps; ++r) {
+      auto t0 = now();
+      internal::host_parallel_for(nrec, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) R[i] = rec{&R[0], double(i), 0.0};
+      });
+      internal::host_parallel_for(nrec, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) P[i] = &R[i];
+      });
+      auto t1 = now();
+      internal::host_parallel_for(nrec, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) R[i].adj = R[i].val + 1.0;
+      });
+      auto t2 = now();
+      wbest = std::min(wbest, sec(t0, t1));
+      cbest = std::min(cbest, sec(t1, t2));
+    }
+    out[0] = double(nrec) * 32 / wbest * 1e-9;
+    out[1] = double(nrec) * sizeof(rec) * 2 / cbest * 1e-9;
+    out[2] = internal::host_threads();
+    out[3] = sizeof(vari);
     return 0;
   } catch (const std::exception& e) {
     return fail(e);

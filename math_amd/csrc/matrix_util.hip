@@ -66,6 +66,32 @@ __global__ __launch_bounds__(256) void k_sym_from_lower(int n, double* __restric
   }
 }
 
+// B += S with S symmetric and only its upper triangle stored: tile pair
+// (bx, by), bx >= by: the upper tile U = S[by.., bx..] is added to B's tile
+// (by, bx) as read and, transposed through LDS, to its mirror (bx, by); on a
+// diagonal tile each entry (i, j) takes S(min, max)
+__global__ __launch_bounds__(256) void k_add_sym_from_upper(int n, const double* __restrict__ S, int lds,
+                                                            double* __restrict__ B, int ldb) {
+  const int bx = blockIdx.x, by = blockIdx.y;
+  if (bx < by) return;
+  __shared__ double t[TT][TT + 1];
+  const int i0 = by * TT, j0 = bx * TT;  // U's rows i0.., columns j0..
+  const int r = threadIdx.x & 63, c4 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    const int i = i0 + r, j = j0 + c;
+    const double u = (i < n && j < n) ? S[i + (size_t)j * lds] : 0.0;
+    t[c][r] = u;
+    if (i < n && j < n && (bx != by || i <= j)) B[i + (size_t)j * ldb] += u;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int c = c4; c < TT; c += 4) {
+    const int i = j0 + r, j = i0 + c;  // B(i, j) += S(j, i), i > j
+    if (i < n && j < n && i > j) B[i + (size_t)j * ldb] += t[r][c];
+  }
+}
+
 __global__ void k_shift(int m, int n, double c, double* __restrict__ Y, int ldy, int uplo) {
   for (smg_mn it(m, n); it.ok(); it.next()) {
     const long long e = it.e;
@@ -250,6 +276,14 @@ int smg_sym_from_lower(smg_ctx* ctx, int n, double* A, int lda) {
   if (!A || lda < n) return SMG_ERR_ARG;
   const int t = smg_ceil_div(n, TT);
   hipLaunchKernelGGL(k_sym_from_lower, dim3(t, t), dim3(256), 0, ctx->stream, n, A, lda);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_add_sym_from_upper(smg_ctx* ctx, int n, const double* S, int lds, double* B, int ldb) {
+  if (n <= 0) return SMG_OK;
+  const int t = smg_ceil_div(n, TT);
+  hipLaunchKernelGGL(k_add_sym_from_upper, dim3(t, t), dim3(256), 0, ctx->stream, n, S, lds, B, ldb);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -197,6 +197,8 @@ int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, 
 int smg_trsm_impl(smg_ctx* ctx, int lower, int trans, const double* A, int lda, const double* W,
                   int ldw, double* B, int ldb, int m, int n, double* X = nullptr, int ldx = 0,
                   const double* aux = nullptr);
+// B (n x n) += S, S symmetric with only its upper triangle stored
+extern "C" int smg_add_sym_from_upper(smg_ctx* ctx, int n, const double* S, int lds, double* B, int ldb);
 int smg_copy_impl(smg_ctx* ctx, int m, int n, const double* A, int lda, double* B, int ldb,
                   double alpha, int accumulate);
 int smg_status_mark_impl(smg_ctx* ctx);
