@@ -403,6 +403,12 @@ int smg_multiply_lower_fwd(smg_ctx* ctx, const double* L, int ldl, const double*
  * through two N-column triangular solves. */
 int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* aux, const double* Ad, int ldad, int n,
                          double* W, double* Wt, double* Y, double* P, double* Ld, int ld);
+/* smg_chol_tangent_fwd on a given W = L^{-1} (ld, lower; its strict upper
+ * is read only inside the 512-row diagonal blocks, as the progressive
+ * factorisation leaves it: smg_cholesky_fwd_checked_mark_winv): Wt, Y, P, Ld
+ * as above, W itself not written. */
+int smg_chol_tangent_fwd_w(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Ad, int ldad, int n,
+                           double* Wt, double* Y, double* P, double* Ld, int ld);
 int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Wt, const double* Y,
                          const double* P, int ld, const double* Ldadj, int ldla, int n, double* Ladj, int ldladj,
                          double* Adadj, int ldaa, double* ws);
@@ -511,6 +517,17 @@ int smg_cholesky_mvn_rev_v(smg_ctx* ctx, int n, const double* s, int k, long lon
  * form (the host layer's history per tape position). */
 int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                                       double* aux, double* ws, int* started);
+/* smg_cholesky_fwd_checked_mark_inv forming W = L^{-1} alone (no K^{-1}
+ * shares): the block rows of W progressively beside the panels, W in ws's
+ * first n^2 doubles (ld n; lower, its strict upper written inside the 512-row
+ * diagonal blocks only) once smg_cholesky_inverse_wait returns; *started = 3
+ * when queued (n % 512 == 0, n >= 1024), 0 when not (the plain
+ * factorisation ran).  For the HVP's value factor, whose W the Cholesky
+ * tangent node reuses (mix/fvar_functors.hpp) instead of forming it after
+ * the factorisation; the reference's fvar<var> cholesky_decompose has no
+ * inverse at all (prim/mat/fun/cholesky_decompose.hpp:31-39, Eigen LLT). */
+int smg_cholesky_fwd_checked_mark_winv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                       double* aux, double* ws, int* started);
 /* smg_cholesky_fwd_checked_mark_inv (ws may be NULL: no K^{-1}) that also
  * streams the factor to the host while it is formed: once panel p (columns
  * [512 p, min(512 (p + 1), n)); one panel when n <= 512) is final, its columns

@@ -73,8 +73,22 @@ int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* a
     if ((rc = smg_add_diag_fwd(ctx, W, ld, n, 1.0, nullptr, W, ld))) return rc;  // W = I
     if ((rc = smg_trsm_impl(ctx, 1, 0, L, ldl, nullptr, 0, W, ld, n, n, nullptr, 0, aux))) return rc;
   }
+  return smg_chol_tangent_fwd_w(ctx, L, ldl, W, Ad, ldad, n, Wt, Y, P, Ld, ld);
+}
+
+int smg_chol_tangent_fwd_w(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Ad, int ldad, int n,
+                           double* Wt, double* Y, double* P, double* Ld, int ld) {
+  if (!ctx || n < 0) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (!L || !W || !Ad || !Wt || !Y || !P || !Ld || ldl < n || ldad < n || ld < n) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_TRSV);
+  int rc;
   // W^T stored for the reverse's M = W^T S (an NN product on the matrix
-  // cores: the TN form ran at 34 TF/s against 75 for NN at N = 4096)
+  // cores: the TN form ran at 34 TF/s against 75 for NN at N = 4096).  W's
+  // strict upper may hold anything outside its 512-row diagonal blocks (the
+  // progressive factorisation's W): every product below cuts K to the
+  // triangles in bands of at most 128 rows / columns, so those entries (and
+  // their transposes in Wt) are never read
   if ((rc = smg_transpose(ctx, n, n, W, ld, Wt, ld, 0.0))) return rc;
   // T = tril(W A') (in Ld's storage), Y = T W^T (lower computed, mirrored):
   // Y_ij, i >= j, sums T_ik W_jk over k <= j <= i, so only T's lower triangle

@@ -1361,7 +1361,7 @@ struct chol_stream_sink {
 };
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
              bool check_sym, bool mark = false, double* inv_ws = nullptr, int* inv_started = nullptr,
-             const chol_stream_sink* sink = nullptr);
+             const chol_stream_sink* sink = nullptr, bool w_only = false);
 
 }  // namespace
 
@@ -1419,6 +1419,14 @@ int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, in
   return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started);
 }
 
+int smg_cholesky_fwd_checked_mark_winv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
+                                       double* Dinv, double* ws, int* started) {
+  if (!started) return SMG_ERR_ARG;
+  *started = 0;
+  if (!ws || !Dinv) return SMG_ERR_ARG;
+  return chol_fwd(ctx, A, lda, n, L, ldl, Dinv, true, true, ws, started, nullptr, true);
+}
+
 int smg_cholesky_inverse_wait(smg_ctx* ctx) {
   if (!ctx) return SMG_ERR_ARG;
   if (!ctx->inv_w_recorded) return SMG_ERR_ARG;
@@ -1461,7 +1469,8 @@ int smg_cholesky_stream_panel_cols(int n, int p, int* j0, int* j1) {
 namespace {
 
 int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, double* Dinv,
-             bool check_sym, bool mark, double* inv_ws, int* inv_started, const chol_stream_sink* sink) {
+             bool check_sym, bool mark, double* inv_ws, int* inv_started, const chol_stream_sink* sink,
+             bool w_only) {
   if (!ctx || n < 0 || (n > 0 && (!A || !L || lda < n || ldl < n))) return SMG_ERR_ARG;
   if (n == 0) return SMG_OK;
   smg_prof_scope prof(ctx, SMG_FAM_CHOL_FWD);
@@ -1563,6 +1572,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     return SMG_OK;
   };
   auto queue_shares = [&](double budget_us) -> int {  // budget < 0: every row queued on zero so far
+    if (w_only) return SMG_OK;  // (W alone: no K^{-1} shares)
     // (a share may overrun the budget by this much -- r05z5, three same-box pairs: 40 379.8, 0 374.4,
     // 80 374.5, 150 375.3 evals/s)
     constexpr double tol = 40.0;
@@ -1583,13 +1593,14 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       return queue_shares(budget_us);
     }
     static const int order[5] = {0, 1, 3, 4, 2};  // W_k first, then its Y contributions, its share last
+    const int nparts = w_only ? 4 : 5;
     while (q_k <= kmax && q_k < rows_prog - 1) {
       const double c = smg_inv_prog_cost(n, q_k, order[q_part], true);
       if (budget_us >= 0 && c > budget_us + 40.0) break;
       budget_us -= c;
       smg_on_side on(ctx);
       if (int rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, q_k, order[q_part], true)) return rc;
-      if (++q_part == 5) {
+      if (++q_part == nparts) {
         q_part = 0;
         ++q_k;
       }
@@ -1739,11 +1750,11 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       if ((rc = record_w_ready(ctx, ctx->zero_stream))) return rc;
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_w, 0));
       smg_on_side on(ctx);
-      if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 2, false))) return rc;
+      if (!w_only && (rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 2, false))) return rc;
     } else {
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
       smg_on_side on(ctx);
-      for (int part = 0; part < 3; ++part) {  // (the last row adds to no later row's Y)
+      for (int part = 0; part < (w_only ? 2 : 3); ++part) {  // (the last row adds to no later row's Y)
         if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, part, false))) return rc;
         if (part == 1 && (rc = record_w_ready(ctx, ctx->side))) return rc;
       }
@@ -1752,7 +1763,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     // touch ws (smg_cholesky_mvn_rev_v / smg_join_async)
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev, ctx->side));
     ctx->inv_pending = 1;
-    *inv_started = 2;
+    *inv_started = w_only ? 3 : 2;
   } else if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, 0, -1, nullptr, true))) {
     return rc;
   }

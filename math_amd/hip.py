@@ -84,6 +84,7 @@ _SIGS = {
     "smg_mdivide_left_tri_aux_fwd": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _P, _I]),
     "smg_mdivide_left_tri_aux_rev": (_I, [_P, _I, _P, _I, _P, _P, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P]),
     "smg_chol_tangent_fwd": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I]),
+    "smg_chol_tangent_fwd_w": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _I]),
     "smg_chol_tangent_rev": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
     "smg_multiply_lower_fwd": (_I, [_P, _P, _I, _P, _I, _I, _P, _I]),
     "smg_multiply_lower_rev": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P]),
@@ -101,6 +102,7 @@ _SIGS = {
     "smg_cholesky_inv_t_async": (_I, [_P, _P, _I, _P, _I, _P, _I, _P]),
     "smg_cholesky_mvn_rev_v": (_I, [_P, _I, _P, _I, _L, _D, _P, _I, _P, _I]),
     "smg_cholesky_fwd_checked_mark_inv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
+    "smg_cholesky_fwd_checked_mark_winv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
     "smg_cholesky_stream_panels": (_I, [_I]),
     "smg_cholesky_stream_panel_cols": (_I, [_I, _I, _P, _P]),
     "smg_sum_strict_upper": (_I, [_P, _I, _P, _I, _P]),

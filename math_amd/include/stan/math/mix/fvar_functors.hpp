@@ -327,10 +327,19 @@ class chol_tangent_dev_vari : public device_vari {
       : device_vari(0.0), L_(L), Ad_(Ad), Ld_(new dev_matrix_vari(L->rows_, L->cols_, dev_structure::lower)) {
     const int n = L->rows_;
     const size_t nn = size_t(n) * n;
-    W_ = amd::alloc_doubles(nn);
     Wt_ = amd::alloc_doubles(nn);
     Y_ = amd::alloc_doubles(nn);
     P_ = amd::alloc_doubles(nn);
+    // W = L^{-1} from the factorisation when it formed it beside its panels
+    // (cholesky_decompose_with_inverse), else here after it
+    const double* Wf = L_->sink_ ? L_->sink_->inverse_factor() : nullptr;
+    if (Wf) {
+      W_ = const_cast<double*>(Wf);  // (read only)
+      amd::check(smg_chol_tangent_fwd_w(amd::ctx(), L_->val_, n, W_, Ad_->val_, n, n, Wt_, Y_, P_, Ld_->val_, n),
+                 "cholesky_decompose");
+      return;
+    }
+    W_ = amd::alloc_doubles(nn);
     amd::check(smg_chol_tangent_fwd(amd::ctx(), L_->val_, n, L_->aux_, Ad_->val_, n, n, W_, Wt_, Y_, P_, Ld_->val_, n),
                "cholesky_decompose");
   }
@@ -353,11 +362,12 @@ inline bool chol_tangent_composed() {
 
 inline dev_fvar_matrix cholesky_decompose(const dev_fvar_matrix& A) {
   dev_fvar_matrix L;
-  L.val_ = cholesky_decompose(A.val_);  // checks + L (structurally lower)
   if (!internal::chol_tangent_composed()) {
+    L.val_ = internal::cholesky_decompose_with_inverse(A.val_);  // checks + L (structurally lower), W = L^{-1}
     L.d_ = dev_var_matrix((new internal::chol_tangent_dev_vari(L.val_.vi_, A.d_.vi_))->Ld_);
     return L;
   }
+  L.val_ = cholesky_decompose(A.val_);
   dev_var_matrix X = mdivide_left_tri<1>(L.val_, A.d_);   // L^{-1} A'
   dev_var_matrix Y = mdivide_left_tri<1>(L.val_, transpose(X));  // L^{-1} A' L^{-T}
   // L' = L Phi(Y): lower times lower

@@ -151,6 +151,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   size_t dep_sweep_ = 0;
   double* ws_ = nullptr;  // smg_cholesky_mvn_rev's workspace [V = L^{-T}, K^{-1}]
   bool early_ = false;    // the factorisation queued all of K^{-1} into ws_ (progressively, with its panels)
+  const double* winv_ = nullptr;  // W = L^{-1} alone, formed with the panels (cholesky_decompose_with_inverse)
   bool v_ready_ = false;  // V queued (smg_cholesky_inv_t_async) by prepare_mvn_adjoint
   bool c_ready_ = false;  // and K^{-1} (after early_)
   // the closed form applied these MVN partials without writing L's dense
@@ -232,6 +233,7 @@ class cholesky_dev_vari : public device_vari, public structured_adjoint_sink {
   // W = L^{-1}: the first n^2 doubles of ws_ once the progressive K^{-1}
   // (early_) has queued all of its block rows (chol_mvn.hip)
   const double* inverse_factor() override {
+    if (winv_) return smg_cholesky_inverse_wait(amd::ctx()) == SMG_OK ? winv_ : nullptr;
     if (!early_ || !ws_ || n_ % 64 != 0) return nullptr;
     if (smg_cholesky_inverse_wait(amd::ctx()) != SMG_OK) return nullptr;
     return ws_;
@@ -381,7 +383,7 @@ namespace internal {
  * throwing reference functor leaves its partial allocations.
  */
 inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host_out,
-                                              const std::function<bool()>* verify = nullptr) {
+                                              const std::function<bool()>* verify = nullptr, bool want_w = false) {
   const char* fn = "cholesky_decompose";
   internal::check_square(fn, "A", A.rows(), A.cols());
   const int n = A.rows();
@@ -399,7 +401,10 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
   // the node's tape position once pushed (cholesky_dev_vari::pos_)
   const size_t pos = ChainableStack::instance_->var_stack_.size();
   double* inv_ws = nullptr;
-  if (internal::cholesky_dev_vari::closed_form_enabled() && internal::cholesky_dev_vari::predicted(pos, n))
+  // want_w: W = L^{-1} alone, progressively (the HVP's value factor, whose
+  // tangent node reads W); n % 512 == 0 and n >= 1024, else not formed
+  want_w = want_w && !host_out && n % 512 == 0 && n >= 1024;
+  if (want_w || (internal::cholesky_dev_vari::closed_form_enabled() && internal::cholesky_dev_vari::predicted(pos, n)))
     inv_ws = amd::alloc_doubles(smg_cholesky_mvn_rev_ws_doubles(n));
   // check_symmetric fused with the factorisation's copy of A (one pass); the
   // status is read at the mark after the panels, so the block inverses that
@@ -441,6 +446,9 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
       host_parallel_for(o1 - o0, [&](size_t s0, size_t s1) { construct_varis(b.first, stage, o0 + s0, o0 + s1); });
       amd::phase_mark(3 + 2 * p);
     }
+  } else if (want_w) {
+    amd::check(smg_cholesky_fwd_checked_mark_winv(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started),
+               fn);
   } else if (inv_ws) {
     amd::check(smg_cholesky_fwd_checked_mark_inv(c, A.val_ptr(), n, n, L->val_, n, L->aux_, inv_ws, &inv_started), fn);
   } else {
@@ -452,8 +460,12 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
   if (st & SMG_ERR_NOT_SYMMETRIC) internal::throw_not_symmetric_dev(fn, "A", A.val_ptr(), n);
   if (st) amd::throw_status(st, fn, "m");
   auto* node = new internal::cholesky_dev_vari(A.vi_, L);
-  node->ws_ = inv_ws;  // (reused by prepare_mvn_adjoint when the factorisation could not form K^{-1})
-  if (inv_started) {
+  if (want_w) {  // W alone (inv_started == 3); the closed form, if taken, gets a workspace of its own
+    if (inv_started == 3) node->winv_ = inv_ws;
+  } else {
+    node->ws_ = inv_ws;  // (reused by prepare_mvn_adjoint when the factorisation could not form K^{-1})
+  }
+  if (inv_started && !want_w) {
     node->early_ = true;
     node->v_ready_ = node->c_ready_ = true;  // all of K^{-1} queued already
   }
@@ -469,6 +481,15 @@ inline dev_var_matrix cholesky_decompose_impl(const dev_var_matrix& A, var* host
 inline dev_var_matrix cholesky_decompose(const dev_var_matrix& A) {
   return internal::cholesky_decompose_impl(A, nullptr);
 }
+
+namespace internal {
+/** cholesky_decompose that also forms W = L^{-1} beside its panels, read
+ * through the factor's sink (inverse_factor()) by the Cholesky tangent node
+ * and the MVN's W-form forward. */
+inline dev_var_matrix cholesky_decompose_with_inverse(const dev_var_matrix& A) {
+  return cholesky_decompose_impl(A, nullptr, nullptr, true);
+}
+}  // namespace internal
 
 }  // namespace math
 }  // namespace stan

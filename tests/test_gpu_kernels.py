@@ -428,6 +428,61 @@ def test_mvn_inverse_from_progressive_factorisation(ctx):
     near_rel(ctx.get(lp1, 1), ctx.get(lp0, 1), 1e-12, what="lp")
 
 
+def test_progressive_w_only_and_tangent_from_it(ctx):
+    """smg_cholesky_fwd_checked_mark_winv (*started == 3): W = L^{-1} formed
+    beside the panels without K^{-1} -- from a NaN workspace, its lower
+    triangle bit-identical to the K^{-1} mode's W (the same parts in the same
+    order) and within 1e-10 of numpy's inverse; then smg_chol_tangent_fwd_w on
+    that W (its strict upper outside the 512-row diagonal blocks left NaN, so
+    any read of it would poison the outputs) against smg_chol_tangent_fwd,
+    which forms its own zero-padded W: Ld, Y, P within 1e-10."""
+    import ctypes
+    N = 2048
+    rng = np.random.default_rng(5)
+    B = rng.uniform(-1, 1, (N, N))
+    A = B @ B.T / N + 0.2 * np.eye(N)
+    A = 0.5 * (A + A.T)
+    Ad = rng.uniform(-1, 1, (N, N))
+    Ad = 0.5 * (Ad + Ad.T)
+    lib = ctx.lib
+    nw = lib.smg_cholesky_mvn_rev_ws_doubles(N)
+    nan_ws = np.full(nw, np.nan)
+    dA = ctx.put(F(A))
+    outs = {}
+    for fn, want in (("smg_cholesky_fwd_checked_mark_winv", 3), ("smg_cholesky_fwd_checked_mark_inv", 2)):
+        dL, dD, ws = ctx.zeros(N * N), ctx.zeros(lib.smg_cholesky_aux_doubles(N)), ctx.put(nan_ws)
+        started = ctypes.c_int(-1)
+        ctx.call(fn, dA, N, N, dL, N, dD, ws, ctypes.byref(started))
+        assert started.value == want
+        st = ctypes.c_int(-1)
+        ctx.call("smg_status_mark_wait", ctypes.byref(st))
+        assert st.value == 0
+        ctx.call("smg_cholesky_inverse_wait")
+        ctx.call("smg_join_async")
+        W = ctx.get(ws, N * N).reshape(N, N, order="F")
+        outs[fn] = (dL, dD, ws, W)
+    Lh = ctx.get(outs["smg_cholesky_fwd_checked_mark_winv"][0], N * N).reshape(N, N, order="F")
+    W3 = np.tril(outs["smg_cholesky_fwd_checked_mark_winv"][3])
+    W2 = np.tril(outs["smg_cholesky_fwd_checked_mark_inv"][3])
+    assert np.array_equal(W3, W2), "W differs between the W-only and the K^{-1} modes"
+    Wref = np.linalg.inv(np.tril(Lh))
+    near_rel(W3, Wref, 1e-10, atol=1e-10 * np.abs(Wref).max(), what="W vs numpy")
+    dL, dD, ws, _ = outs["smg_cholesky_fwd_checked_mark_winv"]
+    dAd = ctx.put(F(Ad))
+    res = []
+    for given in (True, False):
+        Wt, Y, P, Ld = (ctx.zeros(N * N) for _ in range(4))
+        if given:
+            ctx.call("smg_chol_tangent_fwd_w", dL, N, ws, dAd, N, N, Wt, Y, P, Ld, N)
+        else:
+            Wn = ctx.zeros(N * N)
+            ctx.call("smg_chol_tangent_fwd", dL, N, dD, dAd, N, N, Wn, Wt, Y, P, Ld, N)
+        res.append([np.tril(ctx.get(x, N * N).reshape(N, N, order="F")) for x in (Ld, Y, P)])
+    for a, b, what in zip(res[0], res[1], ("Ld", "Y", "P")):
+        assert np.isfinite(a).all(), what
+        near_rel(a, b, 1e-10, atol=1e-10 * np.abs(b).max(), what=what)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_progressive_inverses_from_nan_workspace(ctx, mode):
     """The progressive factorisation's by-products against numpy, from a

@@ -4,7 +4,7 @@ set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O
 cd $GRAFT_REPO_ROOT
 TAG=${1:-hvp}
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread -k "hessian" > $O/${TAG}_pytest.log 2>&1 || { tail -30 $O/${TAG}_pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread -k "${KX:-hessian}" > $O/${TAG}_pytest.log 2>&1 || { tail -30 $O/${TAG}_pytest.log; exit 1; }
 tail -2 $O/${TAG}_pytest.log
 WL=hvp TAG=$TAG bash tools/r06_multi_ab.sh ${R:-2} ${CTL:-base} || exit 1
 if [ "${PROF:-1}" = 1 ]; then
