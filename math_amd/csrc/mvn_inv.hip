@@ -148,6 +148,18 @@ __global__ __launch_bounds__(256) void k_mvn_inv_finish(const double* __restrict
   }
 }
 
+// out = the summed partials of a k_trmv_tiles pass: entries of block b from
+// column tiles c <= b (W x) or row tiles r >= b (W^T x)
+__global__ __launch_bounds__(256) void k_trmv_finish(const double* __restrict__ P, int n, int trans,
+                                                     double* __restrict__ out) {
+  __shared__ double xs[TB];
+  __shared__ double red[4][TB];
+  const int b = blockIdx.x, nb = n / TB;
+  sum_partials(P, n, b, trans ? b : 0, trans ? nb - 1 : b, xs, red);
+  __syncthreads();
+  if (threadIdx.x < TB) out[b * TB + threadIdx.x] = xs[threadIdx.x];
+}
+
 __global__ void k_mvn_inv_lp(const double* __restrict__ part, int nparts, int n, double* out) {
   if (threadIdx.x != 0) return;
   double q = 0.0, ld = 0.0;
@@ -182,6 +194,26 @@ int smg_mvn_cholesky_fwd_inv(smg_ctx* ctx, const double* y, const double* mu, co
                      P2);
   hipLaunchKernelGGL(k_mvn_inv_finish, dim3(nb), dim3(256), 0, ctx->stream, P1, P2, L, ldl, n, ws, part);
   hipLaunchKernelGGL(k_mvn_inv_lp, dim3(1), dim3(64), 0, ctx->stream, part, nb, n, out_lp);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_trmv_inv(smg_ctx* ctx, int trans, const double* W, int ldw, int n, const double* x, double* y) {
+  if (!ctx || n < 0 || (n > 0 && (!W || !x || !y || ldw < n))) return SMG_ERR_ARG;
+  if (n == 0) return SMG_OK;
+  if (n % TB != 0) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_TRSV);
+  const int nb = n / TB;
+  double* P = smg_ws(ctx, SMG_WS_MVN, (size_t)nb * n);
+  if (!P) return SMG_ERR_OOM;
+  const int tiles = nb * (nb + 1) / 2;
+  if (trans)
+    hipLaunchKernelGGL(k_trmv_tiles<true>, dim3(tiles), dim3(256), 0, ctx->stream, W, ldw, n, 0, x, nullptr, nullptr,
+                       P);
+  else
+    hipLaunchKernelGGL(k_trmv_tiles<false>, dim3(tiles), dim3(256), 0, ctx->stream, W, ldw, n, 0, x, nullptr, nullptr,
+                       P);
+  hipLaunchKernelGGL(k_trmv_finish, dim3(nb), dim3(256), 0, ctx->stream, P, n, trans, y);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -25,8 +25,17 @@ class mdivide_left_tri_dev_vari : public device_vari {
   const int lower_;
   dev_operand A_, B_;
   dev_matrix_vari* C_;
+  const double* W_ = nullptr;  // tri(A)^{-1} when A's factorisation formed it (one vector: products, not solves)
   mdivide_left_tri_dev_vari(int lower, const dev_operand& A, const dev_operand& B)
       : device_vari(0.0), lower_(lower), A_(A), B_(B), C_(new dev_matrix_vari(B.rows, B.cols)) {
+    // a Cholesky factor whose W = L^{-1} exists (the HVP's value factor, a
+    // GP's progressive K^{-1}): C = W b, one HBM pass instead of a
+    // latency-bound persistent solve
+    if (lower_ && B_.cols == 1 && B_.rows % 64 == 0 && A_.vi && A_.vi->sink_) W_ = A_.vi->sink_->inverse_factor();
+    if (W_) {
+      amd::check(smg_trmv_inv(amd::ctx(), 0, W_, A_.rows, B_.rows, B_.val(), C_->val_), "mdivide_left_tri");
+      return;
+    }
     amd::check(smg_mdivide_left_tri_aux_fwd(amd::ctx(), lower_, A_.val(), A_.rows, aux(), B_.val(), B_.rows,
                                             B_.rows, B_.cols, C_->val_, C_->rows_),
                "mdivide_left_tri");
@@ -37,6 +46,14 @@ class mdivide_left_tri_dev_vari : public device_vari {
   void chain() override {
     const int m = B_.rows, n = B_.cols;
     double* ws = amd::alloc_doubles(size_t(m) * n);
+    if (W_) {  // ws = W^T Cadj;  Aadj (lower) -= ws C^T;  Badj += ws  (:104-123)
+      smg_ctx* c = amd::ctx();
+      amd::check(smg_trmv_inv(c, 1, W_, A_.rows, m, C_->adj_, ws), "mdivide_left_tri");
+      if (A_.adj())
+        amd::check(smg_gemm(c, 0, 1, 1, m, m, 1, -1.0, ws, m, C_->val_, m, 1.0, A_.adj(), A_.rows), "mdivide_left_tri");
+      if (B_.adj()) amd::check(smg_axpy(c, (long long)m, 1.0, ws, 1, B_.adj(), 1), "mdivide_left_tri");
+      return;
+    }
     amd::check(smg_mdivide_left_tri_aux_rev(amd::ctx(), lower_, A_.val(), A_.rows, aux(), C_->val_, m,
                                             C_->adj_, m, m, n, A_.adj(), A_.rows, B_.adj(), m, ws),
                "mdivide_left_tri");

@@ -483,6 +483,31 @@ def test_progressive_w_only_and_tangent_from_it(ctx):
         near_rel(a, b, 1e-10, atol=1e-10 * np.abs(b).max(), what=what)
 
 
+@pytest.mark.parametrize("trans", [0, 1])
+def test_trmv_inv_vs_numpy(ctx, trans):
+    """smg_trmv_inv: y = W x / W^T x over W's lower 64-row tiles (the strict
+    upper outside the diagonal tiles NaN: never read), against numpy at 1e-13;
+    run twice, bit-identical (fixed-order partial sums)."""
+    N = 1024
+    rng = np.random.default_rng(17)
+    W = np.tril(rng.uniform(-1, 1, (N, N)))
+    Wd = W.copy()
+    for ib in range(N // 64):
+        for jb in range(ib + 1, N // 64):
+            Wd[ib * 64:(ib + 1) * 64, jb * 64:(jb + 1) * 64] = np.nan
+    x = rng.uniform(-1, 1, N)
+    dW, dx = ctx.put(F(Wd)), ctx.put(x)
+    outs = []
+    for _ in range(2):
+        dy = ctx.zeros(N)
+        ctx.call("smg_trmv_inv", trans, dW, N, N, dx, dy)
+        outs.append(ctx.get(dy, N))
+    ref = (W.T if trans else W) @ x
+    near_rel(outs[0], ref, 1e-13, atol=1e-13 * np.abs(ref).max(), what="trmv")
+    assert np.array_equal(outs[0], outs[1])
+    assert ctx.lib.smg_trmv_inv(ctx.ptr, trans, dW, N, N - 1, dx, dx) != 0  # n % 64 != 0
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_progressive_inverses_from_nan_workspace(ctx, mode):
     """The progressive factorisation's by-products against numpy, from a
