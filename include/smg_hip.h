@@ -526,12 +526,13 @@ int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, in
  * tangent node reuses (mix/fvar_functors.hpp) instead of forming it after
  * the factorisation; the reference's fvar<var> cholesky_decompose has no
  * inverse at all (prim/mat/fun/cholesky_decompose.hpp:31-39, Eigen LLT). */
-/* y = W x (trans 0) or W^T x (trans 1) for a lower W = L^{-1} (n x n, ld
- * ldw, n % 64 == 0; W's strict upper read inside its 64-row diagonal tiles
- * only): one HBM pass over the lower tiles plus a deterministic in-order sum
- * of the tile partials.  x and y must not alias.  mdivide_left_tri<Lower>(L, b)
- * = L^{-1} b on a factor that carries W (rev/mat/fun/mdivide_left_tri.hpp:
- * 16-130 solves instead), and its reverse's L^{-T} Cadj. */
+/* y = W x (trans 0) or W^T x (trans 1) for the lower triangle of W (n x n,
+ * ld ldw, n % 64 == 0; W's strict upper never read): one HBM pass over the
+ * lower tiles plus a deterministic in-order sum of the tile partials.  x and
+ * y must not alias.  mdivide_left_tri<Lower>(L, b) = L^{-1} b on a factor
+ * that carries W = L^{-1} (rev/mat/fun/mdivide_left_tri.hpp:16-130 solves
+ * instead) and its reverse's L^{-T} Cadj; multiply(L, b) and its reverse on a
+ * structurally lower L (rev/mat/fun/multiply.hpp:65-135). */
 int smg_trmv_inv(smg_ctx* ctx, int trans, const double* W, int ldw, int n, const double* x, double* y);
 int smg_cholesky_fwd_checked_mark_winv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                                        double* aux, double* ws, int* started);

@@ -11,8 +11,8 @@
 // triangular solves (k_trsv_persist, ~115 us each at n = 4096).
 //
 // Layout: a pass is a grid of 64 x 64 tiles of W's lower triangle (tile
-// (ib, jb), jb <= ib; W's diagonal tiles carry stored zeros above the
-// diagonal, its strict upper outside them is never read).  Each tile writes
+// (ib, jb), jb <= ib; the diagonal tiles' strict upper is masked to zero,
+// W's strict upper outside them is never read).  Each tile writes
 // one 64-vector of partial sums: y = W x into P[jb][ib 64 + r] (per column
 // tile), y = W^T x into P[ib][jb 64 + c] (per row tile).  The next pass
 // (and the finishing kernel) forms its input entries by summing those
@@ -92,6 +92,11 @@ __global__ __launch_bounds__(256) void k_trmv_tiles(const double* __restrict__ W
   const double* col = W + (size_t)ib * TB + r + (size_t)jb * TB * ldw;
 #pragma unroll
   for (int q = 0; q < 16; ++q) wv[q] = col[(size_t)(g + 4 * q) * ldw];
+  if (ib == jb) {  // a diagonal tile: its strict upper is not part of the lower matrix
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (r < g + 4 * q) wv[q] = 0.0;
+  }
   __syncthreads();  // (xs complete; red free again)
   if (!TRANS) {
     double acc = 0.0;

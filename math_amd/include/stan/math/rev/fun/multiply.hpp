@@ -64,10 +64,21 @@ class multiply_dev_vari : public device_vari {
   // reverse then adds this node's share of nothing).  Same derivative as the
   // reference's two products (rev/mat/fun/multiply.hpp:65-135).
   bool gram_;
+  // A structurally lower (a Cholesky factor or its tangent) times a vector:
+  // one pass over A's lower tiles each way (smg_trmv_inv), and A's adjoint
+  // written on its lower triangle only (its upper entries are the
+  // reference's dummy vari)
+  bool lowvec_;
   multiply_dev_vari(const dev_operand& A, const dev_operand& B)
       : device_vari(0.0), A_(A), B_(B), C_(new dev_matrix_vari(A.rows, B.cols)),
-        gram_(A.vi && B.vi && B.vi->transpose_of_ == A.vi) {
+        gram_(A.vi && B.vi && B.vi->transpose_of_ == A.vi),
+        lowvec_(A.vi && A.vi->structure_ == dev_structure::lower && A.rows == A.cols && B.cols == 1 &&
+                A.rows % 64 == 0) {
     smg_ctx* c = amd::ctx();
+    if (lowvec_) {
+      amd::check(smg_trmv_inv(c, 0, A_.val(), A_.rows, A_.rows, B_.val(), C_->val_), "multiply");
+      return;
+    }
     if (gram_) {
       amd::check(smg_gemm(c, 0, 1, 1, A_.rows, A_.rows, A_.cols, 1.0, A_.val(), A_.rows, A_.val(), A_.rows, 0.0,
                           C_->val_, C_->rows_),
@@ -81,6 +92,17 @@ class multiply_dev_vari : public device_vari {
   }
   void chain() override {
     smg_ctx* c = amd::ctx();
+    if (lowvec_) {  // Aadj (lower) += Cadj b^T;  badj += A^T Cadj
+      const int m = A_.rows;
+      if (A_.adj())
+        amd::check(smg_gemm(c, 0, 1, 1, m, m, 1, 1.0, C_->adj_, m, B_.val(), m, 1.0, A_.adj(), m), "multiply");
+      if (B_.adj()) {
+        double* t = amd::alloc_doubles(size_t(m));
+        amd::check(smg_trmv_inv(c, 1, A_.val(), A_.rows, m, C_->adj_, t), "multiply");
+        amd::check(smg_axpy(c, (long long)m, 1.0, t, 1, B_.adj(), 1), "multiply");
+      }
+      return;
+    }
     if (gram_) {
       const int m = C_->rows_;
       double* S = amd::alloc_doubles(size_t(m) * m);  // Cadj + Cadj^T
