@@ -321,6 +321,53 @@ __device__ __noinline__ void chain_leaves_pub(const lds_dbl* D, lds_dbl* X, doub
   trtri_leaf16(D, X, w);
   leaf16_store((const lds_dbl*)X, G, ldg, b, w);
 }
+// the chain's global work beside its leaf inverses, by waves 4-7 (256
+// threads; waves 0-3 form the leaves): L_jj stored (lower, zeros above),
+// then -- when a next tile follows -- its operands A_{t,j} and A_tt loaded
+// (each wave polls the owner's done flag itself: no barrier with the leaf
+// waves) and staged into Y and Zn; all of it hidden under the leaves, which
+// had run with these four waves idle (the stores, the loads and their LDS
+// staging had been 2 us of each chain step)
+__device__ __noinline__ void chain_side(const lds_dbl* Dc, lds_dbl* Y, lds_dbl* Zn, double* L, int ldl, int cj,
+                                        int bj, int rt0, int rt, int bt, int more, const int* flag, int epoch,
+                                        int* status) {
+  const int tid = (int)threadIdx.x - 256;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q;
+    const int c = e >> 6, r = e & 63;
+    if (r < bj && c < bj) st_dev(&L[cj + r + (size_t)(cj + c) * ldl], r >= c ? Dc[r * SMG_NBP + c] : 0.0);
+  }
+  if (!more) return;
+  if (flag && (threadIdx.x & 63) == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        atomicOr(status, (int)SMG_ERR_SYNC);
+        break;
+      }
+    }
+  }
+  double ra[16], rz[16];
+  unsigned oka = 0, okz = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q;
+    const int c = e >> 6, r = e & 63;
+    ra[q] = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)(cj + min(c, bj - 1)) * ldl]);
+    rz[q] = ld_dev(&L[rt0 + min(r, bt - 1) + (size_t)(rt0 + min(c, bt - 1)) * ldl]);
+    oka |= (r < rt && c < bj) ? (1u << q) : 0u;
+    okz |= (r < bt && c < bt && r >= c) ? (1u << q) : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q;
+    const int c = e >> 6, r = e & 63;
+    Y[r * SMG_NBP + c] = ((oka >> q) & 1u) ? ra[q] : 0.0;
+    Zn[r * SMG_NBP + c] = ((okz >> q) & 1u) ? rz[q] : 0.0;
+  }
+}
 __device__ __noinline__ void chain_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) { lds_trsm64_rt(Y, D, X); }
 __device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }
 __device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const lds_dbl* B) {
@@ -672,33 +719,24 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       const bool more = j + 1 < nb;
       const int t = j + 1, rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
       const int bt = min(SMG_NB, K - rt0);
-      panel_regs Ra, Rz;
-      auto load_next = [&] {
-        if (j >= 1) panel_wait(&done[(j - 1) * S + t], epoch, status);
-        PANEL_EV((j << 16) | (t << 8) | 11);
-        panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
-        panel_gload(Rz, L + rt0 + (size_t)rt0 * ldl, ldl, bt, bt, true);
-      };
-      // L_jj is what the other tiles wait for (they solve against it): its
-      // stores are issued right after the factorisation and published after
-      // the leaf inverses, so their latency hides behind them; the next
-      // tile's operands are loaded there too.  No 64 x 64 inverse on the
-      // chain: L_{t,j} = A_{t,j} L_jj^{-T} by the leaf inverses and one
-      // row-tile solve (the inverter workgroup forms Dinv_j beside it)
+      // L_jj is what the other tiles wait for (they solve against it): waves
+      // 0-3 form and store its leaf inverses while waves 4-7 store L_jj and
+      // stage the next tile's operands (chain_side); one publish covers both.
+      // No 64 x 64 inverse on the chain: L_{t,j} = A_{t,j} L_jj^{-T} by the
+      // leaf inverses and one row-tile solve (the inverter workgroup forms
+      // Dinv_j beside it)
       CHAIN_FACTOR(Dc, status);
       __syncthreads();
       PANEL_EV((j << 16) | (j << 8) | 14);
-      panel_gstore_tri(Dc, L + cj + (size_t)cj * ldl, ldl, bj);
-      PANEL_EV((j << 16) | (j << 8) | 15);
-      if (more) load_next();
-      CHAIN_LEAVES_PUB(Dc, X, Dinv + cj, ldd, bj);
+      if (threadIdx.x < 256)
+        CHAIN_LEAVES_PUB(Dc, X, Dinv + cj, ldd, bj);
+      else
+        chain_side((const lds_dbl*)Dc, (lds_dbl*)Y, (lds_dbl*)Zn, L, ldl, cj, bj, rt0, rt, bt, more ? 1 : 0,
+                   j >= 1 ? &done[(j - 1) * S + t] : nullptr, epoch, status);
       PANEL_EV((j << 16) | (j << 8) | 10);
       panel_publish(&diag[j], epoch);
       PANEL_EV((j << 16) | (j << 8) | 4);
       if (!more) break;
-      panel_lstore(Y, Ra);
-      panel_lstore(Zn, Rz);
-      __syncthreads();
       PANEL_EV((j << 16) | (t << 8) | 12);
       CHAIN_TRSM(Y, Dc, X);  // L_{t,j} = A_{t,j} L_jj^{-T} (private)
       __syncthreads();
