@@ -406,8 +406,11 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
   switch (part) {
     case 0:  // W_kk (the block row's 128/256/512 inverses first when asked)
       if (inverses_here) {  // (the solves after the factorisation wait for them: inv_ev_aux)
-        if ((rc = smg_block_inverses_rows(ctx, L, ldl, aux, n, r0, P, T))) return rc;
+        bool wrote = false;  // (the one-launch inverse writes W_kk into W itself)
+        if ((rc = smg_block_inverses_rows(ctx, L, ldl, aux, n, r0, P, T, W + r0 + (size_t)r0 * n, &wrote)))
+          return rc;
         SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_aux, ctx->stream));
+        if (wrote) return SMG_OK;
       }
       return smg_copy_impl(ctx, P, P, Wkk, n, W + r0 + (size_t)r0 * n, n, 1.0, 0);
     case 1:  // W_{k,0:k} = -W_kk Y_k

@@ -1011,7 +1011,7 @@ __device__ inline void ib_sync(unsigned* ctr, unsigned target, int* status) {
 // C[32 x 32 at C] = alpha A[32 x K] B[K x 32] (column-major, sc1 loads and
 // stores); wave w takes the 16 x 16 quadrant (w & 1, w >> 1)
 __device__ inline void ib_tile(const double* A, int lda, const double* B, int ldb, int K, double alpha, double* C,
-                               int ldc) {
+                               int ldc, double* C2 = nullptr, int ldc2 = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wi = (w & 1) * 16, wj = (w >> 1) * 16;
   const int fr = lane & 15, fk = lane >> 4;
@@ -1030,23 +1030,31 @@ __device__ inline void ib_tile(const double* A, int lda, const double* B, int ld
     for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) st_dev(C + (wi + fk + 4 * r) + (size_t)(wj + fr) * ldc, alpha * acc[r]);
+  for (int r = 0; r < 4; ++r) {
+    st_dev(C + (wi + fk + 4 * r) + (size_t)(wj + fr) * ldc, alpha * acc[r]);
+    if (C2) st_dev(C2 + (wi + fk + 4 * r) + (size_t)(wj + fr) * ldc2, alpha * acc[r]);
+  }
 }
 
 // dst[rows x cols] = src (or zero when src is null); the workgroup's share
 // `part` of `parts` of the elements, sc1 loads / stores
 __device__ inline void ib_copy(const double* src, int lds, double* dst, int ldd, int rows, int cols, int part,
-                               int parts) {
+                               int parts, double* dst2 = nullptr, int ldd2 = 0) {
   const int tot = rows * cols;
   for (int e = part * 256 + (int)threadIdx.x; e < tot; e += parts * 256) {
     const int r = e % rows, c = e / rows;
-    st_dev(dst + r + (size_t)c * ldd, src ? ld_dev(src + r + (size_t)c * lds) : 0.0);
+    const double v = src ? ld_dev(src + r + (size_t)c * lds) : 0.0;
+    st_dev(dst + r + (size_t)c * ldd, v);
+    if (dst2) st_dev(dst2 + r + (size_t)c * ldd2, v);
   }
 }
 
 __global__ __launch_bounds__(256) void k_inv_block512(const double* __restrict__ Lb, int ldl, const double* Wi,
                                                       double* W256, double* W512, int ldw, double* T,
-                                                      unsigned* ctr, unsigned base, int* status) {
+                                                      unsigned* ctr, unsigned base, int* status, double* W2,
+                                                      int ldw2) {
+  // W2 (optional, ld ldw2): a second copy of the 512-level result (the
+  // progressive W's diagonal block: no separate copy launch)
   const int g = blockIdx.x;
   // phase 1: T_q = L21_q X11_q (2 x 16 tiles, K = 128); the level-256 diagonal copies
   if (g < 32) {
@@ -1075,15 +1083,18 @@ __global__ __launch_bounds__(256) void k_inv_block512(const double* __restrict__
   {
     const int ti = (g & 7) * 32, tj = (g >> 3) * 32;
     ib_tile(Lb + 256 + ti, ldl, W256 + (size_t)tj * ldw, ldw, 256, 1.0, T + ti + (size_t)tj * 256, 256);
-    ib_copy(W256, ldw, W512, ldw, 256, 256, g, IB_WG);
-    ib_copy(W256 + 256, ldw, W512 + 256 + (size_t)256 * ldw, ldw, 256, 256, g, IB_WG);
-    ib_copy(nullptr, 0, W512 + (size_t)256 * ldw, ldw, 256, 256, g, IB_WG);
+    ib_copy(W256, ldw, W512, ldw, 256, 256, g, IB_WG, W2, ldw2);
+    ib_copy(W256 + 256, ldw, W512 + 256 + (size_t)256 * ldw, ldw, 256, 256, g, IB_WG,
+            W2 ? W2 + 256 + (size_t)256 * ldw2 : nullptr, ldw2);
+    ib_copy(nullptr, 0, W512 + (size_t)256 * ldw, ldw, 256, 256, g, IB_WG, W2 ? W2 + (size_t)256 * ldw2 : nullptr,
+            ldw2);
   }
   ib_sync(ctr, base + 3 * IB_WG, status);
   // phase 4: X21 = -W256_1 T (64 tiles, K = 256)
   {
     const int ti = (g & 7) * 32, tj = (g >> 3) * 32;
-    ib_tile(W256 + 256 + ti, ldw, T + (size_t)tj * 256, 256, 256, -1.0, W512 + 256 + ti + (size_t)tj * ldw, ldw);
+    ib_tile(W256 + 256 + ti, ldw, T + (size_t)tj * 256, 256, 256, -1.0, W512 + 256 + ti + (size_t)tj * ldw, ldw,
+            W2 ? W2 + 256 + ti + (size_t)tj * ldw2 : nullptr, ldw2);
   }
   // (the fourth count: the next launch on this slot starts from base + IB_PHASES * IB_WG)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1199,8 +1210,12 @@ bool inv_fused_ok(smg_ctx* ctx, int n) {
 // levels at the SMG_AUX_W* column offsets (smg_cholesky_aux_doubles).
 // (rows [row0, row0 + nrows) only, nrows < 0: all; T: workspace of
 // nrows / 2 x 256 doubles, NULL: SMG_WS_TMP)
+// (Wout, ld n: when the one-launch form runs, it also writes the 512-level
+// block there and sets *wrote)
 int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0 = 0,
-                        int nrows = -1, double* Tbuf = nullptr, bool skip128 = false) {
+                        int nrows = -1, double* Tbuf = nullptr, bool skip128 = false, double* Wout = nullptr,
+                        bool* wrote = nullptr) {
+  if (wrote) *wrote = false;
   if (nrows < 0) nrows = n;
   L += (size_t)row0 * (ldl + 1);
   // skip128: the 128 level is already there (the panel kernel's inverter forms it)
@@ -1216,9 +1231,10 @@ int chol_block_inverses(smg_ctx* ctx, const double* L, int ldl, double* aux, int
     ctx->status_armed = 1;
     hipLaunchKernelGGL(k_inv_block512, dim3(IB_WG), dim3(256), 0, ctx->stream, L, ldl, Wi,
                        aux + (size_t)n * SMG_AUX_W256 + row0, aux + (size_t)n * SMG_AUX_W512 + row0, n, T, ctr,
-                       base, ctx->status_d);
+                       base, ctx->status_d, Wout, n);
     SMG_LAUNCH_CHECK();
     ctx->inv_launches = e + 1;
+    if (wrote) *wrote = Wout != nullptr;
     return SMG_OK;
   }
   for (int s2 = skip128 ? 4 * SMG_NB : 2 * SMG_NB; s2 <= SMG_NBR; s2 *= 2) {
@@ -1409,8 +1425,8 @@ int smg_block_inverses_impl(smg_ctx* ctx, const double* L, int ldl, double* aux,
   return chol_block_inverses(ctx, L, ldl, aux, n);
 }
 int smg_block_inverses_rows(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0, int nrows,
-                            double* T) {
-  return chol_block_inverses(ctx, L, ldl, aux, n, row0, nrows, T, true);  // (behind chol_fwd's panels)
+                            double* T, double* Wout, bool* wrote) {
+  return chol_block_inverses(ctx, L, ldl, aux, n, row0, nrows, T, true, Wout, wrote);  // (behind chol_fwd's panels)
 }
 
 extern "C" {
@@ -1774,14 +1790,17 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
   if (prog) {
     const int r0 = n - SMG_NBR;
     SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->inv_ev_aux, 0));
-    if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, r0, SMG_NBR, nullptr, true))) return rc;
+    bool wkk = false;  // W_last's diagonal block written by the inverse launch itself
+    if ((rc = chol_block_inverses(ctx, L, ldl, aux, n, r0, SMG_NBR, nullptr, true, inv_ws + r0 + (size_t)r0 * n,
+                                  &wkk)))
+      return rc;
     SMG_HIP_TRY(hipEventRecord(ctx->inv_ev_main, ctx->stream));
     const int klast = n / SMG_NBR - 1;
     if (zero_parts) {  // W_last on the zeroing stream behind the last Y, its share on side
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->inv_ev_main, 0));
       hipStream_t keep = ctx->stream;
       ctx->stream = ctx->zero_stream;
-      rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 0, false);
+      rc = wkk ? SMG_OK : smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 0, false);
       if (!rc) rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, 1, false);
       ctx->stream = keep;
       if (rc) return rc;
@@ -1793,6 +1812,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->inv_ev_main, 0));
       smg_on_side on(ctx);
       for (int part = 0; part < (w_only ? 2 : 3); ++part) {  // (the last row adds to no later row's Y)
+        if (part == 0 && wkk) continue;
         if ((rc = smg_inv_prog_row(ctx, L, ldl, aux, n, inv_ws, klast, part, false))) return rc;
         if (part == 1 && (rc = record_w_ready(ctx, ctx->side))) return rc;
       }

@@ -184,9 +184,10 @@ int smg_inv_prog_row(smg_ctx* ctx, const double* L, int ldl, double* aux, int n,
                      bool inverses_here);
 double smg_inv_prog_cost(int n, int k, int part, bool inverses_here);
 // block inverses of the rows [row0, row0 + nrows) (multiples of 512), T: a
-// workspace (NULL: SMG_WS_TMP)
+// workspace (NULL: SMG_WS_TMP); Wout (ld n, may be NULL): the 512-level
+// block also written there when one launch forms it (*wrote)
 int smg_block_inverses_rows(smg_ctx* ctx, const double* L, int ldl, double* aux, int n, int row0, int nrows,
-                            double* T);
+                            double* T, double* Wout = nullptr, bool* wrote = nullptr);
 // C = beta C (lower != 0: lower triangle only)
 int smg_scale_impl(smg_ctx* ctx, int m, int n, double beta, double* C, int ldc, int lower);
 
