@@ -488,8 +488,15 @@ __host__ __device__ inline int panel_tiles(int n, int J, int nb) {
 }
 
 // column block c of panel tile t is updated by t's helper workgroup
-__device__ __forceinline__ bool panel_helped(int t, int c, int nb, int nh) {
-  return t < nb && t >= 3 && t - 3 < nh && (c & 1) && c <= t - 2;
+// (round 6: two helpers per tile from t = 4 on -- A the odd, B the even
+// column blocks c <= t - 2 -- so the owner keeps only c = t - 1 and its own
+// diagonal block: the late tiles' owners had fallen ~10 us behind the chain
+// over the first steps, which stalled it at step 5, where it needs tile 6)
+// 0: the owner updates column block c of panel tile t; 1 / 2: helper A / B
+__device__ __forceinline__ int panel_helper(int t, int c, int nb, int nha, int nhb) {
+  if (t >= nb || c > t - 2 || c < 1) return 0;  // (block 0 takes no updates)
+  if (c & 1) return (t >= 3 && t - 3 < nha) ? 1 : 0;
+  return (t >= 4 && t - 4 < nhb) ? 2 : 0;
 }
 
 // A workgroup whose only tile t (>= nb) lies below the panel: every step of
@@ -583,7 +590,7 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
 
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status, int gown) {
+                                                    int* flags, int epoch, int* status, int gown, int nha) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -595,21 +602,24 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   int* done = flags + S + S * S;  // done[j S + t]: tile t's step-j updates stored
   int* hflag = flags + S + 2 * S * S;  // hflag[j S + t]: tile t's helper finished step j
   int* dinvf = flags + S + 3 * S * S;  // dinvf[j]: Dinv_j stored (the inverter workgroup)
+  int* hflagb = flags + S + 4 * S * S;  // hflagb[j S + t]: tile t's helper B finished step j
   const int nb = (K - J + SMG_NB - 1) / SMG_NB;
   const int T = panel_tiles(n, J, nb);
   const unsigned bid = blockIdx.x;
-  // Column helpers: panel tile t >= 3 (t < nb) gets workgroup gown + t - 3,
-  // which applies the updates of its odd column blocks c <= t - 2 (panel_helped);
-  // the owner of t does the rest, its L_tj, and waits hflag[(j-1) S + t]
-  // before reading a helped column j.  The owners of the last panel tiles
-  // were the chain's bottleneck (their seven column updates per step).
+  // Column helpers: panel tile t >= 3 (t < nb) gets helper A (workgroup
+  // gown + t - 3) for its odd column blocks c <= t - 2, tile t >= 4 helper B
+  // (workgroup gown + nha + t - 4) for the even ones (panel_helper); the
+  // owner of t does c = t - 1, t and its L_tj, and waits for the helper's
+  // flag of step j - 1 (hflag / hflagb) before reading a helped column j.
+  // The owners of the last panel tiles were the chain's bottleneck (their
+  // seven column updates per step).
   // workgroup 1 is the inverter: Dinv_j = L_jj^{-1} (the aux level SMG_NB)
   // once the chain publishes L_jj; the tiles below the panel multiply by it
   // (their column updates, not the chain, bound the panel's end, so their
   // cheaper product beats the solve), the panel tiles solve against L_jj
   // (the chain needs their updates sooner).  Owners are workgroups
   // 2 .. gown - 1, column helpers gown ...
-  const int nh = gridDim.x - gown;
+  const int nhb = (int)gridDim.x - gown - nha;
   if (bid == 1) {
     // ... and, behind each Dinv_j, the aux 128 level of the previous full
     // block pair (j - 2, j - 1): X = [[D1, 0], [-D2 L21 D1, D2]] (two 64^3
@@ -659,13 +669,15 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   }
 
   if (bid >= gown) {
-    const int t = 3 + (bid - gown);
+    const int hb = (int)bid - gown, kind = hb < nha ? 1 : 2;
+    const int t = kind == 1 ? 3 + hb : 4 + (hb - nha);
     if (t >= nb) return;
+    int* hf = kind == 1 ? hflag : hflagb;
     const int rt0 = J + SMG_NB * t, rt = min(SMG_NB, n - rt0);
     for (int j = 0; j + 2 <= t; ++j) {
       const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
       int c0 = j + 1;
-      while (c0 <= t - 2 && !panel_helped(t, c0, nb, nh)) ++c0;
+      while (c0 <= t - 2 && panel_helper(t, c0, nb, nha, nhb) != kind) ++c0;
       if (c0 <= t - 2) {
         panel_wait(&row[j * S + t], epoch, status);  // the owner's L_tj
         PANEL_EV((j << 16) | (t << 8) | 20);
@@ -676,7 +688,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         __syncthreads();
         panel_lstore(D, Rl);
         for (int c = c0; c <= t - 2; ++c) {
-          if (!panel_helped(t, c, nb, nh)) continue;
+          if (panel_helper(t, c, nb, nha, nhb) != kind) continue;
           const int cc = J + SMG_NB * c, bc = min(SMG_NB, K - cc);
           panel_regs Ry, Rz;
           panel_gload(Rz, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, false);
@@ -689,7 +701,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
           panel_gstore(Z, L + rt0 + (size_t)cc * ldl, ldl, rt, bc, false);
         }
       }
-      panel_publish(&hflag[j * S + t], epoch);
+      panel_publish(&hf[j * S + t], epoch);
       PANEL_EV((j << 16) | (t << 8) | 22);
     }
     return;
@@ -832,7 +844,8 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       PANEL_EV((j << 16) | (t << 8) | 5);
       panel_regs Ra, Rd;
       // a helped column is final once the helper has finished step j - 1
-      if (panel_helped(t, j, nb, nh)) panel_wait(&hflag[(j - 1) * S + t], epoch, status);
+      if (const int hk = panel_helper(t, j, nb, nha, nhb))
+        panel_wait(&(hk == 1 ? hflag : hflagb)[(j - 1) * S + t], epoch, status);
       panel_gload(Ra, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);  // own data, final
       // a panel tile: solve against L_jj (the chain's own solve for tile j + 1: the same bits)
       panel_wait(&diag[j], epoch, status);
@@ -865,7 +878,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         if (!own) panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
       };
       auto next_col = [&](int c) {  // the next column from c on that this workgroup updates
-        while (c <= clast && panel_helped(t, c, nb, nh)) ++c;
+        while (c <= clast && panel_helper(t, c, nb, nha, nhb)) ++c;
         return c;
       };
       int cfirst = next_col(j + 1);
@@ -1201,7 +1214,7 @@ bool inv_fused_ok(smg_ctx* ctx, int n) {
     ctx->inv_cus = cus;
   }
   const int nb0 = smg_ceil_div(min(n, SMG_NBF), SMG_NB), t0 = panel_tiles(n, 0, nb0);
-  const int panel_grid = min(t0, PANEL_MAX_GRID) + 1 + (nb0 > 3 ? nb0 - 3 : 0);
+  const int panel_grid = min(t0, PANEL_MAX_GRID) + 1 + (nb0 > 3 ? nb0 - 3 : 0) + (nb0 > 4 ? nb0 - 4 : 0);
   return (long long)ctx->inv_per_cu * max(0, ctx->inv_cus - panel_grid) >= IB_WG;
 }
 
@@ -1672,16 +1685,16 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       ctx->status_armed = 1;
       // column helpers for panel tiles 3 .. nb-1
       const int nbp = smg_ceil_div(K - J, SMG_NB);
-      int nh = nbp > 3 ? nbp - 3 : 0;
-      if (grid + nh > PANEL_MAX_GRID + 1 || nbp > T) nh = 0;
+      int nha = nbp > 3 ? nbp - 3 : 0, nhb = nbp > 4 ? nbp - 4 : 0;  // helpers A (tiles 3..), B (tiles 4..)
+      if (grid + nha + nhb > PANEL_MAX_GRID + 1 || nbp > T) nha = nhb = 0;
       smg_prof_scope pprof(ctx, SMG_FAM_PANEL);  // (the launch alone: bench.py's dominant-kernel roofline)
       if (ctx->prof_on) {  // in-panel work: the diagonal block's factor + the rows below's solve
         const double m = n - J, b = K - J;
         ctx->prof_flops[SMG_FAM_PANEL] += m * b * b - 2.0 * b * b * b / 3.0;
       }
       panel_host_stamp(epoch);
-      hipLaunchKernelGGL(k_chol_panel, dim3(grid + nh), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid);
+      hipLaunchKernelGGL(k_chol_panel, dim3(grid + nha + nhb), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, nha);
     }
     if (zero_parts && J / NB2 < rows_prog) {  // this panel is final: its block row's inverses may start
       if (!(pe_ev[J / NB2] = smg_event(ctx, nev++))) return SMG_ERR_HIP;

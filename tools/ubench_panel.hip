@@ -8,7 +8,9 @@
 #include <cmath>
 
 int main(int argc, char** argv) {
-  const int nh = argc > 1 ? atoi(argv[1]) : 5;  // column helper workgroups
+  const int nha = argc > 1 ? atoi(argv[1]) : 5;  // column helper workgroups A (tiles 3..7)
+  const int nhb = argc > 2 ? atoi(argv[2]) : 4;  // and B (tiles 4..7)
+  const int nh = nha + nhb;
   const int n = 4096, J = 0, K = 512;
   std::vector<double> A((size_t)n * n);
   for (int j = 0; j < n; ++j)
@@ -48,7 +50,7 @@ int main(int argc, char** argv) {
     hipEventCreate(&e1);
     hipEventRecord(e0);
     hipLaunchKernelGGL(k_chol_panel, dim3(T + 1 + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
-                       status, T + 1);
+                       status, T + 1, nha);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
@@ -91,7 +93,7 @@ int main(int argc, char** argv) {
     unsigned long long t0 = ~0ull;
     for (int w = 0; w < T + 1 + nh; ++w)
       for (int k = 0; k < cnt[w] && k < 64; ++k) t0 = std::min(t0, tr[w * 128 + 2 * k]);
-    for (int w : {0, 1, 6, 7, 8, 11, T - 1, T, T + 4, T + 5}) {
+    for (int w : {0, 1, 6, 7, 8, 11, T - 1, T, T + 4, T + 5, T + 8, T + 9}) {
       if (w >= T + 1 + nh) continue;
       printf("WG %d:", w);
       for (int k = 0; k < cnt[w] && k < 64; ++k) {
