@@ -332,6 +332,29 @@ __device__ __noinline__ void chain_side(const lds_dbl* Dc, lds_dbl* Y, lds_dbl* 
                                         int bj, int rt0, int rt, int bt, int more, const int* flag, int epoch,
                                         int* status) {
   const int tid = (int)threadIdx.x - 256;
+  double ra[16], rz[16];
+  unsigned oka = 0, okz = 0;
+  if (more) {  // the loads first (their latency is the long pole), then L_jj's stores under them
+    if (flag && (threadIdx.x & 63) == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+          atomicOr(status, (int)SMG_ERR_SYNC);
+          break;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 256 * q;
+      const int c = e >> 6, r = e & 63;
+      ra[q] = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)(cj + min(c, bj - 1)) * ldl]);
+      rz[q] = ld_dev(&L[rt0 + min(r, bt - 1) + (size_t)(rt0 + min(c, bt - 1)) * ldl]);
+      oka |= (r < rt && c < bj) ? (1u << q) : 0u;
+      okz |= (r < bt && c < bt && r >= c) ? (1u << q) : 0u;
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int e = tid + 256 * q;
@@ -339,27 +362,6 @@ __device__ __noinline__ void chain_side(const lds_dbl* Dc, lds_dbl* Y, lds_dbl* 
     if (r < bj && c < bj) st_dev(&L[cj + r + (size_t)(cj + c) * ldl], r >= c ? Dc[r * SMG_NBP + c] : 0.0);
   }
   if (!more) return;
-  if (flag && (threadIdx.x & 63) == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
-        atomicOr(status, (int)SMG_ERR_SYNC);
-        break;
-      }
-    }
-  }
-  double ra[16], rz[16];
-  unsigned oka = 0, okz = 0;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = tid + 256 * q;
-    const int c = e >> 6, r = e & 63;
-    ra[q] = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)(cj + min(c, bj - 1)) * ldl]);
-    rz[q] = ld_dev(&L[rt0 + min(r, bt - 1) + (size_t)(rt0 + min(c, bt - 1)) * ldl]);
-    oka |= (r < rt && c < bj) ? (1u << q) : 0u;
-    okz |= (r < bt && c < bt && r >= c) ? (1u << q) : 0u;
-  }
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int e = tid + 256 * q;
