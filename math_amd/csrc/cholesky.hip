@@ -649,8 +649,24 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       }
     };
     auto full = [&](int j) { return j < nb && K - (J + SMG_NB * j) >= SMG_NB; };
+    // the last block pair (nb - 2, nb - 1) after the chain's last step is the
+    // launch's tail: its T = L21 D1 needs only L_{nb-1,nb-2} (tile nb-1's
+    // owner, step nb - 2) and D1, so it is formed into Z (free: the previous
+    // pair is done) BEFORE the wait for L_{nb-1,nb-1}, leaving X21 = -D2 T
+    // after it (one 64^3 product instead of two, and no load, past the chain)
+    const bool early = nb >= 2 && (nb & 1) == 0 && full(nb - 1) && full(nb - 2);
     for (int j = 0; j < nb; ++j) {
       const int cj = J + SMG_NB * j, bj = min(SMG_NB, K - cj);
+      if (early && j == nb - 1) {
+        panel_wait(&row[(j - 1) * S + j], epoch, status);  // L_{j,j-1}, stored by tile j's owner
+        panel_regs Rt;
+        panel_gload(Rt, L + cj + (size_t)(cj - SMG_NB) * ldl, ldl, SMG_NB, SMG_NB, false);
+        __syncthreads();
+        panel_lstore(D, Rt);
+        __syncthreads();
+        lds_mma64_8w<false, false>(Z, D, Y);  // T = L21 D1 (Y = D1)
+        __syncthreads();
+      }
       panel_wait(&diag[j], epoch, status);
       panel_regs Rl;
       panel_gload(Rl, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);
@@ -661,12 +677,24 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       __syncthreads();
       panel_gstore_tri(X, Dinv + cj, ldd, bj);
       panel_publish(&dinvf[j], epoch);
+      if (early && j == nb - 1) {  // X21 = -D2 T (X = D2), the pair's three blocks + the zero one
+        const int c1 = cj - SMG_NB;
+        lds_mma64_8w<false, false>(D, X, Z, -1.0);
+        panel_gstore(Y, W128 + c1, ldd, SMG_NB, SMG_NB, false);
+        panel_gstore(X, W128 + cj + (size_t)SMG_NB * ldd, ldd, SMG_NB, SMG_NB, false);
+        panel_gstore(D, W128 + cj, ldd, SMG_NB, SMG_NB, false);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = threadIdx.x + SMG_DIAG_THREADS * q;
+          W128[c1 + (e & 63) + (size_t)(SMG_NB + (e >> 6)) * ldd] = 0.0;
+        }
+      }
       if ((j & 1) == 0 && j >= 2 && full(j - 1)) pair128(j - 1);  // after Dinv_j: off the tiles' path
       __syncthreads();
       for (int e = threadIdx.x; e < SMG_NB * SMG_NBP; e += SMG_DIAG_THREADS) ((j & 1) ? Z : Y)[e] = X[e];
       __syncthreads();
     }
-    if ((nb & 1) == 0 && full(nb - 1)) pair128(nb - 1);
+    if (!early && (nb & 1) == 0 && full(nb - 1)) pair128(nb - 1);
     return;
   }
 
