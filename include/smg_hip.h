@@ -534,6 +534,10 @@ int smg_cholesky_fwd_checked_mark_inv(smg_ctx* ctx, const double* A, int lda, in
  * instead) and its reverse's L^{-T} Cadj; multiply(L, b) and its reverse on a
  * structurally lower L (rev/mat/fun/multiply.hpp:65-135). */
 int smg_trmv_inv(smg_ctx* ctx, int trans, const double* W, int ldw, int n, const double* x, double* y);
+/* A(i, j) += alpha x_i y_j for i >= j (A n x n, ld lda): the lower-triangle
+ * adjoint of a structurally lower matrix times a vector, and of
+ * mdivide_left_tri's A (rev/mat/fun/mdivide_left_tri.hpp:108-123), one pass */
+int smg_rank1_lower(smg_ctx* ctx, int n, double alpha, const double* x, const double* y, double* A, int lda);
 int smg_cholesky_fwd_checked_mark_winv(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl,
                                        double* aux, double* ws, int* started);
 /* smg_cholesky_fwd_checked_mark_inv (ws may be NULL: no K^{-1}) that also

@@ -113,11 +113,19 @@ int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W
   smg_prof_scope prof(ctx, SMG_FAM_TRSV);
   const size_t nn = (size_t)n * n;
   double* S = ws;       // Padj, then S, then (1/2) M W
-  double* M = ws + nn;  // multiply_lower_rev's scratch, then M
-  int rc = smg_memset(ctx, S, 0, sizeof(double) * nn);
+  double* M = ws + nn;  // tril(Ld_adj), then M
+  // smg_multiply_lower_rev's two products on T = tril(Ld_adj) (one copy
+  // pass zeroing the upper), Padj written (beta 0: its upper is never read,
+  // sym_from_lower forms it from the lower) instead of accumulated into a
+  // cleared S
+  int rc = smg_copy_tril(ctx, n, n, Ldadj, ldla, M, n);
   if (rc) return rc;
-  if ((rc = smg_multiply_lower_rev(ctx, L, ldl, P, ld, Ldadj, ldla, n, Ladj, ldladj, S, n, M))) return rc;
+  if (Ladj && (rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, M, n, P, ld, 1.0, Ladj, ldladj,
+                                  SMG_TRI_A_LOWER | SMG_TRI_B_UPPER)))
+    return rc;
   if (!Ladj && !Adadj) return SMG_OK;
+  if ((rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, M, n, 0.0, S, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
+    return rc;
   if ((rc = smg_sym_from_lower(ctx, n, S, n))) return rc;
   if ((rc = smg_gemm_impl(ctx, 0, 0, 0, n, n, n, 1.0, Wt, ld, S, n, 0.0, M, n, SMG_TRI_A_UPPER))) return rc;
   // (Y is stored mirrored, so Y^T = Y bit for bit, and W = (W^T)^T: both

@@ -165,6 +165,17 @@ __global__ __launch_bounds__(256) void k_trmv_finish(const double* __restrict__ 
   if (threadIdx.x < TB) out[b * TB + threadIdx.x] = xs[threadIdx.x];
 }
 
+// A(i, j) += alpha x_i y_j on the lower triangle (i >= j): a workgroup per
+// column (grid-stride over columns), rows from the diagonal down
+__global__ __launch_bounds__(256) void k_rank1_lower(int n, double alpha, const double* __restrict__ x,
+                                                     const double* __restrict__ y, double* __restrict__ A, int lda) {
+  for (int j = blockIdx.x; j < n; j += gridDim.x) {
+    const double ay = alpha * y[j];
+    double* col = A + (size_t)j * lda;
+    for (int i = j + (int)threadIdx.x; i < n; i += 256) col[i] += x[i] * ay;
+  }
+}
+
 __global__ void k_mvn_inv_lp(const double* __restrict__ part, int nparts, int n, double* out) {
   if (threadIdx.x != 0) return;
   double q = 0.0, ld = 0.0;
@@ -199,6 +210,14 @@ int smg_mvn_cholesky_fwd_inv(smg_ctx* ctx, const double* y, const double* mu, co
                      P2);
   hipLaunchKernelGGL(k_mvn_inv_finish, dim3(nb), dim3(256), 0, ctx->stream, P1, P2, L, ldl, n, ws, part);
   hipLaunchKernelGGL(k_mvn_inv_lp, dim3(1), dim3(64), 0, ctx->stream, part, nb, n, out_lp);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_rank1_lower(smg_ctx* ctx, int n, double alpha, const double* x, const double* y, double* A, int lda) {
+  if (!ctx || n < 0 || (n > 0 && (!x || !y || !A || lda < n))) return SMG_ERR_ARG;
+  if (n == 0 || alpha == 0.0) return SMG_OK;
+  hipLaunchKernelGGL(k_rank1_lower, dim3(n < 2048 ? n : 2048), dim3(256), 0, ctx->stream, n, alpha, x, y, A, lda);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -104,6 +104,7 @@ _SIGS = {
     "smg_cholesky_fwd_checked_mark_inv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
     "smg_cholesky_fwd_checked_mark_winv": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P]),
     "smg_trmv_inv": (_I, [_P, _I, _P, _I, _I, _P, _P]),
+    "smg_rank1_lower": (_I, [_P, _I, _D, _P, _P, _P, _I]),
     "smg_cholesky_stream_panels": (_I, [_I]),
     "smg_cholesky_stream_panel_cols": (_I, [_I, _I, _P, _P]),
     "smg_sum_strict_upper": (_I, [_P, _I, _P, _I, _P]),

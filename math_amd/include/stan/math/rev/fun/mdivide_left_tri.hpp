@@ -49,8 +49,7 @@ class mdivide_left_tri_dev_vari : public device_vari {
     if (W_) {  // ws = W^T Cadj;  Aadj (lower) -= ws C^T;  Badj += ws  (:104-123)
       smg_ctx* c = amd::ctx();
       amd::check(smg_trmv_inv(c, 1, W_, A_.rows, m, C_->adj_, ws), "mdivide_left_tri");
-      if (A_.adj())
-        amd::check(smg_gemm(c, 0, 1, 1, m, m, 1, -1.0, ws, m, C_->val_, m, 1.0, A_.adj(), A_.rows), "mdivide_left_tri");
+      if (A_.adj()) amd::check(smg_rank1_lower(c, m, -1.0, ws, C_->val_, A_.adj(), A_.rows), "mdivide_left_tri");
       if (B_.adj()) amd::check(smg_axpy(c, (long long)m, 1.0, ws, 1, B_.adj(), 1), "mdivide_left_tri");
       return;
     }

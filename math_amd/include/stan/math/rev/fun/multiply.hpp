@@ -94,8 +94,7 @@ class multiply_dev_vari : public device_vari {
     smg_ctx* c = amd::ctx();
     if (lowvec_) {  // Aadj (lower) += Cadj b^T;  badj += A^T Cadj
       const int m = A_.rows;
-      if (A_.adj())
-        amd::check(smg_gemm(c, 0, 1, 1, m, m, 1, 1.0, C_->adj_, m, B_.val(), m, 1.0, A_.adj(), m), "multiply");
+      if (A_.adj()) amd::check(smg_rank1_lower(c, m, 1.0, C_->adj_, B_.val(), A_.adj(), m), "multiply");
       if (B_.adj()) {
         double* t = amd::alloc_doubles(size_t(m));
         amd::check(smg_trmv_inv(c, 1, A_.val(), A_.rows, m, C_->adj_, t), "multiply");

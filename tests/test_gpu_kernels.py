@@ -506,6 +506,22 @@ def test_trmv_inv_vs_numpy(ctx, trans):
     assert ctx.lib.smg_trmv_inv(ctx.ptr, trans, dW, N, N - 1, dx, dx) != 0  # n % 64 != 0
 
 
+@pytest.mark.parametrize("n", [1, 63, 1024])
+def test_rank1_lower(ctx, n):
+    """smg_rank1_lower: A += alpha x y^T on the lower triangle only (the
+    strict upper untouched), against numpy at 1e-15."""
+    rng = np.random.default_rng(n)
+    A = rng.uniform(-1, 1, (n, n))
+    x, y = rng.uniform(-1, 1, n), rng.uniform(-1, 1, n)
+    dA = ctx.put(F(A))
+    ctx.call("smg_rank1_lower", n, -0.75, ctx.put(x), ctx.put(y), dA, n)
+    out = ctx.get(dA, n * n).reshape(n, n).T
+    ref = A - 0.75 * np.tril(np.outer(x, y))
+    lo = np.tril(np.ones((n, n), bool))
+    near_rel(out[lo], ref[lo], 1e-15, atol=1e-15, what="lower")
+    assert np.array_equal(out[~lo], A[~lo])
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_progressive_inverses_from_nan_workspace(ctx, mode):
     """The progressive factorisation's by-products against numpy, from a
