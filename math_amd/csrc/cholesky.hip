@@ -590,9 +590,104 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
   }
 }
 
+// below_resident for a PAIR of adjacent 32-row tiles (one 64-row band, rows
+// rt0 ..): two resident sets in the same accumulator layout (rows 0-31 and
+// 32-63 of D), L_tj for both by one 64-row product, each later update's L_cj
+// loaded and staged once for both halves.  Half the workgroups of the rows
+// below (the first panel: 56 instead of 112), each one CU held through the
+// panel for little MFMA work; the freed CUs go to the trailing updates and
+// the K^{-1} parts beside the panels.
+__device__ __noinline__ void below_resident2(double* __restrict__ L, int ldl, int n, int J, int K,
+                                             double* __restrict__ Dinv, int ldd, int* flags, int epoch, int* status,
+                                             int nb, int rt0, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y) {
+  constexpr int S = PANEL_MAX_STEPS;
+  int* diag = flags;
+  int* row = flags + S;
+  int* dinvf = flags + S + 3 * S * S;
+  const int rt = min(2 * PANEL_BELOW_ROWS, n - rt0);
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ar = 16 * (w & 1) + (l >> 4), ac = 16 * (w >> 1) + (l & 15);  // + 4 q (+ 32 for the second half)
+  double Ra[S][4], Rb[S][4];
+#pragma unroll
+  for (int c = 0; c < S; ++c) {  // the whole band (final: rows are independent), once
+    const int cc = J + SMG_NB * c, bc = min(SMG_NB, K - cc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = ar + 4 * q, r2 = r + 32;
+      const int col = c < nb ? cc + min(ac, bc - 1) : J;
+      const double va = ld_dev(&L[rt0 + min(r, rt - 1) + (size_t)col * ldl]);
+      const double vb = ld_dev(&L[rt0 + min(r2, rt - 1) + (size_t)col * ldl]);
+      Ra[c][q] = (c < nb && r < rt && ac < bc) ? va : 0.0;
+      Rb[c][q] = (c < nb && r2 < rt && ac < bc) ? vb : 0.0;
+    }
+  }
+  for (int j = 0; j < nb; ++j) {
+    const int cj = J + SMG_NB * j;
+    const int bj = min(SMG_NB, K - cj);
+    __syncthreads();  // LDS of the previous step fully consumed
+    PANEL_EV((j << 16) | (t << 8) | 5);
+#pragma unroll
+    for (int c = 0; c < S; ++c)  // block j of both halves into D (its current A_tj)
+      if (c == j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          D[(ar + 4 * q) * SMG_NBP + ac] = Ra[c][q];
+          D[(32 + ar + 4 * q) * SMG_NBP + ac] = Rb[c][q];
+        }
+    panel_regs Rd;
+    if (j + 1 < nb) {
+      panel_wait(&dinvf[j], epoch, status);
+      PANEL_EV((j << 16) | (t << 8) | 6);
+      panel_gload(Rd, Dinv + cj, ldd, bj, bj, true);
+      panel_lstore(X, Rd);
+      __syncthreads();
+      lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(D, D, X);  // L_tj = A_tj Dinv_j^T (64 rows)
+    } else {  // the last step: solve against L_jj
+      panel_wait(&diag[j], epoch, status);
+      PANEL_EV((j << 16) | (t << 8) | 6);
+      panel_gload(Rd, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);  // L_jj
+      panel_leaves Rv;
+      panel_gload_leaves(Rv, Dinv + cj, ldd, bj);  // the chain's leaf inverses
+      panel_lstore_id(X, Rd, bj);
+      panel_lstore_leaves(Y, Rv);
+      __syncthreads();
+      lds_trsm64_rt(D, (const lds_dbl*)X, (const lds_dbl*)Y, 4);
+      __syncthreads();
+    }
+    panel_gstore<64>((const lds_dbl*)D, L + rt0 + (size_t)cj * ldl, ldl, rt, bj, false);
+    PANEL_EV((j << 16) | (t << 8) | 7);
+    if (j + 1 >= nb) break;
+    panel_wait_all(row + j * S, j + 1, nb - 1, 1, epoch, status);
+    panel_regs Ryn;
+    auto issue = [&](int c) {
+      const int cc = J + SMG_NB * c;
+      panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
+    };
+    issue(j + 1);
+    for (int c = j + 1; c < nb; ++c) {
+      __syncthreads();  // previous products' Y consumed
+      panel_lstore(Y, Ryn);
+      __syncthreads();
+      if (c + 1 < nb) issue(c + 1);  // in flight during these products
+      const d4 acc_a = lds_mma32_8w_acc((const lds_dbl*)D, (const lds_dbl*)Y);
+      const d4 acc_b = lds_mma32_8w_acc((const lds_dbl*)(D + 32 * SMG_NBP), (const lds_dbl*)Y);
+#pragma unroll
+      for (int cr = 0; cr < S; ++cr)
+        if (cr == c)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            Ra[cr][q] -= acc_a[q];
+            Rb[cr][q] -= acc_b[q];
+          }
+      PANEL_EV((j << 16) | (t << 8) | (16 + c));
+    }
+  }
+}
+
 __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int ldl, int n, int J,
                                                     int K, double* __restrict__ Dinv, int ldd,
-                                                    int* flags, int epoch, int* status, int gown, int nha) {
+                                                    int* flags, int epoch, int* status, int gown, int nha,
+                                                    int paired) {
   __shared__ double D[SMG_NB * SMG_NBP];
   __shared__ double X[SMG_NB * SMG_NBP];
   __shared__ double Y[SMG_NB * SMG_NBP];
@@ -805,15 +900,24 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   // place, and block j written out once, as L_tj -- instead of loading and
   // storing every later block at every step (the kernel fetched 2.6x and
   // wrote 2.1x its algorithmic bytes)
-  if (bid - 1 >= nb && bid - 1 + (gown - 2) >= T) {
+  // paired: workgroups nb + 1 .. gown - 1 each hold a pair of 32-row tiles
+  // below the panel (below_resident2); the owners 2 .. nb the panel tiles
+  if (paired && (int)bid >= nb + 1) {
+    const int p = (int)bid - (nb + 1);
+    below_resident2(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb,
+                    J + SMG_NB * nb + 2 * PANEL_BELOW_ROWS * p, nb + 2 * p, (lds_dbl*)D, (lds_dbl*)X, (lds_dbl*)Y);
+    return;
+  }
+  if (!paired && bid - 1 >= nb && bid - 1 + (gown - 2) >= T) {
     below_resident(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb, (int)bid - 1, (lds_dbl*)D, (lds_dbl*)X,
                    (lds_dbl*)Y);
     return;
   }
+  const int Tloop = paired ? nb : T;  // (paired: the owners' tiles are the panel's only)
   for (int j = 0; j < nb; ++j) {
     const int cj = J + SMG_NB * j;
     const int bj = min(SMG_NB, K - cj);
-    for (int t = 1 + (bid - 2); t < T; t += gown - 2) {
+    for (int t = 1 + (bid - 2); t < Tloop; t += gown - 2) {
       if (t <= j) continue;  // done
       if (t >= nb) {  // a 32-row tile below the panel: L_tj = A_tj Dinv_j^T, then A_tc -= L_tj L_cj^T (c < nb)
         constexpr int R = PANEL_BELOW_ROWS;
@@ -1244,7 +1348,8 @@ bool inv_fused_ok(smg_ctx* ctx, int n) {
     ctx->inv_cus = cus;
   }
   const int nb0 = smg_ceil_div(min(n, SMG_NBF), SMG_NB), t0 = panel_tiles(n, 0, nb0);
-  const int panel_grid = min(t0, PANEL_MAX_GRID) + 1 + (nb0 > 3 ? nb0 - 3 : 0) + (nb0 > 4 ? nb0 - 4 : 0);
+  const int panel_grid = min(nb0 + 1 + (t0 - nb0 + 1) / 2, PANEL_MAX_GRID + 1) + (nb0 > 3 ? nb0 - 3 : 0) +
+                         (nb0 > 4 ? nb0 - 4 : 0);
   return (long long)ctx->inv_per_cu * max(0, ctx->inv_cus - panel_grid) >= IB_WG;
 }
 
@@ -1709,8 +1814,12 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
     {  // the whole panel in one persistent launch (k_chol_panel)
       // workgroup 0 = diagonal chain; tiles 1 .. T-1 over the others
       const int T = panel_tiles(n, J, smg_ceil_div(K - J, SMG_NB));
-      // chain, inverter, owners of tiles 1..T-1
-      const int grid = (T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID) + 1;
+      // chain, inverter, owners of tiles 1..T-1; paired: owners of the panel
+      // tiles 1..nb-1 and one workgroup per pair of 32-row tiles below
+      const int nbq = smg_ceil_div(K - J, SMG_NB);
+      const int npairs = (T - nbq + 1) / 2;
+      const int paired = nbq + 1 + npairs <= PANEL_MAX_GRID + 1 - (nbq > 3 ? 2 * nbq - 7 : 0) ? 1 : 0;
+      const int grid = paired ? nbq + 1 + npairs : (T < PANEL_MAX_GRID ? T : PANEL_MAX_GRID) + 1;
       const int epoch = ++ctx->flag_epoch;
       ctx->status_armed = 1;
       // column helpers for panel tiles 3 .. nb-1
@@ -1724,7 +1833,7 @@ int chol_fwd(smg_ctx* ctx, const double* A, int lda, int n, double* L, int ldl, 
       }
       panel_host_stamp(epoch);
       hipLaunchKernelGGL(k_chol_panel, dim3(grid + nha + nhb), dim3(SMG_DIAG_THREADS), 0, ctx->stream, L, ldl,
-                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, nha);
+                         n, J, K, Dinv, n, ctx->flags_d, epoch, ctx->status_d, grid, nha, paired);
     }
     if (zero_parts && J / NB2 < rows_prog) {  // this panel is final: its block row's inverses may start
       if (!(pe_ev[J / NB2] = smg_event(ctx, nev++))) return SMG_ERR_HIP;

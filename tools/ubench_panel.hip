@@ -24,6 +24,8 @@ int main(int argc, char** argv) {
   hipMemset(flags, 0, 4096 * 4);
   hipMemset(status, 0, 4);
   const int T = panel_tiles(n, J, K / 64);
+  const int paired = argc > 3 ? atoi(argv[3]) : 1;  // pairs of 32-row tiles below the panel per workgroup
+  const int gown = paired ? K / 64 + 1 + (T - K / 64 + 1) / 2 : T + 1;
   {  // the single-workgroup diagonal kernel alone, back to back
     hipMemcpy(dL, A.data(), 8ull * n * n, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
@@ -49,8 +51,8 @@ int main(int argc, char** argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    hipLaunchKernelGGL(k_chol_panel, dim3(T + 1 + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
-                       status, T + 1, nha);
+    hipLaunchKernelGGL(k_chol_panel, dim3(gown + nh), dim3(512), 0, 0, dL, n, n, J, K, dD, n, flags, rep,
+                       status, gown, nha, paired);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
@@ -91,10 +93,10 @@ int main(int argc, char** argv) {
     hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_panel_trace), tr.size() * 8);
     hipMemcpyFromSymbol(cnt.data(), HIP_SYMBOL(g_panel_trace_n), cnt.size() * 4);
     unsigned long long t0 = ~0ull;
-    for (int w = 0; w < T + 1 + nh; ++w)
+    for (int w = 0; w < gown + nh; ++w)
       for (int k = 0; k < cnt[w] && k < 64; ++k) t0 = std::min(t0, tr[w * 128 + 2 * k]);
-    for (int w : {0, 1, 6, 7, 8, 11, T - 1, T, T + 4, T + 5, T + 8, T + 9}) {
-      if (w >= T + 1 + nh) continue;
+    for (int w : {0, 1, 6, 7, 8, 11, gown - 1, gown, gown + 4, gown + 5, gown + 8}) {
+      if (w >= gown + nh) continue;
       printf("WG %d:", w);
       for (int k = 0; k < cnt[w] && k < 64; ++k) {
         const unsigned long long c = tr[w * 128 + 2 * k + 1];
