@@ -669,8 +669,21 @@ __device__ __noinline__ void below_resident2(double* __restrict__ L, int ldl, in
       panel_lstore(Y, Ryn);
       __syncthreads();
       if (c + 1 < nb) issue(c + 1);  // in flight during these products
-      const d4 acc_a = lds_mma32_8w_acc((const lds_dbl*)D, (const lds_dbl*)Y);
-      const d4 acc_b = lds_mma32_8w_acc((const lds_dbl*)(D + 32 * SMG_NBP), (const lds_dbl*)Y);
+      // both halves' products in one k loop: two independent accumulator
+      // chains per wave (one after the other, each wave's 16 dependent MFMAs
+      // had made an update ~4 us)
+      d4 acc_a = d4{0.0, 0.0, 0.0, 0.0}, acc_b = d4{0.0, 0.0, 0.0, 0.0};
+      {
+        const int fr = l & 15, fk = l >> 4;
+        const int ia = 16 * (w & 1) + fr, jb = 16 * (w >> 1) + fr;
+#pragma unroll 4
+        for (int k0 = 0; k0 < SMG_NB; k0 += 4) {
+          const int kk = k0 + fk;
+          const double bv = Y[jb * SMG_NBP + kk];
+          acc_a = __builtin_amdgcn_mfma_f64_16x16x4f64(D[ia * SMG_NBP + kk], bv, acc_a, 0, 0, 0);
+          acc_b = __builtin_amdgcn_mfma_f64_16x16x4f64(D[(32 + ia) * SMG_NBP + kk], bv, acc_b, 0, 0, 0);
+        }
+      }
 #pragma unroll
       for (int cr = 0; cr < S; ++cr)
         if (cr == c)
