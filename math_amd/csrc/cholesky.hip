@@ -599,7 +599,8 @@ __device__ __noinline__ void below_resident(double* __restrict__ L, int ldl, int
 // the K^{-1} parts beside the panels.
 __device__ __noinline__ void below_resident2(double* __restrict__ L, int ldl, int n, int J, int K,
                                              double* __restrict__ Dinv, int ldd, int* flags, int epoch, int* status,
-                                             int nb, int rt0, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y) {
+                                             int nb, int rt0, int t, lds_dbl* D, lds_dbl* X, lds_dbl* Y,
+                                             lds_dbl* Z) {
   constexpr int S = PANEL_MAX_STEPS;
   int* diag = flags;
   int* row = flags + S;
@@ -658,17 +659,20 @@ __device__ __noinline__ void below_resident2(double* __restrict__ L, int ldl, in
     PANEL_EV((j << 16) | (t << 8) | 7);
     if (j + 1 >= nb) break;
     panel_wait_all(row + j * S, j + 1, nb - 1, 1, epoch, status);
+    // L_cj staged into Y / Z alternately: the next block is stored while this
+    // one's products run, one barrier per update
     panel_regs Ryn;
     auto issue = [&](int c) {
       const int cc = J + SMG_NB * c;
       panel_gload(Ryn, L + cc + (size_t)cj * ldl, ldl, min(SMG_NB, K - cc), bj, false);
     };
     issue(j + 1);
+    __syncthreads();  // (D's L_tj stored above: every wave past its reads of Y)
+    panel_lstore(Y, Ryn);
+    if (j + 2 < nb) issue(j + 2);
+    __syncthreads();
     for (int c = j + 1; c < nb; ++c) {
-      __syncthreads();  // previous products' Y consumed
-      panel_lstore(Y, Ryn);
-      __syncthreads();
-      if (c + 1 < nb) issue(c + 1);  // in flight during these products
+      const lds_dbl* B = ((c - j - 1) & 1) ? (const lds_dbl*)Z : (const lds_dbl*)Y;
       // both halves' products in one k loop: two independent accumulator
       // chains per wave (one after the other, each wave's 16 dependent MFMAs
       // had made an update ~4 us)
@@ -679,10 +683,14 @@ __device__ __noinline__ void below_resident2(double* __restrict__ L, int ldl, in
 #pragma unroll 4
         for (int k0 = 0; k0 < SMG_NB; k0 += 4) {
           const int kk = k0 + fk;
-          const double bv = Y[jb * SMG_NBP + kk];
+          const double bv = B[jb * SMG_NBP + kk];
           acc_a = __builtin_amdgcn_mfma_f64_16x16x4f64(D[ia * SMG_NBP + kk], bv, acc_a, 0, 0, 0);
           acc_b = __builtin_amdgcn_mfma_f64_16x16x4f64(D[(32 + ia) * SMG_NBP + kk], bv, acc_b, 0, 0, 0);
         }
+      }
+      if (c + 1 < nb) {  // the next block into the other buffer (read two updates ago, past a barrier)
+        panel_lstore(((c - j - 1) & 1) ? Y : Z, Ryn);
+        if (c + 2 < nb) issue(c + 2);
       }
 #pragma unroll
       for (int cr = 0; cr < S; ++cr)
@@ -692,6 +700,7 @@ __device__ __noinline__ void below_resident2(double* __restrict__ L, int ldl, in
             Ra[cr][q] -= acc_a[q];
             Rb[cr][q] -= acc_b[q];
           }
+      __syncthreads();
       PANEL_EV((j << 16) | (t << 8) | (16 + c));
     }
   }
@@ -918,7 +927,8 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
   if (paired && (int)bid >= nb + 1) {
     const int p = (int)bid - (nb + 1);
     below_resident2(L, ldl, n, J, K, Dinv, ldd, flags, epoch, status, nb,
-                    J + SMG_NB * nb + 2 * PANEL_BELOW_ROWS * p, nb + 2 * p, (lds_dbl*)D, (lds_dbl*)X, (lds_dbl*)Y);
+                    J + SMG_NB * nb + 2 * PANEL_BELOW_ROWS * p, nb + 2 * p, (lds_dbl*)D, (lds_dbl*)X, (lds_dbl*)Y,
+                    (lds_dbl*)Z);
     return;
   }
   if (!paired && bid - 1 >= nb && bid - 1 + (gown - 2) >= T) {
