@@ -371,6 +371,24 @@ __device__ __noinline__ void chain_side(const lds_dbl* Dc, lds_dbl* Y, lds_dbl* 
   }
 }
 __device__ __noinline__ void chain_trsm(lds_dbl* Y, const lds_dbl* D, const lds_dbl* X) { lds_trsm64_rt(Y, D, X); }
+// X = L^{-1} (64 x 64) given its four 16 x 16 leaf inverses on X's diagonal
+// blocks: lds_trtri64_mfma's phases p = 1..3 (the same arithmetic and order:
+// the same bits); the blocks above the diagonal are not written (a
+// triangle store writes zeros there); T: 3 x 256 doubles
+__device__ __noinline__ void chain_last_inverse(const lds_dbl* D, lds_dbl* X, lds_dbl* T) {
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // the leaves in X complete (and Y free)
+  for (int p = 1; p < 4; ++p) {
+    if (w < p) {
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0}, acc2 = acc;
+      trtri_t_acc(D, (const lds_dbl*)X, p, w, 16 * w, 16 * p, acc, acc2);
+      trtri_t_store(T, w, acc, acc2);
+    }
+    __syncthreads();
+    if (w < p) trtri_x_tile(X, T, p, w);
+    __syncthreads();
+  }
+}
 __device__ __noinline__ void chain_syrk(lds_dbl* Zn, const lds_dbl* Y, int b) { lds_syrk64_8w_next(Zn, Y, b); }
 __device__ __noinline__ void owner_update(lds_dbl* Z, const lds_dbl* D, const lds_dbl* B) {
   lds_mma64_8w<false, true, lds_dbl*, const lds_dbl*>(Z, D, B, -1.0, 1.0);
@@ -784,16 +802,28 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         lds_mma64_8w<false, false>(Z, D, Y);  // T = L21 D1 (Y = D1)
         __syncthreads();
       }
-      panel_wait(&diag[j], epoch, status);
-      panel_regs Rl;
-      panel_gload(Rl, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);
-      __syncthreads();
-      panel_lstore_id(D, Rl, bj);
-      __syncthreads();
-      lds_trtri64_mfma(D, X, Tin);
-      __syncthreads();
-      panel_gstore_tri(X, Dinv + cj, ldd, bj);
-      panel_publish(&dinvf[j], epoch);
+      if (early && j == nb - 1) {  // the chain forms this last Dinv from its own leaves (chain_last_inverse)
+        panel_wait(&dinvf[j], epoch, status);
+        panel_regs Rx;
+        panel_gload(Rx, Dinv + cj, ldd, bj, bj, true);
+        __syncthreads();
+        panel_lstore(X, Rx);
+        __syncthreads();
+        PANEL_EV((j << 16) | (j << 8) | 31);
+      } else {
+        panel_wait(&diag[j], epoch, status);
+        panel_regs Rl;
+        panel_gload(Rl, L + cj + (size_t)cj * ldl, ldl, bj, bj, true);
+        __syncthreads();
+        panel_lstore_id(D, Rl, bj);
+        __syncthreads();
+        lds_trtri64_mfma(D, X, Tin);
+        __syncthreads();
+        PANEL_EV((j << 16) | (j << 8) | 30);
+        panel_gstore_tri(X, Dinv + cj, ldd, bj);
+        panel_publish(&dinvf[j], epoch);
+        PANEL_EV((j << 16) | (j << 8) | 31);
+      }
       if (early && j == nb - 1) {  // X21 = -D2 T (X = D2), the pair's three blocks + the zero one
         const int c1 = cj - SMG_NB;
         lds_mma64_8w<false, false>(D, X, Z, -1.0);
@@ -807,6 +837,7 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
         }
       }
       if ((j & 1) == 0 && j >= 2 && full(j - 1)) pair128(j - 1);  // after Dinv_j: off the tiles' path
+      PANEL_EV((j << 16) | (j << 8) | 32);
       __syncthreads();
       for (int e = threadIdx.x; e < SMG_NB * SMG_NBP; e += SMG_DIAG_THREADS) ((j & 1) ? Z : Y)[e] = X[e];
       __syncthreads();
@@ -895,7 +926,20 @@ __global__ __launch_bounds__(512) void k_chol_panel(double* __restrict__ L, int 
       PANEL_EV((j << 16) | (j << 8) | 10);
       panel_publish(&diag[j], epoch);
       PANEL_EV((j << 16) | (j << 8) | 4);
-      if (!more) break;
+      if (!more) {
+        // the last block's Dinv from the leaves already in X (the inverter's
+        // phases after its leaves; T in Y), stored and published for the
+        // inverter's last 128-level pair: ~7 us sooner than the inverter's
+        // own load, leaves and phases after diag[j] (the launch's tail)
+        const bool chain_inv = nb >= 2 && (nb & 1) == 0 && K - (J + SMG_NB * (nb - 2)) >= 2 * SMG_NB;
+        if (chain_inv) {
+          chain_last_inverse((const lds_dbl*)Dc, (lds_dbl*)X, (lds_dbl*)Y);
+          panel_gstore_tri(X, Dinv + cj, ldd, bj);
+          panel_publish(&dinvf[j], epoch);
+          PANEL_EV((j << 16) | (j << 8) | 33);
+        }
+        break;
+      }
       PANEL_EV((j << 16) | (t << 8) | 12);
       CHAIN_TRSM(Y, Dc, X);  // L_{t,j} = A_{t,j} L_jj^{-T} (private)
       __syncthreads();
