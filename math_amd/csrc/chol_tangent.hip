@@ -46,6 +46,23 @@ int inv_rec(smg_ctx* ctx, const double* L, int ldl, const double* w512, int n, d
                        W + mid + (size_t)lo * ldw, ldw, SMG_TRI_A_LOWER);
 }
 
+// fork: `side` follows everything queued on the main stream so far; join:
+// the main stream follows everything queued on `side` (pooled events i)
+int fork_side(smg_ctx* ctx, int i) {
+  hipEvent_t e = smg_fork_event(ctx, i);
+  if (!e) return SMG_ERR_HIP;
+  SMG_HIP_TRY(hipEventRecord(e, ctx->stream));
+  SMG_HIP_TRY(hipStreamWaitEvent(ctx->side, e, 0));
+  return SMG_OK;
+}
+int join_side(smg_ctx* ctx, int i) {
+  hipEvent_t e = smg_fork_event(ctx, i);
+  if (!e) return SMG_ERR_HIP;
+  SMG_HIP_TRY(hipEventRecord(e, ctx->side));
+  SMG_HIP_TRY(hipStreamWaitEvent(ctx->stream, e, 0));
+  return SMG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -88,8 +105,16 @@ int smg_chol_tangent_fwd_w(smg_ctx* ctx, const double* L, int ldl, const double*
   // strict upper may hold anything outside its 512-row diagonal blocks (the
   // progressive factorisation's W): every product below cuts K to the
   // triangles in bands of at most 128 rows / columns, so those entries (and
-  // their transposes in Wt) are never read
-  if ((rc = smg_transpose(ctx, n, n, W, ld, Wt, ld, 0.0))) return rc;
+  // their transposes in Wt) are never read.  Only the reverse reads Wt: the
+  // transpose runs on `side` beside T's product, joined at the end
+  const bool fork = smg_side_begin(ctx) == SMG_OK;
+  if (fork) {
+    if ((rc = fork_side(ctx, 0))) return rc;
+    smg_on_side on(ctx);
+    if ((rc = smg_transpose(ctx, n, n, W, ld, Wt, ld, 0.0))) return rc;
+  } else if ((rc = smg_transpose(ctx, n, n, W, ld, Wt, ld, 0.0))) {
+    return rc;
+  }
   // T = tril(W A') (in Ld's storage), Y = T W^T (lower computed, mirrored):
   // Y_ij, i >= j, sums T_ik W_jk over k <= j <= i, so only T's lower triangle
   // is read (its upper meets only the discarded upper outputs of the
@@ -100,7 +125,8 @@ int smg_chol_tangent_fwd_w(smg_ctx* ctx, const double* L, int ldl, const double*
   if ((rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, W, ld, Ad, ldad, 0.0, Ld, ld, SMG_TRI_A_LOWER))) return rc;
   if ((rc = smg_gemm_impl(ctx, 0, 1, 3, n, n, n, 1.0, Ld, ld, W, ld, 0.0, Y, ld, SMG_TRI_B_UPPER))) return rc;
   if ((rc = smg_phi(ctx, n, Y, ld, P, ld, 0))) return rc;
-  return smg_multiply_lower_fwd(ctx, L, ldl, P, ld, n, Ld, ld);
+  if ((rc = smg_multiply_lower_fwd(ctx, L, ldl, P, ld, n, Ld, ld))) return rc;
+  return fork ? join_side(ctx, 1) : SMG_OK;
 }
 
 int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W, const double* Wt, const double* Y,
@@ -120,25 +146,41 @@ int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W
   // cleared S
   int rc = smg_copy_tril(ctx, n, n, Ldadj, ldla, M, n);
   if (rc) return rc;
+  if (!Ladj && !Adadj) return SMG_OK;
+  // The two pairs of independent products run at once, one on `side`: the
+  // grids' last partial waves leave CUs to the other launch
+  //   Ladj += tril(T P^T)  (main)  ||  Padj = tril(L^T T), S  (side)
+  //   Ladj -= tril(M Y)    (main)  ||  (1/2) M W, A'adj      (side)
+  const bool fork = Ladj && smg_side_begin(ctx) == SMG_OK;
+  if (fork && (rc = fork_side(ctx, 2))) return rc;
+  {
+    smg_on_side on(ctx);
+    if (!fork) ctx->stream = ctx->main_stream;
+    if ((rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, M, n, 0.0, S, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
+      return rc;
+    if ((rc = smg_sym_from_lower(ctx, n, S, n))) return rc;
+  }
   if (Ladj && (rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, M, n, P, ld, 1.0, Ladj, ldladj,
                                   SMG_TRI_A_LOWER | SMG_TRI_B_UPPER)))
     return rc;
-  if (!Ladj && !Adadj) return SMG_OK;
-  if ((rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, M, n, 0.0, S, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
-    return rc;
-  if ((rc = smg_sym_from_lower(ctx, n, S, n))) return rc;
+  if (fork && (rc = join_side(ctx, 3))) return rc;  // S formed, T no longer read: M may be overwritten
   if ((rc = smg_gemm_impl(ctx, 0, 0, 0, n, n, n, 1.0, Wt, ld, S, n, 0.0, M, n, SMG_TRI_A_UPPER))) return rc;
+  if (Adadj) {
+    if (fork && (rc = fork_side(ctx, 4))) return rc;
+    smg_on_side on(ctx);
+    if (!fork) ctx->stream = ctx->main_stream;
+    // (1/2) M W = (1/2) W^T S W is symmetric: its UPPER triangle is computed
+    // (with op(B) = W lower, tile column j takes K = n - j over j + 1 tiles:
+    // half the lower triangle's multiply-adds, N^3 / 6 instead of N^3 / 3) and
+    // added into A'adj symmetrically
+    if ((rc = smg_gemm_impl(ctx, 0, 1, 2, n, n, n, 0.5, M, n, Wt, ld, 0.0, S, n, SMG_TRI_B_LOWER))) return rc;
+    if ((rc = smg_add_sym_from_upper(ctx, n, S, n, Adadj, ldaa))) return rc;
+  }
   // (Y is stored mirrored, so Y^T = Y bit for bit, and W = (W^T)^T: both
   // right operands enter transposed, as n-contiguous B tiles: in the HVP's
   // trace the NN forms ran tril(M Y) at 42 and (1/2) M W at 23 TF/s)
   if (Ladj && (rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, -1.0, M, n, Y, ld, 1.0, Ladj, ldladj))) return rc;
-  if (!Adadj) return SMG_OK;
-  // (1/2) M W = (1/2) W^T S W is symmetric: its UPPER triangle is computed
-  // (with op(B) = W lower, tile column j takes K = n - j over j + 1 tiles:
-  // half the lower triangle's multiply-adds, N^3 / 6 instead of N^3 / 3) and
-  // added into A'adj symmetrically
-  if ((rc = smg_gemm_impl(ctx, 0, 1, 2, n, n, n, 0.5, M, n, Wt, ld, 0.0, S, n, SMG_TRI_B_LOWER))) return rc;
-  return smg_add_sym_from_upper(ctx, n, S, n, Adadj, ldaa);
+  return fork && Adadj ? join_side(ctx, 5) : SMG_OK;
 }
 
 }  // extern "C"

@@ -172,17 +172,21 @@ int smg_inv_events(smg_ctx* ctx) {
   return SMG_OK;
 }
 
-hipEvent_t smg_event(smg_ctx* ctx, int i) {
-  while ((int)ctx->ev_pool.size() <= i) {
+static hipEvent_t pooled_event(smg_ctx* ctx, std::vector<hipEvent_t>& pool, int i) {
+  while ((int)pool.size() <= i) {
     hipEvent_t e;
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
       ctx->host_status |= SMG_ERR_HIP;
       return nullptr;
     }
-    ctx->ev_pool.push_back(e);
+    pool.push_back(e);
   }
-  return ctx->ev_pool[i];
+  return pool[i];
 }
+
+hipEvent_t smg_event(smg_ctx* ctx, int i) { return pooled_event(ctx, ctx->ev_pool, i); }
+
+hipEvent_t smg_fork_event(smg_ctx* ctx, int i) { return pooled_event(ctx, ctx->ev_fork, i); }
 
 void smg_reduce_partials(smg_ctx* ctx, const double* partials, int nparts,
                          int width, double* out, int accumulate) {
@@ -294,6 +298,7 @@ int smg_ctx_destroy(smg_ctx* ctx) {
   for (auto& b : ctx->blocks) hipFree(b.base);
   for (auto e : ctx->prof_pool) hipEventDestroy(e);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  for (auto e : ctx->ev_fork) hipEventDestroy(e);
   for (auto e : ctx->marker_ev) hipEventDestroy(e);
   if (ctx->status_ev) hipEventDestroy(ctx->status_ev);
   if (ctx->zero_stream) {

@@ -35,6 +35,7 @@ struct smg_ctx {
   hipStream_t side;
   hipStream_t main_stream;  // saved while `stream` temporarily points at `side`
   std::vector<hipEvent_t> ev_pool;
+  std::vector<hipEvent_t> ev_fork;  // smg_fork_event
   std::vector<hipEvent_t> marker_ev;  // smg_marker_record / smg_marker_wait (host pipelining)
   // device bump arena: blocks double in size (memory/stack_alloc.hpp:94-119)
   std::vector<smg_arena_block> blocks;
@@ -162,6 +163,10 @@ extern "C" int smg_wait_done(smg_ctx* ctx, long long seq);
 int smg_side_begin(smg_ctx* ctx);          // ensure `side` exists
 int smg_inv_events(smg_ctx* ctx);          // ensure the inv_ev* events exist
 hipEvent_t smg_event(smg_ctx* ctx, int i); // i-th pooled event (grown on demand)
+// i-th event of a second pool, for the fork / join pairs of the products that
+// run two independent launches on the main and side streams at once (their
+// indices never meet chol_fwd's, which grow with the panel count)
+hipEvent_t smg_fork_event(smg_ctx* ctx, int i);
 // RAII: issue the enclosed launches on the side stream
 struct smg_on_side {
   smg_ctx* ctx;
