@@ -123,8 +123,10 @@ int smg_chol_tangent_fwd_w(smg_ctx* ctx, const double* L, int ldl, const double*
   // it enters as op(B) = A'^T: the B tile then loads n-contiguous runs; the
   // NN form with a k-contiguous B ran 30-50 % slower in the HVP's trace)
   if ((rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, W, ld, Ad, ldad, 0.0, Ld, ld, SMG_TRI_A_LOWER))) return rc;
-  if ((rc = smg_gemm_impl(ctx, 0, 1, 3, n, n, n, 1.0, Ld, ld, W, ld, 0.0, Y, ld, SMG_TRI_B_UPPER))) return rc;
-  if ((rc = smg_phi(ctx, n, Y, ld, P, ld, 0))) return rc;
+  // (P = Phi(Y) from the same epilogue: its strict upper is zeroed inside the
+  // diagonal 64-blocks only -- L P cuts K to k >= j, T P^T to k <= j, in whole
+  // blocks, so no other upper entry is read)
+  if ((rc = smg_gemm_sym_phi_impl(ctx, 0, 1, n, n, 1.0, Ld, ld, W, ld, 0.0, Y, ld, P, ld, SMG_TRI_B_UPPER))) return rc;
   if ((rc = smg_multiply_lower_fwd(ctx, L, ldl, P, ld, n, Ld, ld))) return rc;
   return fork ? join_side(ctx, 1) : SMG_OK;
 }

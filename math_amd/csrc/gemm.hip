@@ -398,7 +398,10 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
       const int il = e % BM, jl = e / BM;
       const int i = i0 + il, j = j0 + c0 + jl;
       if (i >= m || j >= n) continue;
-      if (LOWT && i < j) continue;
+      if (LOWT && i < j) {
+        if (MODE == 3 && C2) C2[i + (size_t)j * ldc2] = 0.0;  // (Phi's zero upper inside the diagonal tiles)
+        continue;
+      }
       if (UPT && i > j) continue;
       const double v = pool[jl * (BM + 1) + il];
       if (slab) {
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
         }
         C[i + (size_t)j * ldc] = out;
         if (MODE == 3 && i > j) C[j + (size_t)i * ldc] = out;
-        if (MODE == 4 && i >= j) C2[i + (size_t)j * ldc2] = i == j ? 0.5 * out : out;
+        if ((MODE == 4 || (MODE == 3 && C2)) && i >= j) C2[i + (size_t)j * ldc2] = i == j ? 0.5 * out : out;
       }
     }
     if (c0 + ECH < BN) __syncthreads();
@@ -541,8 +544,8 @@ int launch(smg_ctx* ctx, int m, int n, int k, double alpha, const double* A,
   }
   hipLaunchKernelGGL((k_gemm<BM, BN, BK, TA, TB, MODE, KS>), dim3(ntp * splits, batch), dim3(256 * KS), 0,
                      ctx->stream, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tm,
-                     ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri, MODE == 4 ? t_c2 : nullptr,
-                     MODE == 4 ? t_ldc2 : 0, t_bz);
+                     ntiles, kchunk, slab, sA, sB, sC, px, ntp, tri, MODE >= 3 ? t_c2 : nullptr,
+                     MODE >= 3 ? t_ldc2 : 0, t_bz);
   if (splits > 1) {
     const long long tot = (long long)m * n;
     if ((m & 1) == 0) {
@@ -748,6 +751,31 @@ int smg_gemm_dual_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double
   else if (ta && !tb) rc = dispatch_tile<true, false, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   else if (!ta && tb) rc = dispatch_tile<false, true, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   else rc = dispatch_tile<true, true, 4>(ctx, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  t_c2 = nullptr;
+  return rc;
+}
+
+// C = alpha op(A) op(B) + beta C, symmetric: its lower triangle computed and
+// stored mirrored (uplo 3), and P = Phi(C) (strict lower, halved diagonal) as
+// a second output.  P's strict upper is written (zeros) only inside the
+// diagonal tiles: a reader must cut K to P's lower triangle
+// (SMG_TRI_B_LOWER / TRI_B_UPPER on P^T), as the Cholesky tangent's do.
+int smg_gemm_sym_phi_impl(smg_ctx* ctx, int ta, int tb, int n, int k, double alpha, const double* A, int lda,
+                          const double* B, int ldb, double beta, double* C, int ldc, double* P, int ldp, int tri) {
+  if (n <= 0) return SMG_OK;
+  if (k <= 0 || alpha == 0.0 || !P) return SMG_ERR_ARG;
+  smg_prof_scope prof(ctx, SMG_FAM_GEMM);
+  if (ctx->prof_on) {
+    const double cut = (tri & 3) && (tri & 12) ? 1.0 / 3.0 : (tri ? 0.5 : 1.0);
+    ctx->prof_flops[SMG_FAM_GEMM] += cut * 2.0 * k * ((double)n * n - (double)n * (n - 1) / 2);
+  }
+  t_c2 = P;
+  t_ldc2 = ldp;
+  int rc;
+  if (!ta && !tb) rc = dispatch_tile<false, false, 3>(ctx, n, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  else if (ta && !tb) rc = dispatch_tile<true, false, 3>(ctx, n, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  else if (!ta && tb) rc = dispatch_tile<false, true, 3>(ctx, n, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
+  else rc = dispatch_tile<true, true, 3>(ctx, n, n, k, alpha, A, lda, B, ldb, beta, C, ldc, tri);
   t_c2 = nullptr;
   return rc;
 }

@@ -244,6 +244,12 @@ int smg_gemm_dual_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double
                        const double* B, int ldb, double beta, double* C, int ldc, double* C2, int ldc2,
                        int tri = 0);
 
+// C = alpha op(A) op(B) + beta C symmetric (lower computed, stored mirrored)
+// and P = Phi(C) (strict lower, halved diagonal; upper zero inside the
+// diagonal 64-blocks only) (one pass, gemm.hip)
+int smg_gemm_sym_phi_impl(smg_ctx* ctx, int ta, int tb, int n, int k, double alpha, const double* A, int lda,
+                          const double* B, int ldb, double beta, double* C, int ldc, double* P, int ldp, int tri);
+
 int smg_gemm_batched_impl(smg_ctx* ctx, int ta, int tb, int m, int n, int k, double alpha,
                           const double* A, int lda, long long sA, const double* B, int ldb,
                           long long sB, double beta, double* C, int ldc, long long sC, int batch);

@@ -435,7 +435,8 @@ def test_progressive_w_only_and_tangent_from_it(ctx):
     order) and within 1e-10 of numpy's inverse; then smg_chol_tangent_fwd_w on
     that W (its strict upper outside the 512-row diagonal blocks left NaN, so
     any read of it would poison the outputs) against smg_chol_tangent_fwd,
-    which forms its own zero-padded W: Ld, Y, P within 1e-10."""
+    which forms its own zero-padded W: Ld, Y, P within 1e-10 (P from a NaN
+    buffer: L P reads only what the fused Y / Phi(Y) epilogue writes)."""
     import ctypes
     N = 2048
     rng = np.random.default_rng(5)
@@ -471,7 +472,8 @@ def test_progressive_w_only_and_tangent_from_it(ctx):
     dAd = ctx.put(F(Ad))
     res = []
     for given in (True, False):
-        Wt, Y, P, Ld = (ctx.zeros(N * N) for _ in range(4))
+        Wt, Y, Ld = (ctx.zeros(N * N) for _ in range(3))
+        P = ctx.put(np.full(N * N, np.nan))  # (P = Phi(Y) is written lower plus the diagonal blocks' zero upper)
         if given:
             ctx.call("smg_chol_tangent_fwd_w", dL, N, ws, dAd, N, N, Wt, Y, P, Ld, N)
         else:
