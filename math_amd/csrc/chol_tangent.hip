@@ -12,7 +12,7 @@
 //   forward   T = tril(W A') (2 N^3 / 3),  Y = T W^T lower-computed and mirrored (N^3/3),
 //             P = Phi(Y),  L' = L P (N^3/3)
 //   reverse   Ladj += tril(tril(Ld_adj) P^T),  Padj = tril(L^T tril(Ld_adj))  (2 N^3/3)
-//             S = Phi(Padj) + Phi(Padj)^T   (sym_from_lower of Padj)
+//             S = Phi(Padj) + Phi(Padj)^T   (Padj's lower mirrored, by its product's store)
 //             M = W^T S (N^3; W^T stored by the forward: an NN product)
 //             Ladj -= tril(M Y) (N^3)
 //             A'adj += (1/2) W^T S W = (1/2) M W, symmetric: its upper triangle (N^3 / 3)
@@ -158,9 +158,9 @@ int smg_chol_tangent_rev(smg_ctx* ctx, const double* L, int ldl, const double* W
   {
     smg_on_side on(ctx);
     if (!fork) ctx->stream = ctx->main_stream;
-    if ((rc = smg_gemm_impl(ctx, 1, 0, 1, n, n, n, 1.0, L, ldl, M, n, 0.0, S, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
+    // (S = Padj's lower triangle mirrored: the product's symmetric store, uplo 3)
+    if ((rc = smg_gemm_impl(ctx, 1, 0, 3, n, n, n, 1.0, L, ldl, M, n, 0.0, S, n, SMG_TRI_A_UPPER | SMG_TRI_B_LOWER)))
       return rc;
-    if ((rc = smg_sym_from_lower(ctx, n, S, n))) return rc;
   }
   if (Ladj && (rc = smg_gemm_impl(ctx, 0, 1, 1, n, n, n, 1.0, M, n, P, ld, 1.0, Ladj, ldladj,
                                   SMG_TRI_A_LOWER | SMG_TRI_B_UPPER)))
