@@ -395,12 +395,15 @@ int smg_multiply_lower_fwd(smg_ctx* ctx, const double* L, int ldl, const double*
  * reference forms the same L' through Eigen's LLT on fvar<var> scalars,
  * prim/mat/fun/cholesky_decompose.hpp).  aux: smg_cholesky_fwd's block
  * inverses of L (NULL: rebuilt).  fwd: W = L^{-1} (lower, zeros
- * above), Wt = W^T, Y = W A' W^T (symmetric, full), P = Phi(Y), Ld = L P
- * (lower); W, Wt, Y, P: n x n, ld.  rev (Ld_adj lower): Ladj += tril(Ld_adj P^T)
- * - tril(W^T S Y), A'adj += (1/2) W^T S W (symmetric, both triangles), with
- * S = Phi(Padj) + Phi(Padj)^T, Padj = tril(L^T tril(Ld_adj)); NULL Ladj /
- * Adadj skip.  ws: 2 n^2 doubles.  ~5.3 n^3 flops for both against 7 n^3
- * through two N-column triangular solves. */
+ * above), Wt = W^T, Y = W A' W^T (symmetric, full), P = Phi(Y) (its strict
+ * upper zeroed only inside the diagonal tiles: the node's own products read
+ * no other part of it), Ld = L P (lower); W, Wt, Y, P: n x n, ld.  rev
+ * (Ld_adj lower): Ladj += tril(Ld_adj P^T) - tril(W^T S Y), A'adj +=
+ * (1/2) W^T S W (symmetric, both triangles), with S = Phi(Padj) + Phi(Padj)^T,
+ * Padj = tril(L^T tril(Ld_adj)); NULL Ladj / Adadj skip.  ws: 2 n^2 doubles.
+ * ~5.3 n^3 flops for both against 7 n^3 through two N-column triangular
+ * solves.  Independent products run on the context's side stream and are
+ * joined before return: the outputs are ordered on the context stream. */
 int smg_chol_tangent_fwd(smg_ctx* ctx, const double* L, int ldl, const double* aux, const double* Ad, int ldad, int n,
                          double* W, double* Wt, double* Y, double* P, double* Ld, int ld);
 /* smg_chol_tangent_fwd on a given W = L^{-1} (ld, lower; its strict upper
