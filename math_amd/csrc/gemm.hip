@@ -131,6 +131,31 @@ __device__ __forceinline__ void tri_decode(int t, int& bi, int& bj) {
   bj = t - r * (r + 1) / 2;
 }
 
+// t -> (bi, bj) over the lower triangle of T x T tiles in groups of 8 block
+// rows, each group column by column (its rows i >= j within a column): the
+// tiles in flight at once share a few A row panels and B column panels, where
+// the row-major order swept every B panel of a row before the next row
+__device__ __forceinline__ void tri_decode_grouped(int t, int T, int& bi, int& bj) {
+  constexpr int G = 8;
+  int r, c;
+  tri_decode(t, r, c);
+  const int r0 = r / G * G, r1 = min(r0 + G, T), h = r1 - r0;
+  int q = t - r0 * (r0 + 1) / 2;
+  if (q < r0 * h) {
+    bi = r0 + q % h;
+    bj = q / h;
+    return;
+  }
+  q -= r0 * h;
+  int j = r0;
+  while (q >= r1 - j) {
+    q -= r1 - j;
+    ++j;
+  }
+  bi = j + q;
+  bj = j;
+}
+
 // MODE: 0 = full C, 1 = lower / 2 = upper triangle of C only (BM == BN, m == n),
 //   3 = the lower triangle computed and stored mirrored too (a symmetric C
 //       from its lower half: no separate sym_from_lower pass),
@@ -231,6 +256,14 @@ __global__ __launch_bounds__(256 * KS) void k_gemm(
       bi = q + (T - 1 - r);
     } else if (tri == SMG_TRI_A_LOWER) {
       tri_decode(ntiles - 1 - tile, bi, bj);
+    } else if (tri == 0 && ntiles >= 64) {
+      // equal-work tiles (no K cut): XCD x (workgroups b = x mod 8, dispatched
+      // round-robin) takes one contiguous run of the grouped tile order, so
+      // its L2 holds a few row panels of A and column panels of B at a time
+      // (row-major over all XCDs, the last K^{-1} share fetched 530 MB
+      // against 151 MB algorithmic, r06 PMC)
+      const int b = tile, x = b & 7, per = ntiles >> 3, extra = ntiles & 7;
+      tri_decode_grouped(x * per + (x < extra ? x : extra) + (b >> 3), tiles_m, bi, bj);
     } else {
       tri_decode(tile, bi, bj);
     }

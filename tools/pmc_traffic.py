@@ -76,15 +76,21 @@ if glob.glob(BASE % (TAG, "gp_fetch")):
                            "write_bytes_per_launch": mean(pw) * 1024.0 * rw, "algorithmic_bytes_per_launch": alg_panel}
     res["k_chol_panel"]["waste_ratio"] = (res["k_chol_panel"]["fetch_bytes_per_launch"] +
                                           res["k_chol_panel"]["write_bytes_per_launch"]) / alg_panel
-    share = [(g, v) for k, g, v in fd if k.startswith("k_gemm<64, 64, 16, true, false, 1")]
-    sharew = [(g, v) for k, g, v in wd if k.startswith("k_gemm<64, 64, 16, true, false, 1")]
+    # the share with the most 64 x 64 tiles (grid_x counts threads: 256 per workgroup, 512 for the 8-wave
+    # ", 2>" variant; until round 6 the widest grid was taken, which picked the 8-wave share of row 5)
+    def tiles(k, g):
+        return g // (512 if k.rstrip().endswith("2>") else 256)
+    share = [(tiles(k, g), v) for k, g, v in fd if k.startswith("k_gemm<64, 64, 16, true, false, 1")]
+    sharew = [(tiles(k, g), v) for k, g, v in wd if k.startswith("k_gemm<64, 64, 16, true, false, 1")]
     if share:
-        gmax = max(g for g, v in share)
-        f1 = [v for g, v in share if g == gmax]
-        w1 = [v for g, v in sharew if g == gmax]
-        # W_7 (512 x N) read + C's lower triangle read and written: 8 (512 N + N^2) B
-        alg_share = 8.0 * (P * N + N * N)
-        res["k_gemm_share_last"] = {"grid": gmax, "launches": len(f1), "fetch_bytes_per_launch": mean(f1) * 1024.0 * rf,
+        tmax = max(t for t, v in share)
+        f1 = [v for t, v in share if t == tmax]
+        w1 = [v for t, v in sharew if t == tmax]
+        r1 = 64 * int(round(((8 * tmax + 1) ** 0.5 - 1) / 2))  # tmax = T (T + 1) / 2 tiles, C is r1 x r1 lower
+        # W_k (512 x r1) read + C's lower triangle (r1 (r1 + 1) / 2) read and written
+        alg_share = 8.0 * (P * r1 + r1 * (r1 + 1))
+        res["k_gemm_share_last"] = {"tiles": tmax, "rows": r1, "launches": len(f1),
+                                    "fetch_bytes_per_launch": mean(f1) * 1024.0 * rf,
                                     "write_bytes_per_launch": mean(w1) * 1024.0 * rw,
                                     "algorithmic_bytes_per_launch": alg_share}
         res["k_gemm_share_last"]["waste_ratio"] = (res["k_gemm_share_last"]["fetch_bytes_per_launch"] +
